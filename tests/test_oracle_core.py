@@ -1,0 +1,85 @@
+"""Pin the CPU oracle's arithmetic core: f128 field, roots of unity, coset NTT, BLAKE3, Merkle.
+
+Field and NTT are checked against independent pure-Python big-int arithmetic; BLAKE3 against the
+published BLAKE3 test vectors (input = i % 251 byte pattern, and "abc").
+"""
+import random
+
+import pytest
+
+P = 2**128 - 45 * 2**40 + 1
+TWO_ADIC_ROOT = 23953097886125630542083529559205016746  # SURVEY Appendix A, winter-math f128
+
+
+def edge_values():
+    return [0, 1, 2, P - 1, P - 2, 2**64 - 1, 2**64, 2**127, P - 2**64, 45 * 2**40, 2**128 - 45 * 2**40]
+
+
+def test_field_ops_vs_bigint(oracle):
+    rnd = random.Random(7)
+    vals = edge_values() + [rnd.randrange(P) for _ in range(300)]
+    for i in range(len(vals)):
+        a, b = vals[i], vals[(i * 7 + 3) % len(vals)]
+        assert oracle.fop("or_fadd", a, b) == (a + b) % P
+        assert oracle.fop("or_fsub", a, b) == (a - b) % P
+        assert oracle.fop("or_fmul", a, b) == (a * b) % P
+    for a in vals[:60]:
+        inv = oracle.fop("or_finv", a)
+        assert inv == (pow(a, P - 2, P) if a else 0)
+        e = rnd.randrange(2**128)
+        assert oracle.fop("or_fexp", a, e) == pow(a, e, P)
+
+
+def test_roots_of_unity(oracle):
+    assert pow(3, (P - 1) >> 40, P) == TWO_ADIC_ROOT
+    assert oracle.root_of_unity(40) == TWO_ADIC_ROOT
+    for k in (1, 3, 8, 20, 23):
+        w = oracle.root_of_unity(k)
+        assert pow(w, 2**k, P) == 1 and pow(w, 2 ** (k - 1), P) == P - 1
+
+
+@pytest.mark.parametrize("size,m,offset", [(8, 8, 1), (16, 5, 3), (32, 32, 3), (64, 8, 12345)])
+def test_coset_ntt_vs_direct(oracle, size, m, offset):
+    rnd = random.Random(size * 31 + m)
+    coeffs = [rnd.randrange(P) for _ in range(m)]
+    w = oracle.root_of_unity(size.bit_length() - 1)
+    direct = []
+    for j in range(size):
+        x = offset * pow(w, j, P) % P
+        direct.append(sum(c * pow(x, k, P) for k, c in enumerate(coeffs)) % P)
+    got = oracle.eval_coset(coeffs, size, offset)
+    assert got == direct
+    back = oracle.interp_coset(got, offset)
+    assert back == coeffs + [0] * (size - m)
+
+
+# Published BLAKE3 hash-mode vectors (BLAKE3 repo test_vectors.json: input[i] = i % 251).
+BLAKE3_VECTORS = {
+    0: "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
+    1: "2d3adedff11b61f14c886e35afa036736dcd87a74d27b5c1510225d0f592e213",
+}
+
+
+def test_blake3_known_answers(oracle):
+    for n, hexd in BLAKE3_VECTORS.items():
+        data = bytes(i % 251 for i in range(n))
+        assert oracle.blake3(data).hex() == hexd
+    assert oracle.blake3(b"abc").hex() == "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"
+
+
+def test_blake3_structure(oracle):
+    # block/chunk boundaries must not collide and must be deterministic
+    seen = set()
+    for n in (63, 64, 65, 127, 128, 448, 1023, 1024, 1025, 2048, 2049, 3072, 5121):
+        d = oracle.blake3(bytes(i % 251 for i in range(n)))
+        assert d not in seen
+        seen.add(d)
+        assert d == oracle.blake3(bytes(i % 251 for i in range(n)))
+
+
+def test_merkle_root(oracle):
+    leaves = [oracle.blake3(bytes([i])) for i in range(8)]
+    lvl = leaves
+    while len(lvl) > 1:
+        lvl = [oracle.blake3(lvl[2 * i] + lvl[2 * i + 1]) for i in range(len(lvl) // 2)]
+    assert oracle.merkle_root(b"".join(leaves)) == lvl[0]
