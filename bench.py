@@ -1,0 +1,198 @@
+"""Benchmark: STARK prove throughput (trace-steps/s) on MI355X, BASELINE.json metric.
+
+Workload (BASELINE.json configs[2]): a 2^20-step Encrypt-zkVM program mixing READ2/ADD2/SMUL
+ciphertext ops (zkvm_amd.workloads.cipher_mix_program), proved with the reference options
+ProofOptions(32, 8, 0, None, 8, 127) (vm/src/lib.rs:20).  One step = one full Prover::prove of that
+trace: trace LDE + commitment, constraint evaluation, composition commitment, OOD/DEEP, FRI,
+queries and proof bytes.  The trace is generated once on the host (VM, untimed) and uploaded to
+HBM before the timed region; each timed step proves it from device memory to proof bytes.
+
+Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
+scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
+whole-job rate.  rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (ROOT, ROOT / "encrypt-zkvm_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+METRIC = "STARK prove: trace-steps/sec at 2^20 steps; achieved HBM GB/s vs 8 TB/s peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg, local):
+    if pg is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize(local)
+    pg.barrier()
+
+
+def max_over_ranks(pg, value, local):
+    if pg is None:
+        return value
+    import torch
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(log_n: int):
+    """The oracle's single-threaded CPU prove (the build's restatement of the reference path; the
+    reference Rust prover cannot be built here) on a bounded sample of the same generator."""
+    from oracle import oracle as orc
+    from zkvm_amd.prover import vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    orc.build()
+    src = ops_for_trace_len(log_n, "cipher")
+    w = make_workload(src, seed=77)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    pub = orc.make_pub(h, outputs)
+    t0 = time.perf_counter()
+    orc.prove(trace, pub)
+    dt = time.perf_counter() - t0
+    n = trace.shape[1]
+    return {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle or_prove (C, 1 thread) on one 2^{log_n}-step trace of the same cipher-mix "
+                      f"generator, reference options: {dt:.1f} s"}
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (tools/pmc_traffic.py), if any."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get("per_launch_bytes", {}).get(kernel)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-n", type=int, default=20)
+    ap.add_argument("--cpu-log-n", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, pg = setup_dist(args.gpus)
+    from zkvm_amd import native
+    from zkvm_amd.prover import GpuProver, ProofOptions, make_pub_inputs, vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+
+    native.lib()  # fail loudly without the HIP library
+    src = ops_for_trace_len(args.log_n, "cipher")
+    w = make_workload(src, seed=1000 + rank)
+    t0 = time.perf_counter()
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    n = trace.shape[1]
+    log(f"[rank {rank}] VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    opts = ProofOptions()
+    gpu = GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor)
+    d_trace, _ = gpu.upload_trace(trace)
+
+    for _ in range(args.warmup):
+        proof, _, _, _ = gpu.prove_device(d_trace, n, pub, opts)
+
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        proof, _, _, _ = gpu.prove_device(d_trace, n, pub, opts)
+    barrier(pg, local)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(pg, elapsed, local)
+    stages = gpu.stage_times()
+
+    # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream)
+    gpu.profile(True)
+    gpu.prove_device(d_trace, n, pub, opts)
+    kstats = gpu.kernel_stats()
+    gpu.profile(False)
+
+    verified = None
+    if rank == 0 and not args.no_verify:
+        import ctypes as C
+        from oracle import oracle as orc
+        orc.build()
+        opub = orc.PubInputs()
+        C.memmove(opub.program_hash, bytes(pub.program_hash), 32)
+        C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
+        opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
+        verified = orc.verify(proof, opub, 95)[0] == 0
+
+    if rank != 0:
+        if pg is not None:
+            pg.destroy_process_group()
+        return
+
+    dom = max(kstats.items(), key=lambda kv: kv[1][0])
+    name, (tot_ms, launches, tot_bytes) = dom
+    avg_ms = tot_ms / launches
+    achieved = tot_bytes / (tot_ms / 1e3) / 1e9
+    prove_total_ms = sum(v[0] for v in kstats.values())
+    roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name),
+                "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
+                "alg_bytes_per_launch": tot_bytes / launches,
+                "kernel_share_of_device_time": round(tot_ms / prove_total_ms, 3)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_log_n)
+    value = world * n * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f128", "data": "synthetic (seeded VM trace)",
+        "config": {"workload": f"configs[2]: 2^{args.log_n}-step READ2/ADD2/SMUL cipher-mix program, full prove",
+                   "trace_len": n, "trace_width": 28, "lde_len": n * opts.blowup_factor,
+                   "options": "ProofOptions(32, 8, 0, None, 8, 127)", "parallelism": f"independent proof per GPU x{world}"},
+        "roofline": roofline, "cpu_baseline": cpu,
+        "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+        "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+        "proof_bytes": len(proof), "proof_verified_by_oracle": verified,
+    }
+    print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,227 @@
+// f128.hpp -- the winterfell f128 prime field, p = 2^128 - 45*2^40 + 1, for gfx950 and host.
+//
+// Canonical representation in [0, p), stored as two little-endian u64 halves: exactly the
+// 16-byte wire format of winter-math `f128::BaseElement` (prover/src/lib.rs:4).
+//
+// Device multiply: 4x4 schoolbook on 32-bit limbs with v_mad_u64_u32 (16 partial products),
+// then two folds of the high half with 2^128 = C (mod p), C = 45*2^40 - 1, and one conditional
+// subtraction.  Everything is branch-free so a wavefront never diverges on data.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ZK_HD __host__ __device__ __forceinline__
+
+struct fe {
+    uint64_t lo, hi;
+};
+
+static constexpr uint64_t ZK_P_LO = 0xffffd30000000001ULL;  // p mod 2^64
+static constexpr uint64_t ZK_P_HI = 0xffffffffffffffffULL;  // p >> 64
+static constexpr uint64_t ZK_C = 0x2cffffffffffULL;         // 2^128 - p = 45*2^40 - 1
+
+ZK_HD fe fe_make(uint64_t lo, uint64_t hi = 0) { return fe{lo, hi}; }
+ZK_HD fe fe_zero() { return fe{0, 0}; }
+ZK_HD fe fe_one() { return fe{1, 0}; }
+ZK_HD bool fe_eq(fe a, fe b) { return a.lo == b.lo && a.hi == b.hi; }
+ZK_HD bool fe_is_zero(fe a) { return (a.lo | a.hi) == 0; }
+
+// a + b mod p.  s = a + b (129 bits); s >= p  <=>  carry(a+b) or carry(s + C); then s - p = s + C.
+ZK_HD fe fe_add(fe a, fe b) {
+    uint64_t lo = a.lo + b.lo;
+    uint64_t c0 = lo < a.lo;
+    uint64_t hi = a.hi + b.hi + c0;
+    uint64_t c1 = (hi < a.hi) | ((hi == a.hi) & c0);
+    uint64_t tlo = lo + ZK_C;
+    uint64_t t0 = tlo < lo;
+    uint64_t thi = hi + t0;
+    uint64_t c2 = (thi < hi);
+    bool wrap = c1 | c2;
+    return fe{wrap ? tlo : lo, wrap ? thi : hi};
+}
+
+// a - b mod p.  On borrow the 128-bit difference d = a - b + 2^128; the result is d - C.
+ZK_HD fe fe_sub(fe a, fe b) {
+    uint64_t lo = a.lo - b.lo;
+    uint64_t bw0 = a.lo < b.lo;
+    uint64_t hi = a.hi - b.hi - bw0;
+    bool bw = (a.hi < b.hi) | ((a.hi == b.hi) & bw0);
+    uint64_t tlo = lo - ZK_C;
+    uint64_t thi = hi - (lo < ZK_C);
+    return fe{bw ? tlo : lo, bw ? thi : hi};
+}
+
+ZK_HD fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
+
+ZK_HD uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+ZK_HD uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+
+// r[0..8) = x[0..4) * y[0..4) (operand scanning; each step fits one v_mad_u64_u32 + carry add)
+ZK_HD void mul_4x4(const uint32_t x[4], const uint32_t y[4], uint32_t r[8]) {
+    uint64_t t;
+    uint32_t c;
+    t = (uint64_t)x[0] * y[0];
+    r[0] = lo32(t);
+    c = hi32(t);
+    t = (uint64_t)x[0] * y[1] + c;
+    r[1] = lo32(t);
+    c = hi32(t);
+    t = (uint64_t)x[0] * y[2] + c;
+    r[2] = lo32(t);
+    c = hi32(t);
+    t = (uint64_t)x[0] * y[3] + c;
+    r[3] = lo32(t);
+    r[4] = hi32(t);
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+        c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            t = (uint64_t)x[i] * y[j] + (uint64_t)r[i + j] + c;
+            r[i + j] = lo32(t);
+            c = hi32(t);
+        }
+        r[i + 4] = c;
+    }
+}
+
+// reduce the 256-bit value r[0..8) mod p
+ZK_HD fe reduce256(const uint32_t r[8]) {
+    // S = L + H*45*2^40 - H   (L = r[0..4), H = r[4..8)); 0 <= S < 2^175
+    uint32_t m[5];
+    uint64_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        t = (uint64_t)r[4 + i] * 45u + (t >> 32);
+        m[i] = lo32(t);
+    }
+    m[4] = hi32(t);
+    // M << 40 as 6 limbs: limb k = (m[k-1] << 8) | (m[k-2] >> 24)
+    uint32_t s6[6];
+    s6[0] = 0;
+    s6[1] = m[0] << 8;
+    s6[2] = (m[1] << 8) | (m[0] >> 24);
+    s6[3] = (m[2] << 8) | (m[1] >> 24);
+    s6[4] = (m[3] << 8) | (m[2] >> 24);
+    s6[5] = (m[4] << 8) | (m[3] >> 24);
+    // + L
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        acc += (uint64_t)s6[i] + (i < 4 ? r[i] : 0u);
+        s6[i] = lo32(acc);
+        acc >>= 32;
+    }
+    // - H
+    int64_t sacc = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        sacc += (int64_t)s6[i] - (int64_t)(i < 4 ? r[4 + i] : 0u);
+        s6[i] = (uint32_t)sacc;
+        sacc >>= 32;  // arithmetic shift: borrow propagates as -1
+    }
+    // second fold: T = S_lo + S_hi*45*2^40 - S_hi, S_hi = s6[4] | s6[5] << 32 (< 2^47)
+    uint64_t sh = (uint64_t)s6[4] | ((uint64_t)s6[5] << 32);
+    uint64_t q = sh * 45u;                        // < 2^53
+    uint64_t add_lo = q << 40, add_hi = q >> 24;  // q * 2^40 as 128 bits
+    uint64_t lo = (uint64_t)s6[0] | ((uint64_t)s6[1] << 32);
+    uint64_t hi = (uint64_t)s6[2] | ((uint64_t)s6[3] << 32);
+    uint64_t nlo = lo + add_lo;
+    uint64_t c = nlo < lo;
+    uint64_t nhi = hi + add_hi + c;
+    uint64_t carry = (nhi < hi) | ((nhi == hi) & c);
+    // subtract S_hi
+    uint64_t blo = nlo - sh;
+    uint64_t b = nlo < sh;
+    uint64_t bhi = nhi - b;
+    carry -= (nhi < b);  // borrow out of the top cancels a carry (value stays >= 0)
+    // if carry: value = 2^128 + (bhi:blo)  ->  (bhi:blo) + C  (cannot overflow again)
+    uint64_t clo = blo + (carry ? ZK_C : 0);
+    uint64_t chi = bhi + (clo < blo);
+    // final conditional subtract: x >= p  <=>  x + C overflows 2^128
+    uint64_t ulo = clo + ZK_C;
+    uint64_t uhi = chi + (ulo < clo);
+    bool ge = uhi < chi;
+    return fe{ge ? ulo : clo, ge ? uhi : chi};
+}
+
+// the device multiply (also callable on the host, for the host-side unit test)
+ZK_HD fe fe_mul_limbs(fe a, fe b) {
+    uint32_t x[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+    uint32_t y[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+    uint32_t r[8];
+    mul_4x4(x, y, r);
+    return reduce256(r);
+}
+
+// device and host overloads (clang resolves by target)
+__device__ __forceinline__ fe fe_mul(fe a, fe b) { return fe_mul_limbs(a, b); }
+// host: unsigned __int128 with the same two folds
+__host__ static inline fe fe_from_u128(unsigned __int128 v) { return fe{(uint64_t)v, (uint64_t)(v >> 64)}; }
+__host__ static inline unsigned __int128 fe_to_u128(fe a) { return ((unsigned __int128)a.hi << 64) | a.lo; }
+__host__ static inline fe fe_mul(fe a, fe b) {
+    typedef unsigned __int128 u128;
+    const u128 M = (u128)UINT64_MAX, C = (u128)ZK_C;
+    const u128 P = ((u128)ZK_P_HI << 64) | ZK_P_LO;
+    u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
+    u128 mid = (p00 >> 64) + (p01 & M) + (p10 & M);
+    u128 lo = (p00 & M) | (mid << 64);
+    u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
+    while (hi) {
+        u128 q00 = (hi & M) * C, q10 = (hi >> 64) * C;
+        u128 add_lo = q00 + (q10 << 64);
+        u128 add_hi = (q10 >> 64) + (add_lo < q00);
+        u128 s = lo + add_lo;
+        hi = add_hi + (s < lo);
+        lo = s;
+    }
+    if (lo >= P) lo -= P;
+    return fe_from_u128(lo);
+}
+
+ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }
+
+ZK_HD fe fe_exp(fe b, uint64_t e_lo, uint64_t e_hi = 0) {
+    // right-to-left square and multiply over the 128-bit exponent (e_hi:e_lo)
+    fe r = fe_one();
+    for (int i = 0; i < 128; i++) {
+        uint64_t word = i < 64 ? e_lo : e_hi;
+        int sh = i & 63;
+        uint64_t remaining = (word >> sh) | (i < 64 ? e_hi : 0);
+        if (remaining == 0) break;
+        if ((word >> sh) & 1) r = fe_mul(r, b);
+        b = fe_mul(b, b);
+    }
+    return r;
+}
+
+// a^(2^k) by repeated squaring
+ZK_HD fe fe_sqr_n(fe a, int k) {
+    for (int i = 0; i < k; i++) a = fe_mul(a, a);
+    return a;
+}
+
+// a^(p-2) with an addition chain: p-2 = 0xffffffffffffffff_ffffd2ff_ffffffff
+// = (2^80 - 1) * 2^48 + 0xd2 * 2^40 + (2^40 - 1).   143 multiplications in total.
+ZK_HD fe fe_inv(fe a) {
+    fe x1 = a;
+    fe x2 = fe_mul(fe_sqr_n(x1, 1), x1);
+    fe x4 = fe_mul(fe_sqr_n(x2, 2), x2);
+    fe x8 = fe_mul(fe_sqr_n(x4, 4), x4);
+    fe x16 = fe_mul(fe_sqr_n(x8, 8), x8);
+    fe x32 = fe_mul(fe_sqr_n(x16, 16), x16);
+    fe x40 = fe_mul(fe_sqr_n(x32, 8), x8);
+    fe x80 = fe_mul(fe_sqr_n(x40, 40), x40);  // a^(2^80 - 1)
+    // append the byte 0xd2 = 1101 0010
+    fe r = x80;
+    const int bits[8] = {1, 1, 0, 1, 0, 0, 1, 0};
+    for (int i = 0; i < 8; i++) {
+        r = fe_mul(r, r);
+        if (bits[i]) r = fe_mul(r, a);
+    }
+    // append 40 ones
+    r = fe_mul(fe_sqr_n(r, 40), x40);
+    return r;
+}
+
+ZK_HD fe fe_from_u64(uint64_t v) { return fe{v, 0}; }

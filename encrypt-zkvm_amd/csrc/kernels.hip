@@ -1,0 +1,822 @@
+// kernels.hip -- gfx950 kernels of the STARK prove path (winterfell 0.9 generate_proof stages
+// S2..S6; kernel list K1..K8 of SURVEY 7).
+//
+// Data layout in HBM (DESIGN.md "Data layout"):
+//   * polynomials: one contiguous array of n coefficients per column;
+//   * LDE values:  coset-major per column, element (c, i) at base[(c*B + i%B)*n + i/B], i the
+//     natural LDE index (x_i = 3 * w_N^i).  A coset is a plain size-n NTT output, rows i and
+//     i + B (the evaluation frame) are neighbours, and 8 consecutive lanes of a wave reading
+//     natural indices touch 8 cosets x 16 B, so every wave load covers whole 128-B lines.
+//   * digests: 32-byte BLAKE3 words, leaves in natural order, nodes[1] = root.
+// All arithmetic is exact f128 (f128.hpp); no floating point anywhere.
+#include <hip/hip_runtime.h>
+
+#include "blake3.hpp"
+#include "rescue_consts.hpp"
+#include "zk_internal.hpp"
+
+namespace zk {
+
+#define ZK_LAUNCH_CHECK() (void)hipGetLastError()
+
+static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+__device__ __forceinline__ fe ld_fe(const fe *p) { return *p; }
+__device__ __forceinline__ void st_fe(fe *p, fe v) { *p = v; }
+
+// w_n^t from split tables (t < n)
+__device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
+    return fe_mul(lo[t & 2047], hi[t >> 11]);
+}
+
+// ================================================================ NTT engine
+// One block owns a tile of TILE field elements in LDS = LPB lines of M = TILE / LPB elements.
+// Each line is loaded in bit-reversed position and transformed in place by log2(M) radix-2
+// decimation-in-time stages; the result is in natural order.  Lines are padded by one element
+// so that LPB lanes writing the same position of consecutive lines hit different banks.
+constexpr int NTT_THREADS = 512;
+
+template <int LOGM>
+__device__ __forceinline__ int lds_idx(int line, int pos) {
+    constexpr int PAD = LOGM >= 4 ? 1 : 0;
+    return line * ((1 << LOGM) + PAD) + pos;
+}
+
+template <int LOGM, int TILE>
+__device__ void lds_dft(fe *s, const fe *tw4096) {
+    constexpr int M = 1 << LOGM;
+    constexpr int BFLY = TILE / 2;
+#pragma unroll 1
+    for (int lg = 1; lg <= LOGM; lg++) {
+        const int half = 1 << (lg - 1);
+        const int twshift = 12 - lg;  // w_len^j = w_4096^(j * 4096/len)
+        for (int bf = threadIdx.x; bf < BFLY; bf += NTT_THREADS) {
+            int line = bf >> (LOGM - 1);
+            int local = bf & (M / 2 - 1);
+            int j = local & (half - 1);
+            int grp = local >> (lg - 1);
+            int i0 = lds_idx<LOGM>(line, grp * 2 * half + j);
+            int i1 = i0 + half;
+            fe w = tw4096[j << twshift];
+            fe u = s[i0];
+            fe v = fe_mul(s[i1], w);
+            s[i0] = fe_add(u, v);
+            s[i1] = fe_sub(u, v);
+        }
+        __syncthreads();
+    }
+}
+
+struct NttArgs {
+    const fe *in;
+    fe *out;
+    size_t in_stride, out_stride;
+    const fe *tw4096;             // DFT-stage table (forward or inverse)
+    const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
+    const fe *pre_lo, *pre_hi;    // optional pre-scale s^k
+    fe post;                      // post-scale constant
+    int has_post;
+    int log_n;
+};
+
+// Single pass: whole polynomial (n = M <= TILE) per line, LPB = TILE / n polys per block.
+template <int LOGM, int TILE>
+__global__ void __launch_bounds__(NTT_THREADS) ntt_single(NttArgs a, int batch) {
+    extern __shared__ fe s[];
+    constexpr int M = 1 << LOGM;
+    constexpr int LPB = TILE / M;
+    const int b0 = blockIdx.x * LPB;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e >> LOGM, k = e & (M - 1);
+        int b = b0 + line;
+        fe v = fe_zero();
+        if (b < batch) {
+            v = a.in[(size_t)b * a.in_stride + k];
+            if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
+        }
+        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
+    }
+    __syncthreads();
+    lds_dft<LOGM, TILE>(s, a.tw4096);
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e >> LOGM, j = e & (M - 1);
+        int b = b0 + line;
+        if (b >= batch) continue;
+        fe v = s[lds_idx<LOGM>(line, j)];
+        if (a.has_post) v = fe_mul(v, a.post);
+        a.out[(size_t)b * a.out_stride + j] = v;
+    }
+}
+
+// Four-step, pass 1.  n = n1 * n2, input index k = k1 + n1*k2.  A block takes LPB consecutive k1
+// (lines of length n2 = 2^LOGM read at stride n1 -> LPB contiguous elements per row), runs the
+// size-n2 DFT over k2, multiplies by w_n^(j2*k1) and writes X[k1*n2 + j2] (contiguous runs).
+template <int LOGM, int TILE>
+__global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a) {
+    extern __shared__ fe s[];
+    constexpr int M = 1 << LOGM;  // n2
+    constexpr int LPB = TILE / M;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n1 = n >> LOGM;
+    const size_t k1_0 = (size_t)blockIdx.x * LPB;
+    const size_t b = blockIdx.y;
+    const fe *in = a.in + b * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e % LPB, k2 = e / LPB;
+        size_t k = k1_0 + line + n1 * (size_t)k2;
+        fe v = in[k];
+        if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
+        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
+    }
+    __syncthreads();
+    lds_dft<LOGM, TILE>(s, a.tw4096);
+    fe *out = a.out + b * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e >> LOGM, j2 = e & (M - 1);
+        size_t k1 = k1_0 + line;
+        fe v = s[lds_idx<LOGM>(line, j2)];
+        size_t t = ((size_t)j2 * k1) & (n - 1);
+        v = fe_mul(v, pow_split(a.big_lo, a.big_hi, t));
+        out[k1 * M + j2] = v;
+    }
+}
+
+// Four-step, pass 2.  Lines over k1 (length n1 = 2^LOGM, stride n2) for LPB consecutive j2;
+// output A[n2*j1 + j2] (LPB contiguous per j1).
+template <int LOGM, int TILE>
+__global__ void __launch_bounds__(NTT_THREADS) ntt_pass2(NttArgs a) {
+    extern __shared__ fe s[];
+    constexpr int M = 1 << LOGM;  // n1
+    constexpr int LPB = TILE / M;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n2 = n >> LOGM;
+    const size_t j2_0 = (size_t)blockIdx.x * LPB;
+    const size_t b = blockIdx.y;
+    const fe *in = a.in + b * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e % LPB, k1 = e / LPB;
+        fe v = in[(size_t)k1 * n2 + j2_0 + line];
+        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = v;
+    }
+    __syncthreads();
+    lds_dft<LOGM, TILE>(s, a.tw4096);
+    fe *out = a.out + b * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int line = e % LPB, j1 = e / LPB;
+        fe v = s[lds_idx<LOGM>(line, j1)];
+        if (a.has_post) v = fe_mul(v, a.post);
+        out[n2 * (size_t)j1 + j2_0 + line] = v;
+    }
+}
+
+template <int TILE>
+static size_t lds_bytes(int logm) {
+    int M = 1 << logm;
+    return (size_t)(TILE + (logm >= 4 ? TILE / M : 0)) * sizeof(fe);
+}
+
+template <int LOGM, int TILE>
+static void launch_single(hipStream_t st, const NttArgs &a, int batch) {
+    constexpr int LPB = TILE / (1 << LOGM);
+    size_t sh = lds_bytes<TILE>(LOGM);
+    hipFuncSetAttribute((const void *)ntt_single<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    ZK_PROF(st, "ntt_single", 32.0 * batch * (1 << LOGM), hipLaunchKernelGGL((ntt_single<LOGM, TILE>), dim3(cdiv(batch, LPB)), dim3(NTT_THREADS), sh, st, a, batch));
+}
+
+template <int LOGM, int TILE>
+static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
+    constexpr int LPB = TILE / (1 << LOGM);
+    size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
+    size_t sh = lds_bytes<TILE>(LOGM);
+    hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    ZK_PROF(st, "ntt_pass1", 32.0 * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+}
+
+template <int LOGM, int TILE>
+static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
+    constexpr int LPB = TILE / (1 << LOGM);
+    size_t n2 = ((size_t)1 << a.log_n) >> LOGM;
+    size_t sh = lds_bytes<TILE>(LOGM);
+    hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    ZK_PROF(st, "ntt_pass2", 32.0 * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+}
+
+#define ZK_DISPATCH_LOGM(logm, FN, ...)           \
+    switch (logm) {                               \
+    case 1: FN<1, TILE>(__VA_ARGS__); break;      \
+    case 2: FN<2, TILE>(__VA_ARGS__); break;      \
+    case 3: FN<3, TILE>(__VA_ARGS__); break;      \
+    case 4: FN<4, TILE>(__VA_ARGS__); break;      \
+    case 5: FN<5, TILE>(__VA_ARGS__); break;      \
+    case 6: FN<6, TILE>(__VA_ARGS__); break;      \
+    case 7: FN<7, TILE>(__VA_ARGS__); break;      \
+    case 8: FN<8, TILE>(__VA_ARGS__); break;      \
+    case 9: FN<9, TILE>(__VA_ARGS__); break;      \
+    case 10: FN<10, TILE>(__VA_ARGS__); break;    \
+    case 11: FN<11, TILE>(__VA_ARGS__); break;    \
+    case 12: FN<12, TILE>(__VA_ARGS__); break;    \
+    default: break;                               \
+    }
+
+void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
+         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
+    constexpr int TILE = 4096;
+    NttArgs a;
+    a.in = in;
+    a.out = out;
+    a.in_stride = in_stride;
+    a.out_stride = out_stride;
+    a.tw4096 = inverse ? T.dft_inv : T.dft_fwd;
+    a.big_lo = inverse ? T.inv_lo : T.fwd_lo;
+    a.big_hi = inverse ? T.inv_hi : T.fwd_hi;
+    a.pre_lo = pre ? pre->lo : nullptr;
+    a.pre_hi = pre ? pre->hi : nullptr;
+    a.has_post = post_scale != nullptr;
+    a.post = post_scale ? *post_scale : fe_zero();
+    a.log_n = T.log_n;
+    const int L = T.log_n;
+    if (L <= 12) {
+        ZK_DISPATCH_LOGM(L, launch_single, st, a, batch);
+        return;
+    }
+    // n = n1 * n2 with n2 = 2^ceil(L/2) (pass-1 lines), n1 = 2^floor(L/2) (pass-2 lines)
+    const int log_n2 = (L + 1) / 2, log_n1 = L / 2;
+    NttArgs a1 = a;
+    a1.out = tmp;
+    a1.out_stride = (size_t)1 << L;
+    a1.has_post = 0;
+    ZK_DISPATCH_LOGM(log_n2, launch_pass1, st, a1, batch);
+    NttArgs a2 = a;
+    a2.in = tmp;
+    a2.in_stride = (size_t)1 << L;
+    a2.pre_lo = a2.pre_hi = nullptr;
+    ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
+}
+
+// ================================================================ hashing and Merkle trees
+__device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t h[8]) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+__device__ __forceinline__ void load_digest(const uint8_t *src, uint32_t h[8]) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(src);
+    uint4 a = s[0], b = s[1];
+    h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w;
+    h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
+}
+
+// leaf hash of natural LDE row i over a coset-major column set (K3/K5 of SURVEY 7)
+__global__ void __launch_bounds__(256) k_hash_rows(const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    const size_t n = (size_t)1 << log_n;
+    const size_t B = (size_t)1 << log_b;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i & (B - 1), q = i >> log_b;
+        const fe *p = base + r * n + q;
+        const size_t cstride = B * n;
+        uint32_t h[8];
+        b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cstride]; }, h);
+        store_digest(leaves + 32 * i, h);
+    }
+}
+
+void hash_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves) {
+    size_t N = (size_t)1 << (log_n + log_b);
+    unsigned blocks = cdiv(N, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "hash_rows", (16.0 * ncols + 32) * N, hipLaunchKernelGGL(k_hash_rows, dim3(blocks), dim3(256), 0, st, base, ncols, log_n, log_b, leaves));
+}
+
+__global__ void __launch_bounds__(256) k_hash_fri_rows(const fe *layer, size_t L, int fold, uint8_t *leaves) {
+    const size_t rows = L / fold;
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h[8];
+        b3::hash_elements(fold, [&](int k) { return layer[r + (size_t)k * rows]; }, h);
+        store_digest(leaves + 32 * r, h);
+    }
+}
+
+void hash_fri_rows(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves) {
+    unsigned blocks = cdiv(L / fold, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "hash_fri_rows", 16.0 * L + 32.0 * (L / fold), hipLaunchKernelGGL(k_hash_fri_rows, dim3(blocks), dim3(256), 0, st, layer, L, fold, leaves));
+}
+
+// one tree level: dst[i] = merge(src[2i], src[2i+1]) for i < cnt
+__global__ void __launch_bounds__(256) k_merge_level(const uint8_t *src, uint8_t *dst, size_t cnt) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cnt; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t l[8], r[8], h[8];
+        load_digest(src + 64 * i, l);
+        load_digest(src + 64 * i + 32, r);
+        b3::merge(l, r, h);
+        store_digest(dst + 32 * i, h);
+    }
+}
+
+// The top of a tree in one block: src holds 2*cnt digests (cnt <= 256); builds nodes[1 .. 2cnt).
+__global__ void __launch_bounds__(256) k_merge_top(const uint8_t *src, size_t cnt, uint8_t *nodes) {
+    __shared__ uint32_t lvl[512][8];
+    for (size_t i = threadIdx.x; i < 2 * cnt; i += blockDim.x) load_digest(src + 32 * i, lvl[i]);
+    __syncthreads();
+    for (size_t c = cnt; c >= 1; c /= 2) {
+        uint32_t h[8];
+        const bool act = threadIdx.x < c;
+        if (act) b3::merge(lvl[2 * threadIdx.x], lvl[2 * threadIdx.x + 1], h);
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) lvl[threadIdx.x][w] = h[w];
+            store_digest(nodes + 32 * (c + threadIdx.x), h);
+        }
+        __syncthreads();
+    }
+}
+
+void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes) {
+    // invariant: src holds 2*cnt digests whose parents go to nodes[cnt .. 2cnt)
+    size_t cnt = nl / 2;
+    const uint8_t *src = leaves;
+    while (cnt > 256) {
+        unsigned blocks = cdiv(cnt, 256);
+        if (blocks > 65536) blocks = 65536;
+        ZK_PROF(st, "merkle_level", 96.0 * cnt, hipLaunchKernelGGL(k_merge_level, dim3(blocks), dim3(256), 0, st, src, nodes + 32 * cnt, cnt));
+        src = nodes + 32 * cnt;
+        cnt /= 2;
+    }
+    ZK_PROF(st, "merkle_top", 128.0 * cnt, hipLaunchKernelGGL(k_merge_top, dim3(1), dim3(256), 0, st, src, cnt, nodes));
+}
+
+__global__ void k_gather_digests(const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out) {
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t < k) {
+        uint32_t h[8];
+        load_digest(src + 32 * idx[t], h);
+        store_digest(out + 32 * t, h);
+    }
+}
+
+void gather_digests(hipStream_t st, const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out) {
+    if (k) hipLaunchKernelGGL(k_gather_digests, dim3(cdiv(k, 64)), dim3(64), 0, st, src, idx, k, out);
+}
+
+__global__ void k_gather_rows(const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,
+                              fe *out) {
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t < k * ncols) {
+        size_t q = t / ncols, c = t % ncols;
+        size_t i = pos[q], n = (size_t)1 << log_n, B = (size_t)1 << log_b;
+        out[t] = base[(c * B + (i & (B - 1))) * n + (i >> log_b)];
+    }
+}
+
+void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,
+                 fe *out) {
+    if (k) hipLaunchKernelGGL(k_gather_rows, dim3(cdiv(k * ncols, 64)), dim3(64), 0, st, base, ncols, log_n, log_b, pos,
+                              k, out);
+}
+
+// ================================================================ batch inversion
+// out[i] = 1 / ((x_i - a)(x_i - b)), x_i = xr[i & (B-1)] * w_n^(i >> log_b), via Montgomery's trick
+// over K elements per thread (strided by the grid so every store is coalesced).
+constexpr int INV_K = 16;
+
+__global__ void __launch_bounds__(256) k_batch_inv_pairs(const fe *xr, int log_b, int log_n, const fe *wlo,
+                                                         const fe *whi, fe a, fe b, fe *out, size_t total_threads) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    const size_t B = (size_t)1 << log_b;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= total_threads) return;
+    fe pre[INV_K];
+    fe acc = fe_one();
+#pragma unroll
+    for (int k = 0; k < INV_K; k++) {
+        size_t i = t + (size_t)k * total_threads;
+        fe d = fe_one();
+        if (i < N) {
+            fe x = fe_mul(xr[i & (B - 1)], pow_split(wlo, whi, i >> log_b));
+            d = fe_mul(fe_sub(x, a), fe_sub(x, b));
+        }
+        acc = fe_mul(acc, d);
+        pre[k] = acc;
+    }
+    fe inv = fe_inv(acc);
+#pragma unroll
+    for (int k = INV_K - 1; k >= 0; k--) {
+        size_t i = t + (size_t)k * total_threads;
+        fe d = fe_one();
+        if (i < N) {
+            fe x = fe_mul(xr[i & (B - 1)], pow_split(wlo, whi, i >> log_b));
+            d = fe_mul(fe_sub(x, a), fe_sub(x, b));
+        }
+        fe r = k > 0 ? fe_mul(inv, pre[k - 1]) : inv;
+        if (i < N) out[i] = r;
+        inv = fe_mul(inv, d);
+    }
+}
+
+void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe a, fe b, fe *out) {
+    size_t N = (size_t)1 << (log_n + log_b);
+    size_t threads = (N + INV_K - 1) / INV_K;
+    ZK_PROF(st, "batch_inv", 16.0 * N, hipLaunchKernelGGL(k_batch_inv_pairs, dim3(cdiv(threads, 256)), dim3(256), 0, st, xr, log_b,
+                                                log_n, Tn.fwd_lo, Tn.fwd_hi, a, b, out, threads));
+}
+
+// ================================================================ constraint evaluation (K3)
+// ProcessorAir::evaluate_transition (air/src/lib.rs:104-168, constrains.rs:95-216, flags.rs:37-91)
+// fused with DefaultConstraintEvaluator's merge (sum of coeff * C_k), the transition divisor and the
+// two boundary groups, one thread per CE-domain step.
+
+__constant__ fe c_mds[16];
+__constant__ fe c_inv_mds[16];
+
+__device__ __forceinline__ fe cube(fe x) { return fe_mul(fe_mul(x, x), x); }
+
+__global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wce_lo,
+                                                          const fe *wce_hi, const fe *periodic, const fe *inv_bd,
+                                                          const AirConsts *K, fe *comp) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t CE = n * 8;
+    const size_t B = (size_t)1 << log_b;
+    const int shift = log_b - 3;  // LDE steps per CE step
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < CE; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t li = i << shift;
+        const size_t r = li & (B - 1), q = li >> log_b, qn = (q + 1) & (n - 1);
+        const fe *cb = lde + r * n;  // column c of the current/next row: cb[c*B*n + q]
+        const size_t cs = B * n;
+#define CUR(c) cb[(size_t)(c)*cs + q]
+#define NXT(c) cb[(size_t)(c)*cs + qn]
+        const fe one = fe_one();
+        const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
+        const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
+                 nb4 = fe_sub(one, b4);
+        // shared prefixes of the degree-5 selectors (flags.rs:45-79)
+        const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
+        const fe is_add = fe_mul(fe_mul(n0_1_n2, nb3), nb4);
+        const fe is_sadd = fe_mul(fe_mul(n0_1_n2, b3), nb4);
+        const fe is_add2 = fe_mul(fe_mul(n0_1_n2, b3), b4);
+        const fe is_mul = fe_mul(fe_mul(n0_1_n2, nb3), b4);
+        const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
+        const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
+        const fe is_push = fe_mul(fe_mul(p0, nb3), nb4);
+        const fe is_read = fe_mul(fe_mul(p0, nb3), b4);
+        const fe is_read2 = fe_mul(fe_mul(p0, b3), nb4);
+        const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
+        const fe s0 = CUR(12), s0n = NXT(12);
+        fe t;   // running sum_k coeff_t[k] * C_k
+        fe v;
+        // 0 clock
+        v = fe_sub(NXT(0), fe_add(CUR(0), one));
+        t = fe_mul(K->coeff_t[0], v);
+        // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2
+        {
+            fe four = fe_make(4);
+            v = fe_sub(NXT(11), CUR(11));
+            v = fe_add(fe_sub(v, b0), b1);
+            v = fe_add(fe_sub(v, fe_mul(is_read2, four)), fe_mul(is_add2, four));
+            t = fe_add(t, fe_mul(K->coeff_t[1], v));
+        }
+        // 2 shift
+        t = fe_add(t, fe_mul(K->coeff_t[2], fe_mul(b0, b1)));
+        // 3 add
+        t = fe_add(t, fe_mul(K->coeff_t[3], fe_mul(is_add, fe_sub(s0n, fe_add(s0, CUR(13))))));
+        // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs
+        {
+            const int L = K->lwe_size;
+            fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
+            for (int k = 0; k < L; k++) {
+                fe sn = NXT(12 + k);
+                fe s1k = CUR(13 + k);
+                fe triv = (k == L - 1) ? fe_mul(K->delta, s0) : fe_zero();
+                acc4 = fe_add(acc4, fe_sub(sn, fe_add(s1k, triv)));
+                acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
+                acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
+            }
+            t = fe_add(t, fe_mul(K->coeff_t[4], fe_mul(is_sadd, acc4)));
+            t = fe_add(t, fe_mul(K->coeff_t[5], fe_mul(is_add2, acc5)));
+            t = fe_add(t, fe_mul(K->coeff_t[7], fe_mul(is_smul, acc7)));
+        }
+        // 6 mul
+        t = fe_add(t, fe_mul(K->coeff_t[6], fe_mul(is_mul, fe_sub(s0n, fe_mul(s0, CUR(13))))));
+        // 8 push / 9 read / 10 read2 / 11 noop
+        {
+            fe d1 = fe_sub(NXT(13), s0);
+            t = fe_add(t, fe_mul(K->coeff_t[8], fe_mul(is_push, d1)));
+            t = fe_add(t, fe_mul(K->coeff_t[9], fe_mul(is_read, d1)));
+            t = fe_add(t, fe_mul(K->coeff_t[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
+            t = fe_add(t, fe_mul(K->coeff_t[11], fe_mul(is_noop, fe_sub(s0n, s0))));
+        }
+        // 12..19 Rescue round / copy (constrains.rs:182-216)
+        {
+            const fe *per = periodic + (i & 127) * 9;
+            const fe hash_flag = per[0];
+            const fe h0 = CUR(6);
+            fe x[4], y[4], m0[4], m1[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
+#pragma unroll
+            for (int r2 = 0; r2 < 4; r2++) {
+                fe acc = fe_zero();
+#pragma unroll
+                for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(c_mds[4 * r2 + c], x[c]));
+                m0[r2] = fe_add(acc, per[1 + r2]);
+            }
+            // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4
+            fe opc = fe_add(fe_add(fe_add(fe_add(fe_mul(b0, fe_make(16)), fe_mul(b1, fe_make(8))),
+                                          fe_mul(b2, fe_make(4))), fe_mul(b3, fe_make(2))), b4);
+            m0[0] = fe_add(m0[0], opc);
+            m0[1] = fe_add(m0[1], fe_mul(s0n, is_push));
+            fe hn[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hn[k] = NXT(7 + k);
+                y[k] = fe_sub(hn[k], per[5 + k]);
+            }
+#pragma unroll
+            for (int r2 = 0; r2 < 4; r2++) {
+                fe acc = fe_zero();
+#pragma unroll
+                for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(c_inv_mds[4 * r2 + c], y[c]));
+                m1[r2] = cube(acc);
+            }
+            const fe fh = fe_mul(hash_flag, h0);
+            const fe nfh = fe_mul(fe_sub(one, hash_flag), h0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) t = fe_add(t, fe_mul(K->coeff_t[12 + k], fe_mul(fe_sub(m1[k], m0[k]), fh)));
+            t = fe_add(t, fe_mul(K->coeff_t[16], fe_mul(fe_sub(hn[0], CUR(7)), nfh)));
+            t = fe_add(t, fe_mul(K->coeff_t[17], fe_mul(fe_sub(hn[1], CUR(8)), nfh)));
+            t = fe_add(t, fe_mul(K->coeff_t[18], fe_mul(hn[2], nfh)));
+            t = fe_add(t, fe_mul(K->coeff_t[19], fe_mul(hn[3], nfh)));
+        }
+        // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
+        const fe x = fe_mul(K->xr[i & 7], pow_split(wce_lo, wce_hi, i >> 3));
+        const fe xa = fe_sub(x, K->g_last2);
+        fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, K->g_last1)), K->inv_zn[i & 7]);
+        fe bsum0 = fe_zero(), bsum1 = fe_zero();
+#pragma unroll
+        for (int k = 0; k < 22; k++) {
+            fe d = fe_sub(CUR(K->assert_col[k]), K->assert_val[k]);
+            fe w = fe_mul(K->coeff_b[k], d);
+            if (K->assert_grp[k] == 0) bsum0 = fe_add(bsum0, w);
+            else bsum1 = fe_add(bsum1, w);
+        }
+        fe num = fe_add(fe_mul(bsum0, xa), fe_mul(bsum1, fe_sub(x, one)));
+        res = fe_add(res, fe_mul(num, inv_bd[i]));
+        comp[(i & 7) * n + (i >> 3)] = res;
+#undef CUR
+#undef NXT
+    }
+}
+
+static bool g_consts_uploaded = false;
+static void upload_rescue(hipStream_t st) {
+    if (g_consts_uploaded) return;
+    fe m[16], im[16];
+    for (int i = 0; i < 16; i++) {
+        m[i] = fe_make(ZK_MDS[i][0], ZK_MDS[i][1]);
+        im[i] = fe_make(ZK_INV_MDS[i][0], ZK_INV_MDS[i][1]);
+    }
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mds), m, sizeof m, 0, hipMemcpyHostToDevice, st);
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(c_inv_mds), im, sizeof im, 0, hipMemcpyHostToDevice, st);
+    hipStreamSynchronize(st);
+    g_consts_uploaded = true;
+}
+
+void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tce, const fe *periodic,
+                      const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
+    upload_rescue(st);
+    size_t CE = (size_t)8 << log_n;
+    unsigned blocks = cdiv(CE, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "eval_constraints", (448.0 * (log_b == 3 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL(k_eval_constraints, dim3(blocks), dim3(256), 0, st, lde, log_n,
+                                                       log_b, Tce.fwd_lo, Tce.fwd_hi, periodic, inv_bd, consts_dev, comp));
+}
+
+// ================================================================ composition interpolation (K4)
+__global__ void __launch_bounds__(256) k_comp_cross(const fe *c, int log_n, const fe *wi_lo, const fe *wi_hi,
+                                                    const fe *i3_lo, const fe *i3_hi, fe scale, fe w8inv,
+                                                    fe inv3n, int ncols, fe *polys, unsigned *nonzero) {
+    const size_t n = (size_t)1 << log_n;
+    for (size_t k1 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k1 < n; k1 += (size_t)gridDim.x * blockDim.x) {
+        // d_r = c_r[k1] * w_8n^(-r k1)
+        fe w = pow_split(wi_lo, wi_hi, k1);  // w_8n^-k1
+        fe d[8];
+        fe wr = fe_one();
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            fe v = c[(size_t)r * n + k1];
+            d[r] = r ? fe_mul(v, wr) : v;
+            wr = fe_mul(wr, w);
+        }
+        // b_k2 = sum_r w8^(-r k2) d_r  (size-8 DFT with w8^-1, direct form: 49 products avoided by radix-2)
+        fe w2 = fe_mul(w8inv, w8inv), w3 = fe_mul(w2, w8inv);
+        // radix-2 DIT on bit-reversed input
+        fe e0 = d[0], e1 = d[4], e2 = d[2], e3 = d[6], e4 = d[1], e5 = d[5], e6 = d[3], e7 = d[7];
+        fe t0 = fe_add(e0, e1), t1 = fe_sub(e0, e1), t2 = fe_add(e2, e3), t3 = fe_sub(e2, e3);
+        fe t4 = fe_add(e4, e5), t5 = fe_sub(e4, e5), t6 = fe_add(e6, e7), t7 = fe_sub(e6, e7);
+        t3 = fe_mul(t3, w2);
+        t7 = fe_mul(t7, w2);
+        fe u0 = fe_add(t0, t2), u2 = fe_sub(t0, t2), u1 = fe_add(t1, t3), u3 = fe_sub(t1, t3);
+        fe u4 = fe_add(t4, t6), u6 = fe_sub(t4, t6), u5 = fe_add(t5, t7), u7 = fe_sub(t5, t7);
+        u5 = fe_mul(u5, w8inv);
+        u6 = fe_mul(u6, w2);
+        u7 = fe_mul(u7, w3);
+        fe bk[8] = {fe_add(u0, u4), fe_add(u1, u5), fe_add(u2, u6), fe_add(u3, u7),
+                    fe_sub(u0, u4), fe_sub(u1, u5), fe_sub(u2, u6), fe_sub(u3, u7)};
+        // a_(k1 + n k2) = b_k2 * scale * 3^-(k1 + n k2)
+        fe s = fe_mul(scale, pow_split(i3_lo, i3_hi, k1));
+        unsigned nz = 0;
+#pragma unroll
+        for (int k2 = 0; k2 < 8; k2++) {
+            fe a = fe_mul(bk[k2], s);
+            if (k2 < ncols) polys[(size_t)k2 * n + k1] = a;
+            else nz |= !fe_is_zero(a);
+            s = fe_mul(s, inv3n);
+        }
+        if (nz) atomicOr(nonzero, 1u);
+    }
+}
+
+void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T8n, const PowTable &inv3, fe scale,
+                      fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag) {
+    size_t n = (size_t)1 << log_n;
+    unsigned blocks = cdiv(n, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "comp_cross", (128.0 + 16.0 * ncols) * n, hipLaunchKernelGGL(k_comp_cross, dim3(blocks), dim3(256), 0, st, c, log_n, T8n.inv_lo,
+                                                 T8n.inv_hi, inv3.lo, inv3.hi, scale, w8inv, inv3n, ncols, polys,
+                                                 nonzero_flag));
+}
+
+// ================================================================ OOD evaluation
+constexpr int EVAL_PER_THREAD = 32;
+
+__global__ void __launch_bounds__(256) k_poly_eval(const fe *polys, int log_n, fe x, fe *partials, int nblk) {
+    const size_t n = (size_t)1 << log_n;
+    const int p = blockIdx.y;
+    const fe *c = polys + (size_t)p * n;
+    __shared__ fe red[256];
+    fe acc = fe_zero();
+    const size_t per_block = (size_t)256 * EVAL_PER_THREAD;
+    for (size_t start = (size_t)blockIdx.x * per_block; start < n; start += (size_t)nblk * per_block) {
+        size_t k0 = start + (size_t)threadIdx.x * EVAL_PER_THREAD;
+        if (k0 >= n) continue;
+        fe h = fe_zero();
+        for (int e = EVAL_PER_THREAD - 1; e >= 0; e--) {
+            size_t k = k0 + e;
+            h = fe_add(fe_mul(h, x), k < n ? c[k] : fe_zero());
+        }
+        acc = fe_add(acc, fe_mul(h, fe_exp(x, (uint64_t)k0)));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[(size_t)p * nblk + blockIdx.x] = red[0];
+}
+
+void poly_eval_many(hipStream_t st, const fe *polys, int npolys, int log_n, fe x, fe *partials, int nblk) {
+    ZK_PROF(st, "poly_eval", 16.0 * npolys * ((size_t)1 << log_n), hipLaunchKernelGGL(k_poly_eval, dim3(nblk, npolys), dim3(256), 0, st, polys, log_n, x, partials, nblk));
+}
+
+__global__ void k_sum_partials(const fe *partials, int nblk, fe *out) {
+    __shared__ fe red[256];
+    fe acc = fe_zero();
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) acc = fe_add(acc, partials[(size_t)blockIdx.x * nblk + b]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out) {
+    hipLaunchKernelGGL(k_sum_partials, dim3(npolys), dim3(256), 0, st, partials, nblk, out);
+}
+
+// ================================================================ DEEP composition (K6)
+__global__ void __launch_bounds__(256) k_deep(const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                                              const DeepConsts *D, const fe *wN_lo, const fe *wN_hi, fe three,
+                                              const fe *inv_d, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i & (B - 1), q = i >> log_b;
+        const fe *p = lde + r * n + q;
+        fe sT = fe_zero();
+#pragma unroll 4
+        for (int c = 0; c < 28; c++) sT = fe_add(sT, fe_mul(D->alpha_t[c], p[(size_t)c * B * n]));
+        const fe *pc = clde + r * n + q;
+        fe sH = fe_zero();
+        for (int j = 0; j < ccols; j++) sH = fe_add(sH, fe_mul(D->alpha_c[j], pc[(size_t)j * B * n]));
+        fe s1 = fe_sub(fe_add(sT, sH), D->k1);
+        fe s2 = fe_sub(sT, D->k2);
+        fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));
+        fe num = fe_add(fe_mul(s1, fe_sub(x, D->zg)), fe_mul(s2, fe_sub(x, D->z)));
+        out[i] = fe_mul(num, inv_d[i]);
+    }
+}
+
+void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                      const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out) {
+    size_t N = (size_t)1 << (log_n + log_b);
+    unsigned blocks = cdiv(N, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "deep", (448.0 + 16.0 * ccols + 32.0) * N, hipLaunchKernelGGL(k_deep, dim3(blocks), dim3(256), 0, st, lde, log_n, log_b, clde, ccols,
+                                           (const DeepConsts *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi, three, inv_d, out));
+}
+
+// ================================================================ FRI fold (K7)
+// next[r] = p_r(alpha), p_r of degree < fold interpolating the layer values at x_r * zeta^k:
+//   p_r(alpha) = (1/fold) * sum_m V_m (alpha / x_r)^m,  V_m = sum_k v_k zeta^(-k m)
+__global__ void __launch_bounds__(256) k_fri_fold(const fe *layer, size_t L, int fold, const FoldConsts *F,
+                                                  const fe *wi_lo, const fe *wi_hi, size_t wstride, fe *next) {
+    const size_t rows = L / fold;
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
+        fe v[16];
+        for (int k = 0; k < fold; k++) v[k] = layer[r + (size_t)k * rows];
+        // beta = alpha / x_r, x_r = offset * w_L^r  ->  1/x_r = offset^-1 * w_L^-r = offset^-1 * w_N^(-r*wstride)
+        fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
+        // V_m via a direct DFT for the general fold (fold <= 16); Horner in beta
+        fe acc = fe_zero();
+        for (int m = fold - 1; m >= 0; m--) {
+            fe Vm = fe_zero();
+            for (int k = 0; k < fold; k++) Vm = fe_add(Vm, fe_mul(v[k], F->zinv[(k * m) & (fold - 1)]));
+            acc = fe_add(fe_mul(acc, beta), Vm);
+        }
+        next[r] = fe_mul(acc, F->inv_fold);
+    }
+}
+
+void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
+                     const NttTables &TN, size_t wstride, fe *next) {
+    unsigned blocks = cdiv(L / fold, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "fri_fold", 16.0 * L + 16.0 * (L / fold), hipLaunchKernelGGL(k_fri_fold, dim3(blocks), dim3(256), 0, st, layer, L, fold,
+                                               (const FoldConsts *)fold_consts_dev, TN.inv_lo, TN.inv_hi, wstride, next));
+}
+
+// ================================================================ elementwise helpers
+__global__ void k_coset_major_to_natural(const fe *src, int log_n, int log_b, fe *dst) {
+    size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[(i & (B - 1)) * n + (i >> log_b)];
+}
+
+__global__ void k_gather_fe(const fe *src, const uint64_t *idx, size_t k, fe *out) {
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t < k) out[t] = src[idx[t]];
+}
+
+void gather_fe(hipStream_t st, const fe *src, const uint64_t *idx, size_t k, fe *out) {
+    if (k) hipLaunchKernelGGL(k_gather_fe, dim3(cdiv(k, 64)), dim3(64), 0, st, src, idx, k, out);
+}
+
+KernelProfiler &profiler() {
+    static KernelProfiler p;
+    return p;
+}
+
+void coset_major_to_natural(hipStream_t st, const fe *src, int log_n, int log_b, fe *dst) {
+    size_t N = (size_t)1 << (log_n + log_b);
+    unsigned blocks = cdiv(N, 256);
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_coset_major_to_natural, dim3(blocks), dim3(256), 0, st, src, log_n, log_b, dst);
+}
+
+}  // namespace zk
+
+// ================================================================ diagnostics (C ABI: zk_diag_*)
+namespace zk {
+__global__ void k_field_op(int op, const fe *a, const fe *b, fe *out, size_t count) {
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    fe x = a[t], y = b[t];
+    fe r;
+    switch (op) {
+    case 0: r = fe_add(x, y); break;
+    case 1: r = fe_sub(x, y); break;
+    case 2: r = fe_mul(x, y); break;
+    case 3: r = fe_inv(x); break;
+    default: r = fe_exp(x, y.lo, y.hi); break;
+    }
+    out[t] = r;
+}
+
+__global__ void k_blake3_elems(const fe *in, int k, size_t count, uint8_t *out) {
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    uint32_t h[8];
+    b3::hash_elements(k, [&](int i) { return in[t * k + i]; }, h);
+    store_digest(out + 32 * t, h);
+}
+
+void diag_field_op(hipStream_t st, int op, const fe *a, const fe *b, fe *out, size_t count) {
+    hipLaunchKernelGGL(k_field_op, dim3(cdiv(count, 256)), dim3(256), 0, st, op, a, b, out, count);
+}
+void diag_blake3_elems(hipStream_t st, const fe *in, int k, size_t count, uint8_t *out) {
+    hipLaunchKernelGGL(k_blake3_elems, dim3(cdiv(count, 256)), dim3(256), 0, st, in, k, count, out);
+}
+}  // namespace zk

@@ -1,0 +1,1083 @@
+// prover.hip -- host orchestration of the gfx950 prove path and the C ABI (include/zkvm_gpu.h).
+//
+// zk_prove_device() runs winterfell 0.9's generate_proof stages for ProcessorAir
+// (prover/src/lib.rs:40-77) on one GPU:
+//   S0 coin seed                       host (Context::to_elements || PublicInputs::to_elements)
+//   S2 trace iNTT + coset LDE + commit  ntt / hash_rows / merkle           (new_trace_lde)
+//   S3 constraint evaluation           batch_inv + eval_constraints       (new_evaluator + evaluate)
+//   S4 composition poly + commit       ntt(inverse) + comp_cross + ntt + hash_rows + merkle
+//   S5 OOD frame, DEEP                 poly_eval + batch_inv + deep
+//   S6 FRI layers + remainder          hash_fri_rows + merkle + fri_fold; remainder on host
+//   S7 grinding + query positions      host
+//   S8 openings                        gather kernels + host batch-proof assembly
+//   S9 proof bytes                     host
+// The public coin runs on the host and sees only 32-byte roots, so each commitment costs one
+// small device->host copy.  Protocol choices are the ones of DESIGN.md "Protocol profile".
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/zkvm_gpu.h"
+#include "host_field.hpp"
+#include "rescue_consts.hpp"
+#include "zk_internal.hpp"
+
+using namespace zk;
+
+static thread_local std::string g_err;
+const char *zk_last_error(void) { return g_err.c_str(); }
+
+#define ZK_CHECK_HIP(expr)                                                                     \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            g_err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #expr;         \
+            return e_ == hipErrorOutOfMemory ? ZK_ERR_OUT_OF_MEMORY : ZK_ERR_DEVICE;           \
+        }                                                                                      \
+    } while (0)
+
+#define ZK_FAIL(code, msg)   \
+    do {                     \
+        g_err = (msg);       \
+        return (code);       \
+    } while (0)
+
+static constexpr int W = ZK_TRACE_WIDTH;
+static constexpr int NUM_TCONS = 20;
+static constexpr int NUM_ASSERTS = 22;
+
+static int ilog2(size_t n) {
+    int r = 0;
+    while (((size_t)1 << r) < n) r++;
+    return r;
+}
+
+// ================================================================ device allocation helpers
+struct DeviceArena {
+    std::vector<void *> ptrs;
+    ~DeviceArena() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t alloc(T **p, size_t count) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, count * sizeof(T) + 256);
+        if (e == hipSuccess) {
+            ptrs.push_back(q);
+            *p = (T *)q;
+        }
+        return e;
+    }
+};
+
+struct Plan {  // everything that depends only on (n, B)
+    int log_n = 0, log_b = 0;
+    NttTables Tn, Tce, TN;    // sizes n, 8n, B*n
+    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B
+    PowTable inv3;                // 3^-k, k < n
+    fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)
+    fe *periodic = nullptr;               // 128 x 9
+};
+
+struct zk_prover {
+    int device = 0;
+    hipStream_t st = nullptr;
+    size_t max_n = 0;
+    uint32_t max_b = 0;
+    DeviceArena arena;
+    fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
+       *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
+    uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
+    fe *partials = nullptr, *ood = nullptr, *gather_out = nullptr;
+    uint64_t *gather_idx = nullptr;
+    unsigned *flag = nullptr;
+    void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
+    std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+    std::vector<fe *> table_bufs;
+    // stage timing
+    std::vector<std::pair<const char *, hipEvent_t>> stage_ev;
+    std::vector<std::pair<const char *, float>> stage_ms;
+    // kernel stats (names / totals of the last profile)
+    std::vector<std::string> kstat_names;
+    std::vector<float> kstat_ms;
+    std::vector<int> kstat_n;
+    std::vector<double> kstat_bytes;
+    // last LDE handle bookkeeping
+    size_t last_n = 0;
+    uint32_t last_b = 0;
+};
+
+struct zk_trace_lde {
+    zk_prover *p;
+    size_t n;
+    uint32_t B;
+    int width;
+};
+
+// ---------------------------------------------------------------- table construction
+static hipError_t upload(zk_prover *p, fe **dst, const std::vector<fe> &v) {
+    hipError_t e = p->arena.alloc(dst, v.size());
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dst, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice);
+}
+
+static hipError_t make_pow_table(zk_prover *p, fe s, size_t n, PowTable *out) {
+    std::vector<fe> lo(2048), hi(n / 2048 + 1);
+    lo[0] = fe_one();
+    for (int t = 1; t < 2048; t++) lo[t] = fe_mul(lo[t - 1], s);
+    fe s2048 = fe_mul(lo[2047], s);
+    hi[0] = fe_one();
+    for (size_t u = 1; u < hi.size(); u++) hi[u] = fe_mul(hi[u - 1], s2048);
+    hipError_t e = upload(p, &out->lo, lo);
+    if (e != hipSuccess) return e;
+    return upload(p, &out->hi, hi);
+}
+
+static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
+    T->log_n = log_n;
+    static std::vector<fe> d4096f, d4096i;
+    if (d4096f.empty()) {
+        d4096f.resize(2048);
+        d4096i.resize(2048);
+        fe w = h_root_of_unity(12), wi = h_inv(w);
+        d4096f[0] = d4096i[0] = fe_one();
+        for (int t = 1; t < 2048; t++) {
+            d4096f[t] = fe_mul(d4096f[t - 1], w);
+            d4096i[t] = fe_mul(d4096i[t - 1], wi);
+        }
+    }
+    hipError_t e = upload(p, &T->dft_fwd, d4096f);
+    if (e == hipSuccess) e = upload(p, &T->dft_inv, d4096i);
+    size_t n = (size_t)1 << log_n;
+    fe w = h_root_of_unity(log_n);
+    PowTable f, i;
+    if (e == hipSuccess) e = make_pow_table(p, w, n, &f);
+    if (e == hipSuccess) e = make_pow_table(p, h_inv(w), n, &i);
+    T->fwd_lo = f.lo;
+    T->fwd_hi = f.hi;
+    T->inv_lo = i.lo;
+    T->inv_hi = i.hi;
+    return e;
+}
+
+// Periodic columns (air/src/lib.rs:201-225): CYCLE_MASK and the 8 ARK columns, interpolated over
+// <w_16> and evaluated at (3 * w_CE^i)^(n/16) for the 128 distinct CE steps i mod 128.
+static std::vector<fe> periodic_table(size_t n) {
+    std::vector<std::vector<fe>> cols(9, std::vector<fe>(16));
+    for (int r = 0; r < 16; r++) {
+        cols[0][r] = fe_make(r < 14 ? 1 : 0);
+        for (int c = 0; c < 8; c++) cols[1 + c][r] = fe_make(ZK_ARK[8 * r + c][0], ZK_ARK[8 * r + c][1]);
+    }
+    for (auto &c : cols) h_interp_coset(c, fe_one());
+    const int log_ce = ilog2(8 * n);
+    fe w = h_root_of_unity(log_ce), x = fe_make(3);
+    std::vector<fe> out(128 * 9);
+    for (int i = 0; i < 128; i++) {
+        fe y = h_pow(x, n / 16);
+        for (int j = 0; j < 9; j++) out[i * 9 + j] = h_poly_eval(cols[j].data(), 16, y);
+        x = fe_mul(x, w);
+    }
+    return out;
+}
+
+static int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
+    auto key = std::make_pair(ilog2(n), ilog2(B));
+    auto it = p->plans.find(key);
+    if (it != p->plans.end()) {
+        *out = it->second.get();
+        return ZK_OK;
+    }
+    auto pl = std::make_unique<Plan>();
+    pl->log_n = key.first;
+    pl->log_b = key.second;
+    ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n, &pl->Tn));
+    ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + 3, &pl->Tce));
+    ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + pl->log_b, &pl->TN));
+    fe wN = h_root_of_unity(pl->log_n + pl->log_b), wce = h_root_of_unity(pl->log_n + 3);
+    std::vector<fe> xrN(B), xrce(8);
+    fe s = fe_make(3);
+    for (uint32_t r = 0; r < B; r++) {
+        xrN[r] = s;
+        PowTable t;
+        ZK_CHECK_HIP(make_pow_table(p, s, n, &t));
+        pl->coset.push_back(t);
+        s = fe_mul(s, wN);
+    }
+    s = fe_make(3);
+    for (int r = 0; r < 8; r++) {
+        xrce[r] = s;
+        s = fe_mul(s, wce);
+    }
+    ZK_CHECK_HIP(upload(p, &pl->xr_N, xrN));
+    ZK_CHECK_HIP(upload(p, &pl->xr_ce, xrce));
+    ZK_CHECK_HIP(make_pow_table(p, h_inv(fe_make(3)), n, &pl->inv3));
+    ZK_CHECK_HIP(upload(p, &pl->periodic, periodic_table(n)));
+    *out = pl.get();
+    p->plans[key] = std::move(pl);
+    return ZK_OK;
+}
+
+// ---------------------------------------------------------------- prover object
+int zk_device_count(int *count) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    if (count) *count = c;
+    return ZK_OK;
+}
+
+int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) {
+    if (!out || max_n < 16 || (max_n & (max_n - 1)) || max_b < 8 || (max_b & (max_b - 1)) || max_b > 64)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "zk_prover_create: max_trace_len must be a power of two >= 16, blowup in [8, 64]");
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) ZK_FAIL(ZK_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= cnt) ZK_FAIL(ZK_ERR_INVALID_ARG, "device index out of range");
+    ZK_CHECK_HIP(hipSetDevice(device));
+    auto p = std::make_unique<zk_prover>();
+    p->device = device;
+    p->max_n = max_n;
+    p->max_b = max_b;
+    ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+    const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
+    DeviceArena &A = p->arena;
+    ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
+    ZK_CHECK_HIP(A.alloc(&p->polys, (size_t)W * n));
+    ZK_CHECK_HIP(A.alloc(&p->tmp, std::max((size_t)W * n, CE)));
+    ZK_CHECK_HIP(A.alloc(&p->lde, (size_t)W * N));
+    ZK_CHECK_HIP(A.alloc(&p->comp, CE));
+    ZK_CHECK_HIP(A.alloc(&p->ctmp, CE));
+    ZK_CHECK_HIP(A.alloc(&p->cpolys, (size_t)ZK_MAX_CCOLS * n));
+    ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * N));
+    ZK_CHECK_HIP(A.alloc(&p->inv, std::max(N, CE)));
+    ZK_CHECK_HIP(A.alloc(&p->deep, N));
+    ZK_CHECK_HIP(A.alloc(&p->fri, N / 2 + 16));
+    ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * N));
+    ZK_CHECK_HIP(A.alloc(&p->nodes, 32 * N));
+    ZK_CHECK_HIP(A.alloc(&p->cleaves, 32 * N));
+    ZK_CHECK_HIP(A.alloc(&p->cnodes, 32 * N));
+    ZK_CHECK_HIP(A.alloc(&p->fri_dig, 32 * N / 2 + 64));
+    ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)64 * 1024));
+    ZK_CHECK_HIP(A.alloc(&p->ood, 256));
+    ZK_CHECK_HIP(A.alloc(&p->gather_out, (size_t)64 * 1024));
+    ZK_CHECK_HIP(A.alloc(&p->gather_idx, (size_t)64 * 1024));
+    ZK_CHECK_HIP(A.alloc(&p->flag, 4));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->fold_consts, sizeof(FoldConsts)));
+    *out = p.release();
+    return ZK_OK;
+}
+
+void zk_prover_destroy(zk_prover *p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    (void)hipStreamSynchronize(p->st);
+    for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
+    (void)hipStreamDestroy(p->st);
+    delete p;
+}
+
+int zk_prover_trace_buffer(zk_prover *p, void **d_trace) {
+    if (!p || !d_trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    *d_trace = p->d_trace;
+    return ZK_OK;
+}
+
+// ---------------------------------------------------------------- stage timing
+static void stage_begin(zk_prover *p) {
+    for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
+    p->stage_ev.clear();
+}
+static void stage_mark(zk_prover *p, const char *name) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, p->st);
+    p->stage_ev.push_back({name, e});
+}
+static void stage_collect(zk_prover *p) {
+    p->stage_ms.clear();
+    for (size_t i = 1; i < p->stage_ev.size(); i++) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p->stage_ev[i - 1].second, p->stage_ev[i].second);
+        p->stage_ms.push_back({p->stage_ev[i].first, ms});
+    }
+}
+
+int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, int *count) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    int k = (int)p->stage_ms.size();
+    for (int i = 0; i < k && i < cap; i++) {
+        if (names) names[i] = p->stage_ms[i].first;
+        if (ms) ms[i] = p->stage_ms[i].second;
+    }
+    if (count) *count = k;
+    return ZK_OK;
+}
+
+int zk_prover_profile(zk_prover *p, int enable) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    profiler().on = enable != 0;
+    profiler().reset();
+    return ZK_OK;
+}
+
+static void collect_kernel_stats(zk_prover *p) {
+    KernelProfiler &P = profiler();
+    if (!P.on) return;
+    (void)hipStreamSynchronize(p->st);
+    for (auto &r : P.recs) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, r.a, r.b);
+        size_t i = 0;
+        for (; i < p->kstat_names.size(); i++)
+            if (p->kstat_names[i] == r.name) break;
+        if (i == p->kstat_names.size()) {
+            p->kstat_names.push_back(r.name);
+            p->kstat_ms.push_back(0);
+            p->kstat_n.push_back(0);
+            p->kstat_bytes.push_back(0);
+        }
+        p->kstat_ms[i] += ms;
+        p->kstat_n[i] += 1;
+        p->kstat_bytes[i] += r.bytes;
+    }
+    P.reset();
+}
+
+int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, int *launches, double *total_bytes,
+                           int cap, int *count) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    int k = (int)p->kstat_names.size();
+    for (int i = 0; i < k && i < cap; i++) {
+        if (names) names[i] = p->kstat_names[i].c_str();
+        if (total_ms) total_ms[i] = p->kstat_ms[i];
+        if (launches) launches[i] = p->kstat_n[i];
+        if (total_bytes) total_bytes[i] = p->kstat_bytes[i];
+    }
+    if (count) *count = k;
+    if (!names && !total_ms && !launches && !total_bytes) {  // reset request
+        p->kstat_names.clear();
+        p->kstat_ms.clear();
+        p->kstat_n.clear();
+        p->kstat_bytes.clear();
+    }
+    return ZK_OK;
+}
+
+// ---------------------------------------------------------------- proof byte writer
+struct Bytes {
+    std::vector<uint8_t> v;
+    void put(const void *d, size_t n) {
+        const uint8_t *b = (const uint8_t *)d;
+        v.insert(v.end(), b, b + n);
+    }
+    void u8(uint8_t x) { v.push_back(x); }
+    void u16(uint16_t x) { put(&x, 2); }
+    void u32(uint32_t x) { put(&x, 4); }
+    void u64(uint64_t x) { put(&x, 8); }
+};
+
+// MerkleTree::prove_batch plan: which leaf / node digests, in serialization order [P12]
+struct BatchPlan {
+    std::vector<uint64_t> norm;                     // normalized (even, sorted, unique) leaf indexes
+    std::vector<std::vector<std::pair<int, uint64_t>>> paths;  // per path: (0 = leaf, 1 = node, index)
+};
+
+static BatchPlan plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
+    BatchPlan bp;
+    int depth = ilog2(nl);
+    for (uint64_t i : idx) bp.norm.push_back(i & ~1ULL);
+    std::sort(bp.norm.begin(), bp.norm.end());
+    bp.norm.erase(std::unique(bp.norm.begin(), bp.norm.end()), bp.norm.end());
+    bp.paths.resize(bp.norm.size());
+    std::vector<uint64_t> next, cur;
+    for (size_t i = 0; i < bp.norm.size(); i++) {
+        for (uint64_t l = bp.norm[i]; l < bp.norm[i] + 2; l++)
+            if (std::find(idx.begin(), idx.end(), l) == idx.end()) bp.paths[i].push_back({0, l});
+        next.push_back((bp.norm[i] + nl) >> 1);
+    }
+    for (int lvl = 1; lvl < depth; lvl++) {
+        cur = next;
+        next.clear();
+        for (size_t i = 0; i < cur.size(); i++) {
+            uint64_t sib = cur[i] ^ 1;
+            if (i + 1 < cur.size() && cur[i + 1] == sib)
+                i++;
+            else
+                bp.paths[i].push_back({1, sib});
+            next.push_back(sib >> 1);
+        }
+    }
+    return bp;
+}
+
+// ---------------------------------------------------------------- the prove path
+struct QueryBatch {  // one Merkle opening: digests come from (leaves, nodes)
+    const uint8_t *leaves, *nodes;
+    BatchPlan plan;
+    size_t dig_off = 0;  // offset into the gathered digest buffer
+};
+
+static int check_options(const zk_options *o) {
+    if (!o) return 0;
+    if (o->field_extension != 1) return 0;
+    if (o->blowup < 8 || (o->blowup & (o->blowup - 1))) return 0;
+    if (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) return 0;
+    if ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) return 0;
+    if (o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES) return 0;
+    return 1;
+}
+
+// num_constraint_composition_columns for the ProcessorAir degrees (air/src/lib.rs:69-90) [P5]
+static int num_comp_cols(size_t n) {
+    static const int base[NUM_TCONS] = {1, 5, 2, 6, 6, 6, 7, 7, 6, 6, 6, 6, 4, 7, 4, 4, 2, 2, 2, 2};
+    static const int cyc[NUM_TCONS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1};
+    size_t hi = 0;
+    for (int k = 0; k < NUM_TCONS; k++) hi = std::max(hi, (size_t)base[k] * (n - 1) + (cyc[k] ? (n / 16) * 15 : 0));
+    size_t c = (hi - (n - 2) + n - 1) / n;
+    return (int)std::max<size_t>(c, 1);
+}
+
+static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, uint32_t B) {
+    const size_t N = n * B;
+    fe inv_n = h_inv(fe_make(n));
+    // interpolate 28 columns (winter-math interpolate_poly over <w_n>)
+    ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+    // coset r of the LDE domain: NTT of the coefficients scaled by (3 w_N^r)^k
+    for (uint32_t r = 0; r < B; r++)
+        ntt(p->st, pl->Tn, p->polys, n, p->lde + r * n, B * n, W, false, &pl->coset[r], nullptr, p->tmp);
+    (void)N;
+    return ZK_OK;
+}
+
+static int commit_rows(zk_prover *p, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves, uint8_t *nodes,
+                       uint8_t root[32]) {
+    size_t N = (size_t)1 << (log_n + log_b);
+    hash_rows_coset_major(p->st, base, ncols, log_n, log_b, leaves);
+    merkle_tree(p->st, leaves, N, nodes);
+    ZK_CHECK_HIP(hipMemcpyAsync(root, nodes + 32, 32, hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    return ZK_OK;
+}
+
+static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, size_t n, uint32_t B, uint8_t *dst) {
+    // dst: N x ncols row-major (natural index)
+    size_t N = n * B;
+    std::vector<fe> h((size_t)ncols * N);
+    (void)hipMemcpy(h.data(), base, h.size() * sizeof(fe), hipMemcpyDeviceToHost);
+    fe *o = reinterpret_cast<fe *>(dst);
+    for (int c = 0; c < ncols; c++)
+        for (size_t i = 0; i < N; i++) o[i * ncols + c] = h[((size_t)c * B + (i % B)) * n + i / B];
+}
+
+int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                    uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
+    if (!p || !d_trace_v || !pub || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (!check_options(opt)) ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
+    if (n < 16 || (n & (n - 1)) || n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace length must be a power of two in [16, max_trace_len]");
+    if (opt->blowup > p->max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "blowup exceeds the prover's max_blowup");
+    if (pub->lwe_size == 0 || pub->lwe_size > 5)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (enforce_add2 reads 2*lwe_size stack items, constrains.rs:129)");
+    const uint32_t B = opt->blowup, fold = opt->fri_folding;
+    const size_t N = n * B, CE = 8 * n;
+    if (opt->num_queries >= N) ZK_FAIL(ZK_ERR_INVALID_ARG, "num_queries must be smaller than the LDE domain");
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    Plan *pl = nullptr;
+    int rc = get_plan(p, n, B, &pl);
+    if (rc) return rc;
+    const int log_n = pl->log_n, log_b = pl->log_b;
+    const int C = num_comp_cols(n);
+    if (C > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition column count exceeds 8");
+    const fe *d_trace = (const fe *)d_trace_v;
+    const fe g = h_root_of_unity(log_n), three = fe_make(3);
+    zk_record R;
+    memset(&R, 0, sizeof R);
+    R.trace_len = (uint32_t)n;
+    R.lde_len = (uint32_t)N;
+    R.width = W;
+    R.num_ccols = (uint32_t)C;
+    stage_begin(p);
+    stage_mark(p, "start");
+
+    // S0: coin seed [P1]
+    Coin coin;
+    {
+        std::vector<fe> e;
+        e.push_back(fe_make((uint64_t)W << 16));
+        e.push_back(fe_make(n));
+        e.push_back(fe_make(ZK_P_LO));
+        e.push_back(fe_make(ZK_P_HI));
+        e.push_back(fe_make(((uint64_t)opt->field_extension << 16) | ((uint64_t)fold << 8) | opt->fri_rem_max_deg));
+        e.push_back(fe_make(opt->grinding));
+        e.push_back(fe_make(B));
+        e.push_back(fe_make(opt->num_queries));
+        for (int i = 0; i < 2; i++) e.push_back(fe_from_bytes(pub->program_hash[i]));
+        for (int i = 0; i < 16; i++) e.push_back(fe_from_bytes(pub->stack_outputs[i]));
+        coin.init(e);
+    }
+
+    // S2: trace LDE + commitment
+    if ((rc = trace_lde_stage(p, pl, d_trace, n, B))) return rc;
+    stage_mark(p, "trace_lde");
+    if ((rc = commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root))) return rc;
+    stage_mark(p, "trace_commit");
+    coin.reseed(R.trace_root);
+
+    // S3: constraint composition coefficients [P4] and evaluation over the CE domain
+    AirConsts K;
+    memset(&K, 0, sizeof K);
+    for (int k = 0; k < NUM_TCONS; k++) fe_to_bytes(K.coeff_t[k] = coin.draw(), R.coeff_t[k]);
+    for (int k = 0; k < NUM_ASSERTS; k++) fe_to_bytes(K.coeff_b[k] = coin.draw(), R.coeff_b[k]);
+    {
+        // assertions sorted by (stride, first_step, column) [P3]
+        const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+        int k = 0;
+        for (int i = 0; i < 12; i++, k++) {
+            K.assert_col[k] = first_cols[i];
+            K.assert_grp[k] = 0;
+            K.assert_val[k] = fe_zero();
+        }
+        for (int i = 0; i < 2; i++, k++) {
+            K.assert_col[k] = 7 + i;
+            K.assert_grp[k] = 1;
+            K.assert_val[k] = fe_from_bytes(pub->program_hash[i]);
+        }
+        for (int i = 0; i < 8; i++, k++) {
+            K.assert_col[k] = 12 + i;
+            K.assert_grp[k] = 1;
+            K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
+        }
+        fe wce = h_root_of_unity(log_n + 3), x = three;
+        for (int r = 0; r < 8; r++) {
+            K.xr[r] = x;
+            K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));  // x^n constant on CE coset r
+            x = fe_mul(x, wce);
+        }
+        K.g_last2 = h_pow(g, n - 2);
+        K.g_last1 = h_pow(g, n - 1);
+        K.delta = fe_make(pub->delta);
+        K.lwe_size = (int)pub->lwe_size;
+    }
+    ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+    batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), K.g_last2, p->inv);
+    eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->air_consts,
+                     p->comp);
+    stage_mark(p, "constraints");
+
+    // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit
+    ntt(p->st, pl->Tn, p->comp, n, p->ctmp, n, 8, true, nullptr, nullptr, p->tmp);
+    ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
+    {
+        fe scale = h_inv(fe_make(CE));
+        fe w8inv = h_inv(h_root_of_unity(3));
+        fe inv3n = h_inv(h_pow(three, n));
+        comp_cross_coset(p->st, p->ctmp, log_n, pl->Tce, pl->inv3, scale, w8inv, inv3n, C, p->cpolys, p->flag);
+    }
+    for (uint32_t r = 0; r < B; r++)
+        ntt(p->st, pl->Tn, p->cpolys, n, p->clde + r * n, B * n, C, false, &pl->coset[r], nullptr, p->tmp);
+    if ((rc = commit_rows(p, p->clde, C, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root))) return rc;
+    stage_mark(p, "composition");
+    unsigned degree_flag = 0;
+    ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
+    coin.reseed(R.constraint_root);
+
+    // S5: OOD frame [P7]
+    fe z = coin.draw(), zg = fe_mul(z, g);
+    fe_to_bytes(z, R.z);
+    fe oz[W], ozg[W], oc[ZK_MAX_CCOLS];
+    {
+        int nblk = std::max<int>(1, (int)std::min<size_t>(128, n / (256 * 32)));
+        poly_eval_many(p->st, p->polys, W, log_n, z, p->partials, nblk);
+        sum_partials(p->st, p->partials, W, nblk, p->ood);
+        poly_eval_many(p->st, p->polys, W, log_n, zg, p->partials, nblk);
+        sum_partials(p->st, p->partials, W, nblk, p->ood + W);
+        poly_eval_many(p->st, p->cpolys, C, log_n, z, p->partials, nblk);
+        sum_partials(p->st, p->partials, C, nblk, p->ood + 2 * W);
+        fe h[2 * W + ZK_MAX_CCOLS];
+        ZK_CHECK_HIP(hipMemcpyAsync(h, p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        for (int c = 0; c < W; c++) {
+            oz[c] = h[c];
+            ozg[c] = h[W + c];
+            fe_to_bytes(oz[c], R.ood_trace_z[c]);
+            fe_to_bytes(ozg[c], R.ood_trace_zg[c]);
+        }
+        for (int j = 0; j < C; j++) fe_to_bytes(oc[j] = h[2 * W + j], R.ood_constraints[j]);
+        uint8_t d[32];
+        hash_elems(h, 2 * W, d);  // T(z) || T(zg)
+        coin.reseed(d);
+        hash_elems(oc, C, d);
+        coin.reseed(d);
+    }
+    stage_mark(p, "ood");
+    // DEEP coefficients [P8] and evaluations
+    {
+        DeepConsts D;
+        memset(&D, 0, sizeof D);
+        for (int c = 0; c < W; c++) fe_to_bytes(D.alpha_t[c] = coin.draw(), R.deep_t[c]);
+        for (int j = 0; j < C; j++) fe_to_bytes(D.alpha_c[j] = coin.draw(), R.deep_c[j]);
+        fe k1 = fe_zero(), k2 = fe_zero();
+        for (int c = 0; c < W; c++) {
+            k1 = fe_add(k1, fe_mul(D.alpha_t[c], oz[c]));
+            k2 = fe_add(k2, fe_mul(D.alpha_t[c], ozg[c]));
+        }
+        for (int j = 0; j < C; j++) k1 = fe_add(k1, fe_mul(D.alpha_c[j], oc[j]));
+        D.k1 = k1;
+        D.k2 = k2;
+        D.z = z;
+        D.zg = zg;
+        ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+        batch_inv_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
+        deep_eval_launch(p->st, p->lde, log_n, log_b, p->clde, C, p->deep_consts, pl->TN, three, p->inv, p->deep);
+    }
+    stage_mark(p, "deep");
+
+    // S6: FRI [P9, P10]
+    size_t max_rem = (size_t)(opt->fri_rem_max_deg + 1) * B;
+    int nl = 0;
+    for (size_t s = N; s > max_rem; s /= fold) nl++;
+    if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
+    R.num_fri_layers = (uint32_t)nl;
+    std::vector<const fe *> layer_vals(nl + 1);
+    std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
+    std::vector<size_t> layer_len(nl + 1);
+    {
+        layer_vals[0] = p->deep;
+        layer_len[0] = N;
+        fe *next = p->fri;
+        uint8_t *dig = p->fri_dig;
+        fe zinv[16];
+        fe zeta_inv = h_inv(h_root_of_unity(ilog2(fold)));
+        zinv[0] = fe_one();
+        for (uint32_t t = 1; t < 16; t++) zinv[t] = t < fold ? fe_mul(zinv[t - 1], zeta_inv) : fe_zero();
+        for (int l = 0; l < nl; l++) {
+            size_t L = layer_len[l], rows = L / fold;
+            layer_leaves[l] = dig;
+            layer_nodes[l] = dig + 32 * rows;
+            dig += 64 * rows;
+            hash_fri_rows(p->st, layer_vals[l], L, (int)fold, layer_leaves[l]);
+            merkle_tree(p->st, layer_leaves[l], rows, layer_nodes[l]);
+            ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
+            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+            coin.reseed(R.fri_roots[l]);
+            fe alpha = coin.draw();
+            fe_to_bytes(alpha, R.fri_alphas[l]);
+            FoldConsts F;
+            memcpy(F.zinv, zinv, sizeof zinv);
+            F.alpha = alpha;
+            F.inv_offset = h_inv(three);
+            F.inv_fold = h_inv(fe_make(fold));
+            ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+            fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
+            layer_vals[l + 1] = next;
+            layer_len[l + 1] = rows;
+            next += rows;
+        }
+        // remainder: interpolate the last layer over 3 * <w_L>, keep L / blowup coefficients
+        size_t L = layer_len[nl];
+        std::vector<fe> rv(L);
+        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], L * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        h_interp_coset(rv, three);
+        size_t rl = L / B;
+        for (size_t k = rl; k < L; k++)
+            if (!fe_is_zero(rv[k])) degree_flag = 1;
+        R.remainder_len = (uint32_t)rl;
+        if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
+        for (size_t k = 0; k < rl; k++) fe_to_bytes(rv[k], R.remainder[k]);
+        hash_elems(rv.data(), rl, R.remainder_commitment);
+        coin.reseed(R.remainder_commitment);
+    }
+    stage_mark(p, "fri");
+
+    // S7: grinding and query positions [P11]
+    uint64_t nonce = 1;
+    for (;; nonce++) {
+        uint8_t d[32];
+        Coin::merge_with_int(coin.seed, nonce, d);
+        uint64_t head;
+        memcpy(&head, d, 8);
+        unsigned tz = head ? (unsigned)__builtin_ctzll(head) : 64;
+        if (tz >= opt->grinding) break;
+    }
+    R.pow_nonce = nonce;
+    Coin::merge_with_int(coin.seed, nonce, coin.seed);
+    coin.counter = 0;
+    std::vector<uint64_t> pos;
+    for (uint32_t q = 0; q < opt->num_queries; q++) {
+        uint8_t d[32];
+        coin.next(d);
+        uint64_t v;
+        memcpy(&v, d, 8);
+        pos.push_back(v & (N - 1));
+    }
+    std::sort(pos.begin(), pos.end());
+    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    const size_t nu = pos.size();
+    R.num_positions = (uint32_t)nu;
+    memcpy(R.positions, pos.data(), nu * 8);
+
+    // S8: openings -- one gather pass for every value and digest the proof needs
+    std::vector<uint64_t> fe_idx_trace, fe_idx_comp;  // handled by gather_rows
+    std::vector<std::vector<uint64_t>> fri_pos(nl);
+    {
+        std::vector<uint64_t> fp = pos;
+        size_t dsz = N;
+        for (int l = 0; l < nl; l++) {
+            size_t target = dsz / fold;
+            std::vector<uint64_t> f;
+            for (uint64_t x : fp) {
+                uint64_t q = x % target;
+                if (std::find(f.begin(), f.end(), q) == f.end()) f.push_back(q);
+            }
+            fri_pos[l] = f;
+            fp = f;
+            dsz = target;
+        }
+    }
+    std::vector<QueryBatch> qb;
+    qb.push_back({p->leaves, p->nodes, plan_batch(N, pos)});
+    qb.push_back({p->cleaves, p->cnodes, plan_batch(N, pos)});
+    for (int l = 0; l < nl; l++) qb.push_back({layer_leaves[l], layer_nodes[l], plan_batch(layer_len[l] / fold, fri_pos[l])});
+    // digests: gather per source array
+    std::vector<uint8_t> digests;
+    {
+        size_t total = 0;
+        for (auto &b : qb) {
+            b.dig_off = total;
+            for (auto &path : b.plan.paths) total += path.size();
+        }
+        digests.resize(32 * total);
+        size_t off = 0;
+        for (auto &b : qb) {
+            for (int src = 0; src < 2; src++) {
+                std::vector<uint64_t> idx;
+                std::vector<size_t> where;
+                size_t k = 0;
+                for (auto &path : b.plan.paths)
+                    for (auto &e : path) {
+                        if (e.first == src) {
+                            idx.push_back(e.second);
+                            where.push_back(b.dig_off + k);
+                        }
+                        k++;
+                    }
+                if (idx.empty()) continue;
+                if (idx.size() > 2048) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many digests to gather");
+                ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, p->st));
+                gather_digests(p->st, src ? b.nodes : b.leaves, p->gather_idx, idx.size(), (uint8_t *)p->gather_out);
+                std::vector<uint8_t> got(32 * idx.size());
+                ZK_CHECK_HIP(hipMemcpyAsync(got.data(), p->gather_out, got.size(), hipMemcpyDeviceToHost, p->st));
+                ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+                for (size_t t = 0; t < idx.size(); t++) memcpy(&digests[32 * where[t]], &got[32 * t], 32);
+            }
+            off++;
+        }
+    }
+    // values
+    std::vector<fe> trace_rows(nu * W), comp_rows(nu * C);
+    {
+        ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, pos.data(), nu * 8, hipMemcpyHostToDevice, p->st));
+        gather_rows(p->st, p->lde, W, log_n, log_b, p->gather_idx, nu, p->gather_out);
+        ZK_CHECK_HIP(hipMemcpyAsync(trace_rows.data(), p->gather_out, nu * W * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        gather_rows(p->st, p->clde, C, log_n, log_b, p->gather_idx, nu, p->gather_out);
+        ZK_CHECK_HIP(hipMemcpyAsync(comp_rows.data(), p->gather_out, nu * C * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    }
+    std::vector<std::vector<fe>> fri_rows(nl);
+    for (int l = 0; l < nl; l++) {
+        size_t rows = layer_len[l] / fold;
+        std::vector<uint64_t> idx;
+        for (uint64_t r : fri_pos[l])
+            for (uint32_t k = 0; k < fold; k++) idx.push_back(r + k * rows);
+        fri_rows[l].resize(idx.size());
+        ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, p->st));
+        gather_fe(p->st, layer_vals[l], p->gather_idx, idx.size(), p->gather_out);
+        ZK_CHECK_HIP(hipMemcpyAsync(fri_rows[l].data(), p->gather_out, idx.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    }
+    stage_mark(p, "queries");
+
+    // S9: proof bytes [P13, P14]
+    Bytes pf;
+    pf.u8(W);
+    pf.u8(0);
+    pf.u8(0);
+    pf.u8((uint8_t)log_n);
+    pf.u16(0);
+    pf.u8(16);
+    pf.u64(ZK_P_LO);
+    pf.u64(ZK_P_HI);
+    pf.u8((uint8_t)opt->num_queries);
+    pf.u8((uint8_t)B);
+    pf.u8((uint8_t)opt->grinding);
+    pf.u8((uint8_t)opt->field_extension);
+    pf.u8((uint8_t)fold);
+    pf.u8((uint8_t)opt->fri_rem_max_deg);
+    pf.u8((uint8_t)nu);
+    pf.u16((uint16_t)(32 * (2 + nl + 1)));
+    pf.put(R.trace_root, 32);
+    pf.put(R.constraint_root, 32);
+    for (int l = 0; l < nl; l++) pf.put(R.fri_roots[l], 32);
+    pf.put(R.remainder_commitment, 32);
+    auto write_paths = [&](const QueryBatch &b, Bytes &out) {
+        out.u8((uint8_t)b.plan.paths.size());
+        size_t k = 0;
+        for (auto &path : b.plan.paths) {
+            out.u8((uint8_t)path.size());
+            for (size_t t = 0; t < path.size(); t++, k++) out.put(&digests[32 * (b.dig_off + k)], 32);
+        }
+    };
+    auto write_queries = [&](const void *vals, size_t vlen, const QueryBatch &b) {
+        Bytes paths;
+        write_paths(b, paths);
+        pf.u32((uint32_t)vlen);
+        pf.put(vals, vlen);
+        pf.u32((uint32_t)paths.v.size());
+        pf.put(paths.v.data(), paths.v.size());
+    };
+    pf.u8(1);
+    write_queries(trace_rows.data(), nu * W * 16, qb[0]);
+    write_queries(comp_rows.data(), nu * C * 16, qb[1]);
+    pf.u16((uint16_t)(1 + 2 * W * 16));
+    pf.u8(2);
+    for (int c = 0; c < W; c++) {
+        pf.put(&oz[c], 16);
+        pf.put(&ozg[c], 16);
+    }
+    pf.u16((uint16_t)(C * 16));
+    pf.put(oc, C * 16);
+    pf.u8((uint8_t)nl);
+    for (int l = 0; l < nl; l++) write_queries(fri_rows[l].data(), fri_rows[l].size() * 16, qb[2 + l]);
+    pf.u16((uint16_t)(R.remainder_len * 16));
+    pf.put(R.remainder, R.remainder_len * 16);
+    pf.u8(0);
+    pf.u64(nonce);
+    pf.u8(0);
+    stage_mark(p, "serialize");
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    stage_collect(p);
+    collect_kernel_stats(p);
+
+    if (rec) *rec = R;
+    if (dump) {
+        if (dump->trace_polys) ZK_CHECK_HIP(hipMemcpy(dump->trace_polys, p->polys, (size_t)W * n * 16, hipMemcpyDeviceToHost));
+        if (dump->trace_lde) coset_major_rows_to_host(p, p->lde, W, n, B, dump->trace_lde);
+        if (dump->trace_leaves) ZK_CHECK_HIP(hipMemcpy(dump->trace_leaves, p->leaves, 32 * N, hipMemcpyDeviceToHost));
+        if (dump->composition) coset_major_rows_to_host(p, p->comp, 1, n, 8, dump->composition);
+        if (dump->comp_polys) ZK_CHECK_HIP(hipMemcpy(dump->comp_polys, p->cpolys, (size_t)C * n * 16, hipMemcpyDeviceToHost));
+        if (dump->comp_lde) coset_major_rows_to_host(p, p->clde, C, n, B, dump->comp_lde);
+        if (dump->deep) ZK_CHECK_HIP(hipMemcpy(dump->deep, p->deep, N * 16, hipMemcpyDeviceToHost));
+        if (dump->fri_layer1 && nl > 0)
+            ZK_CHECK_HIP(hipMemcpy(dump->fri_layer1, layer_vals[1], layer_len[1] * 16, hipMemcpyDeviceToHost));
+    }
+    int status = degree_flag ? ZK_ERR_DEGREE : ZK_OK;
+    if (degree_flag) g_err = "the trace does not satisfy ProcessorAir (composition degree check failed)";
+    if (proof_out && *proof_len >= pf.v.size())
+        memcpy(proof_out, pf.v.data(), pf.v.size());
+    else if (status == ZK_OK) {
+        status = ZK_ERR_BUFFER_TOO_SMALL;
+        g_err = "proof buffer too small";
+    }
+    *proof_len = pf.v.size();
+    p->last_n = n;
+    p->last_b = B;
+    return status;
+}
+
+int zk_prove(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+             uint8_t *proof_out, size_t *proof_len) {
+    if (!p || !trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace longer than max_trace_len");
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
+    return zk_prove_device(p, p->d_trace, n, opt, pub, proof_out, proof_len, nullptr, nullptr);
+}
+
+// ---------------------------------------------------------------- plug point 1: trace LDE
+int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint32_t blowup, zk_trace_lde **out,
+               uint8_t root[32]) {
+    if (!p || !trace || !out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (width != (size_t)W) ZK_FAIL(ZK_ERR_INVALID_ARG, "ProcessorAir traces have 28 columns");
+    if (n < 16 || (n & (n - 1)) || n > p->max_n || blowup < 8 || (blowup & (blowup - 1)) || blowup > p->max_b)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid trace length or blowup");
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    Plan *pl;
+    int rc = get_plan(p, n, blowup, &pl);
+    if (rc) return rc;
+    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
+    if ((rc = trace_lde_stage(p, pl, p->d_trace, n, blowup))) return rc;
+    uint8_t r[32];
+    if ((rc = commit_rows(p, p->lde, W, pl->log_n, pl->log_b, p->leaves, p->nodes, r))) return rc;
+    if (root) memcpy(root, r, 32);
+    *out = new zk_trace_lde{p, n, blowup, W};
+    return ZK_OK;
+}
+
+int zk_lde_read_frame(zk_trace_lde *h, size_t step, uint8_t *cur, uint8_t *next) {
+    if (!h || !cur || !next) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    zk_prover *p = h->p;
+    const size_t N = h->n * h->B;
+    if (step >= N) ZK_FAIL(ZK_ERR_INVALID_ARG, "lde_step out of range");
+    uint64_t idx[2] = {step, (step + h->B) % N};
+    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, idx, 16, hipMemcpyHostToDevice, p->st));
+    gather_rows(p->st, p->lde, W, ilog2(h->n), ilog2(h->B), p->gather_idx, 2, p->gather_out);
+    fe rows[2 * W];
+    ZK_CHECK_HIP(hipMemcpyAsync(rows, p->gather_out, sizeof rows, hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    memcpy(cur, rows, W * 16);
+    memcpy(next, rows + W, W * 16);
+    return ZK_OK;
+}
+
+int zk_lde_query(zk_trace_lde *h, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
+                 size_t *proof_len) {
+    if (!h || !positions || !rows_out || !proof_len || k == 0 || k > ZK_MAX_QUERIES)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid query arguments");
+    zk_prover *p = h->p;
+    const size_t N = h->n * h->B;
+    std::vector<uint64_t> pos(positions, positions + k);
+    for (uint64_t x : pos)
+        if (x >= N) ZK_FAIL(ZK_ERR_INVALID_ARG, "query position out of range");
+    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, pos.data(), k * 8, hipMemcpyHostToDevice, p->st));
+    gather_rows(p->st, p->lde, W, ilog2(h->n), ilog2(h->B), p->gather_idx, k, p->gather_out);
+    ZK_CHECK_HIP(hipMemcpyAsync(rows_out, p->gather_out, k * W * 16, hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    BatchPlan bp = plan_batch(N, pos);
+    Bytes out;
+    out.u8((uint8_t)bp.paths.size());
+    for (auto &path : bp.paths) {
+        out.u8((uint8_t)path.size());
+        for (auto &e : path) {
+            uint8_t d[32];
+            ZK_CHECK_HIP(hipMemcpy(d, (e.first ? p->nodes : p->leaves) + 32 * e.second, 32, hipMemcpyDeviceToHost));
+            out.put(d, 32);
+        }
+    }
+    size_t cap = *proof_len;
+    *proof_len = out.v.size();
+    if (!proof_out || cap < out.v.size()) ZK_FAIL(ZK_ERR_BUFFER_TOO_SMALL, "proof buffer too small");
+    memcpy(proof_out, out.v.data(), out.v.size());
+    return ZK_OK;
+}
+
+void zk_lde_free(zk_trace_lde *h) { delete h; }
+
+// ---------------------------------------------------------------- plug point 2: constraint evaluation
+int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t *coeff_t, const uint8_t *coeff_b,
+                        uint8_t *out) {
+    if (!h || !pub || !coeff_t || !coeff_b || !out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (pub->lwe_size == 0 || pub->lwe_size > 5) ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5]");
+    zk_prover *p = h->p;
+    const size_t n = h->n;
+    Plan *pl;
+    int rc = get_plan(p, n, h->B, &pl);
+    if (rc) return rc;
+    const fe g = h_root_of_unity(pl->log_n);
+    AirConsts K;
+    memset(&K, 0, sizeof K);
+    for (int k = 0; k < NUM_TCONS; k++) K.coeff_t[k] = fe_from_bytes(coeff_t + 16 * k);
+    for (int k = 0; k < NUM_ASSERTS; k++) K.coeff_b[k] = fe_from_bytes(coeff_b + 16 * k);
+    const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+    int k = 0;
+    for (int i = 0; i < 12; i++, k++) K.assert_col[k] = first_cols[i];
+    for (int i = 0; i < 2; i++, k++) {
+        K.assert_col[k] = 7 + i;
+        K.assert_grp[k] = 1;
+        K.assert_val[k] = fe_from_bytes(pub->program_hash[i]);
+    }
+    for (int i = 0; i < 8; i++, k++) {
+        K.assert_col[k] = 12 + i;
+        K.assert_grp[k] = 1;
+        K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
+    }
+    fe wce = h_root_of_unity(pl->log_n + 3), x = fe_make(3);
+    for (int r = 0; r < 8; r++) {
+        K.xr[r] = x;
+        K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));
+        x = fe_mul(x, wce);
+    }
+    K.g_last2 = h_pow(g, n - 2);
+    K.g_last1 = h_pow(g, n - 1);
+    K.delta = fe_make(pub->delta);
+    K.lwe_size = (int)pub->lwe_size;
+    ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+    batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, fe_one(), K.g_last2, p->inv);
+    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->Tn, pl->periodic, p->inv,
+                     (const AirConsts *)p->air_consts, p->comp);
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    coset_major_rows_to_host(p, p->comp, 1, n, 8, out);
+    return ZK_OK;
+}
+
+// ---------------------------------------------------------------- diagnostics
+// Host execution of the exact device multiply (fe_mul_limbs) -- lets CPU tests check the GPU
+// reduction algorithm without a GPU.
+extern "C" void zk_diag_mul_limbs_host(const uint8_t *a, const uint8_t *b, uint8_t *out, size_t count) {
+    for (size_t i = 0; i < count; i++) fe_to_bytes(fe_mul_limbs(fe_from_bytes(a + 16 * i), fe_from_bytes(b + 16 * i)), out + 16 * i);
+}
+extern "C" void zk_diag_blake3_host(const uint8_t *in, size_t len, uint8_t out[32]) { b3::hash_bytes(in, len, out); }
+
+// GPU elementwise field op: 0 add, 1 sub, 2 mul, 3 inv(a), 4 a^b (b as a 128-bit exponent)
+extern "C" int zk_diag_field_op(int device, int op, const uint8_t *a, const uint8_t *b, uint8_t *out, size_t count) {
+    if (!a || !b || !out || count == 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_CHECK_HIP(hipSetDevice(device));
+    fe *d = nullptr;
+    ZK_CHECK_HIP(hipMalloc(&d, 3 * count * sizeof(fe)));
+    ZK_CHECK_HIP(hipMemcpy(d, a, count * 16, hipMemcpyHostToDevice));
+    ZK_CHECK_HIP(hipMemcpy(d + count, b, count * 16, hipMemcpyHostToDevice));
+    diag_field_op(nullptr, op, d, d + count, d + 2 * count, count);
+    hipError_t e = hipMemcpy(out, d + 2 * count, count * 16, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    ZK_CHECK_HIP(e);
+    return ZK_OK;
+}
+
+// GPU BLAKE3 of `count` rows of k field elements (k <= 64)
+extern "C" int zk_diag_blake3_rows(int device, const uint8_t *rows, int k, size_t count, uint8_t *out) {
+    if (!rows || !out || k <= 0 || k > 64 || count == 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid argument");
+    ZK_CHECK_HIP(hipSetDevice(device));
+    fe *d = nullptr;
+    ZK_CHECK_HIP(hipMalloc(&d, count * k * sizeof(fe) + 32 * count));
+    ZK_CHECK_HIP(hipMemcpy(d, rows, count * k * 16, hipMemcpyHostToDevice));
+    uint8_t *dout = (uint8_t *)(d + count * k);
+    diag_blake3_elems(nullptr, d, k, count, dout);
+    hipError_t e = hipMemcpy(out, dout, 32 * count, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    ZK_CHECK_HIP(e);
+    return ZK_OK;
+}
+
+// GPU NTT of `batch` polys of size n: inverse != 0 -> interpolation (with 1/n), else evaluation
+// over offset * <w_n> (offset given as 16 bytes; pass 1 for the plain subgroup)
+extern "C" int zk_diag_ntt(int device, const uint8_t *in, size_t n, int batch, int inverse, const uint8_t *offset,
+                           uint8_t *out) {
+    if (!in || !out || n < 2 || (n & (n - 1)) || batch <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid argument");
+    zk_prover *p = nullptr;
+    int rc = zk_prover_create(device, std::max<size_t>(n, 16), 8, &p);
+    if (rc) return rc;
+    std::unique_ptr<zk_prover, void (*)(zk_prover *)> guard(p, zk_prover_destroy);
+    NttTables T;
+    ZK_CHECK_HIP(make_ntt_tables(p, ilog2(n), &T));
+    PowTable pre;
+    fe off = offset ? fe_from_bytes(offset) : fe_one();
+    bool use_pre = !inverse && !fe_eq(off, fe_one());
+    if (use_pre) ZK_CHECK_HIP(make_pow_table(p, off, n, &pre));
+    fe *d_in = nullptr, *d_out = nullptr, *d_tmp = nullptr;
+    ZK_CHECK_HIP(p->arena.alloc(&d_in, n * batch));
+    ZK_CHECK_HIP(p->arena.alloc(&d_out, n * batch));
+    ZK_CHECK_HIP(p->arena.alloc(&d_tmp, n * batch));
+    ZK_CHECK_HIP(hipMemcpy(d_in, in, n * batch * 16, hipMemcpyHostToDevice));
+    fe inv_n = h_inv(fe_make(n));
+    ntt(p->st, T, d_in, n, d_out, n, batch, inverse != 0, use_pre ? &pre : nullptr, inverse ? &inv_n : nullptr, d_tmp);
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    ZK_CHECK_HIP(hipMemcpy(out, d_out, n * batch * 16, hipMemcpyDeviceToHost));
+    return ZK_OK;
+}

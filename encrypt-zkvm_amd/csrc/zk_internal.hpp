@@ -1,0 +1,148 @@
+// zk_internal.hpp -- shared declarations of the gfx950 prove path (kernels.hip, prover.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "f128.hpp"
+
+namespace zk {
+
+// ---------------------------------------------------------------- kernel profiler
+// When enabled, every kernel launch is bracketed by a pair of HIP events on its own stream, so
+// per-kernel device time is measured on the stream the kernel actually runs on.
+struct KernelProfiler {
+    bool on = false;
+    struct Rec {
+        const char *name;
+        hipEvent_t a, b;
+        double bytes;  // algorithmic HBM bytes of this launch (DESIGN.md "Roofline accounting")
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            hipEventCreate(&e);
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void begin(hipStream_t st, const char *name, double bytes) {
+        Rec r{name, get(), nullptr, bytes};
+        hipEventRecord(r.a, st);
+        recs.push_back(r);
+    }
+    void end(hipStream_t st) {
+        recs.back().b = get();
+        hipEventRecord(recs.back().b, st);
+    }
+    void reset() {
+        recs.clear();
+        used = 0;
+    }
+};
+KernelProfiler &profiler();
+#define ZK_PROF(st, name, bytes, ...)        \
+    do {                                     \
+        ::zk::KernelProfiler &P_ = ::zk::profiler(); \
+        if (P_.on) P_.begin(st, name, (double)(bytes)); \
+        __VA_ARGS__;                         \
+        if (P_.on) P_.end(st);               \
+    } while (0)
+
+// ---------------------------------------------------------------- twiddle plans
+// Every power table the kernels need for one NTT size n, resident in HBM.
+//   dft_fwd / dft_inv : w_4096^t, t < 2048  (DFT stages of the in-LDS engine; smaller sizes stride)
+//   big_lo / big_hi   : w_n^t = big_lo[t & 2047] * big_hi[t >> 11]  (inter-pass twiddles, x values)
+struct NttTables {
+    int log_n = 0;
+    fe *dft_fwd = nullptr, *dft_inv = nullptr;
+    fe *fwd_lo = nullptr, *fwd_hi = nullptr, *inv_lo = nullptr, *inv_hi = nullptr;
+};
+
+// A power series s^k, k < n, as split tables (s^k = lo[k & 2047] * hi[k >> 11])
+struct PowTable {
+    fe *lo = nullptr, *hi = nullptr;
+};
+
+// NTT of `batch` polynomials of size 2^log_n, each at in + b*in_stride -> out + b*out_stride.
+//   inverse     : use w^-1 (no 1/n scale; fold it into post_scale)
+//   pre         : optional s^k pre-scale of input coefficient k (coset evaluation), may be null
+//   post_scale  : optional constant multiplied into every output (e.g. 1/n)
+// in and out must not alias.  tmp must hold batch * n elements when log_n > 12.
+void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride,
+         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp);
+
+// ---------------------------------------------------------------- hashing
+// leaf[i] = BLAKE3(row i) for natural LDE index i < N = B*n of a coset-major column set:
+// element (column c, index i) lives at base[(c*B + i%B)*n + i/B].
+void hash_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves);
+// FRI layer leaves: row r of a natural-order layer of size L (rows = L/fold): [e[r + k*L/fold]]
+void hash_fri_rows(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves);
+// nodes[1..nl) of a binary Merkle tree over nl leaves (nodes[nl/2..nl) = merges of leaf pairs)
+void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes);
+// out[k] = src[idx[k]] for 32-byte digests
+void gather_digests(hipStream_t st, const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out);
+// out[q*ncols + c] = element (c, pos[q]) of a coset-major column set
+void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,
+                 fe *out);
+
+// ---------------------------------------------------------------- AIR / composition
+struct AirConsts {
+    fe coeff_t[20];
+    fe coeff_b[22];
+    int assert_col[22];
+    int assert_grp[22];  // 0: step 0, 1: step n-2
+    fe assert_val[22];
+    fe inv_zn[8];   // 1 / (x^n - 1) on the 8 CE cosets
+    fe xr[8];       // 3 * w_CE^r
+    fe g_last2, g_last1;
+    fe delta;
+    int lwe_size;
+};
+// inverse of (x_i - a) * (x_i - b) for x_i = xr[i % 8] * w_n^(i / 8)-style coset points:
+// x_i = xr[i & (B-1)] * w_n^(i >> log_b), i < B*n
+void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe a, fe b,
+                     fe *out);
+// composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
+void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
+                      const fe *inv_bd, const AirConsts *consts_dev, fe *comp);
+// cross-coset step of the size-8n interpolation: per k1 < n, from the 8 per-coset inverse NTTs
+// (c_r[k1]), produce coefficients a[k1 + n*k2] = 3^-(k1+n k2) / (8n) * sum_r w8^(-r k2) w_8n^(-r k1) c_r[k1]
+// and write column k2 < ncols of the segmented composition polynomial: polys[k2*n + k1].
+void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T8n, const PowTable &inv3,
+                      fe scale, fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
+
+// ---------------------------------------------------------------- OOD / DEEP / FRI
+// out[p*2 + 0/1 ...]: evaluate `npolys` polys (n coeffs, stride n) at point x; partial sums per block
+void poly_eval_many(hipStream_t st, const fe *polys, int npolys, int log_n, fe x, fe *partials, int nblk_per_poly);
+void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out);
+// DEEP over the LDE domain, natural order (consts: DeepConsts in device memory)
+struct DeepConsts {
+    fe alpha_t[32];
+    fe alpha_c[16];
+    fe k1, k2, z, zg;
+};
+void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                      const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
+// FRI fold: next[r] = p_r(alpha) over rows r < L/fold (consts: FoldConsts in device memory)
+struct FoldConsts {
+    fe zinv[16];  // zeta^-t, t < fold
+    fe alpha, inv_offset, inv_fold;
+};
+void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
+                     const NttTables &TN, size_t wstride, fe *next);
+void coset_major_to_natural(hipStream_t st, const fe *src, int log_n, int log_b, fe *dst);
+// out[k] = src[idx[k]] for field elements
+void gather_fe(hipStream_t st, const fe *src, const uint64_t *idx, size_t k, fe *out);
+
+}  // namespace zk
+
+namespace zk {
+void diag_field_op(hipStream_t st, int op, const fe *a, const fe *b, fe *out, size_t count);
+void diag_blake3_elems(hipStream_t st, const fe *in, int k, size_t count, uint8_t *out);
+}  // namespace zk

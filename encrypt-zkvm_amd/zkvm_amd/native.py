@@ -1,0 +1,124 @@
+"""ctypes binding of libzkvm_gpu.so (include/zkvm_gpu.h).
+
+The product path: every prove goes through this library's HIP kernels.  There is no CPU
+fallback -- if the library is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent
+LIB_PATH = PKG_ROOT / "lib" / "libzkvm_gpu.so"
+
+ZK_OK = 0
+ZK_ERR_INVALID_ARG = -1
+ZK_ERR_BUFFER_TOO_SMALL = -2
+ZK_ERR_DEVICE = -3
+ZK_ERR_OUT_OF_MEMORY = -4
+ZK_ERR_PROGRAM = -10
+ZK_ERR_STACK = -11
+ZK_ERR_CHIPLETS = -12
+ZK_ERR_DEGREE = -20
+
+MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 32, 16, 16, 256, 255
+
+# every symbol include/zkvm_gpu.h declares (checked by tests/test_native_abi.py)
+EXPORTED = (
+    "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_destroy", "zk_prover_trace_buffer",
+    "zk_prove", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
+    "zk_eval_constraints", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_vm_trace",
+)
+
+
+class ZkError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+
+
+class Options(C.Structure):
+    _fields_ = [(f, C.c_uint32) for f in
+                ("num_queries", "blowup", "grinding", "field_extension", "fri_folding", "fri_rem_max_deg")]
+
+
+class PubInputs(C.Structure):
+    _fields_ = [("program_hash", C.c_uint8 * 32), ("stack_outputs", C.c_uint8 * 256),
+                ("lwe_size", C.c_uint32), ("delta", C.c_uint32)]
+
+
+class Record(C.Structure):
+    _fields_ = [
+        ("trace_len", C.c_uint32), ("lde_len", C.c_uint32), ("width", C.c_uint32), ("num_ccols", C.c_uint32),
+        ("num_fri_layers", C.c_uint32), ("remainder_len", C.c_uint32), ("num_positions", C.c_uint32),
+        ("_pad", C.c_uint32),
+        ("trace_root", C.c_uint8 * 32),
+        ("coeff_t", C.c_uint8 * (16 * MAX_TCONS)), ("coeff_b", C.c_uint8 * (16 * MAX_ASSERTS)),
+        ("constraint_root", C.c_uint8 * 32), ("z", C.c_uint8 * 16),
+        ("ood_trace_z", C.c_uint8 * (16 * MAX_COLS)), ("ood_trace_zg", C.c_uint8 * (16 * MAX_COLS)),
+        ("ood_constraints", C.c_uint8 * (16 * MAX_CCOLS)),
+        ("deep_t", C.c_uint8 * (16 * MAX_COLS)), ("deep_c", C.c_uint8 * (16 * MAX_CCOLS)),
+        ("fri_roots", C.c_uint8 * (32 * MAX_FRI)), ("fri_alphas", C.c_uint8 * (16 * MAX_FRI)),
+        ("remainder", C.c_uint8 * (16 * MAX_REM)), ("remainder_commitment", C.c_uint8 * 32),
+        ("pow_nonce", C.c_uint64), ("positions", C.c_uint64 * (MAX_Q + 1)),
+    ]
+
+
+class Dump(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in ("trace_polys", "trace_lde", "trace_leaves", "composition",
+                                          "comp_polys", "comp_lde", "deep", "fri_layer1")]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ZkError(ZK_ERR_DEVICE, f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C encrypt-zkvm_amd)")
+        L = C.CDLL(str(LIB_PATH))
+        vp, sz, u32, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_int
+        L.zk_last_error.restype = C.c_char_p
+        L.zk_device_count.argtypes = [C.POINTER(i32)]
+        L.zk_prover_create.argtypes = [i32, sz, u32, C.POINTER(vp)]
+        L.zk_prover_destroy.argtypes = [vp]
+        L.zk_prover_destroy.restype = None
+        L.zk_prover_trace_buffer.argtypes = [vp, C.POINTER(vp)]
+        L.zk_prove.argtypes = [vp, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp, C.POINTER(sz)]
+        L.zk_prove_device.argtypes = [vp, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp, C.POINTER(sz),
+                                      C.POINTER(Record), C.POINTER(Dump)]
+        L.zk_lde_new.argtypes = [vp, vp, sz, sz, u32, C.POINTER(vp), vp]
+        L.zk_lde_read_frame.argtypes = [vp, sz, vp, vp]
+        L.zk_lde_query.argtypes = [vp, vp, sz, vp, vp, C.POINTER(sz)]
+        L.zk_lde_free.argtypes = [vp]
+        L.zk_lde_free.restype = None
+        L.zk_eval_constraints.argtypes = [vp, C.POINTER(PubInputs), vp, vp, vp]
+        L.zk_prover_stage_times.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32, C.POINTER(i32)]
+        L.zk_prover_profile.argtypes = [vp, i32]
+        L.zk_prover_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(i32),
+                                             C.POINTER(C.c_double), i32, C.POINTER(i32)]
+        L.zk_vm_trace.argtypes = [C.c_char_p, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp, vp]
+        L.zk_vm_last_error.restype = C.c_char_p
+        L.zk_diag_mul_limbs_host.argtypes = [vp, vp, vp, sz]
+        L.zk_diag_mul_limbs_host.restype = None
+        L.zk_diag_blake3_host.argtypes = [vp, sz, vp]
+        L.zk_diag_blake3_host.restype = None
+        L.zk_diag_field_op.argtypes = [i32, i32, vp, vp, vp, sz]
+        L.zk_diag_blake3_rows.argtypes = [i32, vp, i32, sz, vp]
+        L.zk_diag_ntt.argtypes = [i32, vp, sz, i32, i32, vp, vp]
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != ZK_OK:
+        msg = lib().zk_last_error()
+        raise ZkError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    lib().zk_device_count(C.byref(c))
+    return c.value

@@ -1,0 +1,216 @@
+"""Host-side mirror of the reference's prover surface, driving the gfx950 library.
+
+Reference interface mirrored here (same names, argument meaning and error behaviour):
+  * ProofOptions::new(num_queries, blowup, grinding, field_extension, fri_folding, rem_max_degree)
+    (winterfell 0.9; hard-coded as (32, 8, 0, None, 8, 127) at vm/src/lib.rs:20)
+  * ExecutionProver::new(options, program_hash, stack_outputs, server_key)  prover/src/lib.rs:25-37
+  * Prover::prove(trace) -> Proof                                           prover/src/lib.rs:40-77
+  * vm::prove(program, inputs) -> (hash, outputs, proof)                     vm/src/lib.rs:13-29
+The trace is the 28-column matrix of vm/src/processor/mod.rs:71-95 as a (28, n, 2) uint64 array
+(low, high halves of each canonical f128 value) or any buffer with that byte layout.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import native
+from .native import Dump, Options, PubInputs, Record, ZkError, check, lib
+
+P = 2**128 - 45 * 2**40 + 1
+FIELD_EXTENSION_NONE = 1
+
+
+@dataclass(frozen=True)
+class ProofOptions:
+    num_queries: int = 32
+    blowup_factor: int = 8
+    grinding_factor: int = 0
+    field_extension: int = FIELD_EXTENSION_NONE
+    fri_folding_factor: int = 8
+    fri_remainder_max_degree: int = 127
+
+    def to_c(self) -> Options:
+        return Options(self.num_queries, self.blowup_factor, self.grinding_factor, self.field_extension,
+                       self.fri_folding_factor, self.fri_remainder_max_degree)
+
+
+REFERENCE_OPTIONS = ProofOptions()  # vm/src/lib.rs:20
+
+
+def elems_bytes(values) -> bytes:
+    return b"".join(int(v).to_bytes(16, "little") for v in values)
+
+
+def bytes_elems(b: bytes) -> list[int]:
+    return [int.from_bytes(b[i:i + 16], "little") for i in range(0, len(b), 16)]
+
+
+def make_pub_inputs(program_hash, stack_outputs, lwe_size: int, delta: int) -> PubInputs:
+    p = PubInputs()
+    C.memmove(p.program_hash, elems_bytes(program_hash), 32)
+    C.memmove(p.stack_outputs, elems_bytes(list(stack_outputs)[:16]), 256)
+    p.lwe_size, p.delta = lwe_size, delta
+    return p
+
+
+class GpuProver:
+    """One GPU's device memory and stream (zk_prover)."""
+
+    def __init__(self, device: int = 0, max_trace_len: int = 1 << 16, max_blowup: int = 8):
+        h = C.c_void_p()
+        check(lib().zk_prover_create(device, max_trace_len, max_blowup, C.byref(h)), "zk_prover_create")
+        self.handle = h
+        self.max_trace_len = max_trace_len
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().zk_prover_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def trace_buffer(self) -> int:
+        p = C.c_void_p()
+        check(lib().zk_prover_trace_buffer(self.handle, C.byref(p)), "zk_prover_trace_buffer")
+        return p.value
+
+    def prove_device(self, d_trace: int, n: int, pub: PubInputs, options: ProofOptions = REFERENCE_OPTIONS,
+                     record: bool = False, dump=(), allow_degree_error=False):
+        opt = options.to_c()
+        cap = 4 << 20
+        buf = C.create_string_buffer(cap)
+        plen = C.c_size_t(cap)
+        rec = Record() if record else None
+        dmp = Dump()
+        held = {}
+        N = n * options.blowup_factor
+        sizes = {"trace_polys": 28 * n, "trace_lde": N * 28, "trace_leaves": N * 2, "composition": 8 * n,
+                 "comp_polys": 16 * n, "comp_lde": N * 16, "deep": N,
+                 "fri_layer1": max(1, N // options.fri_folding_factor)}
+        for name in dump:
+            held[name] = np.zeros((sizes[name], 2), dtype=np.uint64)
+            setattr(dmp, name, held[name].ctypes.data)
+        rc = lib().zk_prove_device(self.handle, C.c_void_p(d_trace), n, C.byref(opt), C.byref(pub), buf,
+                                   C.byref(plen), C.byref(rec) if rec is not None else None,
+                                   C.byref(dmp) if dump else None)
+        if not (rc == 0 or (allow_degree_error and rc == native.ZK_ERR_DEGREE)):
+            check(rc, "zk_prove_device")
+        return buf.raw[:plen.value], rec, held, rc
+
+    def upload_trace(self, trace: np.ndarray) -> tuple[int, int]:
+        """Copy a (28, n, 2) uint64 host trace into this prover's device trace buffer."""
+        import ctypes
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        assert trace.shape[0] == 28 and trace.shape[2] == 2
+        n = trace.shape[1]
+        if n > self.max_trace_len:
+            raise ZkError(native.ZK_ERR_INVALID_ARG, "trace longer than max_trace_len")
+        d = self.trace_buffer()
+        hip = _hip()
+        rc = hip.hipMemcpy(ctypes.c_void_p(d), trace.ctypes.data_as(ctypes.c_void_p), trace.nbytes, 1)
+        if rc != 0:
+            raise ZkError(native.ZK_ERR_DEVICE, f"hipMemcpy failed ({rc})")
+        return d, n
+
+    def prove(self, trace: np.ndarray, pub: PubInputs, options: ProofOptions = REFERENCE_OPTIONS, **kw):
+        d, n = self.upload_trace(trace)
+        return self.prove_device(d, n, pub, options, **kw)
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 32)()
+        ms = (C.c_float * 32)()
+        cnt = C.c_int(0)
+        check(lib().zk_prover_stage_times(self.handle, names, ms, 32, C.byref(cnt)))
+        return {names[i].decode(): ms[i] for i in range(min(cnt.value, 32))}
+
+    def profile(self, on: bool):
+        check(lib().zk_prover_profile(self.handle, 1 if on else 0))
+        check(lib().zk_prover_kernel_stats(self.handle, None, None, None, None, 0, None))  # reset
+
+    def kernel_stats(self) -> dict:
+        """{kernel: (total_ms, launches, algorithmic_bytes)} since the last profile(True)."""
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        nl = (C.c_int * 64)()
+        by = (C.c_double * 64)()
+        cnt = C.c_int(0)
+        check(lib().zk_prover_kernel_stats(self.handle, names, ms, nl, by, 64, C.byref(cnt)))
+        return {names[i].decode(): (ms[i], nl[i], by[i]) for i in range(min(cnt.value, 64))}
+
+
+_hip_lib = None
+
+
+def _hip():
+    global _hip_lib
+    if _hip_lib is None:
+        _hip_lib = C.CDLL("libamdhip64.so")
+        _hip_lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return _hip_lib
+
+
+class ExecutionProver:
+    """prover/src/lib.rs:17-77 -- `ExecutionProver::new(options, program_hash, stack_outputs, server_key)`
+    then `.prove(trace)`.  Panics in the reference (`prove(...).unwrap()`, vm/src/lib.rs:26) become
+    ZkError here."""
+
+    def __init__(self, options: ProofOptions, program_hash, stack_outputs, server_key, gpu: GpuProver | None = None):
+        self.options = options
+        self.program_hash = list(program_hash)
+        self.stack_outputs = list(stack_outputs)
+        self.server_key = server_key
+        self._gpu = gpu
+
+    def get_pub_inputs(self) -> PubInputs:
+        return make_pub_inputs(self.program_hash, self.stack_outputs, self.server_key.lwe_size(),
+                               self.server_key.parameters.delta)
+
+    def prove(self, trace: np.ndarray) -> bytes:
+        n = trace.shape[1]
+        gpu = self._gpu or GpuProver(0, max(n, 16), max(8, self.options.blowup_factor))
+        proof, _, _, _ = gpu.prove(trace, self.get_pub_inputs(), self.options)
+        return proof
+
+
+# ------------------------------------------------------------------ VM harness (vm::prove)
+def vm_trace(source: str, public, secret, server_key, last_row):
+    """Processor::run + trace (vm/src/processor/mod.rs:61-95) via the native VM.
+    Returns (trace (28, n, 2) uint64, outputs[16], program_hash[2])."""
+    L = server_key.lwe_size()
+    sec = elems_bytes([v for ct in secret for v in ct])
+    nops_hint = 16 * len(source) + 64
+    cap = 16
+    while cap <= nops_hint:
+        cap *= 2
+    cap *= 2
+    n = C.c_size_t(0)
+    outputs = C.create_string_buffer(256)
+    h = C.create_string_buffer(32)
+    # first call: size query
+    rc = lib().zk_vm_trace(source.encode(), bytes(public), len(public), sec, len(secret), L,
+                           server_key.parameters.delta, elems_bytes(last_row), None, 0, C.byref(n), outputs, h)
+    if rc not in (0, native.ZK_ERR_BUFFER_TOO_SMALL):
+        raise ZkError(rc, lib().zk_vm_last_error().decode())
+    trace = np.zeros((28, n.value, 2), dtype=np.uint64)
+    rc = lib().zk_vm_trace(source.encode(), bytes(public), len(public), sec, len(secret), L,
+                           server_key.parameters.delta, elems_bytes(last_row), trace.ctypes.data, n.value,
+                           C.byref(n), outputs, h)
+    if rc:
+        raise ZkError(rc, lib().zk_vm_last_error().decode())
+    return trace, bytes_elems(outputs.raw), bytes_elems(h.raw)
+
+
+def prove(source: str, public, secret, server_key, last_row, options: ProofOptions = REFERENCE_OPTIONS,
+          gpu: GpuProver | None = None):
+    """vm::prove (vm/src/lib.rs:13-29): run -> output -> trace -> options -> hash -> prove."""
+    trace, outputs, program_hash = vm_trace(source, public, secret, server_key, last_row)
+    prover = ExecutionProver(options, program_hash, outputs, server_key, gpu)
+    return program_hash, outputs, prover.prove(trace)

@@ -109,16 +109,39 @@ def cipher_mix_program(blocks: int) -> tuple[str, int, int]:
     return "\n".join(lines) + "\n", n_pub, n_sec
 
 
+def padded_length(source: str) -> int:
+    """Length of Program::compile's padded op list (vm/src/program/mod.rs:65-86), without hashing."""
+    n = 0
+    for line in source.splitlines():
+        tok = line.split("#")[0].strip()
+        if not tok:
+            continue
+        if tok.startswith("push"):
+            n += (8 - n % 8) % 8
+        if n % 16 >= 14:
+            n += 16 - n % 16
+        n += 1
+    return n + (16 - n % 16)
+
+
+def trace_length(source: str) -> int:
+    """Processor::trace length: capacity = smallest 16*2^k > padded ops; n = next_pow2(capacity + 1)."""
+    p = padded_length(source)
+    cap = 16
+    while cap <= p:
+        cap *= 2
+    return 2 * cap
+
+
 def ops_for_trace_len(log_n: int, kind: str = "cipher") -> str:
-    """Pick a program size whose trace length is exactly 2^log_n (n = 2 * next_pow2(P + 1))."""
-    target_cap = 2 ** (log_n - 1)  # capacity must be the smallest 16*2^k > padded length
-    if kind == "pushadd":
-        # each (push.1, add) pair occupies 8 slots; push.1 head 8 slots; final pad 16
-        k = max(1, (target_cap * 3 // 4) // 8)
-        return push_add_program(k)
-    # cipher block: 12 ops; two pushes aligned to 8 -> measure by compiling in the caller
-    blocks = max(1, (target_cap * 3 // 4) // 24)
-    return cipher_mix_program(blocks)[0]
+    """A program whose trace is exactly 2^log_n rows, with its padded length ~3/4 of the capacity."""
+    cap = 2 ** (log_n - 1)
+    make = (lambda k: push_add_program(k)) if kind == "pushadd" else (lambda k: cipher_mix_program(k)[0])
+    per = (padded_length(make(65)) - padded_length(make(1))) // 64
+    k = max(1, (cap * 3 // 4) // per)
+    src = make(k)
+    assert trace_length(src) == 2 ** log_n, (log_n, k, padded_length(src))
+    return src
 
 
 @dataclass

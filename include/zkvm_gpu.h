@@ -1,0 +1,168 @@
+/*
+ * zkvm_gpu.h -- C ABI of the MI355X (gfx950) STARK prover for the Encrypt-zkVM execution trace.
+ *
+ * Drop-in boundary: every entry point below replaces one piece of the reference's
+ * `impl winterfell::Prover for ExecutionProver` (prover/src/lib.rs:40-77) as driven by
+ * `vm::prove` (vm/src/lib.rs:13-29).  The reference Rust host would bind these through a
+ * thin FFI (see INTEGRATION.md for the cgo-style/Rust `extern "C"` stubs).
+ *
+ * Conventions
+ *  - Field elements are winterfell f128 values (p = 2^128 - 45*2^40 + 1), canonical,
+ *    16 bytes little-endian each (the `f128::BaseElement` byte format).
+ *  - Trace matrices are column-major: column c occupies bytes [c*n*16, (c+1)*n*16).  The
+ *    column order is the one `Processor::trace` emits (vm/src/processor/mod.rs:76-84):
+ *    clk, 5 opcode bits, hash flag, 4 sponge words, stack depth, 16 stack registers (28 total).
+ *  - All functions return ZK_OK (0) or a negative status, never abort, and leave a message
+ *    for zk_last_error() (thread-local).  Buffers are owned by the caller.
+ *  - A zk_prover owns one GPU's device memory and one HIP stream.  Calls on one prover are not
+ *    reentrant; different provers may be used from different threads concurrently.
+ */
+#ifndef ZKVM_GPU_H
+#define ZKVM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZK_OK 0
+#define ZK_ERR_INVALID_ARG -1
+#define ZK_ERR_BUFFER_TOO_SMALL -2
+#define ZK_ERR_DEVICE -3
+#define ZK_ERR_OUT_OF_MEMORY -4
+#define ZK_ERR_PROGRAM -10  /* ProgramError (vm/src/program/errors.rs) */
+#define ZK_ERR_STACK -11    /* StackError (vm/src/processor/errors.rs:4-42) */
+#define ZK_ERR_CHIPLETS -12 /* ChipletsError (vm/src/processor/errors.rs:44-71) */
+#define ZK_ERR_DEGREE -20   /* proof written, but the trace does not satisfy ProcessorAir */
+
+#define ZK_TRACE_WIDTH 28
+#define ZK_MAX_COLS 32
+#define ZK_MAX_TCONS 32
+#define ZK_MAX_ASSERTS 32
+#define ZK_MAX_CCOLS 16
+#define ZK_MAX_FRI_LAYERS 16
+#define ZK_MAX_REMAINDER 256
+#define ZK_MAX_QUERIES 255
+
+/* ProofOptions::new(num_queries, blowup, grinding, field_extension, fri_folding, fri_rem_max_deg)
+ * -- the reference hard-codes (32, 8, 0, None, 8, 127) at vm/src/lib.rs:20.
+ * field_extension: 1 = FieldExtension::None (the only value this build accepts). */
+typedef struct {
+    uint32_t num_queries;
+    uint32_t blowup;
+    uint32_t grinding;
+    uint32_t field_extension;
+    uint32_t fri_folding;
+    uint32_t fri_rem_max_deg;
+} zk_options;
+
+/* air::PublicInputs (air/src/lib.rs:18-47) plus the two ServerKey values the constraints use
+ * (lwe_size = k + 1, delta = q / p; fhe/src/server_key.rs:78-124, fhe/src/parameters.rs:17).
+ * The reference also carries the ServerKey's secret bits here; the constraints never read them. */
+typedef struct {
+    uint8_t program_hash[2][16];
+    uint8_t stack_outputs[16][16];
+    uint32_t lwe_size;
+    uint32_t delta;
+} zk_pub_inputs;
+
+/* Every deterministic intermediate of one proof (for stage-wise parity checks).  Same layout as
+ * the oracle's or_record. */
+typedef struct {
+    uint32_t trace_len, lde_len, width, num_ccols, num_fri_layers, remainder_len;
+    uint32_t num_positions;
+    uint32_t _pad;
+    uint8_t trace_root[32];
+    uint8_t coeff_t[ZK_MAX_TCONS][16];
+    uint8_t coeff_b[ZK_MAX_ASSERTS][16];
+    uint8_t constraint_root[32];
+    uint8_t z[16];
+    uint8_t ood_trace_z[ZK_MAX_COLS][16];
+    uint8_t ood_trace_zg[ZK_MAX_COLS][16];
+    uint8_t ood_constraints[ZK_MAX_CCOLS][16];
+    uint8_t deep_t[ZK_MAX_COLS][16];
+    uint8_t deep_c[ZK_MAX_CCOLS][16];
+    uint8_t fri_roots[ZK_MAX_FRI_LAYERS][32];
+    uint8_t fri_alphas[ZK_MAX_FRI_LAYERS][16];
+    uint8_t remainder[ZK_MAX_REMAINDER][16];
+    uint8_t remainder_commitment[32];
+    uint64_t pow_nonce;
+    uint64_t positions[ZK_MAX_QUERIES + 1];
+} zk_record;
+
+/* Optional host copies of full-size intermediates (NULL = skip), natural LDE order. */
+typedef struct {
+    uint8_t *trace_polys;  /* 28 * n coefficients, column-major */
+    uint8_t *trace_lde;    /* N * 28, row-major */
+    uint8_t *trace_leaves; /* N * 32 */
+    uint8_t *composition;  /* 8n evaluations over the constraint-evaluation domain */
+    uint8_t *comp_polys;   /* c * n coefficients, column-major */
+    uint8_t *comp_lde;     /* N * c, row-major */
+    uint8_t *deep;         /* N evaluations */
+    uint8_t *fri_layer1;   /* N / fold evaluations */
+} zk_dump;
+
+typedef struct zk_prover zk_prover;
+typedef struct zk_trace_lde zk_trace_lde;
+
+const char *zk_last_error(void);
+int zk_device_count(int *count);
+
+/* ---- prover object: device memory sized for traces up to max_trace_len rows ---- */
+int zk_prover_create(int device, size_t max_trace_len, uint32_t max_blowup, zk_prover **out);
+void zk_prover_destroy(zk_prover *p);
+/* device pointer to a scratch region large enough for a 28 x max_trace_len trace (so callers can
+ * stage a device-resident trace without their own allocator) */
+int zk_prover_trace_buffer(zk_prover *p, void **d_trace);
+
+/* Prover::prove (vm/src/lib.rs:26 -> winterfell generate_proof), whole proof.
+ * Host trace variant: trace is 28 x n, column-major, host memory. */
+int zk_prove(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+             uint8_t *proof_out, size_t *proof_len);
+/* Device trace variant (trace already resident in HBM on this prover's device), with optional
+ * record / dumps.  proof_len is in/out: capacity in, bytes written out; ZK_ERR_BUFFER_TOO_SMALL
+ * reports the needed size. */
+int zk_prove_device(zk_prover *p, const void *d_trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                    uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump);
+
+/* ---- plug point 1: Prover::new_trace_lde (prover/src/lib.rs:55-62) -> DefaultTraceLde ---- */
+/* interpolate the trace, extend it over the blowup coset domain and commit to its rows.
+ * The LDE lives in the prover's device memory until zk_lde_free. */
+int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint32_t blowup, zk_trace_lde **out,
+               uint8_t root[32]);
+/* TraceLde::read_main_trace_frame_into: rows lde_step and (lde_step + blowup) mod N */
+int zk_lde_read_frame(zk_trace_lde *lde, size_t lde_step, uint8_t *cur, uint8_t *next);
+/* TraceLde::query: rows at positions (width elements each) + batch Merkle proof bytes */
+int zk_lde_query(zk_trace_lde *lde, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
+                 size_t *proof_len);
+void zk_lde_free(zk_trace_lde *lde);
+
+/* ---- plug point 2: Prover::new_evaluator (prover/src/lib.rs:65-72) + evaluate ----
+ * DefaultConstraintEvaluator over ProcessorAir: coeff_t = 20 transition coefficients,
+ * coeff_b = 22 boundary coefficients (assertions sorted by (stride, step, column));
+ * out receives the 8n composition-trace values in natural CE-domain order. */
+int zk_eval_constraints(zk_trace_lde *lde, const zk_pub_inputs *pub, const uint8_t *coeff_t, const uint8_t *coeff_b,
+                        uint8_t *out);
+
+/* ---- per-stage timing of the last proof (ms), for benchmarks ---- */
+int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, int *count);
+/* per-kernel device time (HIP events on the prover's stream) and algorithmic HBM bytes accumulated
+ * since the last reset; enabled by zk_prover_profile(p, 1).  Passing all-NULL arrays resets. */
+int zk_prover_profile(zk_prover *p, int enable);
+int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, int *launches, double *total_bytes,
+                           int cap, int *count);
+
+/* ---- VM trace generator (harness; vm::Processor::run + trace, vm/src/processor/mod.rs:61-95) ----
+ * source: assembly text (Program::compile); public: u8 inputs; secret: ciphertexts of lwe_size
+ * elements; last_row: the 28 values the reference draws from thread_rng().  trace_out receives
+ * 28 x n column-major with n <= cap_rows; outputs = 16 stack values; hash = program hash. */
+int zk_vm_trace(const char *source, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
+                size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, uint8_t *trace_out,
+                size_t cap_rows, size_t *n_out, uint8_t *outputs, uint8_t *program_hash);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
