@@ -154,8 +154,108 @@ ZK_HD fe fe_mul_limbs(fe a, fe b) {
     return reduce256(r);
 }
 
+// ---- gfx950 device multiply: product scanning with v_mad_u64_u32 hardware carry-outs ----
+// Same algorithm as fe_mul_limbs (schoolbook + two folds with C = 2^128 - p), hand-scheduled:
+// 94 VALU instructions instead of ~151 from the C formulation (DESIGN.md "Field multiply").
+// One column of a product-scanning multiply: a += sum x_i*y_i (64-bit); h := sum of the carry-outs
+// (h is the high word of the next column's accumulator).  All MADs first, carry-outs to distinct
+// SGPR pairs, then the carry adds: gfx950 needs 2 wait states between a VALU writing an SGPR and a
+// VALU reading it as carry-in, which the other instructions (or an s_nop) provide.
+__device__ __forceinline__ void col1(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0) {
+    uint64_t k0, kd;
+    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32 %1, %3, 0, 0, %2"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(kd) : "v"(x0), "v"(y0));
+}
+__device__ __forceinline__ void col2(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    uint64_t k0, k1, kd;
+    asm("v_mad_u64_u32 %0, %2, %5, %6, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %7, %8, %0\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32 %1, %4, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %4, %1, 0, %3"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(kd) : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+}
+__device__ __forceinline__ void col3(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                     uint32_t x2, uint32_t y2) {
+    uint64_t k0, k1, k2, kd;
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %8, %9, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %10, %11, %0\n\t"
+        "v_addc_co_u32 %1, %5, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %4"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(kd)
+        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2));
+}
+__device__ __forceinline__ void col4(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                     uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+    uint64_t k0, k1, k2, k3, kd;
+    asm("v_mad_u64_u32 %0, %2, %7, %8, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %11, %12, %0\n\t"
+        "v_mad_u64_u32 %0, %5, %13, %14, %0\n\t"
+        "v_addc_co_u32 %1, %6, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %4\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %5"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(kd)
+        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2), "v"(x3), "v"(y3));
+}
+#define ZK_SHIFT(a, h, out) do { out = (uint32_t)(a); a = ((a) >> 32) | ((uint64_t)(h) << 32); h = 0; } while (0)
+
+__device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    const uint32_t y0 = lo32(Bv.lo), y1 = hi32(Bv.lo), y2 = lo32(Bv.hi), y3 = hi32(Bv.hi);
+    uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+    uint64_t a = (uint64_t)x0 * y0;
+    uint32_t h = 0;
+    ZK_SHIFT(a, h, r0);
+    col2(a, h, x0, y1, x1, y0);               ZK_SHIFT(a, h, r1);
+    col3(a, h, x0, y2, x1, y1, x2, y0);       ZK_SHIFT(a, h, r2);
+    col4(a, h, x0, y3, x1, y2, x2, y1, x3, y0); ZK_SHIFT(a, h, r3);
+    col3(a, h, x1, y3, x2, y2, x3, y1);       ZK_SHIFT(a, h, r4);
+    col2(a, h, x2, y3, x3, y2);               ZK_SHIFT(a, h, r5);
+    col1(a, h, x3, y3);                       ZK_SHIFT(a, h, r6);
+    r7 = (uint32_t)a;
+    // S = L + H*C, C = (c0, c1) = (0xffffffff, 0x2cff).  The accumulator starts at (L0, L1); L2 and
+    // L3 join their columns as products L_k * 1 so their carries ride the same chains.
+    const uint32_t c0 = 0xffffffffu, c1 = 0x2cffu, one = 1u;
+    uint32_t s0, s1, s2, s3, s4, s5;
+    uint64_t b = (uint64_t)r0 | ((uint64_t)r1 << 32);
+    uint32_t g;
+    col1(b, g, r4, c0);                        ZK_SHIFT(b, g, s0);
+    col2(b, g, r4, c1, r5, c0);                ZK_SHIFT(b, g, s1);
+    col3(b, g, r5, c1, r6, c0, r2, one);       ZK_SHIFT(b, g, s2);
+    col3(b, g, r6, c1, r7, c0, r3, one);       ZK_SHIFT(b, g, s3);
+    col1(b, g, r7, c1);                        ZK_SHIFT(b, g, s4);
+    s5 = (uint32_t)b;
+    // T = S_lo + S_hi*C, S_hi = (s4, s5) < 2^47
+    uint64_t d = (uint64_t)s0 | ((uint64_t)s1 << 32);
+    uint32_t e, t0, t1, t2, t3;
+    col1(d, e, s4, c0);                        ZK_SHIFT(d, e, t0);
+    col2(d, e, s4, c1, s5, c0);                ZK_SHIFT(d, e, t1);
+    col2(d, e, s5, c1, s2, one);               ZK_SHIFT(d, e, t2);
+    col1(d, e, s3, one);                       ZK_SHIFT(d, e, t3);
+    uint32_t tc = (uint32_t)d;                 // bit 128 (0 or 1)
+    // result = (tc | carry(T + C)) ? T + C : T
+    uint32_t cy, u0, u1, u2, u3, uc;
+    u0 = __builtin_addc(t0, c0, 0u, &cy);
+    u1 = __builtin_addc(t1, c1, cy, &cy);
+    u2 = __builtin_addc(t2, 0u, cy, &cy);
+    u3 = __builtin_addc(t3, 0u, cy, &uc);
+    // branch-free select (one v_bfi_b32 per limb): m = all ones when T + C is the result
+    const uint32_t m = 0u - ((tc | uc) & 1u);
+    fe res;
+    res.lo = ((uint64_t)((u1 & m) | (t1 & ~m)) << 32) | ((u0 & m) | (t0 & ~m));
+    res.hi = ((uint64_t)((u3 & m) | (t3 & ~m)) << 32) | ((u2 & m) | (t2 & ~m));
+    return res;
+}
+#undef ZK_SHIFT
+
 // device and host overloads (clang resolves by target)
-__device__ __forceinline__ fe fe_mul(fe a, fe b) { return fe_mul_limbs(a, b); }
+__device__ __forceinline__ fe fe_mul(fe a, fe b) { return fe_mul_asm(a, b); }
 // host: unsigned __int128 with the same two folds
 __host__ static inline fe fe_from_u128(unsigned __int128 v) { return fe{(uint64_t)v, (uint64_t)(v >> 64)}; }
 __host__ static inline unsigned __int128 fe_to_u128(fe a) { return ((unsigned __int128)a.hi << 64) | a.lo; }
@@ -180,6 +280,46 @@ __host__ static inline fe fe_mul(fe a, fe b) {
 }
 
 ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }
+
+// ---- multiply-accumulate by small (< 2^32) constants, reduced once: for the Rescue MDS matrix,
+// whose entries are small signed integers (crypto/src/rescue.rs:197-214).
+struct acc160 {
+    uint32_t w[5];
+};
+ZK_HD acc160 acc160_zero() { return acc160{{0, 0, 0, 0, 0}}; }
+// acc += x * c  (acc stays < 2^160 for a handful of terms)
+ZK_HD void acc160_madd(acc160 &acc, fe x, uint32_t c) {
+    const uint32_t xs[4] = {lo32(x.lo), hi32(x.lo), lo32(x.hi), hi32(x.hi)};
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        t = (uint64_t)xs[k] * c + acc.w[k] + (t >> 32);
+        acc.w[k] = lo32(t);
+    }
+    acc.w[4] += hi32(t);
+}
+// reduce a < 2^160 value: L + H*C with H < 2^32, C = 45*2^40 - 1
+ZK_HD fe acc160_reduce(const acc160 &a) {
+    uint64_t lo = (uint64_t)a.w[0] | ((uint64_t)a.w[1] << 32);
+    uint64_t hi = (uint64_t)a.w[2] | ((uint64_t)a.w[3] << 32);
+    uint64_t sh = a.w[4];
+    uint64_t q = sh * 45u;
+    uint64_t add_lo = q << 40, add_hi = q >> 24;
+    uint64_t nlo = lo + add_lo;
+    uint64_t c = nlo < lo;
+    uint64_t nhi = hi + add_hi + c;
+    uint64_t carry = (nhi < hi) | ((nhi == hi) & c);
+    uint64_t blo = nlo - sh;
+    uint64_t b = nlo < sh;
+    uint64_t bhi = nhi - b;
+    carry -= (nhi < b);
+    uint64_t clo = blo + (carry ? ZK_C : 0);
+    uint64_t chi = bhi + (clo < blo);
+    uint64_t ulo = clo + ZK_C;
+    uint64_t uhi = chi + (ulo < clo);
+    bool ge = uhi < chi;
+    return fe{ge ? ulo : clo, ge ? uhi : chi};
+}
 
 ZK_HD fe fe_exp(fe b, uint64_t e_lo, uint64_t e_hi = 0) {
     // right-to-left square and multiply over the 128-bit exponent (e_hi:e_lo)

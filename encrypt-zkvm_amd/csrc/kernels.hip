@@ -42,12 +42,60 @@ __device__ __forceinline__ int lds_idx(int line, int pos) {
     return line * ((1 << LOGM) + PAD) + pos;
 }
 
+// Radix-4 rounds: each radix-4 butterfly performs DIT stages lg and lg+1 (half h = 2^(lg-1)) on
+// positions p0 + {0, h, 2h, 3h}, p0 = grp*4h + j, j < h:
+//   stage lg   : (x0, x1), (x2, x3) with w_2h^j
+//   stage lg+1 : (x0, x2) with w_4h^j, (x1, x3) with w_4h^(j+h)
+// so a round reads and writes each LDS element once for two stages.  The first round (h = 1, j = 0)
+// has w_2 = w_4^0 = 1 and needs a single multiply by w_4.  An odd log2(M) ends with one radix-2 stage.
 template <int LOGM, int TILE>
 __device__ void lds_dft(fe *s, const fe *tw4096) {
     constexpr int M = 1 << LOGM;
     constexpr int BFLY = TILE / 2;
+    constexpr int Q = TILE / 4;
+    int lg0 = 1;
+    if constexpr (LOGM >= 2) {
+        const fe w4 = tw4096[1024];
+#pragma unroll
+        for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
+            int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+            int p = lds_idx<LOGM>(line, local * 4);
+            fe x0 = s[p], x1 = s[p + 1], x2 = s[p + 2], x3 = s[p + 3];
+            fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+            fe a3 = fe_mul(fe_sub(x2, x3), w4);
+            s[p] = fe_add(a0, a2);
+            s[p + 2] = fe_sub(a0, a2);
+            s[p + 1] = fe_add(a1, a3);
+            s[p + 3] = fe_sub(a1, a3);
+        }
+        __syncthreads();
+        lg0 = 3;
 #pragma unroll 1
-    for (int lg = 1; lg <= LOGM; lg++) {
+        for (int lg = 3; lg + 1 <= LOGM; lg += 2) {
+            const int h = 1 << (lg - 1);
+#pragma unroll
+            for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
+                int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+                int j = local & (h - 1), grp = local >> (lg - 1);
+                int p = lds_idx<LOGM>(line, grp * 4 * h + j);
+                fe w1 = tw4096[j << (12 - lg)];
+                fe w2 = tw4096[j << (11 - lg)];
+                fe w3 = tw4096[(j + h) << (11 - lg)];
+                fe x0 = s[p], x1 = s[p + h], x2 = s[p + 2 * h], x3 = s[p + 3 * h];
+                fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
+                fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+                fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
+                s[p] = fe_add(a0, u2);
+                s[p + 2 * h] = fe_sub(a0, u2);
+                s[p + h] = fe_add(a1, u3);
+                s[p + 3 * h] = fe_sub(a1, u3);
+            }
+            __syncthreads();
+            lg0 = lg + 2;
+        }
+    }
+#pragma unroll 1
+    for (int lg = lg0; lg <= LOGM; lg++) {
         const int half = 1 << (lg - 1);
         const int twshift = 12 - lg;  // w_len^j = w_4096^(j * 4096/len)
         for (int bf = threadIdx.x; bf < BFLY; bf += NTT_THREADS) {
@@ -432,140 +480,176 @@ __constant__ fe c_inv_mds[16];
 
 __device__ __forceinline__ fe cube(fe x) { return fe_mul(fe_mul(x, x), x); }
 
-__global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wce_lo,
-                                                          const fe *wce_hi, const fe *periodic, const fe *inv_bd,
+// Rescue MDS (crypto/src/rescue.rs:197-214) as signed small integers: row r = (-a, +b, -c, +d)
+__device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
+    constexpr uint32_t M[16] = {729, 1080, 390, 40, 29160, 42471, 14520, 1210,
+                                882090, 1277640, 429429, 33880, 24698520, 35708310, 11935560, 925771};
+    acc160 pos = acc160_zero(), neg = acc160_zero();
+    acc160_madd(neg, x[0], M[4 * r + 0]);
+    acc160_madd(pos, x[1], M[4 * r + 1]);
+    acc160_madd(neg, x[2], M[4 * r + 2]);
+    acc160_madd(pos, x[3], M[4 * r + 3]);
+    return fe_sub(acc160_reduce(pos), acc160_reduce(neg));
+}
+
+// Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
+// SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
+struct EvalShared {
+    fe ct[20], cb[22], v1[10], xr[8], inv_zn[8], inv_mds[16];
+    fe g_last2, g_last1, delta;
+};
+
+__global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wn_lo,
+                                                          const fe *wn_hi, const fe *periodic, const fe *inv_bd,
                                                           const AirConsts *K, fe *comp) {
+    __shared__ EvalShared S;
+    {
+        const int t = threadIdx.x;
+        if (t < 20) S.ct[t] = K->coeff_t[t];
+        else if (t < 42) S.cb[t - 20] = K->coeff_b[t - 20];
+        else if (t < 52) S.v1[t - 42] = K->assert_val[12 + t - 42];
+        else if (t < 60) S.xr[t - 52] = K->xr[t - 52];
+        else if (t < 68) S.inv_zn[t - 60] = K->inv_zn[t - 60];
+        else if (t < 84) S.inv_mds[t - 68] = c_inv_mds[t - 68];
+        else if (t == 84) S.g_last2 = K->g_last2;
+        else if (t == 85) S.g_last1 = K->g_last1;
+        else if (t == 86) S.delta = K->delta;
+        __syncthreads();
+    }
+    const int L = K->lwe_size;
     const size_t n = (size_t)1 << log_n;
     const size_t CE = n * 8;
     const size_t B = (size_t)1 << log_b;
     const int shift = log_b - 3;  // LDE steps per CE step
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < CE; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t li = i << shift;
-        const size_t r = li & (B - 1), q = li >> log_b, qn = (q + 1) & (n - 1);
-        const fe *cb = lde + r * n;  // column c of the current/next row: cb[c*B*n + q]
-        const size_t cs = B * n;
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= CE) return;
+    const size_t li = i << shift;
+    const size_t r = li & (B - 1), q = li >> log_b, qn = (q + 1) & (n - 1);
+    const fe *cb = lde + r * n;
+    const size_t cs = B * n;
 #define CUR(c) cb[(size_t)(c)*cs + q]
 #define NXT(c) cb[(size_t)(c)*cs + qn]
-        const fe one = fe_one();
-        const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
-        const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
-                 nb4 = fe_sub(one, b4);
-        // shared prefixes of the degree-5 selectors (flags.rs:45-79)
-        const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
-        const fe is_add = fe_mul(fe_mul(n0_1_n2, nb3), nb4);
-        const fe is_sadd = fe_mul(fe_mul(n0_1_n2, b3), nb4);
-        const fe is_add2 = fe_mul(fe_mul(n0_1_n2, b3), b4);
-        const fe is_mul = fe_mul(fe_mul(n0_1_n2, nb3), b4);
-        const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
-        const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
-        const fe is_push = fe_mul(fe_mul(p0, nb3), nb4);
-        const fe is_read = fe_mul(fe_mul(p0, nb3), b4);
-        const fe is_read2 = fe_mul(fe_mul(p0, b3), nb4);
-        const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
-        const fe s0 = CUR(12), s0n = NXT(12);
-        fe t;   // running sum_k coeff_t[k] * C_k
-        fe v;
-        // 0 clock
-        v = fe_sub(NXT(0), fe_add(CUR(0), one));
-        t = fe_mul(K->coeff_t[0], v);
-        // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2
-        {
-            fe four = fe_make(4);
-            v = fe_sub(NXT(11), CUR(11));
-            v = fe_add(fe_sub(v, b0), b1);
-            v = fe_add(fe_sub(v, fe_mul(is_read2, four)), fe_mul(is_add2, four));
-            t = fe_add(t, fe_mul(K->coeff_t[1], v));
+    const fe one = fe_one();
+    const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
+    const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
+             nb4 = fe_sub(one, b4);
+    // degree-5 selectors (flags.rs:45-79) with shared prefixes
+    const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
+    const fe n0_1_n2_n3 = fe_mul(n0_1_n2, nb3), n0_1_n2_3 = fe_mul(n0_1_n2, b3);
+    const fe is_add = fe_mul(n0_1_n2_n3, nb4);
+    const fe is_mul = fe_mul(n0_1_n2_n3, b4);
+    const fe is_sadd = fe_mul(n0_1_n2_3, nb4);
+    const fe is_add2 = fe_mul(n0_1_n2_3, b4);
+    const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
+    const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
+    const fe p0n3 = fe_mul(p0, nb3);
+    const fe is_push = fe_mul(p0n3, nb4);
+    const fe is_read = fe_mul(p0n3, b4);
+    const fe is_read2 = fe_mul(fe_mul(p0, b3), nb4);
+    const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
+    const fe s0 = CUR(12), s0n = NXT(12);
+    fe t, v;
+    // 0 clock
+    t = fe_mul(S.ct[0], fe_sub(NXT(0), fe_add(CUR(0), one)));
+    // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
+    {
+        v = fe_add(fe_sub(fe_sub(NXT(11), CUR(11)), b0), b1);
+        fe d = fe_sub(is_add2, is_read2);
+        d = fe_add(d, d);
+        d = fe_add(d, d);
+        t = fe_add(t, fe_mul(S.ct[1], fe_add(v, d)));
+    }
+    // 2 shift
+    t = fe_add(t, fe_mul(S.ct[2], fe_mul(b0, b1)));
+    // 3 add, 6 mul
+    const fe s1 = CUR(13);
+    t = fe_add(t, fe_mul(S.ct[3], fe_mul(is_add, fe_sub(s0n, fe_add(s0, s1)))));
+    t = fe_add(t, fe_mul(S.ct[6], fe_mul(is_mul, fe_sub(s0n, fe_mul(s0, s1)))));
+    // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs (fhe/src/server_key.rs:89-124)
+    {
+        fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
+        for (int k = 0; k < L; k++) {
+            fe sn = NXT(12 + k);
+            fe s1k = CUR(13 + k);
+            acc4 = fe_add(acc4, fe_sub(sn, s1k));
+            acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
+            acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
         }
-        // 2 shift
-        t = fe_add(t, fe_mul(K->coeff_t[2], fe_mul(b0, b1)));
-        // 3 add
-        t = fe_add(t, fe_mul(K->coeff_t[3], fe_mul(is_add, fe_sub(s0n, fe_add(s0, CUR(13))))));
-        // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs
-        {
-            const int L = K->lwe_size;
-            fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
-            for (int k = 0; k < L; k++) {
-                fe sn = NXT(12 + k);
-                fe s1k = CUR(13 + k);
-                fe triv = (k == L - 1) ? fe_mul(K->delta, s0) : fe_zero();
-                acc4 = fe_add(acc4, fe_sub(sn, fe_add(s1k, triv)));
-                acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
-                acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
-            }
-            t = fe_add(t, fe_mul(K->coeff_t[4], fe_mul(is_sadd, acc4)));
-            t = fe_add(t, fe_mul(K->coeff_t[5], fe_mul(is_add2, acc5)));
-            t = fe_add(t, fe_mul(K->coeff_t[7], fe_mul(is_smul, acc7)));
+        acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
+        t = fe_add(t, fe_mul(S.ct[4], fe_mul(is_sadd, acc4)));
+        t = fe_add(t, fe_mul(S.ct[5], fe_mul(is_add2, acc5)));
+        t = fe_add(t, fe_mul(S.ct[7], fe_mul(is_smul, acc7)));
+    }
+    // 8 push / 9 read / 10 read2 / 11 noop
+    {
+        fe d1 = fe_sub(NXT(13), s0);
+        t = fe_add(t, fe_mul(S.ct[8], fe_mul(is_push, d1)));
+        t = fe_add(t, fe_mul(S.ct[9], fe_mul(is_read, d1)));
+        t = fe_add(t, fe_mul(S.ct[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
+        t = fe_add(t, fe_mul(S.ct[11], fe_mul(is_noop, fe_sub(s0n, s0))));
+    }
+    // 12..19 Rescue round / copy (constrains.rs:182-216)
+    {
+        const fe *per = periodic + (i & 127) * 9;
+        const fe hash_flag = per[0];
+        const fe h0 = CUR(6);
+        fe x[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
+        fe m0[4];
+#pragma unroll
+        for (int r2 = 0; r2 < 4; r2++) m0[r2] = fe_add(mds_row(r2, x), per[1 + r2]);
+        // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4  (Horner by doubling: bits are field elements)
+        fe opc = b0;
+        opc = fe_add(fe_add(opc, opc), b1);
+        opc = fe_add(fe_add(opc, opc), b2);
+        opc = fe_add(fe_add(opc, opc), b3);
+        opc = fe_add(fe_add(opc, opc), b4);
+        m0[0] = fe_add(m0[0], opc);
+        m0[1] = fe_add(m0[1], fe_mul(s0n, is_push));
+        fe hn[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hn[k] = NXT(7 + k);
+            y[k] = fe_sub(hn[k], per[5 + k]);
         }
-        // 6 mul
-        t = fe_add(t, fe_mul(K->coeff_t[6], fe_mul(is_mul, fe_sub(s0n, fe_mul(s0, CUR(13))))));
-        // 8 push / 9 read / 10 read2 / 11 noop
-        {
-            fe d1 = fe_sub(NXT(13), s0);
-            t = fe_add(t, fe_mul(K->coeff_t[8], fe_mul(is_push, d1)));
-            t = fe_add(t, fe_mul(K->coeff_t[9], fe_mul(is_read, d1)));
-            t = fe_add(t, fe_mul(K->coeff_t[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
-            t = fe_add(t, fe_mul(K->coeff_t[11], fe_mul(is_noop, fe_sub(s0n, s0))));
+        const fe fh = fe_mul(hash_flag, h0);
+        const fe nfh = fe_sub(h0, fh);  // (1 - hash_flag) * h0
+#pragma unroll
+        for (int r2 = 0; r2 < 4; r2++) {
+            fe acc = fe_zero();
+#pragma unroll
+            for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(S.inv_mds[4 * r2 + c], y[c]));
+            t = fe_add(t, fe_mul(S.ct[12 + r2], fe_mul(fe_sub(cube(acc), m0[r2]), fh)));
         }
-        // 12..19 Rescue round / copy (constrains.rs:182-216)
-        {
-            const fe *per = periodic + (i & 127) * 9;
-            const fe hash_flag = per[0];
-            const fe h0 = CUR(6);
-            fe x[4], y[4], m0[4], m1[4];
+        t = fe_add(t, fe_mul(S.ct[16], fe_mul(fe_sub(hn[0], CUR(7)), nfh)));
+        t = fe_add(t, fe_mul(S.ct[17], fe_mul(fe_sub(hn[1], CUR(8)), nfh)));
+        t = fe_add(t, fe_mul(S.ct[18], fe_mul(hn[2], nfh)));
+        t = fe_add(t, fe_mul(S.ct[19], fe_mul(hn[3], nfh)));
+    }
+    // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
+    const fe x = fe_mul(S.xr[i & 7], pow_split(wn_lo, wn_hi, i >> 3));
+    const fe xa = fe_sub(x, S.g_last2);
+    fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, S.g_last1)), S.inv_zn[i & 7]);
+    // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
+    // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
+    fe bs0 = fe_mul(S.cb[0], CUR(0));
+    bs0 = fe_add(bs0, fe_mul(S.cb[1], CUR(7)));
+    bs0 = fe_add(bs0, fe_mul(S.cb[2], CUR(8)));
+    bs0 = fe_add(bs0, fe_mul(S.cb[3], CUR(11)));
+    fe bs1 = fe_mul(S.cb[12], fe_sub(CUR(7), S.v1[0]));
+    bs1 = fe_add(bs1, fe_mul(S.cb[13], fe_sub(CUR(8), S.v1[1])));
 #pragma unroll
-            for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
-#pragma unroll
-            for (int r2 = 0; r2 < 4; r2++) {
-                fe acc = fe_zero();
-#pragma unroll
-                for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(c_mds[4 * r2 + c], x[c]));
-                m0[r2] = fe_add(acc, per[1 + r2]);
-            }
-            // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4
-            fe opc = fe_add(fe_add(fe_add(fe_add(fe_mul(b0, fe_make(16)), fe_mul(b1, fe_make(8))),
-                                          fe_mul(b2, fe_make(4))), fe_mul(b3, fe_make(2))), b4);
-            m0[0] = fe_add(m0[0], opc);
-            m0[1] = fe_add(m0[1], fe_mul(s0n, is_push));
-            fe hn[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                hn[k] = NXT(7 + k);
-                y[k] = fe_sub(hn[k], per[5 + k]);
-            }
-#pragma unroll
-            for (int r2 = 0; r2 < 4; r2++) {
-                fe acc = fe_zero();
-#pragma unroll
-                for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(c_inv_mds[4 * r2 + c], y[c]));
-                m1[r2] = cube(acc);
-            }
-            const fe fh = fe_mul(hash_flag, h0);
-            const fe nfh = fe_mul(fe_sub(one, hash_flag), h0);
-#pragma unroll
-            for (int k = 0; k < 4; k++) t = fe_add(t, fe_mul(K->coeff_t[12 + k], fe_mul(fe_sub(m1[k], m0[k]), fh)));
-            t = fe_add(t, fe_mul(K->coeff_t[16], fe_mul(fe_sub(hn[0], CUR(7)), nfh)));
-            t = fe_add(t, fe_mul(K->coeff_t[17], fe_mul(fe_sub(hn[1], CUR(8)), nfh)));
-            t = fe_add(t, fe_mul(K->coeff_t[18], fe_mul(hn[2], nfh)));
-            t = fe_add(t, fe_mul(K->coeff_t[19], fe_mul(hn[3], nfh)));
-        }
-        // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
-        const fe x = fe_mul(K->xr[i & 7], pow_split(wce_lo, wce_hi, i >> 3));
-        const fe xa = fe_sub(x, K->g_last2);
-        fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, K->g_last1)), K->inv_zn[i & 7]);
-        fe bsum0 = fe_zero(), bsum1 = fe_zero();
-#pragma unroll
-        for (int k = 0; k < 22; k++) {
-            fe d = fe_sub(CUR(K->assert_col[k]), K->assert_val[k]);
-            fe w = fe_mul(K->coeff_b[k], d);
-            if (K->assert_grp[k] == 0) bsum0 = fe_add(bsum0, w);
-            else bsum1 = fe_add(bsum1, w);
-        }
-        fe num = fe_add(fe_mul(bsum0, xa), fe_mul(bsum1, fe_sub(x, one)));
-        res = fe_add(res, fe_mul(num, inv_bd[i]));
-        comp[(i & 7) * n + (i >> 3)] = res;
+    for (int k = 0; k < 8; k++) {
+        fe c = CUR(12 + k);
+        bs0 = fe_add(bs0, fe_mul(S.cb[4 + k], c));
+        bs1 = fe_add(bs1, fe_mul(S.cb[14 + k], fe_sub(c, S.v1[2 + k])));
+    }
+    fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
+    res = fe_add(res, fe_mul(num, inv_bd[i]));
+    comp[(i & 7) * n + (i >> 3)] = res;
 #undef CUR
 #undef NXT
-    }
 }
 
 static bool g_consts_uploaded = false;
@@ -587,7 +671,6 @@ void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const
     upload_rescue(st);
     size_t CE = (size_t)8 << log_n;
     unsigned blocks = cdiv(CE, 256);
-    if (blocks > 65536) blocks = 65536;
     ZK_PROF(st, "eval_constraints", (448.0 * (log_b == 3 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL(k_eval_constraints, dim3(blocks), dim3(256), 0, st, lde, log_n,
                                                        log_b, Tce.fwd_lo, Tce.fwd_hi, periodic, inv_bd, consts_dev, comp));
 }
