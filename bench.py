@@ -57,6 +57,8 @@ def barrier(pg, local):
     if torch.cuda.is_available():
         torch.cuda.synchronize(local)
     pg.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize(local)
 
 
 def max_over_ranks(pg, value, local):
@@ -67,6 +69,19 @@ def max_over_ranks(pg, value, local):
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
+
+
+def timed_loop(step, steps: int, warmup: int, pg, local: int) -> float:
+    """W untimed warmup steps, then exactly K steps bracketed by barrier + device sync on both
+    sides; returns the max over ranks of the elapsed wall time (seconds)."""
+    for _ in range(warmup):
+        step()
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier(pg, local)
+    return max_over_ranks(pg, time.perf_counter() - t0, local)
 
 
 def cpu_baseline(log_n: int):
@@ -129,16 +144,13 @@ def main():
     gpu = GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor)
     d_trace, _ = gpu.upload_trace(trace)
 
-    for _ in range(args.warmup):
-        proof, _, _, _ = gpu.prove_device(d_trace, n, pub, opts)
+    last = {}
 
-    barrier(pg, local)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        proof, _, _, _ = gpu.prove_device(d_trace, n, pub, opts)
-    barrier(pg, local)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(pg, elapsed, local)
+    def step():
+        last["proof"] = gpu.prove_device(d_trace, n, pub, opts)[0]
+
+    elapsed = timed_loop(step, args.steps, args.warmup, pg, local)
+    proof = last["proof"]
     stages = gpu.stage_times()
 
     # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream)

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: parity tests, rocprofv3 kernel-trace stats of the bench, two PMC passes
+# (FETCH_SIZE / WRITE_SIZE, separately) -> pmc_traffic.json, then the default bench line.
+# Usage (from the repo root, via gpurun):  bash tools/gpu_profile.sh <tag> [tests|notests]
+set -eo pipefail
+TAG=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+BENCH_ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-verify"
+
+if [ "${2:-tests}" = "tests" ]; then
+  (cd "$R" && timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$O/gpu_tests_$TAG.log" 2>&1)
+  echo "gpu tests ok"
+fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o "$TAG" -- \
+  python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench_$TAG.json" 2> "$O/prof_bench_$TAG.err"
+echo "kernel trace ok"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o f -- \
+  python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_fetch_$TAG.err"
+echo "pmc fetch ok"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write_$TAG" -o w -- \
+  python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_write_$TAG.err"
+echo "pmc write ok"
+python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -o "$O/pmc_traffic_$TAG.json"
+cp "$O/pmc_traffic_$TAG.json" "$R/profiles/pmc_traffic.json"
+# keep only the summaries (the per-dispatch counter CSVs are large)
+find "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
+(cd "$R" && timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err")
+echo "bench ok"
+cat "$O/bench_$TAG.json"
