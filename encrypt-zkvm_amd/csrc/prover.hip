@@ -256,12 +256,13 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * N));
     ZK_CHECK_HIP(A.alloc(&p->inv, std::max(N, CE)));
     ZK_CHECK_HIP(A.alloc(&p->deep, N));
-    ZK_CHECK_HIP(A.alloc(&p->fri, N / 2 + 16));
+    // FRI layers: sum over layers of L/fold values and 2*L/fold digests; worst case fold = 2
+    ZK_CHECK_HIP(A.alloc(&p->fri, N + 16));
     ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * N));
     ZK_CHECK_HIP(A.alloc(&p->nodes, 32 * N));
     ZK_CHECK_HIP(A.alloc(&p->cleaves, 32 * N));
     ZK_CHECK_HIP(A.alloc(&p->cnodes, 32 * N));
-    ZK_CHECK_HIP(A.alloc(&p->fri_dig, 32 * N / 2 + 64));
+    ZK_CHECK_HIP(A.alloc(&p->fri_dig, 64 * N + 64));
     ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)64 * 1024));
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
     ZK_CHECK_HIP(A.alloc(&p->gather_out, (size_t)64 * 1024));
@@ -644,6 +645,11 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     for (size_t s = N; s > max_rem; s /= fold) nl++;
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
+    {
+        size_t tot = 0, s = N;
+        for (int l = 0; l < nl; l++) tot += (s /= fold);
+        if (tot > p->max_n * p->max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "FRI layers exceed the prover's buffers");
+    }
     std::vector<const fe *> layer_vals(nl + 1);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
@@ -754,7 +760,6 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             for (auto &path : b.plan.paths) total += path.size();
         }
         digests.resize(32 * total);
-        size_t off = 0;
         for (auto &b : qb) {
             for (int src = 0; src < 2; src++) {
                 std::vector<uint64_t> idx;
@@ -777,7 +782,6 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
                 ZK_CHECK_HIP(hipStreamSynchronize(p->st));
                 for (size_t t = 0; t < idx.size(); t++) memcpy(&digests[32 * where[t]], &got[32 * t], 32);
             }
-            off++;
         }
     }
     // values

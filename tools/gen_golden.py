@@ -35,6 +35,8 @@ CASES = [
     ("pushadd12", push_add_program(12), 2, {}),
     ("cipher8_b16_f4", cipher_mix_program(8)[0], 3, {"blowup": 16, "fri_folding": 4, "fri_rem_max_deg": 31}),
     ("cipher20", cipher_mix_program(20)[0], 4, {"num_queries": 40}),
+    ("pushadd12_f2_r7", push_add_program(12), 6, {"fri_folding": 2, "fri_rem_max_deg": 7, "num_queries": 50}),
+    ("lr_f16_r15", LR_PROGRAM, 7, {"fri_folding": 16, "fri_rem_max_deg": 15, "blowup": 32}),
 ]
 
 
