@@ -85,78 +85,72 @@ ZK_HD void mul_4x4(const uint32_t x[4], const uint32_t y[4], uint32_t r[8]) {
     }
 }
 
-// reduce the 256-bit value r[0..8) mod p
-ZK_HD fe reduce256(const uint32_t r[8]) {
-    // S = L + H*45*2^40 - H   (L = r[0..4), H = r[4..8)); 0 <= S < 2^175
-    uint32_t m[5];
-    uint64_t t = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        t = (uint64_t)r[4 + i] * 45u + (t >> 32);
-        m[i] = lo32(t);
-    }
-    m[4] = hi32(t);
-    // M << 40 as 6 limbs: limb k = (m[k-1] << 8) | (m[k-2] >> 24)
-    uint32_t s6[6];
-    s6[0] = 0;
-    s6[1] = m[0] << 8;
-    s6[2] = (m[1] << 8) | (m[0] >> 24);
-    s6[3] = (m[2] << 8) | (m[1] >> 24);
-    s6[4] = (m[3] << 8) | (m[2] >> 24);
-    s6[5] = (m[4] << 8) | (m[3] >> 24);
-    // + L
-    uint64_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        acc += (uint64_t)s6[i] + (i < 4 ? r[i] : 0u);
-        s6[i] = lo32(acc);
-        acc >>= 32;
-    }
-    // - H
-    int64_t sacc = 0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        sacc += (int64_t)s6[i] - (int64_t)(i < 4 ? r[4 + i] : 0u);
-        s6[i] = (uint32_t)sacc;
-        sacc >>= 32;  // arithmetic shift: borrow propagates as -1
-    }
-    // second fold: T = S_lo + S_hi*45*2^40 - S_hi, S_hi = s6[4] | s6[5] << 32 (< 2^47)
-    uint64_t sh = (uint64_t)s6[4] | ((uint64_t)s6[5] << 32);
-    uint64_t q = sh * 45u;                        // < 2^53
-    uint64_t add_lo = q << 40, add_hi = q >> 24;  // q * 2^40 as 128 bits
-    uint64_t lo = (uint64_t)s6[0] | ((uint64_t)s6[1] << 32);
-    uint64_t hi = (uint64_t)s6[2] | ((uint64_t)s6[3] << 32);
-    uint64_t nlo = lo + add_lo;
-    uint64_t c = nlo < lo;
-    uint64_t nhi = hi + add_hi + c;
-    uint64_t carry = (nhi < hi) | ((nhi == hi) & c);
-    // subtract S_hi
-    uint64_t blo = nlo - sh;
-    uint64_t b = nlo < sh;
-    uint64_t bhi = nhi - b;
-    carry -= (nhi < b);  // borrow out of the top cancels a carry (value stays >= 0)
-    // if carry: value = 2^128 + (bhi:blo)  ->  (bhi:blo) + C  (cannot overflow again)
-    uint64_t clo = blo + (carry ? ZK_C : 0);
-    uint64_t chi = bhi + (clo < blo);
-    // final conditional subtract: x >= p  <=>  x + C overflows 2^128
-    uint64_t ulo = clo + ZK_C;
-    uint64_t uhi = chi + (ulo < clo);
-    bool ge = uhi < chi;
-    return fe{ge ? ulo : clo, ge ? uhi : chi};
+// Reduction used by the device multiply (shared with the host so the unit test covers it).
+// With C = 2^128 - p = 0x2D00 * 2^32 - 1:  x*C = (x * 0x2D00) << 32 - x, so each fold is a short
+// multiply by the 14-bit constant K = 0x2D00 plus add/subtract carry chains:
+//   S = L - H + (H*K) << 32          (0 <= S < 2^175, computed mod 2^192)
+//   T = S_lo - S_hi + (S_hi*K) << 32 (S_hi < 2^47; T < 2^128 + 2^93, bit 128 = tc)
+// then one conditional subtract of p (add C, keep on carry).
+ZK_HD fe reduce_fold(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t r4, uint32_t r5, uint32_t r6,
+                     uint32_t r7) {
+    const uint32_t K = 0x2d00u;
+    uint64_t q = (uint64_t)r4 * K;
+    const uint32_t q0 = lo32(q);
+    q = (uint64_t)r5 * K + (q >> 32);
+    const uint32_t q1 = lo32(q);
+    q = (uint64_t)r6 * K + (q >> 32);
+    const uint32_t q2 = lo32(q);
+    q = (uint64_t)r7 * K + (q >> 32);
+    const uint32_t q3 = lo32(q), q4 = hi32(q);
+    uint32_t b, c;
+    const uint32_t d0 = __builtin_subc(r0, r4, 0u, &b);
+    const uint32_t d1 = __builtin_subc(r1, r5, b, &b);
+    const uint32_t d2 = __builtin_subc(r2, r6, b, &b);
+    const uint32_t d3 = __builtin_subc(r3, r7, b, &b);
+    const uint32_t dm = 0u - b;  // sign extension of L - H into limbs 4, 5
+    const uint32_t s1 = __builtin_addc(d1, q0, 0u, &c);
+    const uint32_t s2 = __builtin_addc(d2, q1, c, &c);
+    const uint32_t s3 = __builtin_addc(d3, q2, c, &c);
+    const uint32_t s4 = __builtin_addc(dm, q3, c, &c);
+    const uint32_t s5 = dm + q4 + c;
+    uint64_t p = (uint64_t)s4 * K;
+    const uint32_t p0 = lo32(p);
+    p = (uint64_t)s5 * K + (p >> 32);
+    const uint32_t p1 = lo32(p), p2 = hi32(p);
+    const uint32_t e0 = __builtin_subc(d0, s4, 0u, &b);
+    const uint32_t e1 = __builtin_subc(s1, s5, b, &b);
+    const uint32_t e2 = __builtin_subc(s2, 0u, b, &b);
+    const uint32_t e3 = __builtin_subc(s3, 0u, b, &b);
+    const uint32_t t0 = e0;
+    const uint32_t t1 = __builtin_addc(e1, p0, 0u, &c);
+    const uint32_t t2 = __builtin_addc(e2, p1, c, &c);
+    const uint32_t t3 = __builtin_addc(e3, p2, c, &c);
+    const uint32_t tc = c ^ b;  // T >= 0, so a borrow out always meets a carry out
+    // result = (tc | carry(T + C)) ? T + C : T
+    uint32_t cy, uc;
+    const uint32_t u0 = __builtin_addc(t0, 0xffffffffu, 0u, &cy);
+    const uint32_t u1 = __builtin_addc(t1, 0x2cffu, cy, &cy);
+    const uint32_t u2 = __builtin_addc(t2, 0u, cy, &cy);
+    const uint32_t u3 = __builtin_addc(t3, 0u, cy, &uc);
+    const uint32_t m = 0u - ((tc | uc) & 1u);
+    fe res;
+    res.lo = ((uint64_t)((u1 & m) | (t1 & ~m)) << 32) | ((u0 & m) | (t0 & ~m));
+    res.hi = ((uint64_t)((u3 & m) | (t3 & ~m)) << 32) | ((u2 & m) | (t2 & ~m));
+    return res;
 }
 
-// the device multiply (also callable on the host, for the host-side unit test)
+// the device multiply's algorithm in portable form (host unit test: schoolbook + reduce_fold)
 ZK_HD fe fe_mul_limbs(fe a, fe b) {
     uint32_t x[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
     uint32_t y[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
     uint32_t r[8];
     mul_4x4(x, y, r);
-    return reduce256(r);
+    return reduce_fold(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
 }
 
 // ---- gfx950 device multiply: product scanning with v_mad_u64_u32 hardware carry-outs ----
 // Same algorithm as fe_mul_limbs (schoolbook + two folds with C = 2^128 - p), hand-scheduled:
-// 94 VALU instructions instead of ~151 from the C formulation (DESIGN.md "Field multiply").
+// (DESIGN.md "Field multiply").
 // One column of a product-scanning multiply: a += sum x_i*y_i (64-bit); h := sum of the carry-outs
 // (h is the high word of the next column's accumulator).  All MADs first, carry-outs to distinct
 // SGPR pairs, then the carry adds: gfx950 needs 2 wait states between a VALU writing an SGPR and a
@@ -219,38 +213,7 @@ __device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
     col2(a, h, x2, y3, x3, y2);               ZK_SHIFT(a, h, r5);
     col1(a, h, x3, y3);                       ZK_SHIFT(a, h, r6);
     r7 = (uint32_t)a;
-    // S = L + H*C, C = (c0, c1) = (0xffffffff, 0x2cff).  The accumulator starts at (L0, L1); L2 and
-    // L3 join their columns as products L_k * 1 so their carries ride the same chains.
-    const uint32_t c0 = 0xffffffffu, c1 = 0x2cffu, one = 1u;
-    uint32_t s0, s1, s2, s3, s4, s5;
-    uint64_t b = (uint64_t)r0 | ((uint64_t)r1 << 32);
-    uint32_t g;
-    col1(b, g, r4, c0);                        ZK_SHIFT(b, g, s0);
-    col2(b, g, r4, c1, r5, c0);                ZK_SHIFT(b, g, s1);
-    col3(b, g, r5, c1, r6, c0, r2, one);       ZK_SHIFT(b, g, s2);
-    col3(b, g, r6, c1, r7, c0, r3, one);       ZK_SHIFT(b, g, s3);
-    col1(b, g, r7, c1);                        ZK_SHIFT(b, g, s4);
-    s5 = (uint32_t)b;
-    // T = S_lo + S_hi*C, S_hi = (s4, s5) < 2^47
-    uint64_t d = (uint64_t)s0 | ((uint64_t)s1 << 32);
-    uint32_t e, t0, t1, t2, t3;
-    col1(d, e, s4, c0);                        ZK_SHIFT(d, e, t0);
-    col2(d, e, s4, c1, s5, c0);                ZK_SHIFT(d, e, t1);
-    col2(d, e, s5, c1, s2, one);               ZK_SHIFT(d, e, t2);
-    col1(d, e, s3, one);                       ZK_SHIFT(d, e, t3);
-    uint32_t tc = (uint32_t)d;                 // bit 128 (0 or 1)
-    // result = (tc | carry(T + C)) ? T + C : T
-    uint32_t cy, u0, u1, u2, u3, uc;
-    u0 = __builtin_addc(t0, c0, 0u, &cy);
-    u1 = __builtin_addc(t1, c1, cy, &cy);
-    u2 = __builtin_addc(t2, 0u, cy, &cy);
-    u3 = __builtin_addc(t3, 0u, cy, &uc);
-    // branch-free select (one v_bfi_b32 per limb): m = all ones when T + C is the result
-    const uint32_t m = 0u - ((tc | uc) & 1u);
-    fe res;
-    res.lo = ((uint64_t)((u1 & m) | (t1 & ~m)) << 32) | ((u0 & m) | (t0 & ~m));
-    res.hi = ((uint64_t)((u3 & m) | (t3 & ~m)) << 32) | ((u2 & m) | (t2 & ~m));
-    return res;
+    return reduce_fold(r0, r1, r2, r3, r4, r5, r6, r7);
 }
 #undef ZK_SHIFT
 

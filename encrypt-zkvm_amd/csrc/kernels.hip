@@ -115,6 +115,13 @@ __device__ void lds_dft(fe *s, const fe *tw4096) {
     }
 }
 
+// XCD-aware block order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs
+// (separate L2s).  Neighbouring line groups share 128-B lines (each block reads 64-B row segments),
+// so give XCD x the contiguous range [x*G/8, (x+1)*G/8) in dispatch order.  Needs G % 8 == 0.
+__device__ __forceinline__ size_t xcd_block(size_t b, size_t G) {
+    return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+}
+
 struct NttArgs {
     const fe *in;
     fe *out;
@@ -166,7 +173,7 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a) {
     constexpr int LPB = TILE / M;
     const size_t n = (size_t)1 << a.log_n;
     const size_t n1 = n >> LOGM;
-    const size_t k1_0 = (size_t)blockIdx.x * LPB;
+    const size_t k1_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
     const size_t b = blockIdx.y;
     const fe *in = a.in + b * a.in_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
@@ -198,7 +205,7 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass2(NttArgs a) {
     constexpr int LPB = TILE / M;
     const size_t n = (size_t)1 << a.log_n;
     const size_t n2 = n >> LOGM;
-    const size_t j2_0 = (size_t)blockIdx.x * LPB;
+    const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
     const size_t b = blockIdx.y;
     const fe *in = a.in + b * a.in_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
@@ -731,36 +738,98 @@ void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T
 }
 
 // ================================================================ OOD evaluation
-constexpr int EVAL_PER_THREAD = 32;
+// One pass over every polynomial of the OOD frame: T_c(z), T_c(zg) for the trace columns and
+// H_j(z) for the composition columns.  A wave owns the coefficient chunk [base, base + 64E):
+// lane l sums c[base + l + 64e] * y^e (Horner in y = x^64, coalesced loads), scales by
+// x^(base + l) = tab_lane[l] * tab_wave[w] and the wave reduces by shuffles.  blockIdx.y picks a
+// group of OOD_GROUP polynomials so a proof launches ~5x the waves of one poly sweep.
+constexpr int OOD_GROUP = 7;
 
-__global__ void __launch_bounds__(256) k_poly_eval(const fe *polys, int log_n, fe x, fe *partials, int nblk) {
-    const size_t n = (size_t)1 << log_n;
-    const int p = blockIdx.y;
-    const fe *c = polys + (size_t)p * n;
-    __shared__ fe red[256];
-    fe acc = fe_zero();
-    const size_t per_block = (size_t)256 * EVAL_PER_THREAD;
-    for (size_t start = (size_t)blockIdx.x * per_block; start < n; start += (size_t)nblk * per_block) {
-        size_t k0 = start + (size_t)threadIdx.x * EVAL_PER_THREAD;
-        if (k0 >= n) continue;
-        fe h = fe_zero();
-        for (int e = EVAL_PER_THREAD - 1; e >= 0; e--) {
-            size_t k = k0 + e;
-            h = fe_add(fe_mul(h, x), k < n ? c[k] : fe_zero());
-        }
-        acc = fe_add(acc, fe_mul(h, fe_exp(x, (uint64_t)k0)));
+__device__ __forceinline__ fe wave_sum(fe v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        fe o;
+        o.lo = __shfl_xor(v.lo, s, 64);
+        o.hi = __shfl_xor(v.hi, s, 64);
+        v = fe_add(v, o);
     }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + s]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partials[(size_t)p * nblk + blockIdx.x] = red[0];
+    return v;
 }
 
-void poly_eval_many(hipStream_t st, const fe *polys, int npolys, int log_n, fe x, fe *partials, int nblk) {
-    ZK_PROF(st, "poly_eval", 16.0 * npolys * ((size_t)1 << log_n), hipLaunchKernelGGL(k_poly_eval, dim3(nblk, npolys), dim3(256), 0, st, polys, log_n, x, partials, nblk));
+__global__ void k_ood_tables(fe z, fe zg, uint64_t chunk, int nw, fe *tab) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 128 + 2 * nw) return;
+    fe x;
+    uint64_t e;
+    if (t < 128) {
+        x = t < 64 ? z : zg;
+        e = t & 63;
+    } else {
+        const int u = t - 128;
+        x = u < nw ? z : zg;
+        e = chunk * (uint64_t)(u < nw ? u : u - nw);
+    }
+    tab[t] = fe_exp(x, e);
+}
+
+template <int E>
+__global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const fe *cpolys, int C, size_t n,
+                                                  const fe *tab, int nw, fe *partials) {
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (gw >= nw) return;
+    const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
+    const int g = blockIdx.y;
+    const bool comp = g >= tgroups;
+    const int p0 = comp ? 0 : g * OOD_GROUP;
+    const int p1 = comp ? C : min(W, p0 + OOD_GROUP);
+    const size_t base = (size_t)gw * 64 * E + lane;
+    const fe y0 = fe_mul(tab[63], tab[1]), y1 = fe_mul(tab[127], tab[65]);  // x^64
+    const fe wz = fe_mul(tab[lane], tab[128 + gw]);
+    const fe wzg = comp ? fe_zero() : fe_mul(tab[64 + lane], tab[128 + nw + gw]);
+    for (int p = p0; p < p1; p++) {
+        const fe *c = (comp ? cpolys : tpolys) + (size_t)p * n;
+        fe v[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const size_t k = base + 64 * (size_t)e;
+            v[e] = k < n ? c[k] : fe_zero();
+        }
+        fe hz = v[E - 1];
+#pragma unroll
+        for (int e = E - 2; e >= 0; e--) hz = fe_add(fe_mul(hz, y0), v[e]);
+        hz = wave_sum(fe_mul(hz, wz));
+        if (lane == 0) partials[(size_t)(comp ? 2 * W + p : p) * nw + gw] = hz;
+        if (!comp) {
+            fe hg = v[E - 1];
+#pragma unroll
+            for (int e = E - 2; e >= 0; e--) hg = fe_add(fe_mul(hg, y1), v[e]);
+            hg = wave_sum(fe_mul(hg, wzg));
+            if (lane == 0) partials[(size_t)(W + p) * nw + gw] = hg;
+        }
+    }
+}
+
+int ood_waves(size_t n) { return (int)std::max<size_t>(1, n / 1024); }
+
+void ood_eval(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe z, fe zg, fe *tab,
+              fe *partials, fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    const int E = n >= 1024 ? 16 : std::max<int>(1, (int)(n / 64));
+    const int nw = (int)((n + 64 * E - 1) / (64 * E));
+    hipLaunchKernelGGL(k_ood_tables, dim3(cdiv(128 + 2 * nw, 256)), dim3(256), 0, st, z, zg, (uint64_t)64 * E, nw, tab);
+    const dim3 grid(cdiv(nw, 4), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
+#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, tab, nw, partials)
+    const double bytes = 16.0 * (W + C) * n;
+    switch (E) {
+        case 16: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(16)); break;
+        case 8: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(8)); break;
+        case 4: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(4)); break;
+        case 2: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(2)); break;
+        default: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(1)); break;
+    }
+#undef ZK_OOD
+    sum_partials(st, partials, 2 * W + C, nw, out);
 }
 
 __global__ void k_sum_partials(const fe *partials, int nblk, fe *out) {

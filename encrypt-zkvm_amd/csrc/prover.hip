@@ -94,7 +94,7 @@ struct zk_prover {
     fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
        *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
-    fe *partials = nullptr, *ood = nullptr, *gather_out = nullptr;
+    fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;
     unsigned *flag = nullptr;
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
@@ -263,7 +263,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->cleaves, 32 * N));
     ZK_CHECK_HIP(A.alloc(&p->cnodes, 32 * N));
     ZK_CHECK_HIP(A.alloc(&p->fri_dig, 64 * N + 64));
-    ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)64 * 1024));
+    ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)(2 * ZK_MAX_COLS + ZK_MAX_CCOLS) * ood_waves(max_n)));
+    ZK_CHECK_HIP(A.alloc(&p->ood_tab, (size_t)128 + 2 * ood_waves(max_n)));
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
     ZK_CHECK_HIP(A.alloc(&p->gather_out, (size_t)64 * 1024));
     ZK_CHECK_HIP(A.alloc(&p->gather_idx, (size_t)64 * 1024));
@@ -593,13 +594,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     fe_to_bytes(z, R.z);
     fe oz[W], ozg[W], oc[ZK_MAX_CCOLS];
     {
-        int nblk = std::max<int>(1, (int)std::min<size_t>(128, n / (256 * 32)));
-        poly_eval_many(p->st, p->polys, W, log_n, z, p->partials, nblk);
-        sum_partials(p->st, p->partials, W, nblk, p->ood);
-        poly_eval_many(p->st, p->polys, W, log_n, zg, p->partials, nblk);
-        sum_partials(p->st, p->partials, W, nblk, p->ood + W);
-        poly_eval_many(p->st, p->cpolys, C, log_n, z, p->partials, nblk);
-        sum_partials(p->st, p->partials, C, nblk, p->ood + 2 * W);
+        ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
         fe h[2 * W + ZK_MAX_CCOLS];
         ZK_CHECK_HIP(hipMemcpyAsync(h, p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));

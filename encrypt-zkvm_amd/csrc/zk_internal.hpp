@@ -119,7 +119,11 @@ void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T
 
 // ---------------------------------------------------------------- OOD / DEEP / FRI
 // out[p*2 + 0/1 ...]: evaluate `npolys` polys (n coeffs, stride n) at point x; partial sums per block
-void poly_eval_many(hipStream_t st, const fe *polys, int npolys, int log_n, fe x, fe *partials, int nblk_per_poly);
+// OOD frame in one pass: out = [T_c(z)]_W ++ [T_c(zg)]_W ++ [H_j(z)]_C.  tab: 128 + 2*ood_waves(n)
+// elements, partials: (2W + C) * ood_waves(n) elements of scratch.
+int ood_waves(size_t n);
+void ood_eval(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe z, fe zg, fe *tab,
+              fe *partials, fe *out);
 void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out);
 // DEEP over the LDE domain, natural order (consts: DeepConsts in device memory)
 struct DeepConsts {
