@@ -485,6 +485,11 @@ void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_
 __constant__ fe c_mds[16];
 __constant__ fe c_inv_mds[16];
 
+// Sequence the row loads of one section after the arithmetic of the previous one: the row pointer
+// is laundered through an empty asm that consumes `dep`, so the scheduler cannot hoist ~45 independent
+// loads to the top of the kernel (which by itself needs ~180 VGPRs and halves occupancy).
+#define ZK_SEQ(ptr, dep) asm volatile("" : "+v"(ptr) : "v"(dep))
+
 __device__ __forceinline__ fe cube(fe x) { return fe_mul(fe_mul(x, x), x); }
 
 // Rescue MDS (crypto/src/rescue.rs:197-214) as signed small integers: row r = (-a, +b, -c, +d)
@@ -506,7 +511,10 @@ struct EvalShared {
     fe g_last2, g_last1, delta;
 };
 
-__global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wn_lo,
+#ifndef ZK_EVAL_WAVES
+#define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
+#endif
+__global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wn_lo,
                                                           const fe *wn_hi, const fe *periodic, const fe *inv_bd,
                                                           const AirConsts *K, fe *comp) {
     __shared__ EvalShared S;
@@ -532,96 +540,44 @@ __global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log
     if (i >= CE) return;
     const size_t li = i << shift;
     const size_t r = li & (B - 1), q = li >> log_b, qn = (q + 1) & (n - 1);
-    const fe *cb = lde + r * n;
+    const fe *cb = lde + r * n;  // laundered by ZK_SEQ between sections
     const size_t cs = B * n;
 #define CUR(c) cb[(size_t)(c)*cs + q]
 #define NXT(c) cb[(size_t)(c)*cs + qn]
     const fe one = fe_one();
-    const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
-    const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
-             nb4 = fe_sub(one, b4);
-    // degree-5 selectors (flags.rs:45-79) with shared prefixes
-    const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
-    const fe n0_1_n2_n3 = fe_mul(n0_1_n2, nb3), n0_1_n2_3 = fe_mul(n0_1_n2, b3);
-    const fe is_add = fe_mul(n0_1_n2_n3, nb4);
-    const fe is_mul = fe_mul(n0_1_n2_n3, b4);
-    const fe is_sadd = fe_mul(n0_1_n2_3, nb4);
-    const fe is_add2 = fe_mul(n0_1_n2_3, b4);
-    const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
-    const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
-    const fe p0n3 = fe_mul(p0, nb3);
-    const fe is_push = fe_mul(p0n3, nb4);
-    const fe is_read = fe_mul(p0n3, b4);
-    const fe is_read2 = fe_mul(fe_mul(p0, b3), nb4);
-    const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
-    const fe s0 = CUR(12), s0n = NXT(12);
-    fe t, v;
-    // 0 clock
-    t = fe_mul(S.ct[0], fe_sub(NXT(0), fe_add(CUR(0), one)));
-    // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
+    const fe s0n = NXT(12);
+    fe t;
+    // 12..19 Rescue round / copy (constrains.rs:182-216) first: it needs only the opcode value and
+    // is_push from the flags, so the ten selectors below are never live across it.
     {
-        v = fe_add(fe_sub(fe_sub(NXT(11), CUR(11)), b0), b1);
-        fe d = fe_sub(is_add2, is_read2);
-        d = fe_add(d, d);
-        d = fe_add(d, d);
-        t = fe_add(t, fe_mul(S.ct[1], fe_add(v, d)));
-    }
-    // 2 shift
-    t = fe_add(t, fe_mul(S.ct[2], fe_mul(b0, b1)));
-    // 3 add, 6 mul
-    const fe s1 = CUR(13);
-    t = fe_add(t, fe_mul(S.ct[3], fe_mul(is_add, fe_sub(s0n, fe_add(s0, s1)))));
-    t = fe_add(t, fe_mul(S.ct[6], fe_mul(is_mul, fe_sub(s0n, fe_mul(s0, s1)))));
-    // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs (fhe/src/server_key.rs:89-124)
-    {
-        fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
-        for (int k = 0; k < L; k++) {
-            fe sn = NXT(12 + k);
-            fe s1k = CUR(13 + k);
-            acc4 = fe_add(acc4, fe_sub(sn, s1k));
-            acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
-            acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
-        }
-        acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
-        t = fe_add(t, fe_mul(S.ct[4], fe_mul(is_sadd, acc4)));
-        t = fe_add(t, fe_mul(S.ct[5], fe_mul(is_add2, acc5)));
-        t = fe_add(t, fe_mul(S.ct[7], fe_mul(is_smul, acc7)));
-    }
-    // 8 push / 9 read / 10 read2 / 11 noop
-    {
-        fe d1 = fe_sub(NXT(13), s0);
-        t = fe_add(t, fe_mul(S.ct[8], fe_mul(is_push, d1)));
-        t = fe_add(t, fe_mul(S.ct[9], fe_mul(is_read, d1)));
-        t = fe_add(t, fe_mul(S.ct[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
-        t = fe_add(t, fe_mul(S.ct[11], fe_mul(is_noop, fe_sub(s0n, s0))));
-    }
-    // 12..19 Rescue round / copy (constrains.rs:182-216)
-    {
-        const fe *per = periodic + (i & 127) * 9;
-        const fe hash_flag = per[0];
-        const fe h0 = CUR(6);
-        fe x[4], y[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
-        fe m0[4];
-#pragma unroll
-        for (int r2 = 0; r2 < 4; r2++) m0[r2] = fe_add(mds_row(r2, x), per[1 + r2]);
+        const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
         // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4  (Horner by doubling: bits are field elements)
         fe opc = b0;
         opc = fe_add(fe_add(opc, opc), b1);
         opc = fe_add(fe_add(opc, opc), b2);
         opc = fe_add(fe_add(opc, opc), b3);
         opc = fe_add(fe_add(opc, opc), b4);
-        m0[0] = fe_add(m0[0], opc);
-        m0[1] = fe_add(m0[1], fe_mul(s0n, is_push));
-        fe hn[4];
+        // is_push = b0 (1-b1)(1-b2)(1-b3)(1-b4)  (flags.rs)
+        const fe push_term = fe_mul(s0n, fe_mul(fe_mul(fe_mul(fe_mul(b0, fe_sub(one, b1)), fe_sub(one, b2)),
+                                                            fe_sub(one, b3)), fe_sub(one, b4)));
+        ZK_SEQ(cb, push_term.lo);
+        const fe *per = periodic + (i & 127) * 9;
+        fe x[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            hn[k] = NXT(7 + k);
-            y[k] = fe_sub(hn[k], per[5 + k]);
-        }
-        const fe fh = fe_mul(hash_flag, h0);
+        for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
+        fe m0[4];
+#pragma unroll
+        for (int r2 = 0; r2 < 4; r2++) m0[r2] = fe_add(mds_row(r2, x), per[1 + r2]);
+        m0[0] = fe_add(m0[0], opc);
+        m0[1] = fe_add(m0[1], push_term);
+        ZK_SEQ(cb, m0[3].lo);
+        const fe h0 = CUR(6);
+        const fe fh = fe_mul(per[0], h0);
         const fe nfh = fe_sub(h0, fh);  // (1 - hash_flag) * h0
+        fe y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) y[k] = fe_sub(NXT(7 + k), per[5 + k]);
+        t = fe_zero();
 #pragma unroll
         for (int r2 = 0; r2 < 4; r2++) {
             fe acc = fe_zero();
@@ -629,11 +585,77 @@ __global__ void __launch_bounds__(256) k_eval_constraints(const fe *lde, int log
             for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(S.inv_mds[4 * r2 + c], y[c]));
             t = fe_add(t, fe_mul(S.ct[12 + r2], fe_mul(fe_sub(cube(acc), m0[r2]), fh)));
         }
-        t = fe_add(t, fe_mul(S.ct[16], fe_mul(fe_sub(hn[0], CUR(7)), nfh)));
-        t = fe_add(t, fe_mul(S.ct[17], fe_mul(fe_sub(hn[1], CUR(8)), nfh)));
-        t = fe_add(t, fe_mul(S.ct[18], fe_mul(hn[2], nfh)));
-        t = fe_add(t, fe_mul(S.ct[19], fe_mul(hn[3], nfh)));
+        ZK_SEQ(cb, t.lo);
+        t = fe_add(t, fe_mul(S.ct[16], fe_mul(fe_sub(NXT(7), CUR(7)), nfh)));
+        t = fe_add(t, fe_mul(S.ct[17], fe_mul(fe_sub(NXT(8), CUR(8)), nfh)));
+        t = fe_add(t, fe_mul(S.ct[18], fe_mul(NXT(9), nfh)));
+        t = fe_add(t, fe_mul(S.ct[19], fe_mul(NXT(10), nfh)));
     }
+    ZK_SEQ(cb, t.lo);
+    // 0..11: degree-5 selectors (flags.rs:45-79) with shared prefixes, each consumed right away
+    {
+        const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
+        const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
+                 nb4 = fe_sub(one, b4);
+        const fe s0 = CUR(12), s1 = CUR(13);
+        // 0 clock, 2 shift
+        t = fe_add(t, fe_mul(S.ct[0], fe_sub(NXT(0), fe_add(CUR(0), one))));
+        t = fe_add(t, fe_mul(S.ct[2], fe_mul(b0, b1)));
+        // 11 noop
+        {
+            const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
+            t = fe_add(t, fe_mul(S.ct[11], fe_mul(is_noop, fe_sub(s0n, s0))));
+        }
+        ZK_SEQ(cb, t.lo);
+        const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
+        fe is_add2, is_read2;
+        {
+            const fe n0_1_n2_n3 = fe_mul(n0_1_n2, nb3);
+            // 3 add, 6 mul
+            t = fe_add(t, fe_mul(S.ct[3], fe_mul(fe_mul(n0_1_n2_n3, nb4), fe_sub(s0n, fe_add(s0, s1)))));
+            t = fe_add(t, fe_mul(S.ct[6], fe_mul(fe_mul(n0_1_n2_n3, b4), fe_sub(s0n, fe_mul(s0, s1)))));
+        }
+        ZK_SEQ(cb, t.lo);
+        {
+            // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs (fhe/src/server_key.rs:89-124)
+            const fe n0_1_n2_3 = fe_mul(n0_1_n2, b3);
+            const fe is_sadd = fe_mul(n0_1_n2_3, nb4);
+            is_add2 = fe_mul(n0_1_n2_3, b4);
+            const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
+            fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
+            for (int k = 0; k < L; k++) {
+                fe sn = NXT(12 + k);
+                fe s1k = CUR(13 + k);
+                acc4 = fe_add(acc4, fe_sub(sn, s1k));
+                acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
+                acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
+            }
+            acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
+            t = fe_add(t, fe_mul(S.ct[4], fe_mul(is_sadd, acc4)));
+            t = fe_add(t, fe_mul(S.ct[5], fe_mul(is_add2, acc5)));
+            t = fe_add(t, fe_mul(S.ct[7], fe_mul(is_smul, acc7)));
+        }
+        ZK_SEQ(cb, t.lo);
+        {
+            // 8 push / 9 read / 10 read2
+            const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
+            const fe p0n3 = fe_mul(p0, nb3);
+            is_read2 = fe_mul(fe_mul(p0, b3), nb4);
+            const fe d1 = fe_sub(NXT(13), s0);
+            t = fe_add(t, fe_mul(S.ct[8], fe_mul(fe_mul(p0n3, nb4), d1)));
+            t = fe_add(t, fe_mul(S.ct[9], fe_mul(fe_mul(p0n3, b4), d1)));
+            t = fe_add(t, fe_mul(S.ct[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
+        }
+        // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
+        {
+            fe v = fe_add(fe_sub(fe_sub(NXT(11), CUR(11)), b0), b1);
+            fe d = fe_sub(is_add2, is_read2);
+            d = fe_add(d, d);
+            d = fe_add(d, d);
+            t = fe_add(t, fe_mul(S.ct[1], fe_add(v, d)));
+        }
+    }
+    ZK_SEQ(cb, t.lo);
     // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
     const fe x = fe_mul(S.xr[i & 7], pow_split(wn_lo, wn_hi, i >> 3));
     const fe xa = fe_sub(x, S.g_last2);

@@ -10,7 +10,8 @@ import os
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent
-LIB_PATH = PKG_ROOT / "lib" / "libzkvm_gpu.so"
+# ZKVM_GPU_LIB selects an alternative in-tree build (A/B experiments); default lib/libzkvm_gpu.so
+LIB_PATH = Path(os.environ.get("ZKVM_GPU_LIB", PKG_ROOT / "lib" / "libzkvm_gpu.so"))
 
 ZK_OK = 0
 ZK_ERR_INVALID_ARG = -1
