@@ -26,35 +26,42 @@ ZK_HD fe fe_one() { return fe{1, 0}; }
 ZK_HD bool fe_eq(fe a, fe b) { return a.lo == b.lo && a.hi == b.hi; }
 ZK_HD bool fe_is_zero(fe a) { return (a.lo | a.hi) == 0; }
 
-// a + b mod p.  s = a + b (129 bits); s >= p  <=>  carry(a+b) or carry(s + C); then s - p = s + C.
+ZK_HD uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+ZK_HD uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+ZK_HD uint64_t join32(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// a + b mod p on 32-bit carry chains.  s = a + b (129 bits); s >= p  <=>  carry(a+b) or
+// carry(s + C), and then s - p = s + C (mod 2^128).
 ZK_HD fe fe_add(fe a, fe b) {
-    uint64_t lo = a.lo + b.lo;
-    uint64_t c0 = lo < a.lo;
-    uint64_t hi = a.hi + b.hi + c0;
-    uint64_t c1 = (hi < a.hi) | ((hi == a.hi) & c0);
-    uint64_t tlo = lo + ZK_C;
-    uint64_t t0 = tlo < lo;
-    uint64_t thi = hi + t0;
-    uint64_t c2 = (thi < hi);
-    bool wrap = c1 | c2;
-    return fe{wrap ? tlo : lo, wrap ? thi : hi};
+    uint32_t c, d, c1, c2;
+    const uint32_t s0 = __builtin_addc(lo32(a.lo), lo32(b.lo), 0u, &c);
+    const uint32_t s1 = __builtin_addc(hi32(a.lo), hi32(b.lo), c, &c);
+    const uint32_t s2 = __builtin_addc(lo32(a.hi), lo32(b.hi), c, &c);
+    const uint32_t s3 = __builtin_addc(hi32(a.hi), hi32(b.hi), c, &c1);
+    const uint32_t t0 = __builtin_addc(s0, 0xffffffffu, 0u, &d);
+    const uint32_t t1 = __builtin_addc(s1, 0x2cffu, d, &d);
+    const uint32_t t2 = __builtin_addc(s2, 0u, d, &d);
+    const uint32_t t3 = __builtin_addc(s3, 0u, d, &c2);
+    const uint32_t m = 0u - ((c1 | c2) & 1u);
+    return fe{join32((t0 & m) | (s0 & ~m), (t1 & m) | (s1 & ~m)), join32((t2 & m) | (s2 & ~m), (t3 & m) | (s3 & ~m))};
 }
 
-// a - b mod p.  On borrow the 128-bit difference d = a - b + 2^128; the result is d - C.
+// a - b mod p.  d = a - b (mod 2^128); on borrow the value is d - 2^128 = d - C - p, i.e. d - C.
 ZK_HD fe fe_sub(fe a, fe b) {
-    uint64_t lo = a.lo - b.lo;
-    uint64_t bw0 = a.lo < b.lo;
-    uint64_t hi = a.hi - b.hi - bw0;
-    bool bw = (a.hi < b.hi) | ((a.hi == b.hi) & bw0);
-    uint64_t tlo = lo - ZK_C;
-    uint64_t thi = hi - (lo < ZK_C);
-    return fe{bw ? tlo : lo, bw ? thi : hi};
+    uint32_t bw, e;
+    const uint32_t d0 = __builtin_subc(lo32(a.lo), lo32(b.lo), 0u, &bw);
+    const uint32_t d1 = __builtin_subc(hi32(a.lo), hi32(b.lo), bw, &bw);
+    const uint32_t d2 = __builtin_subc(lo32(a.hi), lo32(b.hi), bw, &bw);
+    const uint32_t d3 = __builtin_subc(hi32(a.hi), hi32(b.hi), bw, &bw);
+    const uint32_t m = 0u - (bw & 1u);
+    const uint32_t r0 = __builtin_subc(d0, m, 0u, &e);
+    const uint32_t r1 = __builtin_subc(d1, m & 0x2cffu, e, &e);
+    const uint32_t r2 = __builtin_subc(d2, 0u, e, &e);
+    const uint32_t r3 = __builtin_subc(d3, 0u, e, &e);
+    return fe{join32(r0, r1), join32(r2, r3)};
 }
 
 ZK_HD fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
-
-ZK_HD uint32_t lo32(uint64_t v) { return (uint32_t)v; }
-ZK_HD uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
 
 // r[0..8) = x[0..4) * y[0..4) (operand scanning; each step fits one v_mad_u64_u32 + carry add)
 ZK_HD void mul_4x4(const uint32_t x[4], const uint32_t y[4], uint32_t r[8]) {

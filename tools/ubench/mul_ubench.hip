@@ -52,6 +52,18 @@ __global__ void k_fadd(uint64_t *out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+__global__ void k_fsub(uint64_t *out, uint32_t seed) {
+    fe a[4], b = fe_make(threadIdx.x + seed, 12345);
+    for (int i = 0; i < 4; i++) a[i] = fe_make(i + 1, blockIdx.x);
+    for (int it = 0; it < ITERS / 4; it++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) a[i] = fe_sub(a[i], b);
+    }
+    uint64_t s = 0;
+    for (int i = 0; i < 4; i++) s ^= a[i].lo ^ a[i].hi;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <typename K>
 float timeit(K k, uint64_t *out, int blocks) {
     hipEvent_t a, b;
@@ -81,5 +93,7 @@ int main() {
     printf("fe_mul       : %.3f ms, %.2f G muls/s\n", t, lanes * (ITERS / 16) * 4 / (t * 1e6));
     t = timeit(k_fadd, out, blocks);
     printf("fe_add       : %.3f ms, %.2f G adds/s\n", t, lanes * (ITERS / 4) * 4 / (t * 1e6));
+    t = timeit(k_fsub, out, blocks);
+    printf("fe_sub       : %.3f ms, %.2f G subs/s\n", t, lanes * (ITERS / 4) * 4 / (t * 1e6));
     return 0;
 }
