@@ -34,7 +34,13 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 // Each line is loaded in bit-reversed position and transformed in place by log2(M) radix-2
 // decimation-in-time stages; the result is in natural order.  Lines are padded by one element
 // so that LPB lanes writing the same position of consecutive lines hit different banks.
-constexpr int NTT_THREADS = 512;
+#ifndef ZK_NTT_THREADS
+#define ZK_NTT_THREADS 512
+#endif
+#ifndef ZK_NTT_TILE
+#define ZK_NTT_TILE 4096
+#endif
+constexpr int NTT_THREADS = ZK_NTT_THREADS;
 
 template <int LOGM>
 __device__ __forceinline__ int lds_idx(int line, int pos) {
@@ -128,7 +134,8 @@ struct NttArgs {
     size_t in_stride, out_stride;
     const fe *tw4096;             // DFT-stage table (forward or inverse)
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
-    const fe *pre_lo, *pre_hi;    // optional pre-scale s^k
+    const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
+    const fe *pre_full;           // ... or the same from a full table (preferred when present)
     fe post;                      // post-scale constant
     int has_post;
     int log_n;
@@ -147,7 +154,8 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_single(NttArgs a, int batch) 
         fe v = fe_zero();
         if (b < batch) {
             v = a.in[(size_t)b * a.in_stride + k];
-            if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
+            if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
+            else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
         }
         s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
     }
@@ -180,7 +188,8 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a) {
         int line = e % LPB, k2 = e / LPB;
         size_t k = k1_0 + line + n1 * (size_t)k2;
         fe v = in[k];
-        if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
+        if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
+        else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
         s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
@@ -275,7 +284,7 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
 
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
          bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
-    constexpr int TILE = 4096;
+    constexpr int TILE = ZK_NTT_TILE;
     NttArgs a;
     a.in = in;
     a.out = out;
@@ -286,6 +295,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.big_hi = inverse ? T.inv_hi : T.fwd_hi;
     a.pre_lo = pre ? pre->lo : nullptr;
     a.pre_hi = pre ? pre->hi : nullptr;
+    a.pre_full = pre ? pre->full : nullptr;
     a.has_post = post_scale != nullptr;
     a.post = post_scale ? *post_scale : fe_zero();
     a.log_n = T.log_n;
@@ -304,8 +314,17 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     NttArgs a2 = a;
     a2.in = tmp;
     a2.in_stride = (size_t)1 << L;
-    a2.pre_lo = a2.pre_hi = nullptr;
+    a2.pre_lo = a2.pre_hi = a2.pre_full = nullptr;
     ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
+}
+
+__global__ void k_pow_expand(const fe *lo, const fe *hi, size_t n, fe *out) {
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x)
+        out[t] = pow_split(lo, hi, t);
+}
+
+void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out) {
+    hipLaunchKernelGGL(k_pow_expand, dim3(std::min<size_t>(cdiv(n, 256), 65536)), dim3(256), 0, st, lo, hi, n, out);
 }
 
 // ================================================================ hashing and Merkle trees
@@ -937,6 +956,15 @@ __global__ void k_coset_major_to_natural(const fe *src, int log_n, int log_b, fe
     size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = src[(i & (B - 1)) * n + (i >> log_b)];
+}
+
+__global__ void k_gather_chunks(const uint64_t *addr, size_t k, fe *out) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t < k) out[t] = *reinterpret_cast<const fe *>((uintptr_t)addr[t]);
+}
+
+void gather_chunks(hipStream_t st, const uint64_t *addr, size_t k, fe *out) {
+    if (k) ZK_PROF(st, "gather_chunks", 24.0 * k, hipLaunchKernelGGL(k_gather_chunks, dim3(cdiv(k, 256)), dim3(256), 0, st, addr, k, out));
 }
 
 __global__ void k_gather_fe(const fe *src, const uint64_t *idx, size_t k, fe *out) {

@@ -206,6 +206,9 @@ static int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
         xrN[r] = s;
         PowTable t;
         ZK_CHECK_HIP(make_pow_table(p, s, n, &t));
+        // full table for the LDE pre-scale (B * n elements: 128 MiB at n = 2^20, B = 8)
+        ZK_CHECK_HIP(p->arena.alloc(&t.full, n));
+        pow_expand(p->st, t.lo, t.hi, n, t.full);
         pl->coset.push_back(t);
         s = fe_mul(s, wN);
     }
@@ -218,6 +221,7 @@ static int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     ZK_CHECK_HIP(upload(p, &pl->xr_ce, xrce));
     ZK_CHECK_HIP(make_pow_table(p, h_inv(fe_make(3)), n, &pl->inv3));
     ZK_CHECK_HIP(upload(p, &pl->periodic, periodic_table(n)));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     *out = pl.get();
     p->plans[key] = std::move(pl);
     return ZK_OK;
@@ -266,8 +270,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)(2 * ZK_MAX_COLS + ZK_MAX_CCOLS) * ood_waves(max_n)));
     ZK_CHECK_HIP(A.alloc(&p->ood_tab, (size_t)128 + 2 * ood_waves(max_n)));
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
-    ZK_CHECK_HIP(A.alloc(&p->gather_out, (size_t)64 * 1024));
-    ZK_CHECK_HIP(A.alloc(&p->gather_idx, (size_t)64 * 1024));
+    ZK_CHECK_HIP(A.alloc(&p->gather_out, ZK_GATHER_CAP));
+    ZK_CHECK_HIP(A.alloc(&p->gather_idx, ZK_GATHER_CAP));
     ZK_CHECK_HIP(A.alloc(&p->flag, 4));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
@@ -746,62 +750,47 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     qb.push_back({p->leaves, p->nodes, plan_batch(N, pos)});
     qb.push_back({p->cleaves, p->cnodes, plan_batch(N, pos)});
     for (int l = 0; l < nl; l++) qb.push_back({layer_leaves[l], layer_nodes[l], plan_batch(layer_len[l] / fold, fri_pos[l])});
-    // digests: gather per source array
-    std::vector<uint8_t> digests;
-    {
-        size_t total = 0;
-        for (auto &b : qb) {
-            b.dig_off = total;
-            for (auto &path : b.plan.paths) total += path.size();
-        }
-        digests.resize(32 * total);
-        for (auto &b : qb) {
-            for (int src = 0; src < 2; src++) {
-                std::vector<uint64_t> idx;
-                std::vector<size_t> where;
-                size_t k = 0;
-                for (auto &path : b.plan.paths)
-                    for (auto &e : path) {
-                        if (e.first == src) {
-                            idx.push_back(e.second);
-                            where.push_back(b.dig_off + k);
-                        }
-                        k++;
-                    }
-                if (idx.empty()) continue;
-                if (idx.size() > 2048) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many digests to gather");
-                ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, p->st));
-                gather_digests(p->st, src ? b.nodes : b.leaves, p->gather_idx, idx.size(), (uint8_t *)p->gather_out);
-                std::vector<uint8_t> got(32 * idx.size());
-                ZK_CHECK_HIP(hipMemcpyAsync(got.data(), p->gather_out, got.size(), hipMemcpyDeviceToHost, p->st));
-                ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-                for (size_t t = 0; t < idx.size(); t++) memcpy(&digests[32 * where[t]], &got[32 * t], 32);
-            }
-        }
-    }
-    // values
-    std::vector<fe> trace_rows(nu * W), comp_rows(nu * C);
-    {
-        ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, pos.data(), nu * 8, hipMemcpyHostToDevice, p->st));
-        gather_rows(p->st, p->lde, W, log_n, log_b, p->gather_idx, nu, p->gather_out);
-        ZK_CHECK_HIP(hipMemcpyAsync(trace_rows.data(), p->gather_out, nu * W * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        gather_rows(p->st, p->clde, C, log_n, log_b, p->gather_idx, nu, p->gather_out);
-        ZK_CHECK_HIP(hipMemcpyAsync(comp_rows.data(), p->gather_out, nu * C * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    }
-    std::vector<std::vector<fe>> fri_rows(nl);
+    // Every value and digest the proof opens, as a list of 16-byte device chunks: one address upload,
+    // one gather kernel, one download.
+    std::vector<uint64_t> addr;
+    auto fe_at = [&](const fe *base, size_t idx) { addr.push_back((uint64_t)(uintptr_t)(base + idx)); };
+    auto row_at = [&](const fe *base, int ncols, uint64_t i) {  // coset-major LDE row i
+        for (int c = 0; c < ncols; c++) fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
+    };
+    const size_t off_trace = addr.size();
+    for (size_t q = 0; q < nu; q++) row_at(p->lde, W, pos[q]);
+    const size_t off_comp = addr.size();
+    for (size_t q = 0; q < nu; q++) row_at(p->clde, C, pos[q]);
+    std::vector<size_t> off_fri(nl);
     for (int l = 0; l < nl; l++) {
-        size_t rows = layer_len[l] / fold;
-        std::vector<uint64_t> idx;
+        off_fri[l] = addr.size();
+        const size_t rows = layer_len[l] / fold;
         for (uint64_t r : fri_pos[l])
-            for (uint32_t k = 0; k < fold; k++) idx.push_back(r + k * rows);
-        fri_rows[l].resize(idx.size());
-        ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, p->st));
-        gather_fe(p->st, layer_vals[l], p->gather_idx, idx.size(), p->gather_out);
-        ZK_CHECK_HIP(hipMemcpyAsync(fri_rows[l].data(), p->gather_out, idx.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+            for (uint32_t k = 0; k < fold; k++) fe_at(layer_vals[l], r + k * rows);
     }
+    const size_t off_dig = addr.size();
+    size_t ndig = 0;
+    for (auto &b : qb) {
+        b.dig_off = ndig;
+        for (auto &path : b.plan.paths)
+            for (auto &e : path) {
+                const uint8_t *d = (e.first ? b.nodes : b.leaves) + 32 * e.second;
+                addr.push_back((uint64_t)(uintptr_t)d);
+                addr.push_back((uint64_t)(uintptr_t)(d + 16));
+                ndig++;
+            }
+    }
+    if (addr.size() > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
+    std::vector<fe> got(addr.size());
+    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, addr.data(), addr.size() * 8, hipMemcpyHostToDevice, p->st));
+    gather_chunks(p->st, p->gather_idx, addr.size(), p->gather_out);
+    ZK_CHECK_HIP(hipMemcpyAsync(got.data(), p->gather_out, got.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    const fe *trace_rows = got.data() + off_trace, *comp_rows = got.data() + off_comp;
+    const uint8_t *digests = (const uint8_t *)(got.data() + off_dig);
+    std::vector<std::vector<fe>> fri_rows(nl);
+    for (int l = 0; l < nl; l++)
+        fri_rows[l].assign(got.begin() + off_fri[l], got.begin() + off_fri[l] + fri_pos[l].size() * fold);
     stage_mark(p, "queries");
 
     // S9: proof bytes [P13, P14]
@@ -843,8 +832,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         pf.put(paths.v.data(), paths.v.size());
     };
     pf.u8(1);
-    write_queries(trace_rows.data(), nu * W * 16, qb[0]);
-    write_queries(comp_rows.data(), nu * C * 16, qb[1]);
+    write_queries(trace_rows, nu * W * 16, qb[0]);
+    write_queries(comp_rows, nu * C * 16, qb[1]);
     pf.u16((uint16_t)(1 + 2 * W * 16));
     pf.u8(2);
     for (int c = 0; c < W; c++) {

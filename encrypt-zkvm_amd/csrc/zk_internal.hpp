@@ -66,8 +66,11 @@ struct NttTables {
 
 // A power series s^k, k < n, as split tables (s^k = lo[k & 2047] * hi[k >> 11])
 struct PowTable {
-    fe *lo = nullptr, *hi = nullptr;
+    fe *lo = nullptr, *hi = nullptr;  // s^t = lo[t & 2047] * hi[t >> 11]
+    fe *full = nullptr;               // optional s^t for every t < n (one multiply less per use)
 };
+// out[t] = lo[t & 2047] * hi[t >> 11] for t < n
+void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out);
 
 // NTT of `batch` polynomials of size 2^log_n, each at in + b*in_stride -> out + b*out_stride.
 //   inverse     : use w^-1 (no 1/n scale; fold it into post_scale)
@@ -86,6 +89,9 @@ void hash_fri_rows(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t 
 // nodes[1..nl) of a binary Merkle tree over nl leaves (nodes[nl/2..nl) = merges of leaf pairs)
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes);
 // out[k] = src[idx[k]] for 32-byte digests
+// out[t] = the 16 bytes at device address addr[t] (query openings: LDE values and Merkle digests)
+constexpr size_t ZK_GATHER_CAP = 1 << 17;
+void gather_chunks(hipStream_t st, const uint64_t *addr, size_t k, fe *out);
 void gather_digests(hipStream_t st, const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out);
 // out[q*ncols + c] = element (c, pos[q]) of a coset-major column set
 void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,
