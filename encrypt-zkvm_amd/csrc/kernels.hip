@@ -341,6 +341,8 @@ __device__ __forceinline__ void load_digest(const uint8_t *src, uint32_t h[8]) {
 }
 
 // leaf hash of natural LDE row i over a coset-major column set (K3/K5 of SURVEY 7)
+// Leaf digests of coset-major LDE rows, one thread per row.  (Fusing the bottom Merkle levels into
+// this kernel was measured: the merges are compute-bound either way and the fused form lost.)
 __global__ void __launch_bounds__(256) k_hash_rows(const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves) {
     const size_t N = (size_t)1 << (log_n + log_b);
     const size_t n = (size_t)1 << log_n;
@@ -355,11 +357,12 @@ __global__ void __launch_bounds__(256) k_hash_rows(const fe *base, int ncols, in
     }
 }
 
-void hash_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves) {
-    size_t N = (size_t)1 << (log_n + log_b);
-    unsigned blocks = cdiv(N, 256);
-    if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "hash_rows", (16.0 * ncols + 32) * N, hipLaunchKernelGGL(k_hash_rows, dim3(blocks), dim3(256), 0, st, base, ncols, log_n, log_b, leaves));
+// Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).
+void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
+                             uint8_t *nodes) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    ZK_PROF(st, "hash_rows", (16.0 * ncols + 32) * N, hipLaunchKernelGGL(k_hash_rows, dim3(cdiv(N, 256)), dim3(256), 0, st, base, ncols, log_n, log_b, leaves));
+    merkle_tree(st, leaves, N, nodes);
 }
 
 __global__ void __launch_bounds__(256) k_hash_fri_rows(const fe *layer, size_t L, int fold, uint8_t *leaves) {
@@ -371,13 +374,12 @@ __global__ void __launch_bounds__(256) k_hash_fri_rows(const fe *layer, size_t L
     }
 }
 
-void hash_fri_rows(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves) {
-    unsigned blocks = cdiv(L / fold, 256);
-    if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "hash_fri_rows", 16.0 * L + 32.0 * (L / fold), hipLaunchKernelGGL(k_hash_fri_rows, dim3(blocks), dim3(256), 0, st, layer, L, fold, leaves));
+void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes) {
+    const size_t rows = L / fold;
+    ZK_PROF(st, "hash_fri_rows", 16.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, leaves));
+    merkle_tree(st, leaves, rows, nodes);
 }
 
-// one tree level: dst[i] = merge(src[2i], src[2i+1]) for i < cnt
 __global__ void __launch_bounds__(256) k_merge_level(const uint8_t *src, uint8_t *dst, size_t cnt) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cnt; i += (size_t)gridDim.x * blockDim.x) {
         uint32_t l[8], r[8], h[8];

@@ -7,7 +7,7 @@
 //   S3 constraint evaluation           batch_inv + eval_constraints       (new_evaluator + evaluate)
 //   S4 composition poly + commit       ntt(inverse) + comp_cross + ntt + hash_rows + merkle
 //   S5 OOD frame, DEEP                 poly_eval + batch_inv + deep
-//   S6 FRI layers + remainder          hash_fri_rows + merkle + fri_fold; remainder on host
+//   S6 FRI layers + remainder          commit_fri_layer + fri_fold; remainder on host
 //   S7 grinding + query positions      host
 //   S8 openings                        gather kernels + host batch-proof assembly
 //   S9 proof bytes                     host
@@ -464,9 +464,7 @@ static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, 
 
 static int commit_rows(zk_prover *p, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves, uint8_t *nodes,
                        uint8_t root[32]) {
-    size_t N = (size_t)1 << (log_n + log_b);
-    hash_rows_coset_major(p->st, base, ncols, log_n, log_b, leaves);
-    merkle_tree(p->st, leaves, N, nodes);
+    commit_rows_coset_major(p->st, base, ncols, log_n, log_b, leaves, nodes);
     ZK_CHECK_HIP(hipMemcpyAsync(root, nodes + 32, 32, hipMemcpyDeviceToHost, p->st));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     return ZK_OK;
@@ -666,8 +664,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             layer_leaves[l] = dig;
             layer_nodes[l] = dig + 32 * rows;
             dig += 64 * rows;
-            hash_fri_rows(p->st, layer_vals[l], L, (int)fold, layer_leaves[l]);
-            merkle_tree(p->st, layer_leaves[l], rows, layer_nodes[l]);
+            commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
             ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
             ZK_CHECK_HIP(hipStreamSynchronize(p->st));
             coin.reseed(R.fri_roots[l]);

@@ -83,9 +83,11 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
 // ---------------------------------------------------------------- hashing
 // leaf[i] = BLAKE3(row i) for natural LDE index i < N = B*n of a coset-major column set:
 // element (column c, index i) lives at base[(c*B + i%B)*n + i/B].
-void hash_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves);
+// leaves (N x 32 B) and the heap-ordered Merkle tree nodes[1..N) of coset-major rows / FRI layer rows
+void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
+                             uint8_t *nodes);
 // FRI layer leaves: row r of a natural-order layer of size L (rows = L/fold): [e[r + k*L/fold]]
-void hash_fri_rows(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves);
+void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes);
 // nodes[1..nl) of a binary Merkle tree over nl leaves (nodes[nl/2..nl) = merges of leaf pairs)
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes);
 // out[k] = src[idx[k]] for 32-byte digests
