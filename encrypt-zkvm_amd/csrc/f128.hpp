@@ -206,10 +206,11 @@ __device__ __forceinline__ void col4(uint64_t &a, uint32_t &h, uint32_t x0, uint
 }
 #define ZK_SHIFT(a, h, out) do { out = (uint32_t)(a); a = ((a) >> 32) | ((uint64_t)(h) << 32); h = 0; } while (0)
 
-__device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
+// full 256-bit product r[0..8) of two 128-bit values
+__device__ __forceinline__ void mul_wide(fe A, fe Bv, uint32_t r[8]) {
     const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
     const uint32_t y0 = lo32(Bv.lo), y1 = hi32(Bv.lo), y2 = lo32(Bv.hi), y3 = hi32(Bv.hi);
-    uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+    uint32_t &r0 = r[0], &r1 = r[1], &r2 = r[2], &r3 = r[3], &r4 = r[4], &r5 = r[5], &r6 = r[6], &r7 = r[7];
     uint64_t a = (uint64_t)x0 * y0;
     uint32_t h = 0;
     ZK_SHIFT(a, h, r0);
@@ -220,9 +221,50 @@ __device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
     col2(a, h, x2, y3, x3, y2);               ZK_SHIFT(a, h, r5);
     col1(a, h, x3, y3);                       ZK_SHIFT(a, h, r6);
     r7 = (uint32_t)a;
-    return reduce_fold(r0, r1, r2, r3, r4, r5, r6, r7);
 }
 #undef ZK_SHIFT
+
+__device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
+    uint32_t r[8];
+    mul_wide(A, Bv, r);
+    return reduce_fold(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+}
+__host__ inline void mul_wide(fe a, fe b, uint32_t r[8]) {
+    const uint32_t x[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+    const uint32_t y[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+    mul_4x4(x, y, r);
+}
+
+// Lazy dot products: sum unreduced 256-bit products in 288 bits (up to 2^32 terms) and reduce once.
+// 2^256 = C^2 (mod p) with C^2 < 2^92 < p, so the top limb folds in as w8 * C^2 < 2^124.
+struct acc288 {
+    uint32_t w[9];
+};
+ZK_HD acc288 acc288_zero() { return acc288{{0, 0, 0, 0, 0, 0, 0, 0, 0}}; }
+ZK_HD void acc288_madd(acc288 &acc, fe a, fe b) {
+    uint32_t r[8], c;
+#ifdef __HIP_DEVICE_COMPILE__
+    // order the products by the accumulation chain: an unreduced product holds 8 VGPRs, and left
+    // alone the scheduler computes every product of a long sum up front
+    asm volatile("" : "+v"(a.lo), "+v"(a.hi) : "v"(acc.w[0]));
+#endif
+    mul_wide(a, b, r);
+    acc.w[0] = __builtin_addc(acc.w[0], r[0], 0u, &c);
+#pragma unroll
+    for (int k = 1; k < 8; k++) acc.w[k] = __builtin_addc(acc.w[k], r[k], c, &c);
+    acc.w[8] += c;
+}
+ZK_HD fe acc288_reduce(const acc288 &acc) {
+    const fe v = reduce_fold(acc.w[0], acc.w[1], acc.w[2], acc.w[3], acc.w[4], acc.w[5], acc.w[6], acc.w[7]);
+    // w8 * C^2 with C^2 = 2025*2^80 - 90*2^40 + 1 (92 bits), as (lo 64, hi 28) limbs
+    constexpr uint64_t C2_LO = (uint64_t)(((unsigned __int128)ZK_C * ZK_C) & ~0ULL);
+    constexpr uint64_t C2_HI = (uint64_t)(((unsigned __int128)ZK_C * ZK_C) >> 64);
+    const uint64_t t_lo = (uint64_t)lo32(C2_LO) * acc.w[8];
+    const uint64_t t_mid = (uint64_t)hi32(C2_LO) * acc.w[8] + (t_lo >> 32);
+    const uint64_t t_hi = C2_HI * acc.w[8] + (t_mid >> 32);  // < 2^60
+    const fe top = fe{(t_lo & 0xffffffffull) | (t_mid << 32), t_hi};
+    return fe_add(v, top);
+}
 
 // device and host overloads (clang resolves by target)
 __device__ __forceinline__ fe fe_mul(fe a, fe b) { return fe_mul_asm(a, b); }

@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
 #define NXT(c) cb[(size_t)(c)*cs + qn]
     const fe one = fe_one();
     const fe s0n = NXT(12);
-    fe t;
+    fe t = fe_zero();  // sum of coeff_t[k] * C_k (kept reduced: a lazy 288-bit sum here costs 130 spills)
     // 12..19 Rescue round / copy (constrains.rs:182-216) first: it needs only the opcode value and
     // is_push from the flags, so the ten selectors below are never live across it.
     {
@@ -598,12 +598,12 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
         fe y[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) y[k] = fe_sub(NXT(7 + k), per[5 + k]);
-        t = fe_zero();
 #pragma unroll
         for (int r2 = 0; r2 < 4; r2++) {
-            fe acc = fe_zero();
+            acc288 am = acc288_zero();
 #pragma unroll
-            for (int c = 0; c < 4; c++) acc = fe_add(acc, fe_mul(S.inv_mds[4 * r2 + c], y[c]));
+            for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
+            const fe acc = acc288_reduce(am);
             t = fe_add(t, fe_mul(S.ct[12 + r2], fe_mul(fe_sub(cube(acc), m0[r2]), fh)));
         }
         ZK_SEQ(cb, t.lo);
@@ -643,14 +643,17 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
             const fe is_sadd = fe_mul(n0_1_n2_3, nb4);
             is_add2 = fe_mul(n0_1_n2_3, b4);
             const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
-            fe acc4 = fe_zero(), acc5 = fe_zero(), acc7 = fe_zero();
+            // sum_k (sn_k - s1_k * s0) = sum sn_k - s0 * sum s1_k  (one multiply instead of L)
+            fe acc4 = fe_zero(), acc5 = fe_zero(), sum_sn = fe_zero(), sum_s1 = fe_zero();
             for (int k = 0; k < L; k++) {
                 fe sn = NXT(12 + k);
                 fe s1k = CUR(13 + k);
                 acc4 = fe_add(acc4, fe_sub(sn, s1k));
                 acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
-                acc7 = fe_add(acc7, fe_sub(sn, fe_mul(s1k, s0)));
+                sum_sn = fe_add(sum_sn, sn);
+                sum_s1 = fe_add(sum_s1, s1k);
             }
+            const fe acc7 = fe_sub(sum_sn, fe_mul(sum_s1, s0));
             acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
             t = fe_add(t, fe_mul(S.ct[4], fe_mul(is_sadd, acc4)));
             t = fe_add(t, fe_mul(S.ct[5], fe_mul(is_add2, acc5)));
@@ -683,18 +686,20 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, S.g_last1)), S.inv_zn[i & 7]);
     // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
     // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
-    fe bs0 = fe_mul(S.cb[0], CUR(0));
-    bs0 = fe_add(bs0, fe_mul(S.cb[1], CUR(7)));
-    bs0 = fe_add(bs0, fe_mul(S.cb[2], CUR(8)));
-    bs0 = fe_add(bs0, fe_mul(S.cb[3], CUR(11)));
-    fe bs1 = fe_mul(S.cb[12], fe_sub(CUR(7), S.v1[0]));
-    bs1 = fe_add(bs1, fe_mul(S.cb[13], fe_sub(CUR(8), S.v1[1])));
+    acc288 a0 = acc288_zero(), a1 = acc288_zero();
+    acc288_madd(a0, S.cb[0], CUR(0));
+    acc288_madd(a0, S.cb[1], CUR(7));
+    acc288_madd(a0, S.cb[2], CUR(8));
+    acc288_madd(a0, S.cb[3], CUR(11));
+    acc288_madd(a1, S.cb[12], fe_sub(CUR(7), S.v1[0]));
+    acc288_madd(a1, S.cb[13], fe_sub(CUR(8), S.v1[1]));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         fe c = CUR(12 + k);
-        bs0 = fe_add(bs0, fe_mul(S.cb[4 + k], c));
-        bs1 = fe_add(bs1, fe_mul(S.cb[14 + k], fe_sub(c, S.v1[2 + k])));
+        acc288_madd(a0, S.cb[4 + k], c);
+        acc288_madd(a1, S.cb[14 + k], fe_sub(c, S.v1[2 + k]));
     }
+    const fe bs0 = acc288_reduce(a0), bs1 = acc288_reduce(a1);
     fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
     res = fe_add(res, fe_mul(num, inv_bd[i]));
     comp[(i & 7) * n + (i >> 3)] = res;
@@ -900,12 +905,14 @@ __global__ void __launch_bounds__(256) k_deep(const fe *lde, int log_n, int log_
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
         const size_t r = i & (B - 1), q = i >> log_b;
         const fe *p = lde + r * n + q;
-        fe sT = fe_zero();
+        acc288 aT = acc288_zero();
 #pragma unroll 4
-        for (int c = 0; c < 28; c++) sT = fe_add(sT, fe_mul(D->alpha_t[c], p[(size_t)c * B * n]));
+        for (int c = 0; c < 28; c++) acc288_madd(aT, D->alpha_t[c], p[(size_t)c * B * n]);
+        const fe sT = acc288_reduce(aT);
         const fe *pc = clde + r * n + q;
-        fe sH = fe_zero();
-        for (int j = 0; j < ccols; j++) sH = fe_add(sH, fe_mul(D->alpha_c[j], pc[(size_t)j * B * n]));
+        acc288 aH = acc288_zero();
+        for (int j = 0; j < ccols; j++) acc288_madd(aH, D->alpha_c[j], pc[(size_t)j * B * n]);
+        const fe sH = acc288_reduce(aH);
         fe s1 = fe_sub(fe_add(sT, sH), D->k1);
         fe s2 = fe_sub(sT, D->k2);
         fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));

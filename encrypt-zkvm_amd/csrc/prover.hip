@@ -1003,6 +1003,13 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
 }
 
 // ---------------------------------------------------------------- diagnostics
+// Host execution of the lazy dot product (acc288: unreduced 256-bit products, one reduction)
+extern "C" void zk_diag_dot_host(const uint8_t *a, const uint8_t *b, size_t count, uint8_t *out) {
+    acc288 acc = acc288_zero();
+    for (size_t i = 0; i < count; i++) acc288_madd(acc, fe_from_bytes(a + 16 * i), fe_from_bytes(b + 16 * i));
+    fe_to_bytes(acc288_reduce(acc), out);
+}
+
 // Host execution of the exact device multiply (fe_mul_limbs) -- lets CPU tests check the GPU
 // reduction algorithm without a GPU.
 extern "C" void zk_diag_mul_limbs_host(const uint8_t *a, const uint8_t *b, uint8_t *out, size_t count) {

@@ -104,6 +104,8 @@ def lib():
         L.zk_vm_last_error.restype = C.c_char_p
         L.zk_diag_mul_limbs_host.argtypes = [vp, vp, vp, sz]
         L.zk_diag_mul_limbs_host.restype = None
+        L.zk_diag_dot_host.argtypes = [vp, vp, sz, vp]
+        L.zk_diag_dot_host.restype = None
         L.zk_diag_blake3_host.argtypes = [vp, sz, vp]
         L.zk_diag_blake3_host.restype = None
         L.zk_diag_field_op.argtypes = [i32, i32, vp, vp, vp, sz]

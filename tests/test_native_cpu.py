@@ -54,6 +54,17 @@ def test_device_mul_algorithm_on_host():
         assert r == x * y % P, (x, y)
 
 
+def test_lazy_dot_product_on_host():
+    """acc288: sums of unreduced 256-bit products with one final reduction (constraint evaluator, DEEP)."""
+    rnd = random.Random(11)
+    cases = [[P - 1] * 40, [0] * 3, edge_values()] + [[rnd.randrange(P) for _ in range(k)] for k in (1, 2, 7, 28, 300)]
+    for a in cases:
+        b = list(reversed(a)) if len(a) > 3 else a
+        out = C.create_string_buffer(16)
+        native.lib().zk_diag_dot_host(elems_bytes(a), elems_bytes(b), len(a), out)
+        assert bytes_elems(out.raw)[0] == sum(x * y for x, y in zip(a, b)) % P
+
+
 def test_host_blake3_matches_oracle(oracle):
     for n in (0, 1, 40, 63, 64, 65, 448, 1024, 1025, 2048, 4100):
         data = bytes((7 * i + 3) % 256 for i in range(n))
