@@ -253,7 +253,7 @@ static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
     size_t sh = lds_bytes<TILE>(LOGM);
     hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    ZK_PROF(st, "ntt_pass1", 32.0 * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+    ZK_PROF(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB), batch), dim3(NTT_THREADS), sh, st, a));
 }
 
 template <int LOGM, int TILE>
