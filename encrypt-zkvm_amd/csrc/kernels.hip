@@ -460,17 +460,17 @@ constexpr int INV_K = 16;
 __global__ void __launch_bounds__(256) k_batch_inv_pairs(const fe *xr, int log_b, int log_n, const fe *wlo,
                                                          const fe *whi, fe a, fe b, fe *out, size_t total_threads) {
     const size_t N = (size_t)1 << (log_n + log_b);
-    const size_t B = (size_t)1 << log_b;
+    const size_t n = (size_t)1 << log_n;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= total_threads) return;
     fe pre[INV_K];
     fe acc = fe_one();
 #pragma unroll
     for (int k = 0; k < INV_K; k++) {
-        size_t i = t + (size_t)k * total_threads;
+        size_t i = t + (size_t)k * total_threads;  // coset-major: coset i >> log_n, position i % n
         fe d = fe_one();
         if (i < N) {
-            fe x = fe_mul(xr[i & (B - 1)], pow_split(wlo, whi, i >> log_b));
+            fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (n - 1)));
             d = fe_mul(fe_sub(x, a), fe_sub(x, b));
         }
         acc = fe_mul(acc, d);
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(256) k_batch_inv_pairs(const fe *xr, int log_b
         size_t i = t + (size_t)k * total_threads;
         fe d = fe_one();
         if (i < N) {
-            fe x = fe_mul(xr[i & (B - 1)], pow_split(wlo, whi, i >> log_b));
+            fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (n - 1)));
             d = fe_mul(fe_sub(x, a), fe_sub(x, b));
         }
         fe r = k > 0 ? fe_mul(inv, pre[k - 1]) : inv;
@@ -557,10 +557,13 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     const size_t CE = n * 8;
     const size_t B = (size_t)1 << log_b;
     const int shift = log_b - 3;  // LDE steps per CE step
-    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= CE) return;
-    const size_t li = i << shift;
-    const size_t r = li & (B - 1), q = li >> log_b, qn = (q + 1) & (n - 1);
+    // thread t -> CE coset rc = t / n, position q = t % n (a wave reads 64 consecutive positions of one
+    // coset); CE step i = rc + 8q lives in LDE coset rc << shift at the same position.
+    const size_t t_id = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t_id >= CE) return;
+    const size_t rc = t_id >> log_n, q = t_id & (n - 1), qn = (q + 1) & (n - 1);
+    const size_t i = rc + 8 * q;
+    const size_t r = rc << shift;
     const fe *cb = lde + r * n;  // laundered by ZK_SEQ between sections
     const size_t cs = B * n;
 #define CUR(c) cb[(size_t)(c)*cs + q]
@@ -681,9 +684,9 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     }
     ZK_SEQ(cb, t.lo);
     // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
-    const fe x = fe_mul(S.xr[i & 7], pow_split(wn_lo, wn_hi, i >> 3));
+    const fe x = fe_mul(S.xr[rc], pow_split(wn_lo, wn_hi, q));
     const fe xa = fe_sub(x, S.g_last2);
-    fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, S.g_last1)), S.inv_zn[i & 7]);
+    fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, S.g_last1)), S.inv_zn[rc]);
     // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
     // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
     acc288 a0 = acc288_zero(), a1 = acc288_zero();
@@ -701,8 +704,8 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     }
     const fe bs0 = acc288_reduce(a0), bs1 = acc288_reduce(a1);
     fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
-    res = fe_add(res, fe_mul(num, inv_bd[i]));
-    comp[(i & 7) * n + (i >> 3)] = res;
+    res = fe_add(res, fe_mul(num, inv_bd[t_id]));  // coset-major, like comp
+    comp[t_id] = res;
 #undef CUR
 #undef NXT
 }
@@ -917,7 +920,7 @@ __global__ void __launch_bounds__(256) k_deep(const fe *lde, int log_n, int log_
         fe s2 = fe_sub(sT, D->k2);
         fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));
         fe num = fe_add(fe_mul(s1, fe_sub(x, D->zg)), fe_mul(s2, fe_sub(x, D->z)));
-        out[i] = fe_mul(num, inv_d[i]);
+        out[i] = fe_mul(num, inv_d[r * n + q]);  // inverses are coset-major
     }
 }
 

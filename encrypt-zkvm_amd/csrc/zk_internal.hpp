@@ -112,8 +112,8 @@ struct AirConsts {
     fe delta;
     int lwe_size;
 };
-// inverse of (x_i - a) * (x_i - b) for x_i = xr[i % 8] * w_n^(i / 8)-style coset points:
-// x_i = xr[i & (B-1)] * w_n^(i >> log_b), i < B*n
+// inverse of (x - a) * (x - b) over the B cosets, written coset-major: out[r*n + q] for the point
+// x = xr[r] * w_n^q (natural domain index i = r + B*q)
 void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe a, fe b,
                      fe *out);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
