@@ -23,95 +23,15 @@
 #include <string>
 #include <vector>
 
-#include "../../include/zkvm_gpu.h"
-#include "host_field.hpp"
+#include "prover_internal.hpp"
 #include "rescue_consts.hpp"
-#include "zk_internal.hpp"
 
+namespace zk {
+thread_local std::string g_err;
+}
 using namespace zk;
 
-static thread_local std::string g_err;
 const char *zk_last_error(void) { return g_err.c_str(); }
-
-#define ZK_CHECK_HIP(expr)                                                                     \
-    do {                                                                                       \
-        hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess) {                                                                \
-            g_err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #expr;         \
-            return e_ == hipErrorOutOfMemory ? ZK_ERR_OUT_OF_MEMORY : ZK_ERR_DEVICE;           \
-        }                                                                                      \
-    } while (0)
-
-#define ZK_FAIL(code, msg)   \
-    do {                     \
-        g_err = (msg);       \
-        return (code);       \
-    } while (0)
-
-static constexpr int W = ZK_TRACE_WIDTH;
-static constexpr int NUM_TCONS = 20;
-static constexpr int NUM_ASSERTS = 22;
-
-static int ilog2(size_t n) {
-    int r = 0;
-    while (((size_t)1 << r) < n) r++;
-    return r;
-}
-
-// ================================================================ device allocation helpers
-struct DeviceArena {
-    std::vector<void *> ptrs;
-    ~DeviceArena() {
-        for (void *p : ptrs) (void)hipFree(p);
-    }
-    template <typename T>
-    hipError_t alloc(T **p, size_t count) {
-        void *q = nullptr;
-        hipError_t e = hipMalloc(&q, count * sizeof(T) + 256);
-        if (e == hipSuccess) {
-            ptrs.push_back(q);
-            *p = (T *)q;
-        }
-        return e;
-    }
-};
-
-struct Plan {  // everything that depends only on (n, B)
-    int log_n = 0, log_b = 0;
-    NttTables Tn, Tce, TN;    // sizes n, 8n, B*n
-    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B
-    PowTable inv3;                // 3^-k, k < n
-    fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)
-    fe *periodic = nullptr;               // 128 x 9
-};
-
-struct zk_prover {
-    int device = 0;
-    hipStream_t st = nullptr;
-    size_t max_n = 0;
-    uint32_t max_b = 0;
-    DeviceArena arena;
-    fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
-       *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
-    uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
-    fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
-    uint64_t *gather_idx = nullptr;
-    unsigned *flag = nullptr;
-    void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
-    std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
-    std::vector<fe *> table_bufs;
-    // stage timing
-    std::vector<std::pair<const char *, hipEvent_t>> stage_ev;
-    std::vector<std::pair<const char *, float>> stage_ms;
-    // kernel stats (names / totals of the last profile)
-    std::vector<std::string> kstat_names;
-    std::vector<float> kstat_ms;
-    std::vector<int> kstat_n;
-    std::vector<double> kstat_bytes;
-    // last LDE handle bookkeeping
-    size_t last_n = 0;
-    uint32_t last_b = 0;
-};
 
 struct zk_trace_lde {
     zk_prover *p;
@@ -186,7 +106,7 @@ static std::vector<fe> periodic_table(size_t n) {
     return out;
 }
 
-static int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
+int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     auto key = std::make_pair(ilog2(n), ilog2(B));
     auto it = p->plans.find(key);
     if (it != p->plans.end()) {
@@ -296,17 +216,17 @@ int zk_prover_trace_buffer(zk_prover *p, void **d_trace) {
 }
 
 // ---------------------------------------------------------------- stage timing
-static void stage_begin(zk_prover *p) {
+void zk::stage_begin(zk_prover *p) {
     for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
     p->stage_ev.clear();
 }
-static void stage_mark(zk_prover *p, const char *name) {
+void zk::stage_mark(zk_prover *p, const char *name) {
     hipEvent_t e;
     (void)hipEventCreate(&e);
     (void)hipEventRecord(e, p->st);
     p->stage_ev.push_back({name, e});
 }
-static void stage_collect(zk_prover *p) {
+void zk::stage_collect(zk_prover *p) {
     p->stage_ms.clear();
     for (size_t i = 1; i < p->stage_ev.size(); i++) {
         float ms = 0;
@@ -333,7 +253,7 @@ int zk_prover_profile(zk_prover *p, int enable) {
     return ZK_OK;
 }
 
-static void collect_kernel_stats(zk_prover *p) {
+void zk::collect_kernel_stats(zk_prover *p) {
     KernelProfiler &P = profiler();
     if (!P.on) return;
     (void)hipStreamSynchronize(p->st);
@@ -376,26 +296,8 @@ int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, in
     return ZK_OK;
 }
 
-// ---------------------------------------------------------------- proof byte writer
-struct Bytes {
-    std::vector<uint8_t> v;
-    void put(const void *d, size_t n) {
-        const uint8_t *b = (const uint8_t *)d;
-        v.insert(v.end(), b, b + n);
-    }
-    void u8(uint8_t x) { v.push_back(x); }
-    void u16(uint16_t x) { put(&x, 2); }
-    void u32(uint32_t x) { put(&x, 4); }
-    void u64(uint64_t x) { put(&x, 8); }
-};
-
-// MerkleTree::prove_batch plan: which leaf / node digests, in serialization order [P12]
-struct BatchPlan {
-    std::vector<uint64_t> norm;                     // normalized (even, sorted, unique) leaf indexes
-    std::vector<std::vector<std::pair<int, uint64_t>>> paths;  // per path: (0 = leaf, 1 = node, index)
-};
-
-static BatchPlan plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
+// ---------------------------------------------------------------- Merkle batch openings
+BatchPlan zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
     BatchPlan bp;
     int depth = ilog2(nl);
     for (uint64_t i : idx) bp.norm.push_back(i & ~1ULL);
@@ -424,24 +326,23 @@ static BatchPlan plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
 }
 
 // ---------------------------------------------------------------- the prove path
-struct QueryBatch {  // one Merkle opening: digests come from (leaves, nodes)
-    const uint8_t *leaves, *nodes;
-    BatchPlan plan;
-    size_t dig_off = 0;  // offset into the gathered digest buffer
-};
-
-static int check_options(const zk_options *o) {
-    if (!o) return 0;
-    if (o->field_extension != 1) return 0;
-    if (o->blowup < 8 || (o->blowup & (o->blowup - 1))) return 0;
-    if (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) return 0;
-    if ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) return 0;
-    if (o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES) return 0;
-    return 1;
+// ---------------------------------------------------------------- protocol steps (host side)
+int zk::check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_options *o, const zk_pub_inputs *pub) {
+    if (!o || !pub) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (o->field_extension != 1 || o->blowup < 8 || (o->blowup & (o->blowup - 1)) ||
+        (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) ||
+        ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) || o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
+    if (n < 16 || (n & (n - 1)) || n > max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace length must be a power of two in [16, max_trace_len]");
+    if (o->blowup > max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "blowup exceeds the prover's max_blowup");
+    if (pub->lwe_size == 0 || pub->lwe_size > 5)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (enforce_add2 reads 2*lwe_size stack items, constrains.rs:129)");
+    if (o->num_queries >= n * o->blowup) ZK_FAIL(ZK_ERR_INVALID_ARG, "num_queries must be smaller than the LDE domain");
+    return ZK_OK;
 }
 
 // num_constraint_composition_columns for the ProcessorAir degrees (air/src/lib.rs:69-90) [P5]
-static int num_comp_cols(size_t n) {
+int zk::num_comp_cols(size_t n) {
     static const int base[NUM_TCONS] = {1, 5, 2, 6, 6, 6, 7, 7, 6, 6, 6, 6, 4, 7, 4, 4, 2, 2, 2, 2};
     static const int cyc[NUM_TCONS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1};
     size_t hi = 0;
@@ -450,6 +351,248 @@ static int num_comp_cols(size_t n) {
     return (int)std::max<size_t>(c, 1);
 }
 
+Coin zk::seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub) {
+    std::vector<fe> e;
+    e.push_back(fe_make((uint64_t)W << 16));
+    e.push_back(fe_make(n));
+    e.push_back(fe_make(ZK_P_LO));
+    e.push_back(fe_make(ZK_P_HI));
+    e.push_back(fe_make(((uint64_t)opt->field_extension << 16) | ((uint64_t)opt->fri_folding << 8) | opt->fri_rem_max_deg));
+    e.push_back(fe_make(opt->grinding));
+    e.push_back(fe_make(opt->blowup));
+    e.push_back(fe_make(opt->num_queries));
+    for (int i = 0; i < 2; i++) e.push_back(fe_from_bytes(pub->program_hash[i]));
+    for (int i = 0; i < 16; i++) e.push_back(fe_from_bytes(pub->stack_outputs[i]));
+    Coin coin;
+    coin.init(e);
+    return coin;
+}
+
+// assertions (air/src/lib.rs:170-195) sorted by (stride, first_step, column) [P3]; CE-coset constants
+static void air_static_consts(const zk_pub_inputs *pub, size_t n, AirConsts &K) {
+    const int log_n = ilog2(n);
+    const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+    int k = 0;
+    for (int i = 0; i < 12; i++, k++) {
+        K.assert_col[k] = first_cols[i];
+        K.assert_grp[k] = 0;
+        K.assert_val[k] = fe_zero();
+    }
+    for (int i = 0; i < 2; i++, k++) {
+        K.assert_col[k] = 7 + i;
+        K.assert_grp[k] = 1;
+        K.assert_val[k] = fe_from_bytes(pub->program_hash[i]);
+    }
+    for (int i = 0; i < 8; i++, k++) {
+        K.assert_col[k] = 12 + i;
+        K.assert_grp[k] = 1;
+        K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
+    }
+    const fe g = h_root_of_unity(log_n);
+    fe wce = h_root_of_unity(log_n + 3), x = fe_make(3);
+    for (int r = 0; r < 8; r++) {
+        K.xr[r] = x;
+        K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));  // x^n constant on CE coset r
+        x = fe_mul(x, wce);
+    }
+    K.g_last2 = h_pow(g, n - 2);
+    K.g_last1 = h_pow(g, n - 1);
+    K.delta = fe_make(pub->delta);
+    K.lwe_size = (int)pub->lwe_size;
+}
+
+void zk::draw_air_consts(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &K, zk_record &R) {
+    memset(&K, 0, sizeof K);
+    for (int k = 0; k < NUM_TCONS; k++) fe_to_bytes(K.coeff_t[k] = coin.draw(), R.coeff_t[k]);
+    for (int k = 0; k < NUM_ASSERTS; k++) fe_to_bytes(K.coeff_b[k] = coin.draw(), R.coeff_b[k]);
+    air_static_consts(pub, n, K);
+}
+
+void zk::ood_reseed(Coin &coin, const fe *h, int C, zk_record &R) {
+    for (int c = 0; c < W; c++) {
+        fe_to_bytes(h[c], R.ood_trace_z[c]);
+        fe_to_bytes(h[W + c], R.ood_trace_zg[c]);
+    }
+    for (int j = 0; j < C; j++) fe_to_bytes(h[2 * W + j], R.ood_constraints[j]);
+    uint8_t d[32];
+    hash_elems(h, 2 * W, d);  // T(z) || T(zg)
+    coin.reseed(d);
+    hash_elems(h + 2 * W, C, d);
+    coin.reseed(d);
+}
+
+DeepConsts zk::draw_deep_consts(Coin &coin, const fe *h, int C, fe z, fe zg, zk_record &R) {
+    DeepConsts D;
+    memset(&D, 0, sizeof D);
+    for (int c = 0; c < W; c++) fe_to_bytes(D.alpha_t[c] = coin.draw(), R.deep_t[c]);
+    for (int j = 0; j < C; j++) fe_to_bytes(D.alpha_c[j] = coin.draw(), R.deep_c[j]);
+    fe k1 = fe_zero(), k2 = fe_zero();
+    for (int c = 0; c < W; c++) {
+        k1 = fe_add(k1, fe_mul(D.alpha_t[c], h[c]));
+        k2 = fe_add(k2, fe_mul(D.alpha_t[c], h[W + c]));
+    }
+    for (int j = 0; j < C; j++) k1 = fe_add(k1, fe_mul(D.alpha_c[j], h[2 * W + j]));
+    D.k1 = k1;
+    D.k2 = k2;
+    D.z = z;
+    D.zg = zg;
+    return D;
+}
+
+int zk::fri_num_layers(size_t N, const zk_options *opt) {
+    const size_t max_rem = (size_t)(opt->fri_rem_max_deg + 1) * opt->blowup;
+    int nl = 0;
+    for (size_t s = N; s > max_rem; s /= opt->fri_folding) nl++;
+    return nl;
+}
+
+FoldConsts zk::fold_consts(fe alpha, uint32_t fold) {
+    FoldConsts F;
+    memset(&F, 0, sizeof F);
+    const fe zeta_inv = h_inv(h_root_of_unity(ilog2(fold)));
+    F.zinv[0] = fe_one();
+    for (uint32_t t = 1; t < 16; t++) F.zinv[t] = t < fold ? fe_mul(F.zinv[t - 1], zeta_inv) : fe_zero();
+    F.alpha = alpha;
+    F.inv_offset = h_inv(fe_make(3));
+    F.inv_fold = h_inv(fe_make(fold));
+    return F;
+}
+
+int zk::remainder_step(std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag) {
+    const size_t L = rv.size();
+    h_interp_coset(rv, fe_make(3));
+    const size_t rl = L / B;
+    for (size_t k = rl; k < L; k++)
+        if (!fe_is_zero(rv[k])) degree_flag = 1;
+    if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
+    R.remainder_len = (uint32_t)rl;
+    for (size_t k = 0; k < rl; k++) fe_to_bytes(rv[k], R.remainder[k]);
+    hash_elems(rv.data(), rl, R.remainder_commitment);
+    coin.reseed(R.remainder_commitment);
+    return ZK_OK;
+}
+
+std::vector<uint64_t> zk::grind_and_positions(Coin &coin, const zk_options *opt, size_t N, zk_record &R) {
+    uint64_t nonce = 1;
+    for (;; nonce++) {
+        uint8_t d[32];
+        Coin::merge_with_int(coin.seed, nonce, d);
+        uint64_t head;
+        memcpy(&head, d, 8);
+        unsigned tz = head ? (unsigned)__builtin_ctzll(head) : 64;
+        if (tz >= opt->grinding) break;
+    }
+    R.pow_nonce = nonce;
+    Coin::merge_with_int(coin.seed, nonce, coin.seed);
+    coin.counter = 0;
+    std::vector<uint64_t> pos;
+    for (uint32_t q = 0; q < opt->num_queries; q++) {
+        uint8_t d[32];
+        coin.next(d);
+        uint64_t v;
+        memcpy(&v, d, 8);
+        pos.push_back(v & (N - 1));
+    }
+    std::sort(pos.begin(), pos.end());
+    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    R.num_positions = (uint32_t)pos.size();
+    memcpy(R.positions, pos.data(), pos.size() * 8);
+    return pos;
+}
+
+std::vector<std::vector<uint64_t>> zk::fri_fold_positions(const std::vector<uint64_t> &pos, size_t N, uint32_t fold,
+                                                          int nl) {
+    std::vector<std::vector<uint64_t>> out(nl);
+    std::vector<uint64_t> fp = pos;
+    size_t dsz = N;
+    for (int l = 0; l < nl; l++) {
+        const size_t target = dsz / fold;
+        std::vector<uint64_t> f;
+        for (uint64_t x : fp) {
+            const uint64_t q = x % target;
+            if (std::find(f.begin(), f.end(), q) == f.end()) f.push_back(q);
+        }
+        out[l] = f;
+        fp = f;
+        dsz = target;
+    }
+    return out;
+}
+
+std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood,
+                                         const Openings &O) {
+    const int nl = (int)R.num_fri_layers;
+    const size_t nu = R.num_positions;
+    Bytes pf;
+    pf.u8(W);
+    pf.u8(0);
+    pf.u8(0);
+    pf.u8((uint8_t)ilog2(n));
+    pf.u16(0);
+    pf.u8(16);
+    pf.u64(ZK_P_LO);
+    pf.u64(ZK_P_HI);
+    pf.u8((uint8_t)opt->num_queries);
+    pf.u8((uint8_t)opt->blowup);
+    pf.u8((uint8_t)opt->grinding);
+    pf.u8((uint8_t)opt->field_extension);
+    pf.u8((uint8_t)opt->fri_folding);
+    pf.u8((uint8_t)opt->fri_rem_max_deg);
+    pf.u8((uint8_t)nu);
+    pf.u16((uint16_t)(32 * (2 + nl + 1)));
+    pf.put(R.trace_root, 32);
+    pf.put(R.constraint_root, 32);
+    for (int l = 0; l < nl; l++) pf.put(R.fri_roots[l], 32);
+    pf.put(R.remainder_commitment, 32);
+    auto write_queries = [&](const void *vals, size_t vlen, int b) {
+        Bytes paths;
+        const BatchPlan &plan = O.plans[b];
+        paths.u8((uint8_t)plan.paths.size());
+        size_t k = 0;
+        for (auto &path : plan.paths) {
+            paths.u8((uint8_t)path.size());
+            for (size_t t = 0; t < path.size(); t++, k++) paths.put(&O.digests[b][32 * k], 32);
+        }
+        pf.u32((uint32_t)vlen);
+        pf.put(vals, vlen);
+        pf.u32((uint32_t)paths.v.size());
+        pf.put(paths.v.data(), paths.v.size());
+    };
+    pf.u8(1);
+    write_queries(O.trace_rows.data(), nu * W * 16, 0);
+    write_queries(O.comp_rows.data(), nu * C * 16, 1);
+    pf.u16((uint16_t)(1 + 2 * W * 16));
+    pf.u8(2);
+    for (int c = 0; c < W; c++) {
+        pf.put(&ood[c], 16);
+        pf.put(&ood[W + c], 16);
+    }
+    pf.u16((uint16_t)(C * 16));
+    pf.put(ood + 2 * W, C * 16);
+    pf.u8((uint8_t)nl);
+    for (int l = 0; l < nl; l++) write_queries(O.fri_rows[l].data(), O.fri_rows[l].size() * 16, 2 + l);
+    pf.u16((uint16_t)(R.remainder_len * 16));
+    pf.put(R.remainder, R.remainder_len * 16);
+    pf.u8(0);
+    pf.u64(R.pow_nonce);
+    pf.u8(0);
+    return pf.v;
+}
+
+int zk::deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, uint8_t *proof_out, size_t *proof_len) {
+    int status = degree_flag ? ZK_ERR_DEGREE : ZK_OK;
+    if (degree_flag) g_err = "the trace does not satisfy ProcessorAir (composition degree check failed)";
+    if (proof_out && *proof_len >= bytes.size())
+        memcpy(proof_out, bytes.data(), bytes.size());
+    else if (status == ZK_OK) {
+        status = ZK_ERR_BUFFER_TOO_SMALL;
+        g_err = "proof buffer too small";
+    }
+    *proof_len = bytes.size();
+    return status;
+}
+
+// ---------------------------------------------------------------- the single-GPU prove path
 static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, uint32_t B) {
     const size_t N = n * B;
     fe inv_n = h_inv(fe_make(n));
@@ -482,19 +625,13 @@ static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, si
 
 int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                     uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
-    if (!p || !d_trace_v || !pub || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
-    if (!check_options(opt)) ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
-    if (n < 16 || (n & (n - 1)) || n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace length must be a power of two in [16, max_trace_len]");
-    if (opt->blowup > p->max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "blowup exceeds the prover's max_blowup");
-    if (pub->lwe_size == 0 || pub->lwe_size > 5)
-        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (enforce_add2 reads 2*lwe_size stack items, constrains.rs:129)");
+    if (!p || !d_trace_v || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B, CE = 8 * n;
-    if (opt->num_queries >= N) ZK_FAIL(ZK_ERR_INVALID_ARG, "num_queries must be smaller than the LDE domain");
     ZK_CHECK_HIP(hipSetDevice(p->device));
     Plan *pl = nullptr;
-    int rc = get_plan(p, n, B, &pl);
-    if (rc) return rc;
+    ZK_TRY(get_plan(p, n, B, &pl));
     const int log_n = pl->log_n, log_b = pl->log_b;
     const int C = num_comp_cols(n);
     if (C > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition column count exceeds 8");
@@ -510,64 +647,18 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "start");
 
     // S0: coin seed [P1]
-    Coin coin;
-    {
-        std::vector<fe> e;
-        e.push_back(fe_make((uint64_t)W << 16));
-        e.push_back(fe_make(n));
-        e.push_back(fe_make(ZK_P_LO));
-        e.push_back(fe_make(ZK_P_HI));
-        e.push_back(fe_make(((uint64_t)opt->field_extension << 16) | ((uint64_t)fold << 8) | opt->fri_rem_max_deg));
-        e.push_back(fe_make(opt->grinding));
-        e.push_back(fe_make(B));
-        e.push_back(fe_make(opt->num_queries));
-        for (int i = 0; i < 2; i++) e.push_back(fe_from_bytes(pub->program_hash[i]));
-        for (int i = 0; i < 16; i++) e.push_back(fe_from_bytes(pub->stack_outputs[i]));
-        coin.init(e);
-    }
+    Coin coin = seed_coin(n, opt, pub);
 
     // S2: trace LDE + commitment
-    if ((rc = trace_lde_stage(p, pl, d_trace, n, B))) return rc;
+    ZK_TRY(trace_lde_stage(p, pl, d_trace, n, B));
     stage_mark(p, "trace_lde");
-    if ((rc = commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root))) return rc;
+    ZK_TRY(commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root));
     stage_mark(p, "trace_commit");
     coin.reseed(R.trace_root);
 
     // S3: constraint composition coefficients [P4] and evaluation over the CE domain
     AirConsts K;
-    memset(&K, 0, sizeof K);
-    for (int k = 0; k < NUM_TCONS; k++) fe_to_bytes(K.coeff_t[k] = coin.draw(), R.coeff_t[k]);
-    for (int k = 0; k < NUM_ASSERTS; k++) fe_to_bytes(K.coeff_b[k] = coin.draw(), R.coeff_b[k]);
-    {
-        // assertions sorted by (stride, first_step, column) [P3]
-        const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
-        int k = 0;
-        for (int i = 0; i < 12; i++, k++) {
-            K.assert_col[k] = first_cols[i];
-            K.assert_grp[k] = 0;
-            K.assert_val[k] = fe_zero();
-        }
-        for (int i = 0; i < 2; i++, k++) {
-            K.assert_col[k] = 7 + i;
-            K.assert_grp[k] = 1;
-            K.assert_val[k] = fe_from_bytes(pub->program_hash[i]);
-        }
-        for (int i = 0; i < 8; i++, k++) {
-            K.assert_col[k] = 12 + i;
-            K.assert_grp[k] = 1;
-            K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
-        }
-        fe wce = h_root_of_unity(log_n + 3), x = three;
-        for (int r = 0; r < 8; r++) {
-            K.xr[r] = x;
-            K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));  // x^n constant on CE coset r
-            x = fe_mul(x, wce);
-        }
-        K.g_last2 = h_pow(g, n - 2);
-        K.g_last1 = h_pow(g, n - 1);
-        K.delta = fe_make(pub->delta);
-        K.lwe_size = (int)pub->lwe_size;
-    }
+    draw_air_consts(coin, pub, n, K, R);
     ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
     batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), K.g_last2, p->inv);
     eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->air_consts,
@@ -577,59 +668,27 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit
     ntt(p->st, pl->Tn, p->comp, n, p->ctmp, n, 8, true, nullptr, nullptr, p->tmp);
     ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
-    {
-        fe scale = h_inv(fe_make(CE));
-        fe w8inv = h_inv(h_root_of_unity(3));
-        fe inv3n = h_inv(h_pow(three, n));
-        comp_cross_coset(p->st, p->ctmp, log_n, pl->Tce, pl->inv3, scale, w8inv, inv3n, C, p->cpolys, p->flag);
-    }
+    comp_cross_coset(p->st, p->ctmp, log_n, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
+                     h_inv(h_pow(three, n)), C, p->cpolys, p->flag);
     for (uint32_t r = 0; r < B; r++)
         ntt(p->st, pl->Tn, p->cpolys, n, p->clde + r * n, B * n, C, false, &pl->coset[r], nullptr, p->tmp);
-    if ((rc = commit_rows(p, p->clde, C, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root))) return rc;
+    ZK_TRY(commit_rows(p, p->clde, C, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
     ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
     coin.reseed(R.constraint_root);
 
-    // S5: OOD frame [P7]
-    fe z = coin.draw(), zg = fe_mul(z, g);
+    // S5: OOD frame [P7], DEEP coefficients [P8] and evaluations
+    const fe z = coin.draw(), zg = fe_mul(z, g);
     fe_to_bytes(z, R.z);
-    fe oz[W], ozg[W], oc[ZK_MAX_CCOLS];
-    {
-        ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
-        fe h[2 * W + ZK_MAX_CCOLS];
-        ZK_CHECK_HIP(hipMemcpyAsync(h, p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        for (int c = 0; c < W; c++) {
-            oz[c] = h[c];
-            ozg[c] = h[W + c];
-            fe_to_bytes(oz[c], R.ood_trace_z[c]);
-            fe_to_bytes(ozg[c], R.ood_trace_zg[c]);
-        }
-        for (int j = 0; j < C; j++) fe_to_bytes(oc[j] = h[2 * W + j], R.ood_constraints[j]);
-        uint8_t d[32];
-        hash_elems(h, 2 * W, d);  // T(z) || T(zg)
-        coin.reseed(d);
-        hash_elems(oc, C, d);
-        coin.reseed(d);
-    }
+    fe h[2 * W + ZK_MAX_CCOLS];
+    ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
+    ZK_CHECK_HIP(hipMemcpyAsync(h, p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    ood_reseed(coin, h, C, R);
     stage_mark(p, "ood");
-    // DEEP coefficients [P8] and evaluations
     {
-        DeepConsts D;
-        memset(&D, 0, sizeof D);
-        for (int c = 0; c < W; c++) fe_to_bytes(D.alpha_t[c] = coin.draw(), R.deep_t[c]);
-        for (int j = 0; j < C; j++) fe_to_bytes(D.alpha_c[j] = coin.draw(), R.deep_c[j]);
-        fe k1 = fe_zero(), k2 = fe_zero();
-        for (int c = 0; c < W; c++) {
-            k1 = fe_add(k1, fe_mul(D.alpha_t[c], oz[c]));
-            k2 = fe_add(k2, fe_mul(D.alpha_t[c], ozg[c]));
-        }
-        for (int j = 0; j < C; j++) k1 = fe_add(k1, fe_mul(D.alpha_c[j], oc[j]));
-        D.k1 = k1;
-        D.k2 = k2;
-        D.z = z;
-        D.zg = zg;
+        const DeepConsts D = draw_deep_consts(coin, h, C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         batch_inv_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
         deep_eval_launch(p->st, p->lde, log_n, log_b, p->clde, C, p->deep_consts, pl->TN, three, p->inv, p->deep);
@@ -637,9 +696,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "deep");
 
     // S6: FRI [P9, P10]
-    size_t max_rem = (size_t)(opt->fri_rem_max_deg + 1) * B;
-    int nl = 0;
-    for (size_t s = N; s > max_rem; s /= fold) nl++;
+    const int nl = fri_num_layers(N, opt);
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
     {
@@ -650,17 +707,13 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     std::vector<const fe *> layer_vals(nl + 1);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
+    layer_vals[0] = p->deep;
+    layer_len[0] = N;
     {
-        layer_vals[0] = p->deep;
-        layer_len[0] = N;
         fe *next = p->fri;
         uint8_t *dig = p->fri_dig;
-        fe zinv[16];
-        fe zeta_inv = h_inv(h_root_of_unity(ilog2(fold)));
-        zinv[0] = fe_one();
-        for (uint32_t t = 1; t < 16; t++) zinv[t] = t < fold ? fe_mul(zinv[t - 1], zeta_inv) : fe_zero();
         for (int l = 0; l < nl; l++) {
-            size_t L = layer_len[l], rows = L / fold;
+            const size_t L = layer_len[l], rows = L / fold;
             layer_leaves[l] = dig;
             layer_nodes[l] = dig + 32 * rows;
             dig += 64 * rows;
@@ -668,113 +721,54 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
             ZK_CHECK_HIP(hipStreamSynchronize(p->st));
             coin.reseed(R.fri_roots[l]);
-            fe alpha = coin.draw();
+            const fe alpha = coin.draw();
             fe_to_bytes(alpha, R.fri_alphas[l]);
-            FoldConsts F;
-            memcpy(F.zinv, zinv, sizeof zinv);
-            F.alpha = alpha;
-            F.inv_offset = h_inv(three);
-            F.inv_fold = h_inv(fe_make(fold));
+            const FoldConsts F = fold_consts(alpha, fold);
             ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
             fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
             layer_vals[l + 1] = next;
             layer_len[l + 1] = rows;
             next += rows;
         }
-        // remainder: interpolate the last layer over 3 * <w_L>, keep L / blowup coefficients
-        size_t L = layer_len[nl];
-        std::vector<fe> rv(L);
-        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], L * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        std::vector<fe> rv(layer_len[nl]);
+        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        h_interp_coset(rv, three);
-        size_t rl = L / B;
-        for (size_t k = rl; k < L; k++)
-            if (!fe_is_zero(rv[k])) degree_flag = 1;
-        R.remainder_len = (uint32_t)rl;
-        if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
-        for (size_t k = 0; k < rl; k++) fe_to_bytes(rv[k], R.remainder[k]);
-        hash_elems(rv.data(), rl, R.remainder_commitment);
-        coin.reseed(R.remainder_commitment);
+        ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
     }
     stage_mark(p, "fri");
 
-    // S7: grinding and query positions [P11]
-    uint64_t nonce = 1;
-    for (;; nonce++) {
-        uint8_t d[32];
-        Coin::merge_with_int(coin.seed, nonce, d);
-        uint64_t head;
-        memcpy(&head, d, 8);
-        unsigned tz = head ? (unsigned)__builtin_ctzll(head) : 64;
-        if (tz >= opt->grinding) break;
-    }
-    R.pow_nonce = nonce;
-    Coin::merge_with_int(coin.seed, nonce, coin.seed);
-    coin.counter = 0;
-    std::vector<uint64_t> pos;
-    for (uint32_t q = 0; q < opt->num_queries; q++) {
-        uint8_t d[32];
-        coin.next(d);
-        uint64_t v;
-        memcpy(&v, d, 8);
-        pos.push_back(v & (N - 1));
-    }
-    std::sort(pos.begin(), pos.end());
-    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    // S7: grinding and query positions [P10, P11]
+    const std::vector<uint64_t> pos = grind_and_positions(coin, opt, N, R);
     const size_t nu = pos.size();
-    R.num_positions = (uint32_t)nu;
-    memcpy(R.positions, pos.data(), nu * 8);
+    const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
 
-    // S8: openings -- one gather pass for every value and digest the proof needs
-    std::vector<uint64_t> fe_idx_trace, fe_idx_comp;  // handled by gather_rows
-    std::vector<std::vector<uint64_t>> fri_pos(nl);
-    {
-        std::vector<uint64_t> fp = pos;
-        size_t dsz = N;
-        for (int l = 0; l < nl; l++) {
-            size_t target = dsz / fold;
-            std::vector<uint64_t> f;
-            for (uint64_t x : fp) {
-                uint64_t q = x % target;
-                if (std::find(f.begin(), f.end(), q) == f.end()) f.push_back(q);
-            }
-            fri_pos[l] = f;
-            fp = f;
-            dsz = target;
-        }
-    }
-    std::vector<QueryBatch> qb;
-    qb.push_back({p->leaves, p->nodes, plan_batch(N, pos)});
-    qb.push_back({p->cleaves, p->cnodes, plan_batch(N, pos)});
-    for (int l = 0; l < nl; l++) qb.push_back({layer_leaves[l], layer_nodes[l], plan_batch(layer_len[l] / fold, fri_pos[l])});
-    // Every value and digest the proof opens, as a list of 16-byte device chunks: one address upload,
-    // one gather kernel, one download.
+    // S8: openings.  Every value and digest the proof opens, as a list of 16-byte device chunks: one
+    // address upload, one gather kernel, one download.
+    Openings O;
+    O.plans.push_back(plan_batch(N, pos));
+    O.plans.push_back(plan_batch(N, pos));
+    for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(layer_len[l] / fold, fri_pos[l]));
     std::vector<uint64_t> addr;
     auto fe_at = [&](const fe *base, size_t idx) { addr.push_back((uint64_t)(uintptr_t)(base + idx)); };
     auto row_at = [&](const fe *base, int ncols, uint64_t i) {  // coset-major LDE row i
         for (int c = 0; c < ncols; c++) fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
     };
-    const size_t off_trace = addr.size();
     for (size_t q = 0; q < nu; q++) row_at(p->lde, W, pos[q]);
-    const size_t off_comp = addr.size();
     for (size_t q = 0; q < nu; q++) row_at(p->clde, C, pos[q]);
-    std::vector<size_t> off_fri(nl);
     for (int l = 0; l < nl; l++) {
-        off_fri[l] = addr.size();
         const size_t rows = layer_len[l] / fold;
         for (uint64_t r : fri_pos[l])
             for (uint32_t k = 0; k < fold; k++) fe_at(layer_vals[l], r + k * rows);
     }
     const size_t off_dig = addr.size();
-    size_t ndig = 0;
-    for (auto &b : qb) {
-        b.dig_off = ndig;
-        for (auto &path : b.plan.paths)
+    for (int b = 0; b < 2 + nl; b++) {
+        const uint8_t *lv = b == 0 ? p->leaves : b == 1 ? p->cleaves : layer_leaves[b - 2];
+        const uint8_t *nd = b == 0 ? p->nodes : b == 1 ? p->cnodes : layer_nodes[b - 2];
+        for (auto &path : O.plans[b].paths)
             for (auto &e : path) {
-                const uint8_t *d = (e.first ? b.nodes : b.leaves) + 32 * e.second;
+                const uint8_t *d = (e.first ? nd : lv) + 32 * e.second;
                 addr.push_back((uint64_t)(uintptr_t)d);
                 addr.push_back((uint64_t)(uintptr_t)(d + 16));
-                ndig++;
             }
     }
     if (addr.size() > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
@@ -783,69 +777,27 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     gather_chunks(p->st, p->gather_idx, addr.size(), p->gather_out);
     ZK_CHECK_HIP(hipMemcpyAsync(got.data(), p->gather_out, got.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    const fe *trace_rows = got.data() + off_trace, *comp_rows = got.data() + off_comp;
-    const uint8_t *digests = (const uint8_t *)(got.data() + off_dig);
-    std::vector<std::vector<fe>> fri_rows(nl);
-    for (int l = 0; l < nl; l++)
-        fri_rows[l].assign(got.begin() + off_fri[l], got.begin() + off_fri[l] + fri_pos[l].size() * fold);
+    {
+        size_t off = 0;
+        O.trace_rows.assign(got.begin(), got.begin() + nu * W);
+        off += nu * W;
+        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * C);
+        off += nu * C;
+        for (int l = 0; l < nl; l++) {
+            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold);
+            off += fri_pos[l].size() * fold;
+        }
+        const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
+        for (int b = 0; b < 2 + nl; b++) {
+            const size_t bytes = 32 * O.plans[b].count();
+            O.digests.emplace_back(dg, dg + bytes);
+            dg += bytes;
+        }
+    }
     stage_mark(p, "queries");
 
     // S9: proof bytes [P13, P14]
-    Bytes pf;
-    pf.u8(W);
-    pf.u8(0);
-    pf.u8(0);
-    pf.u8((uint8_t)log_n);
-    pf.u16(0);
-    pf.u8(16);
-    pf.u64(ZK_P_LO);
-    pf.u64(ZK_P_HI);
-    pf.u8((uint8_t)opt->num_queries);
-    pf.u8((uint8_t)B);
-    pf.u8((uint8_t)opt->grinding);
-    pf.u8((uint8_t)opt->field_extension);
-    pf.u8((uint8_t)fold);
-    pf.u8((uint8_t)opt->fri_rem_max_deg);
-    pf.u8((uint8_t)nu);
-    pf.u16((uint16_t)(32 * (2 + nl + 1)));
-    pf.put(R.trace_root, 32);
-    pf.put(R.constraint_root, 32);
-    for (int l = 0; l < nl; l++) pf.put(R.fri_roots[l], 32);
-    pf.put(R.remainder_commitment, 32);
-    auto write_paths = [&](const QueryBatch &b, Bytes &out) {
-        out.u8((uint8_t)b.plan.paths.size());
-        size_t k = 0;
-        for (auto &path : b.plan.paths) {
-            out.u8((uint8_t)path.size());
-            for (size_t t = 0; t < path.size(); t++, k++) out.put(&digests[32 * (b.dig_off + k)], 32);
-        }
-    };
-    auto write_queries = [&](const void *vals, size_t vlen, const QueryBatch &b) {
-        Bytes paths;
-        write_paths(b, paths);
-        pf.u32((uint32_t)vlen);
-        pf.put(vals, vlen);
-        pf.u32((uint32_t)paths.v.size());
-        pf.put(paths.v.data(), paths.v.size());
-    };
-    pf.u8(1);
-    write_queries(trace_rows, nu * W * 16, qb[0]);
-    write_queries(comp_rows, nu * C * 16, qb[1]);
-    pf.u16((uint16_t)(1 + 2 * W * 16));
-    pf.u8(2);
-    for (int c = 0; c < W; c++) {
-        pf.put(&oz[c], 16);
-        pf.put(&ozg[c], 16);
-    }
-    pf.u16((uint16_t)(C * 16));
-    pf.put(oc, C * 16);
-    pf.u8((uint8_t)nl);
-    for (int l = 0; l < nl; l++) write_queries(fri_rows[l].data(), fri_rows[l].size() * 16, qb[2 + l]);
-    pf.u16((uint16_t)(R.remainder_len * 16));
-    pf.put(R.remainder, R.remainder_len * 16);
-    pf.u8(0);
-    pf.u64(nonce);
-    pf.u8(0);
+    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h, O);
     stage_mark(p, "serialize");
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     stage_collect(p);
@@ -863,18 +815,9 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         if (dump->fri_layer1 && nl > 0)
             ZK_CHECK_HIP(hipMemcpy(dump->fri_layer1, layer_vals[1], layer_len[1] * 16, hipMemcpyDeviceToHost));
     }
-    int status = degree_flag ? ZK_ERR_DEGREE : ZK_OK;
-    if (degree_flag) g_err = "the trace does not satisfy ProcessorAir (composition degree check failed)";
-    if (proof_out && *proof_len >= pf.v.size())
-        memcpy(proof_out, pf.v.data(), pf.v.size());
-    else if (status == ZK_OK) {
-        status = ZK_ERR_BUFFER_TOO_SMALL;
-        g_err = "proof buffer too small";
-    }
-    *proof_len = pf.v.size();
     p->last_n = n;
     p->last_b = B;
-    return status;
+    return deliver_proof(bytes, degree_flag, proof_out, proof_len);
 }
 
 int zk_prove(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
@@ -965,34 +908,11 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
     Plan *pl;
     int rc = get_plan(p, n, h->B, &pl);
     if (rc) return rc;
-    const fe g = h_root_of_unity(pl->log_n);
     AirConsts K;
     memset(&K, 0, sizeof K);
     for (int k = 0; k < NUM_TCONS; k++) K.coeff_t[k] = fe_from_bytes(coeff_t + 16 * k);
     for (int k = 0; k < NUM_ASSERTS; k++) K.coeff_b[k] = fe_from_bytes(coeff_b + 16 * k);
-    const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
-    int k = 0;
-    for (int i = 0; i < 12; i++, k++) K.assert_col[k] = first_cols[i];
-    for (int i = 0; i < 2; i++, k++) {
-        K.assert_col[k] = 7 + i;
-        K.assert_grp[k] = 1;
-        K.assert_val[k] = fe_from_bytes(pub->program_hash[i]);
-    }
-    for (int i = 0; i < 8; i++, k++) {
-        K.assert_col[k] = 12 + i;
-        K.assert_grp[k] = 1;
-        K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
-    }
-    fe wce = h_root_of_unity(pl->log_n + 3), x = fe_make(3);
-    for (int r = 0; r < 8; r++) {
-        K.xr[r] = x;
-        K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));
-        x = fe_mul(x, wce);
-    }
-    K.g_last2 = h_pow(g, n - 2);
-    K.g_last1 = h_pow(g, n - 1);
-    K.delta = fe_make(pub->delta);
-    K.lwe_size = (int)pub->lwe_size;
+    air_static_consts(pub, n, K);
     ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
     batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, fe_one(), K.g_last2, p->inv);
     eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->Tn, pl->periodic, p->inv,

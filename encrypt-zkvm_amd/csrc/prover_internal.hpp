@@ -1,0 +1,177 @@
+// prover_internal.hpp -- host-side state and protocol steps shared by the single-GPU prover
+// (prover.hip) and the coset-sharded multi-GPU prover (shard.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/zkvm_gpu.h"
+#include "host_field.hpp"
+#include "zk_internal.hpp"
+
+namespace zk {
+
+extern thread_local std::string g_err;
+
+#define ZK_CHECK_HIP(expr)                                                                     \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            ::zk::g_err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #expr;   \
+            return e_ == hipErrorOutOfMemory ? ZK_ERR_OUT_OF_MEMORY : ZK_ERR_DEVICE;           \
+        }                                                                                      \
+    } while (0)
+
+#define ZK_FAIL(code, msg)    \
+    do {                      \
+        ::zk::g_err = (msg);  \
+        return (code);        \
+    } while (0)
+
+#define ZK_TRY(expr)                 \
+    do {                             \
+        int rc_ = (expr);            \
+        if (rc_ != ZK_OK) return rc_; \
+    } while (0)
+
+static constexpr int W = ZK_TRACE_WIDTH;
+static constexpr int NUM_TCONS = 20;
+static constexpr int NUM_ASSERTS = 22;
+
+inline int ilog2(size_t n) {
+    int r = 0;
+    while (((size_t)1 << r) < n) r++;
+    return r;
+}
+
+// ---------------------------------------------------------------- device state
+struct DeviceArena {
+    std::vector<void *> ptrs;
+    ~DeviceArena() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t alloc(T **p, size_t count) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, count * sizeof(T) + 256);
+        if (e == hipSuccess) {
+            ptrs.push_back(q);
+            *p = (T *)q;
+        }
+        return e;
+    }
+};
+
+struct Plan {  // everything that depends only on (n, B)
+    int log_n = 0, log_b = 0;
+    NttTables Tn, Tce, TN;        // sizes n, 8n, B*n
+    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B
+    PowTable inv3;                // 3^-k, k < n
+    fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)
+    fe *periodic = nullptr;               // 128 x 9
+};
+
+}  // namespace zk
+
+struct zk_prover {
+    int device = 0;
+    hipStream_t st = nullptr;
+    size_t max_n = 0;
+    uint32_t max_b = 0;
+    zk::DeviceArena arena;
+    fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
+       *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
+    uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
+    fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
+    uint64_t *gather_idx = nullptr;
+    unsigned *flag = nullptr;
+    void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
+    std::map<std::pair<int, int>, std::unique_ptr<zk::Plan>> plans;
+    // stage timing
+    std::vector<std::pair<const char *, hipEvent_t>> stage_ev;
+    std::vector<std::pair<const char *, float>> stage_ms;
+    // kernel stats (names / totals of the last profile)
+    std::vector<std::string> kstat_names;
+    std::vector<float> kstat_ms;
+    std::vector<int> kstat_n;
+    std::vector<double> kstat_bytes;
+    size_t last_n = 0;
+    uint32_t last_b = 0;
+};
+
+namespace zk {
+
+int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out);
+void stage_begin(zk_prover *p);
+void stage_mark(zk_prover *p, const char *name);
+void stage_collect(zk_prover *p);
+void collect_kernel_stats(zk_prover *p);
+
+// ---------------------------------------------------------------- proof bytes and Merkle openings
+struct Bytes {
+    std::vector<uint8_t> v;
+    void put(const void *d, size_t n) {
+        const uint8_t *b = (const uint8_t *)d;
+        v.insert(v.end(), b, b + n);
+    }
+    void u8(uint8_t x) { v.push_back(x); }
+    void u16(uint16_t x) { put(&x, 2); }
+    void u32(uint32_t x) { put(&x, 4); }
+    void u64(uint64_t x) { put(&x, 8); }
+};
+
+// MerkleTree::prove_batch plan: which leaf / node digests, in serialization order [P12]
+struct BatchPlan {
+    std::vector<uint64_t> norm;                                // normalized (even, sorted, unique) leaf indexes
+    std::vector<std::vector<std::pair<int, uint64_t>>> paths;  // per path: (0 = leaf, 1 = node, index)
+    size_t count() const {
+        size_t k = 0;
+        for (auto &p : paths) k += p.size();
+        return k;
+    }
+};
+BatchPlan plan_batch(size_t nl, const std::vector<uint64_t> &idx);
+
+// ---------------------------------------------------------------- protocol steps (host side)
+// argument checks shared by every prove entry point; returns ZK_OK or a status (g_err set)
+int check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_options *opt, const zk_pub_inputs *pub);
+// num_constraint_composition_columns for the ProcessorAir degrees [P5]
+int num_comp_cols(size_t n);
+// S0: public coin seeded with Context::to_elements || PublicInputs::to_elements [P1]
+Coin seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub);
+// S3: composition coefficients (20 transition, 22 boundary) and the evaluator's constants [P3, P4]
+void draw_air_consts(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &K, zk_record &R);
+// S5: record the OOD frame h = T(z) || T(zg) || H(z) and reseed the coin with its two hashes [P7]
+void ood_reseed(Coin &coin, const fe *h, int C, zk_record &R);
+// S5: DEEP coefficients and the combined constants k1, k2 [P8]
+DeepConsts draw_deep_consts(Coin &coin, const fe *h, int C, fe z, fe zg, zk_record &R);
+// S6: number of FRI layers for an LDE domain of N points [P9]
+int fri_num_layers(size_t N, const zk_options *opt);
+FoldConsts fold_consts(fe alpha, uint32_t fold);
+// S6: interpolate the last layer (natural order, over 3 * <w_L>), keep L/B coefficients, commit [P9]
+int remainder_step(std::vector<fe> &last, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag);
+// S7: grinding nonce and the sorted unique query positions [P10, P11]
+std::vector<uint64_t> grind_and_positions(Coin &coin, const zk_options *opt, size_t N, zk_record &R);
+// positions folded down the FRI layers, first-occurrence order [P12]
+std::vector<std::vector<uint64_t>> fri_fold_positions(const std::vector<uint64_t> &pos, size_t N, uint32_t fold,
+                                                      int nl);
+
+// Everything the proof bytes contain besides the record: opened values and, per Merkle opening
+// (trace, constraint, FRI layers), the batch plan and its digests in serialization order.
+struct Openings {
+    std::vector<fe> trace_rows, comp_rows;       // nu x W, nu x C
+    std::vector<std::vector<fe>> fri_rows;       // per layer: |fri_pos[l]| x fold
+    std::vector<BatchPlan> plans;                // 2 + nl
+    std::vector<std::vector<uint8_t>> digests;   // 2 + nl, 32 B each, plan order
+};
+// S9: Proof::to_bytes [P13, P14]
+std::vector<uint8_t> serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood,
+                                     const Openings &O);
+// copy the proof out (proof_len in/out) and fold the degree flag into the status
+int deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, uint8_t *proof_out, size_t *proof_len);
+
+}  // namespace zk
