@@ -535,7 +535,7 @@ struct EvalShared {
 #ifndef ZK_EVAL_WAVES
 #define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
 #endif
-__global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const fe *lde, int log_n, int log_b, const fe *wn_lo,
+__global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *wn_lo,
                                                           const fe *wn_hi, const fe *periodic, const fe *inv_bd,
                                                           const AirConsts *K, fe *comp) {
     __shared__ EvalShared S;
@@ -554,18 +554,18 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     }
     const int L = K->lwe_size;
     const size_t n = (size_t)1 << log_n;
-    const size_t CE = n * 8;
-    const size_t B = (size_t)1 << log_b;
-    const int shift = log_b - 3;  // LDE steps per CE step
-    // thread t -> CE coset rc = t / n, position q = t % n (a wave reads 64 consecutive positions of one
-    // coset); CE step i = rc + 8q lives in LDE coset rc << shift at the same position.
+    const size_t CE = n * map.nce;
+    // thread t -> local CE coset jl = t / n, position q = t % n (a wave reads 64 consecutive positions of
+    // one coset).  Global CE coset rc = ce0 + cestep * jl; CE step i = rc + 8q; its LDE rows sit in local
+    // LDE coset slot jl << lshift at the same position.
     const size_t t_id = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t_id >= CE) return;
-    const size_t rc = t_id >> log_n, q = t_id & (n - 1), qn = (q + 1) & (n - 1);
+    const size_t jl = t_id >> log_n, q = t_id & (n - 1), qn = (q + 1) & (n - 1);
+    const size_t rc = map.ce0 + map.cestep * jl;
     const size_t i = rc + 8 * q;
-    const size_t r = rc << shift;
+    const size_t r = jl << map.lshift;
     const fe *cb = lde + r * n;  // laundered by ZK_SEQ between sections
-    const size_t cs = B * n;
+    const size_t cs = (size_t)map.lde_cosets * n;
 #define CUR(c) cb[(size_t)(c)*cs + q]
 #define NXT(c) cb[(size_t)(c)*cs + qn]
     const fe one = fe_one();
@@ -724,28 +724,33 @@ static void upload_rescue(hipStream_t st) {
     g_consts_uploaded = true;
 }
 
-void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tce, const fe *periodic,
+void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
                       const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
+    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, Tn, periodic, inv_bd, consts_dev,
+                            comp);
+}
+
+void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
+                             const fe *periodic, const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
     upload_rescue(st);
-    size_t CE = (size_t)8 << log_n;
-    unsigned blocks = cdiv(CE, 256);
-    ZK_PROF(st, "eval_constraints", (448.0 * (log_b == 3 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL(k_eval_constraints, dim3(blocks), dim3(256), 0, st, lde, log_n,
-                                                       log_b, Tce.fwd_lo, Tce.fwd_hi, periodic, inv_bd, consts_dev, comp));
+    const size_t CE = (size_t)map.nce << log_n;
+    ZK_PROF(st, "eval_constraints", (448.0 * (map.lshift == 0 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL(k_eval_constraints, dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
+                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts_dev, comp));
 }
 
 // ================================================================ composition interpolation (K4)
-__global__ void __launch_bounds__(256) k_comp_cross(const fe *c, int log_n, const fe *wi_lo, const fe *wi_hi,
+__global__ void __launch_bounds__(256) k_comp_cross(CrossMap m, const fe *wi_lo, const fe *wi_hi,
                                                     const fe *i3_lo, const fe *i3_hi, fe scale, fe w8inv,
                                                     fe inv3n, int ncols, fe *polys, unsigned *nonzero) {
-    const size_t n = (size_t)1 << log_n;
-    for (size_t k1 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k1 < n; k1 += (size_t)gridDim.x * blockDim.x) {
+    for (size_t kl = blockIdx.x * (size_t)blockDim.x + threadIdx.x; kl < m.kcount; kl += (size_t)gridDim.x * blockDim.x) {
+        const size_t k1 = m.k0 + kl;
         // d_r = c_r[k1] * w_8n^(-r k1)
         fe w = pow_split(wi_lo, wi_hi, k1);  // w_8n^-k1
         fe d[8];
         fe wr = fe_one();
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            fe v = c[(size_t)r * n + k1];
+            fe v = m.c[r][kl];
             d[r] = r ? fe_mul(v, wr) : v;
             wr = fe_mul(wr, w);
         }
@@ -770,7 +775,7 @@ __global__ void __launch_bounds__(256) k_comp_cross(const fe *c, int log_n, cons
 #pragma unroll
         for (int k2 = 0; k2 < 8; k2++) {
             fe a = fe_mul(bk[k2], s);
-            if (k2 < ncols) polys[(size_t)k2 * n + k1] = a;
+            if (k2 < ncols) polys[(size_t)k2 * m.pstride + kl] = a;
             else nz |= !fe_is_zero(a);
             s = fe_mul(s, inv3n);
         }
@@ -780,10 +785,20 @@ __global__ void __launch_bounds__(256) k_comp_cross(const fe *c, int log_n, cons
 
 void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T8n, const PowTable &inv3, fe scale,
                       fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag) {
-    size_t n = (size_t)1 << log_n;
-    unsigned blocks = cdiv(n, 256);
+    const size_t n = (size_t)1 << log_n;
+    CrossMap m;
+    for (int r = 0; r < 8; r++) m.c[r] = c + (size_t)r * n;
+    m.k0 = 0;
+    m.kcount = n;
+    m.pstride = n;
+    comp_cross_mapped(st, m, T8n, inv3, scale, w8inv, inv3n, ncols, polys, nonzero_flag);
+}
+
+void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, const PowTable &inv3, fe scale,
+                       fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag) {
+    unsigned blocks = cdiv(m.kcount, 256);
     if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "comp_cross", (128.0 + 16.0 * ncols) * n, hipLaunchKernelGGL(k_comp_cross, dim3(blocks), dim3(256), 0, st, c, log_n, T8n.inv_lo,
+    ZK_PROF(st, "comp_cross", (128.0 + 16.0 * ncols) * m.kcount, hipLaunchKernelGGL(k_comp_cross, dim3(blocks), dim3(256), 0, st, m, T8n.inv_lo,
                                                  T8n.inv_hi, inv3.lo, inv3.hi, scale, w8inv, inv3n, ncols, polys,
                                                  nonzero_flag));
 }

@@ -90,6 +90,12 @@ struct zk_prover {
     uint64_t *gather_idx = nullptr;
     unsigned *flag = nullptr;
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
+    // coset-sharded proving (shard.hip), allocated on first use
+    fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
+    fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
+    fe *sh_zero = nullptr;      // one zero chunk (stands in for openings another rank owns)
+    uint8_t *sh_roots = nullptr;  // world subtree roots
+    unsigned *sh_flags = nullptr;  // world degree flags
     std::map<std::pair<int, int>, std::unique_ptr<zk::Plan>> plans;
     // stage timing
     std::vector<std::pair<const char *, hipEvent_t>> stage_ev;

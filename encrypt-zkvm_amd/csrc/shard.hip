@@ -1,0 +1,685 @@
+// shard.hip -- one proof with the LDE domain sharded by coset over `world` GPUs.
+//
+// Rank g of G owns the LDE cosets r = g + G*j, j < Bl = 8/G (blowup 8).  Per stage:
+//   trace interpolation          replicated (every rank holds the trace)
+//   trace LDE, constraint eval,  local: a coset's LDE is an independent size-n NTT, and constraint
+//   DEEP, first FRI fold         row i+8 / a fold row {e[r' + k N/fold]} stay inside one coset
+//   Merkle trees                 all-to-all of leaf digests into contiguous leaf ranges, a local
+//   (trace, composition, FRI 0)  subtree per rank, all-gather of the G subtree roots
+//   composition interpolation    per-coset inverse NTT local; all-to-all of coefficient slices for the
+//                                cross-coset radix-8 step; all-gather of the 7 column polynomials
+//   FRI layers >= 1              all-gather of layer 1, then replicated (small)
+//   openings                     every rank gathers what it owns, all-gather, the host combines
+// The Fiat-Shamir transcript runs on every process's host over identical (all-gathered) roots, so no
+// challenge is ever broadcast.  The proof bytes equal the single-GPU prover's (tests/test_sharded.py).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <string>
+#include <vector>
+
+#include "blake3.hpp"
+#include "comm.hpp"
+#include "prover_internal.hpp"
+
+using namespace zk;
+
+namespace {
+
+static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------- loopback communicator
+struct LoopbackComm : zk_comm {
+    bool loopback() const override { return true; }
+    static int sync(const std::vector<zk_prover *> &P) {
+        for (auto *p : P) ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        return ZK_OK;
+    }
+    int all_to_all(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
+                   const std::vector<void *> &recv, size_t bytes) override {
+        if ((int)P.size() != world) ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator drives every rank");
+        ZK_TRY(sync(P));
+        for (int d = 0; d < world; d++)
+            for (int s = 0; s < world; s++)
+                ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, (const uint8_t *)send[s] + d * bytes, bytes,
+                                            hipMemcpyDefault, P[d]->st));
+        return sync(P);
+    }
+    int all_gather(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
+                   const std::vector<void *> &recv, size_t bytes) override {
+        if ((int)P.size() != world) ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator drives every rank");
+        ZK_TRY(sync(P));
+        for (int d = 0; d < world; d++)
+            for (int s = 0; s < world; s++)
+                ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, send[s], bytes, hipMemcpyDefault, P[d]->st));
+        return sync(P);
+    }
+};
+
+// ---------------------------------------------------------------- local-coset kernels
+__device__ __forceinline__ void st_digest(uint8_t *dst, const uint32_t h[8]) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+// all-to-all slot of local coset j, position q when rank d receives positions [d*mg, (d+1)*mg)
+__device__ __forceinline__ size_t a2a_slot(size_t j, size_t q, int Bl, int log_mg) {
+    return ((((q >> log_mg) * Bl) + j) << log_mg) + (q & (((size_t)1 << log_mg) - 1));
+}
+
+// leaf digests of the local LDE rows (column c, local coset j at base[(c*Bl + j)*n + q]), in all-to-all order
+__global__ void __launch_bounds__(256) k_sh_hash_rows(const fe *base, int ncols, int log_n, int Bl, int log_mg,
+                                                      uint8_t *send) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_n)) return;
+    const size_t j = t >> log_n, q = t & (n - 1);
+    const fe *p = base + j * n + q;
+    const size_t cs = (size_t)Bl * n;
+    uint32_t h[8];
+    b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
+    st_digest(send + 32 * a2a_slot(j, q, Bl, log_mg), h);
+}
+
+// FRI layer-0 leaves of the local cosets: row r' = r + 8*q0 holds deep[j][q0 + k*m], m = n / fold
+__global__ void __launch_bounds__(256) k_sh_hash_fri0(const fe *deep, int log_n, int Bl, int fold, int log_m,
+                                                      int log_mg, uint8_t *send) {
+    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_m)) return;
+    const size_t j = t >> log_m, q0 = t & (m - 1);
+    const fe *p = deep + j * n + q0;
+    uint32_t h[8];
+    b3::hash_elements(fold, [&](int k) { return p[(size_t)k << log_m]; }, h);
+    st_digest(send + 32 * a2a_slot(j, q0, Bl, log_mg), h);
+}
+
+// received chunks [s][j][q'] -> natural order of this rank's range: item (s + G*j) + 8*q'
+__global__ void k_sh_permute(const uint8_t *recv, int G, int Bl, int log_mg, int esize, uint8_t *out) {
+    const size_t per = (size_t)Bl << log_mg;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= per * G) return;
+    const size_t s = t / per, rem = t % per, j = rem >> log_mg, qp = rem & (((size_t)1 << log_mg) - 1);
+    const size_t idx = (s + (size_t)G * j) + 8 * qp;
+    const uint4 *src = reinterpret_cast<const uint4 *>(recv + t * esize);
+    uint4 *dst = reinterpret_cast<uint4 *>(out + idx * esize);
+    for (int w = 0; w < esize / 16; w++) dst[w] = src[w];
+}
+
+// coefficient slices for the cross-coset all-to-all: send[d][j][k'] = c[j][d*kg + k']
+__global__ void k_sh_pack(const fe *c, int log_n, int Bl, int log_kg, fe *send) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_n)) return;
+    const size_t j = t >> log_n, k = t & (n - 1);
+    send[((((k >> log_kg) * Bl) + j) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[t];
+}
+
+// DEEP composition over the local cosets: out[j*n + q] at natural LDE index i = (g + G*j) + 8*q
+__global__ void __launch_bounds__(256) k_sh_deep(const fe *lde, int log_n, int Bl, int g, int G, const fe *clde,
+                                                 int ccols, const DeepConsts *D, const fe *wN_lo, const fe *wN_hi,
+                                                 fe three, const fe *inv_d, fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_n)) return;
+    const size_t j = t >> log_n, q = t & (n - 1);
+    const size_t i = (size_t)(g + G * (int)j) + 8 * q;
+    const size_t cs = (size_t)Bl * n;
+    const fe *p = lde + j * n + q;
+    acc288 aT = acc288_zero();
+#pragma unroll 4
+    for (int c = 0; c < 28; c++) acc288_madd(aT, D->alpha_t[c], p[(size_t)c * cs]);
+    const fe sT = acc288_reduce(aT);
+    const fe *pc = clde + j * n + q;
+    acc288 aH = acc288_zero();
+    for (int k = 0; k < ccols; k++) acc288_madd(aH, D->alpha_c[k], pc[(size_t)k * cs]);
+    const fe sH = acc288_reduce(aH);
+    const fe s1 = fe_sub(fe_add(sT, sH), D->k1), s2 = fe_sub(sT, D->k2);
+    const fe x = fe_mul(three, fe_mul(wN_lo[i & 2047], wN_hi[i >> 11]));
+    const fe num = fe_add(fe_mul(s1, fe_sub(x, D->zg)), fe_mul(s2, fe_sub(x, D->z)));
+    out[t] = fe_mul(num, inv_d[t]);
+}
+
+// first FRI fold over the local cosets: row r' = r + 8*q0 (values deep[j][q0 + k*m]) -> out[j*m + q0]
+__global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n, int Bl, int g, int G, int fold,
+                                                      int log_m, const FoldConsts *F, const fe *wi_lo,
+                                                      const fe *wi_hi, fe *out) {
+    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_m)) return;
+    const size_t j = t >> log_m, q0 = t & (m - 1);
+    const size_t rp = (size_t)(g + G * (int)j) + 8 * q0;  // row index in layer 0 (size N, wstride 1)
+    fe v[16];
+    for (int k = 0; k < fold; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
+    const fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    fe acc = fe_zero();
+    for (int mm = fold - 1; mm >= 0; mm--) {
+        fe Vm = fe_zero();
+        for (int k = 0; k < fold; k++) Vm = fe_add(Vm, fe_mul(v[k], F->zinv[(k * mm) & (fold - 1)]));
+        acc = fe_add(fe_mul(acc, beta), Vm);
+    }
+    out[t] = fe_mul(acc, F->inv_fold);
+}
+
+// ---------------------------------------------------------------- a Merkle tree split over G ranks
+// M leaves in natural order; rank d holds leaves [d*M/G, (d+1)*M/G) and the subtree above them; the
+// top (G leaves = subtree roots) is kept on the host.
+struct DistTree {
+    size_t M = 0, Mr = 0;
+    int G = 1;
+    std::vector<uint8_t *> leaves, nodes;            // per local rank
+    std::vector<std::array<uint8_t, 32>> top;        // heap nodes 1 .. 2G-1
+    uint8_t root[32];
+    // chunk source of global heap node k (leaves are M + i): owner rank, buffer, byte offset; owner -1 =
+    // host top node (copied into `host`)
+    struct Loc {
+        int owner;
+        int which;  // 0 leaves, 1 nodes
+        size_t off;
+    };
+    Loc locate(int is_node, uint64_t idx) const {
+        if (!is_node) return {(int)(idx / Mr), 0, 32 * (idx % Mr)};
+        const uint64_t k = idx;
+        int L = 1;
+        while ((M >> L) > k) L++;
+        const size_t c = Mr >> L;
+        if (c == 0) return {-1, 0, 32 * k};
+        const size_t mpos = k - (M >> L);
+        return {(int)(mpos / c), 1, 32 * (c + mpos % c)};
+    }
+};
+
+struct Ctx {
+    zk_comm *comm;
+    std::vector<zk_prover *> P;
+    std::vector<int> rank;  // rank of each local prover
+    std::vector<Plan *> pl;
+    int G, Bl, log_n, C;
+    size_t n;
+};
+
+// leaves (hash kernel writes all-to-all order into a2a_send), all-to-all, permute, subtree, roots
+template <typename HashFn>
+int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
+                const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes) {
+    const int nl = (int)X.P.size();
+    T.M = M;
+    T.G = X.G;
+    T.Mr = M / X.G;
+    T.leaves = leaves;
+    T.nodes = nodes;
+    const size_t mg = T.Mr / 8;  // positions per destination rank per coset
+    const int log_mg = ilog2(mg);
+    std::vector<const void *> snd(nl);
+    std::vector<void *> rcv(nl);
+    for (int l = 0; l < nl; l++) {
+        ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
+        hash(l, scratch[l], log_mg);
+        snd[l] = scratch[l];
+        rcv[l] = scratch[l] + 32 * T.Mr;
+    }
+    ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, 32 * (size_t)X.Bl * mg));
+    std::vector<const void *> rs(nl);
+    std::vector<void *> rr(nl);
+    for (int l = 0; l < nl; l++) {
+        zk_prover *p = X.P[l];
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr, 256)), dim3(256), 0, p->st, (const uint8_t *)rcv[l], X.G, X.Bl,
+                           log_mg, 32, leaves[l]);
+        merkle_tree(p->st, leaves[l], T.Mr, nodes[l]);
+        rs[l] = T.Mr >= 2 ? nodes[l] + 32 : leaves[l];
+        rr[l] = p->sh_roots;
+    }
+    ZK_TRY(X.comm->all_gather(X.P, rs, rr, 32));
+    std::vector<uint8_t> roots(32 * X.G);
+    ZK_CHECK_HIP(hipMemcpyAsync(roots.data(), X.P[0]->sh_roots, roots.size(), hipMemcpyDeviceToHost, X.P[0]->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(X.P[0]->st));
+    T.top.assign(2 * X.G, {});
+    for (int d = 0; d < X.G; d++) memcpy(T.top[X.G + d].data(), &roots[32 * d], 32);
+    for (int k = X.G - 1; k >= 1; k--) {
+        uint8_t buf[64];
+        memcpy(buf, T.top[2 * k].data(), 32);
+        memcpy(buf + 32, T.top[2 * k + 1].data(), 32);
+        b3::hash_bytes(buf, 64, T.top[k].data());
+    }
+    memcpy(T.root, T.top[1].data(), 32);
+    return ZK_OK;
+}
+
+int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out,
+                  size_t *proof_len, zk_record *rec) {
+    const int G = X.G, Bl = X.Bl, log_n = X.log_n, C = X.C, nlp = (int)X.P.size();
+    const size_t n = X.n, N = 8 * n, CE = 8 * n;
+    const uint32_t fold = opt->fri_folding;
+    const size_t m = n / fold;          // FRI layer-0 positions per coset
+    const int log_m = ilog2(m);
+    const fe g = h_root_of_unity(log_n), three = fe_make(3);
+    zk_prover *P0 = X.P[0];
+    zk_record R;
+    memset(&R, 0, sizeof R);
+    R.trace_len = (uint32_t)n;
+    R.lde_len = (uint32_t)N;
+    R.width = W;
+    R.num_ccols = (uint32_t)C;
+    stage_begin(P0);
+    stage_mark(P0, "start");
+    Coin coin = seed_coin(n, opt, pub);
+
+    // S2: replicated interpolation, local coset LDE, distributed commitment
+    const fe inv_n = h_inv(fe_make(n));
+    for (int l = 0; l < nlp; l++) {
+        zk_prover *p = X.P[l];
+        Plan *pl = X.pl[l];
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
+        ntt(p->st, pl->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+        for (int j = 0; j < Bl; j++)
+            ntt(p->st, pl->Tn, p->polys, n, p->lde + j * n, (size_t)Bl * n, W, false, &pl->coset[X.rank[l] + G * j],
+                nullptr, p->tmp);
+    }
+    stage_mark(P0, "trace_lde");
+    std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);
+    for (int l = 0; l < nlp; l++) {
+        scratch[l] = X.P[l]->fri_dig;
+        lv[l] = X.P[l]->leaves;
+        nd[l] = X.P[l]->nodes;
+    }
+    DistTree Ttrace;
+    ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_mg) {
+        zk_prover *p = X.P[l];
+        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, W, log_n, Bl,
+                           log_mg, send);
+    }, scratch, lv, nd));
+    memcpy(R.trace_root, Ttrace.root, 32);
+    stage_mark(P0, "trace_commit");
+    coin.reseed(R.trace_root);
+
+    // S3: constraint evaluation over the local CE cosets (CE domain = LDE domain at blowup 8)
+    AirConsts K;
+    draw_air_consts(coin, pub, n, K, R);
+    for (int l = 0; l < nlp; l++) {
+        zk_prover *p = X.P[l];
+        Plan *pl = X.pl[l];
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        fe xr[8];
+        for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] + G * j];
+        ZK_CHECK_HIP(hipMemcpyAsync(p->sh_xr, xr, Bl * sizeof(fe), hipMemcpyHostToDevice, p->st));
+        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+        batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, fe_one(), K.g_last2, p->inv);
+        eval_constraints_mapped(p->st, p->lde, log_n, EvalMap{Bl, X.rank[l], G, 0, Bl}, pl->Tn, pl->periodic, p->inv,
+                                (const AirConsts *)p->air_consts, p->comp);
+    }
+    stage_mark(P0, "constraints");
+
+    // S4: composition polynomial: per-coset inverse NTT, all-to-all of coefficient slices, cross-coset
+    // step on this rank's slice, all-gather of the C columns; then local coset LDE + commitment
+    const size_t kg = n / G;
+    {
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ntt(p->st, X.pl[l]->Tn, p->comp, n, p->ctmp, n, Bl, true, nullptr, nullptr, p->tmp);
+            hipLaunchKernelGGL(k_sh_pack, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->ctmp, log_n, Bl,
+                               ilog2(kg), p->tmp);
+            snd[l] = p->tmp;
+            rcv[l] = p->comp;
+        }
+        ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, (size_t)Bl * kg * sizeof(fe)));
+        const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
+        std::vector<const void *> fs(nlp);
+        std::vector<void *> fr(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            CrossMap cm;
+            for (int r = 0; r < 8; r++) cm.c[r] = p->comp + ((size_t)(r % G) * Bl + r / G) * kg;
+            cm.k0 = (size_t)X.rank[l] * kg;
+            cm.kcount = kg;
+            cm.pstride = kg;
+            ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
+            comp_cross_mapped(p->st, cm, X.pl[l]->Tce, X.pl[l]->inv3, scale, w8inv, inv3n, C, p->ctmp, p->flag);
+            fs[l] = p->flag;
+            fr[l] = p->sh_flags;
+        }
+        for (int c = 0; c < C; c++) {
+            std::vector<const void *> s2(nlp);
+            std::vector<void *> r2(nlp);
+            for (int l = 0; l < nlp; l++) {
+                s2[l] = X.P[l]->ctmp + c * kg;
+                r2[l] = X.P[l]->cpolys + (size_t)c * n;
+            }
+            ZK_TRY(X.comm->all_gather(X.P, s2, r2, kg * sizeof(fe)));
+        }
+        ZK_TRY(X.comm->all_gather(X.P, fs, fr, sizeof(unsigned)));
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            for (int j = 0; j < Bl; j++)
+                ntt(p->st, X.pl[l]->Tn, p->cpolys, n, p->clde + j * n, (size_t)Bl * n, C, false,
+                    &X.pl[l]->coset[X.rank[l] + G * j], nullptr, p->tmp);
+        }
+    }
+    for (int l = 0; l < nlp; l++) {
+        lv[l] = X.P[l]->cleaves;
+        nd[l] = X.P[l]->cnodes;
+    }
+    DistTree Tcomp;
+    ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_mg) {
+        zk_prover *p = X.P[l];
+        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->clde, C, log_n, Bl,
+                           log_mg, send);
+    }, scratch, lv, nd));
+    memcpy(R.constraint_root, Tcomp.root, 32);
+    stage_mark(P0, "composition");
+    unsigned degree_flag = 0;
+    {
+        std::vector<unsigned> f(G);
+        ZK_CHECK_HIP(hipMemcpy(f.data(), P0->sh_flags, G * sizeof(unsigned), hipMemcpyDeviceToHost));
+        for (unsigned v : f) degree_flag |= v;
+    }
+    coin.reseed(R.constraint_root);
+
+    // S5: OOD frame (every process evaluates the replicated polynomials), DEEP over the local cosets
+    const fe z = coin.draw(), zg = fe_mul(z, g);
+    fe_to_bytes(z, R.z);
+    fe h[2 * W + ZK_MAX_CCOLS];
+    ZK_CHECK_HIP(hipSetDevice(P0->device));
+    ood_eval(P0->st, P0->polys, W, P0->cpolys, C, log_n, z, zg, P0->ood_tab, P0->partials, P0->ood);
+    ZK_CHECK_HIP(hipMemcpyAsync(h, P0->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+    ood_reseed(coin, h, C, R);
+    stage_mark(P0, "ood");
+    const DeepConsts D = draw_deep_consts(coin, h, C, z, zg, R);
+    for (int l = 0; l < nlp; l++) {
+        zk_prover *p = X.P[l];
+        Plan *pl = X.pl[l];
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+        batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
+        hipLaunchKernelGGL(k_sh_deep, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl, X.rank[l],
+                           G, p->clde, C, (const DeepConsts *)p->deep_consts, pl->TN.fwd_lo, pl->TN.fwd_hi, three,
+                           p->inv, p->deep);
+    }
+    stage_mark(P0, "deep");
+
+    // S6: FRI.  Layer 0 is sharded (its fold rows stay in one coset); layer 1 is all-gathered and the
+    // remaining layers run on local rank 0 of every process.
+    const int nl = fri_num_layers(N, opt);
+    if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
+    R.num_fri_layers = (uint32_t)nl;
+    std::vector<uint8_t *> f0l(nlp), f0n(nlp);
+    const size_t rows0 = N / fold;  // layer-0 Merkle leaves
+    std::vector<const fe *> layer_vals(nl + 1);
+    std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
+    std::vector<size_t> layer_len(nl + 1);
+    layer_len[0] = N;
+    DistTree Tfri0;
+    if (nl == 0) {
+        // no folding: the remainder is the whole DEEP layer, all-gathered into natural order
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int l = 0; l < nlp; l++) {
+            snd[l] = X.P[l]->deep;
+            rcv[l] = X.P[l]->comp;
+        }
+        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)Bl * n * sizeof(fe)));
+        ZK_CHECK_HIP(hipSetDevice(P0->device));
+        hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(N, 256)), dim3(256), 0, P0->st, (const uint8_t *)P0->comp, G, Bl,
+                           log_n, 16, (uint8_t *)P0->fri);
+        std::vector<fe> rv(N);
+        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), P0->fri, N * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        ZK_TRY(remainder_step(rv, 8, coin, R, degree_flag));
+    } else {
+        for (int l = 0; l < nlp; l++) {
+            f0l[l] = (uint8_t *)X.P[l]->tmp;
+            f0n[l] = f0l[l] + 32 * (rows0 / G);
+        }
+        ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_mg) {
+            zk_prover *p = X.P[l];
+            hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n, Bl,
+                               (int)fold, log_m, log_mg, send);
+        }, scratch, f0l, f0n));
+        memcpy(R.fri_roots[0], Tfri0.root, 32);
+        coin.reseed(R.fri_roots[0]);
+        fe alpha = coin.draw();
+        fe_to_bytes(alpha, R.fri_alphas[0]);
+        {
+            const FoldConsts F = fold_consts(alpha, fold);
+            std::vector<const void *> snd(nlp);
+            std::vector<void *> rcv(nlp);
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+                hipLaunchKernelGGL(k_sh_fri_fold0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n, Bl,
+                                   X.rank[l], G, (int)fold, log_m, (const FoldConsts *)p->fold_consts, X.pl[l]->TN.inv_lo,
+                                   X.pl[l]->TN.inv_hi, p->ctmp);
+                snd[l] = p->ctmp;
+                rcv[l] = p->comp;
+            }
+            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)Bl * m * sizeof(fe)));
+            ZK_CHECK_HIP(hipSetDevice(P0->device));
+            hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st, (const uint8_t *)P0->comp, G, Bl,
+                               log_m, 16, (uint8_t *)P0->fri);
+        }
+        layer_vals[1] = P0->fri;
+        layer_len[1] = rows0;
+        {
+            fe *next = P0->fri + rows0;
+            uint8_t *dig = P0->fri_dig;  // the all-to-all scratch is free once layer 0 is committed
+            for (int l = 1; l < nl; l++) {
+                const size_t L = layer_len[l], rows = L / fold;
+                layer_leaves[l] = dig;
+                layer_nodes[l] = dig + 32 * rows;
+                dig += 64 * rows;
+                commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+                ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, P0->st));
+                ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+                coin.reseed(R.fri_roots[l]);
+                alpha = coin.draw();
+                fe_to_bytes(alpha, R.fri_alphas[l]);
+                const FoldConsts F = fold_consts(alpha, fold);
+                ZK_CHECK_HIP(hipMemcpyAsync(P0->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
+                fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
+                layer_vals[l + 1] = next;
+                layer_len[l + 1] = rows;
+                next += rows;
+            }
+            std::vector<fe> rv(layer_len[nl]);
+            ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+            ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+            ZK_TRY(remainder_step(rv, 8, coin, R, degree_flag));
+        }
+    }
+    stage_mark(P0, "fri");
+
+    // S7 / S8: positions, then every rank gathers the chunks it owns; all-gather; the host combines
+    const std::vector<uint64_t> pos = grind_and_positions(coin, opt, N, R);
+    const size_t nu = pos.size();
+    const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
+    Openings O;
+    O.plans.push_back(plan_batch(N, pos));
+    O.plans.push_back(plan_batch(N, pos));
+    for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l]));
+    // chunk requests: owner rank (-1: host top node), local buffer id, byte offset
+    enum { B_LDE, B_CLDE, B_DEEP, B_TL, B_TN, B_CL, B_CN, B_F0L, B_F0N, B_FRI };
+    struct Req {
+        int owner, buf;
+        size_t off;
+        const uint8_t *host;
+    };
+    std::vector<Req> req;
+    auto lde_row = [&](int buf, int ncols, uint64_t i) {
+        const int r = (int)(i & 7), own = r % G, j = r / G;
+        const size_t q = i >> 3;
+        for (int c = 0; c < ncols; c++) req.push_back({own, buf, 16 * (((size_t)c * Bl + j) * n + q), nullptr});
+    };
+    for (size_t q = 0; q < nu; q++) lde_row(B_LDE, W, pos[q]);
+    for (size_t q = 0; q < nu; q++) lde_row(B_CLDE, C, pos[q]);
+    for (uint64_t rp : (nl > 0 ? fri_pos[0] : std::vector<uint64_t>())) {
+        const int r = (int)(rp & 7), own = r % G, j = r / G;
+        const size_t q0 = rp >> 3;
+        for (uint32_t k = 0; k < fold; k++) req.push_back({own, B_DEEP, 16 * (j * n + q0 + k * m), nullptr});
+    }
+    for (int l = 1; l < nl; l++) {
+        const size_t rows = layer_len[l] / fold;
+        for (uint64_t r : fri_pos[l])
+            for (uint32_t k = 0; k < fold; k++)
+                req.push_back({0, B_FRI,
+                               (size_t)((const uint8_t *)(layer_vals[l] + r + k * rows) - (const uint8_t *)P0->fri), nullptr});
+    }
+    const size_t off_dig = req.size();
+    const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
+    const int tbuf[3][2] = {{B_TL, B_TN}, {B_CL, B_CN}, {B_F0L, B_F0N}};
+    for (int b = 0; b < 2 + nl; b++)
+        for (auto &path : O.plans[b].paths)
+            for (auto &e : path) {
+                if (b < 3) {
+                    const DistTree::Loc L = trees[b]->locate(e.first, e.second);
+                    if (L.owner < 0) {
+                        const uint8_t *hp = trees[b]->top[e.second].data();
+                        req.push_back({-1, 0, 0, hp});
+                        req.push_back({-1, 0, 0, hp + 16});
+                    } else {
+                        req.push_back({L.owner, tbuf[b][L.which], L.off, nullptr});
+                        req.push_back({L.owner, tbuf[b][L.which], L.off + 16, nullptr});
+                    }
+                } else {  // replicated FRI layers >= 1 (local rank 0 of every process, i.e. rank 0 serves)
+                    const uint8_t *base = e.first ? layer_nodes[b - 2] : layer_leaves[b - 2];
+                    const size_t off = (size_t)(base + 32 * e.second - P0->fri_dig);
+                    req.push_back({0, B_FRI + 1, off, nullptr});
+                    req.push_back({0, B_FRI + 1, off + 16, nullptr});
+                }
+            }
+    const size_t NK = req.size();
+    if (NK > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
+    {
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)p->clde, (const uint8_t *)p->deep,
+                                        p->leaves, p->nodes, p->cleaves, p->cnodes, f0l[l], f0n[l],
+                                        (const uint8_t *)p->fri, p->fri_dig};
+            std::vector<uint64_t> addr(NK);
+            for (size_t t = 0; t < NK; t++) {
+                const Req &q = req[t];
+                addr[t] = (q.owner == X.rank[l]) ? (uint64_t)(uintptr_t)(bases[q.buf] + q.off)
+                                                 : (uint64_t)(uintptr_t)p->sh_zero;
+            }
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, addr.data(), NK * 8, hipMemcpyHostToDevice, p->st));
+            gather_chunks(p->st, p->gather_idx, NK, p->gather_out);
+            ZK_CHECK_HIP(hipStreamSynchronize(p->st));  // addr is a host temporary
+            snd[l] = p->gather_out;
+            rcv[l] = p->sh_buf;
+        }
+        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, NK * sizeof(fe)));
+    }
+    std::vector<fe> all((size_t)G * NK), got(NK);
+    ZK_CHECK_HIP(hipMemcpyAsync(all.data(), P0->sh_buf, all.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+    for (size_t t = 0; t < NK; t++) {
+        if (req[t].owner < 0)
+            memcpy(&got[t], req[t].host, 16);
+        else
+            got[t] = all[(size_t)req[t].owner * NK + t];
+    }
+    {
+        size_t off = 0;
+        O.trace_rows.assign(got.begin(), got.begin() + nu * W);
+        off += nu * W;
+        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * C);
+        off += nu * C;
+        for (int l = 0; l < nl; l++) {
+            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold);
+            off += fri_pos[l].size() * fold;
+        }
+        const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
+        for (int b = 0; b < 2 + nl; b++) {
+            const size_t bytes = 32 * O.plans[b].count();
+            O.digests.emplace_back(dg, dg + bytes);
+            dg += bytes;
+        }
+    }
+    stage_mark(P0, "queries");
+    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h, O);
+    stage_mark(P0, "serialize");
+    ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+    stage_collect(P0);
+    collect_kernel_stats(P0);
+    if (rec) *rec = R;
+    return deliver_proof(bytes, degree_flag, proof_out, proof_len);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+int zk_comm_create_loopback(int world, zk_comm **out) {
+    if (!out || (world != 1 && world != 2 && world != 4 && world != 8))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "world must be 1, 2, 4 or 8 (ranks own 8/world cosets)");
+    auto *c = new LoopbackComm();
+    c->world = world;
+    c->rank = 0;
+    *out = c;
+    return ZK_OK;
+}
+
+int zk_comm_unique_id(uint8_t id[128]) {
+    if (!id) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    return zk_rccl_unique_id(id);
+}
+
+int zk_comm_create_rccl(const uint8_t id[128], int rank, int world, int device, zk_comm **out) {
+    if (!id || !out || rank < 0 || rank >= world || (world != 1 && world != 2 && world != 4 && world != 8))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid rank / world (world must be 1, 2, 4 or 8)");
+    return zk_make_rccl_comm(id, rank, world, device, out);
+}
+
+void zk_comm_destroy(zk_comm *c) { delete c; }
+
+int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
+                     const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
+                     zk_record *rec) {
+    if (!comm || !provers || !trace || !proof_len || nlocal <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (comm->loopback() ? nlocal != comm->world : nlocal != 1)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator needs one prover per rank, an RCCL one exactly one");
+    Ctx X;
+    X.comm = comm;
+    X.G = comm->world;
+    X.Bl = 8 / X.G;
+    X.n = n;
+    for (int l = 0; l < nlocal; l++) {
+        zk_prover *p = provers[l];
+        if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+        ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
+        X.P.push_back(p);
+        X.rank.push_back(comm->loopback() ? l : comm->rank);
+    }
+    if (opt->blowup != 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "the sharded prover needs blowup 8 (LDE cosets = CE cosets)");
+    const size_t m = n / opt->fri_folding;
+    if (m < 8 * (size_t)X.G || n / X.G < 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace too short to shard over this many ranks");
+    X.log_n = ilog2(n);
+    X.C = num_comp_cols(n);
+    if (X.C > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition column count exceeds 8");
+    for (auto *p : X.P) {
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        Plan *pl = nullptr;
+        ZK_TRY(get_plan(p, n, 8, &pl));
+        X.pl.push_back(pl);
+        if (!p->sh_buf) {
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_buf, (size_t)8 * ZK_GATHER_CAP));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_xr, 8));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_zero, 1));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_roots, 32 * 8));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_flags, 8));
+            ZK_CHECK_HIP(hipMemset(p->sh_zero, 0, sizeof(fe)));
+        }
+    }
+    return prove_sharded(X, trace, opt, pub, proof_out, proof_len, rec);
+}

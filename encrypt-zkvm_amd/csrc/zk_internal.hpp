@@ -116,6 +116,21 @@ struct AirConsts {
 // x = xr[r] * w_n^q (natural domain index i = r + B*q)
 void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe a, fe b,
                      fe *out);
+// Which CE cosets one launch evaluates: local coset jl < nce is global CE coset ce0 + cestep*jl, and its
+// LDE rows are LDE coset slot jl << lshift of a buffer holding lde_cosets cosets per column.
+struct EvalMap {
+    int nce, ce0, cestep, lshift, lde_cosets;
+};
+void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
+                             const fe *periodic, const fe *inv_bd, const AirConsts *consts_dev, fe *comp);
+// Inputs of the cross-coset step for coefficients k0 .. k0+kcount: c[r][kl] = c_r[k0 + kl]; output
+// polys[k2 * pstride + kl].
+struct CrossMap {
+    const fe *c[8];
+    size_t k0, kcount, pstride;
+};
+void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, const PowTable &inv3, fe scale,
+                       fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
                       const fe *inv_bd, const AirConsts *consts_dev, fe *comp);

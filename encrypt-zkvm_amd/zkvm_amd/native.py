@@ -30,6 +30,7 @@ EXPORTED = (
     "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_destroy", "zk_prover_trace_buffer",
     "zk_prove", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_vm_trace",
+    "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_destroy", "zk_prove_sharded",
 )
 
 
@@ -100,6 +101,13 @@ def lib():
         L.zk_prover_profile.argtypes = [vp, i32]
         L.zk_prover_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(i32),
                                              C.POINTER(C.c_double), i32, C.POINTER(i32)]
+        L.zk_comm_create_loopback.argtypes = [i32, C.POINTER(vp)]
+        L.zk_comm_unique_id.argtypes = [vp]
+        L.zk_comm_create_rccl.argtypes = [vp, i32, i32, i32, C.POINTER(vp)]
+        L.zk_comm_destroy.argtypes = [vp]
+        L.zk_comm_destroy.restype = None
+        L.zk_prove_sharded.argtypes = [vp, C.POINTER(vp), i32, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp,
+                                       C.POINTER(sz), C.POINTER(Record)]
         L.zk_vm_trace.argtypes = [C.c_char_p, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp, vp]
         L.zk_vm_last_error.restype = C.c_char_p
         L.zk_diag_mul_limbs_host.argtypes = [vp, vp, vp, sz]

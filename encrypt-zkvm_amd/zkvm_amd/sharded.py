@@ -1,0 +1,80 @@
+"""One proof with the LDE domain sharded by coset over several GPUs (zk_prove_sharded).
+
+Rank g of `world` owns LDE cosets r = g (mod world); leaf digests, composition coefficient slices,
+FRI layer 1 and the openings are exchanged through a communicator:
+
+  * ShardedProver.loopback(world)       -- every rank driven from this process (one prover per rank,
+                                           in-process copies); used by the tests on one GPU;
+  * ShardedProver.rccl(rank, world, id) -- one process per GPU, RCCL over xGMI; the 128-byte id comes
+                                           from ShardedProver.unique_id() on rank 0 and is shared out of
+                                           band (bench.py uses torch.distributed).
+Every rank returns the same proof bytes, identical to the single-GPU prover's.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import native
+from .native import Record, check, lib
+from .prover import REFERENCE_OPTIONS, ProofOptions
+
+
+class ShardedProver:
+    def __init__(self, comm, provers, rank: int, world: int):
+        self.comm, self.provers, self.rank, self.world = comm, provers, rank, world
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().zk_comm_unique_id(buf), "zk_comm_unique_id")
+        return buf.raw
+
+    @classmethod
+    def loopback(cls, world: int, device: int = 0, max_trace_len: int = 1 << 16) -> "ShardedProver":
+        comm = C.c_void_p()
+        check(lib().zk_comm_create_loopback(world, C.byref(comm)), "zk_comm_create_loopback")
+        provers = []
+        for _ in range(world):
+            p = C.c_void_p()
+            check(lib().zk_prover_create(device, max_trace_len, 8, C.byref(p)), "zk_prover_create")
+            provers.append(p)
+        return cls(comm, provers, 0, world)
+
+    @classmethod
+    def rccl(cls, rank: int, world: int, uid: bytes, device: int, max_trace_len: int) -> "ShardedProver":
+        comm = C.c_void_p()
+        check(lib().zk_comm_create_rccl(uid, rank, world, device, C.byref(comm)), "zk_comm_create_rccl")
+        p = C.c_void_p()
+        check(lib().zk_prover_create(device, max_trace_len, 8, C.byref(p)), "zk_prover_create")
+        return cls(comm, [p], rank, world)
+
+    def prove(self, trace: np.ndarray, pub, options: ProofOptions = REFERENCE_OPTIONS, record: bool = False):
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        n = trace.shape[1]
+        opt = options.to_c()
+        cap = 4 << 20
+        buf = C.create_string_buffer(cap)
+        plen = C.c_size_t(cap)
+        rec = Record() if record else None
+        arr = (C.c_void_p * len(self.provers))(*[p.value for p in self.provers])
+        rc = lib().zk_prove_sharded(self.comm, arr, len(self.provers), trace.ctypes.data, n, C.byref(opt),
+                                    C.byref(pub), buf, C.byref(plen), C.byref(rec) if rec is not None else None)
+        check(rc, "zk_prove_sharded")
+        return buf.raw[:plen.value], rec
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 32)()
+        ms = (C.c_float * 32)()
+        cnt = C.c_int(0)
+        lib().zk_prover_stage_times(self.provers[0], names, ms, 32, C.byref(cnt))
+        return {names[i].decode(): ms[i] for i in range(cnt.value)}
+
+    def close(self):
+        for p in self.provers:
+            lib().zk_prover_destroy(p)
+        self.provers = []
+        if self.comm:
+            lib().zk_comm_destroy(self.comm)
+            self.comm = None

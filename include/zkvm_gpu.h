@@ -146,6 +146,22 @@ void zk_lde_free(zk_trace_lde *lde);
 int zk_eval_constraints(zk_trace_lde *lde, const zk_pub_inputs *pub, const uint8_t *coeff_t, const uint8_t *coeff_b,
                         uint8_t *out);
 
+/* ---- one proof sharded over several GPUs ----
+ * The LDE domain is split by coset: rank g of `world` (1, 2, 4 or 8; blowup 8) owns cosets
+ * r = g (mod world).  Exchanges (leaf digests, composition coefficient slices, FRI layer 1, openings)
+ * go through a zk_comm: RCCL over xGMI with one process per GPU (zk_comm_unique_id on rank 0,
+ * shared out of band, then zk_comm_create_rccl on every rank), or an in-process loopback that drives
+ * every rank from one process (tests; one prover per rank).  Every rank passes the same host trace;
+ * every rank receives the same proof bytes, identical to zk_prove's. */
+typedef struct zk_comm zk_comm;
+int zk_comm_create_loopback(int world, zk_comm **out);
+int zk_comm_unique_id(uint8_t id[128]);
+int zk_comm_create_rccl(const uint8_t id[128], int rank, int world, int device, zk_comm **out);
+void zk_comm_destroy(zk_comm *comm);
+int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
+                     const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
+                     zk_record *rec);
+
 /* ---- per-stage timing of the last proof (ms), for benchmarks ---- */
 int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, int *count);
 /* per-kernel device time (HIP events on the prover's stream) and algorithmic HBM bytes accumulated
