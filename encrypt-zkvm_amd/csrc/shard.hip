@@ -273,7 +273,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         zk_prover *p = X.P[l];
         Plan *pl = X.pl[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
+        if (trace) ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
         ntt(p->st, pl->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
         for (int j = 0; j < Bl; j++)
             ntt(p->st, pl->Tn, p->polys, n, p->lde + j * n, (size_t)Bl * n, W, false, &pl->coset[X.rank[l] + G * j],
@@ -646,7 +646,7 @@ void zk_comm_destroy(zk_comm *c) { delete c; }
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec) {
-    if (!comm || !provers || !trace || !proof_len || nlocal <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (!comm || !provers || !proof_len || nlocal <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     if (comm->loopback() ? nlocal != comm->world : nlocal != 1)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator needs one prover per rank, an RCCL one exactly one");
     Ctx X;

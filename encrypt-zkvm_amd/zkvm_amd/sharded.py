@@ -50,16 +50,31 @@ class ShardedProver:
         check(lib().zk_prover_create(device, max_trace_len, 8, C.byref(p)), "zk_prover_create")
         return cls(comm, [p], rank, world)
 
-    def prove(self, trace: np.ndarray, pub, options: ProofOptions = REFERENCE_OPTIONS, record: bool = False):
+    def upload_trace(self, trace: np.ndarray) -> int:
+        """Copy the trace into every local prover's device trace buffer (then prove(None, n=...))."""
+        from .prover import _hip
         trace = np.ascontiguousarray(trace, dtype=np.uint64)
-        n = trace.shape[1]
+        for p in self.provers:
+            d = C.c_void_p()
+            check(lib().zk_prover_trace_buffer(p, C.byref(d)), "zk_prover_trace_buffer")
+            rc = _hip().hipMemcpy(d, trace.ctypes.data_as(C.c_void_p), trace.nbytes, 1)
+            if rc != 0:
+                raise native.ZkError(native.ZK_ERR_DEVICE, f"hipMemcpy failed ({rc})")
+        return trace.shape[1]
+
+    def prove(self, trace, pub, options: ProofOptions = REFERENCE_OPTIONS, record: bool = False, n: int = 0):
+        """trace: (28, n, 2) uint64 host array, or None with n= to prove the uploaded trace."""
+        if trace is not None:
+            trace = np.ascontiguousarray(trace, dtype=np.uint64)
+            n = trace.shape[1]
         opt = options.to_c()
         cap = 4 << 20
         buf = C.create_string_buffer(cap)
         plen = C.c_size_t(cap)
         rec = Record() if record else None
         arr = (C.c_void_p * len(self.provers))(*[p.value for p in self.provers])
-        rc = lib().zk_prove_sharded(self.comm, arr, len(self.provers), trace.ctypes.data, n, C.byref(opt),
+        rc = lib().zk_prove_sharded(self.comm, arr, len(self.provers),
+                                    trace.ctypes.data if trace is not None else None, n, C.byref(opt),
                                     C.byref(pub), buf, C.byref(plen), C.byref(rec) if rec is not None else None)
         check(rc, "zk_prove_sharded")
         return buf.raw[:plen.value], rec

@@ -151,8 +151,9 @@ int zk_eval_constraints(zk_trace_lde *lde, const zk_pub_inputs *pub, const uint8
  * r = g (mod world).  Exchanges (leaf digests, composition coefficient slices, FRI layer 1, openings)
  * go through a zk_comm: RCCL over xGMI with one process per GPU (zk_comm_unique_id on rank 0,
  * shared out of band, then zk_comm_create_rccl on every rank), or an in-process loopback that drives
- * every rank from one process (tests; one prover per rank).  Every rank passes the same host trace;
- * every rank receives the same proof bytes, identical to zk_prove's. */
+ * every rank from one process (tests; one prover per rank).  Every rank passes the same host trace
+ * (or NULL: the trace already sits in each prover's zk_prover_trace_buffer); every rank receives the
+ * same proof bytes, identical to zk_prove's. */
 typedef struct zk_comm zk_comm;
 int zk_comm_create_loopback(int world, zk_comm **out);
 int zk_comm_unique_id(uint8_t id[128]);

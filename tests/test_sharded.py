@@ -77,6 +77,22 @@ def test_sharded_matches_single_gpu_2_14(world):
     assert hashlib.sha256(got).hexdigest() == hashlib.sha256(single).hexdigest()
 
 
+@pytest.mark.gpu
+def test_sharded_rccl_world1_and_device_trace():
+    """The RCCL communicator (one rank on this GPU) and the device-resident trace path."""
+    c = next(c for c in CASES if c["name"] == "cipher20")
+    trace, proof, pub, opts = case_inputs(c)
+    sp = ShardedProver.rccl(0, 1, ShardedProver.unique_id(), 0, trace.shape[1])
+    try:
+        got, _ = sp.prove(trace, pub, opts)
+        assert got == proof
+        n = sp.upload_trace(trace)
+        got2, _ = sp.prove(None, pub, opts, n=n)
+        assert got2 == proof
+    finally:
+        sp.close()
+
+
 def test_sharded_rejects_bad_world():
     import ctypes as C
     comm = C.c_void_p()
