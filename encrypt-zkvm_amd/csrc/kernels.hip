@@ -455,38 +455,42 @@ void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b
 // ================================================================ batch inversion
 // out[i] = 1 / ((x_i - a)(x_i - b)), x_i = xr[i & (B-1)] * w_n^(i >> log_b), via Montgomery's trick
 // over K elements per thread (strided by the grid so every store is coalesced).
-constexpr int INV_K = 16;
+// Montgomery's trick over INV_K elements per thread (strided by the thread count T for coalescing):
+// the running products are parked in `out` itself, so K can be large (one inversion per 64 elements)
+// without holding them in registers.
+#ifndef ZK_INV_K
+#define ZK_INV_K 64
+#endif
+constexpr int INV_K = ZK_INV_K;
+
+__device__ __forceinline__ fe inv_pair_denominator(const fe *xr, const fe *wlo, const fe *whi, size_t i, int log_n,
+                                                   fe a, fe b) {
+    const fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (((size_t)1 << log_n) - 1)));
+    return fe_mul(fe_sub(x, a), fe_sub(x, b));
+}
 
 __global__ void __launch_bounds__(256) k_batch_inv_pairs(const fe *xr, int log_b, int log_n, const fe *wlo,
                                                          const fe *whi, fe a, fe b, fe *out, size_t total_threads) {
     const size_t N = (size_t)1 << (log_n + log_b);
-    const size_t n = (size_t)1 << log_n;
+    const size_t T = total_threads;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= total_threads) return;
-    fe pre[INV_K];
+    if (t >= T) return;
     fe acc = fe_one();
-#pragma unroll
+#pragma unroll 4
     for (int k = 0; k < INV_K; k++) {
-        size_t i = t + (size_t)k * total_threads;  // coset-major: coset i >> log_n, position i % n
-        fe d = fe_one();
+        const size_t i = t + (size_t)k * T;  // coset-major: coset i >> log_n, position i % n
         if (i < N) {
-            fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (n - 1)));
-            d = fe_mul(fe_sub(x, a), fe_sub(x, b));
+            acc = fe_mul(acc, inv_pair_denominator(xr, wlo, whi, i, log_n, a, b));
+            out[i] = acc;
         }
-        acc = fe_mul(acc, d);
-        pre[k] = acc;
     }
     fe inv = fe_inv(acc);
-#pragma unroll
+#pragma unroll 4
     for (int k = INV_K - 1; k >= 0; k--) {
-        size_t i = t + (size_t)k * total_threads;
-        fe d = fe_one();
-        if (i < N) {
-            fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (n - 1)));
-            d = fe_mul(fe_sub(x, a), fe_sub(x, b));
-        }
-        fe r = k > 0 ? fe_mul(inv, pre[k - 1]) : inv;
-        if (i < N) out[i] = r;
+        const size_t i = t + (size_t)k * T;
+        if (i >= N) continue;
+        const fe d = inv_pair_denominator(xr, wlo, whi, i, log_n, a, b);
+        out[i] = k > 0 ? fe_mul(inv, out[i - T]) : inv;
         inv = fe_mul(inv, d);
     }
 }
@@ -951,22 +955,53 @@ void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const
 // ================================================================ FRI fold (K7)
 // next[r] = p_r(alpha), p_r of degree < fold interpolating the layer values at x_r * zeta^k:
 //   p_r(alpha) = (1/fold) * sum_m V_m (alpha / x_r)^m,  V_m = sum_k v_k zeta^(-k m)
-__global__ void __launch_bounds__(256) k_fri_fold(const fe *layer, size_t L, int fold, const FoldConsts *F,
-                                                  const fe *wi_lo, const fe *wi_hi, size_t wstride, fe *next) {
-    const size_t rows = L / fold;
-    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
-        fe v[16];
-        for (int k = 0; k < fold; k++) v[k] = layer[r + (size_t)k * rows];
-        // beta = alpha / x_r, x_r = offset * w_L^r  ->  1/x_r = offset^-1 * w_L^-r = offset^-1 * w_N^(-r*wstride)
-        fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
-        // V_m via a direct DFT for the general fold (fold <= 16); Horner in beta
-        fe acc = fe_zero();
-        for (int m = fold - 1; m >= 0; m--) {
-            fe Vm = fe_zero();
-            for (int k = 0; k < fold; k++) Vm = fe_add(Vm, fe_mul(v[k], F->zinv[(k * m) & (fold - 1)]));
-            acc = fe_add(fe_mul(acc, beta), Vm);
+// V_m = sum_k v_k * zeta^(-k m), m < F: in-register radix-2 DIT on bit-reversed input (zinv[t] = zeta^-t);
+// the j = 0 twiddles are compile-time 1, so F = 8 costs 5 multiplies instead of 64.
+template <int F>
+__device__ __forceinline__ void idft_small(fe v[F], const fe *zinv) {
+    constexpr int LOGF = F == 2 ? 1 : F == 4 ? 2 : F == 8 ? 3 : 4;
+    fe w[F];
+#pragma unroll
+    for (int k = 0; k < F; k++) {
+        int r = 0;
+#pragma unroll
+        for (int b = 0; b < LOGF; b++) r |= ((k >> b) & 1) << (LOGF - 1 - b);
+        w[r] = v[k];
+    }
+#pragma unroll
+    for (int len = 2; len <= F; len <<= 1) {
+#pragma unroll
+        for (int start = 0; start < F; start += len) {
+#pragma unroll
+            for (int j = 0; j < len / 2; j++) {
+                const fe u = w[start + j];
+                const fe t = j == 0 ? w[start + j + len / 2] : fe_mul(w[start + j + len / 2], zinv[j * (F / len)]);
+                w[start + j] = fe_add(u, t);
+                w[start + j + len / 2] = fe_sub(u, t);
+            }
         }
-        next[r] = fe_mul(acc, F->inv_fold);
+    }
+#pragma unroll
+    for (int k = 0; k < F; k++) v[k] = w[k];
+}
+
+// One FRI fold: row r = [e(r + k*rows)] at x_r * zeta^k -> the degree-respecting projection at alpha:
+// sum_m V_m (alpha / x_r)^m / F, with x_r = offset * w_L^r.
+template <int F>
+__global__ void __launch_bounds__(256) k_fri_fold(const fe *layer, size_t L, const FoldConsts *Fc, const fe *wi_lo,
+                                                  const fe *wi_hi, size_t wstride, fe *next) {
+    const size_t rows = L / F;
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
+        fe v[F];
+#pragma unroll
+        for (int k = 0; k < F; k++) v[k] = layer[r + (size_t)k * rows];
+        // beta = alpha / x_r, 1/x_r = offset^-1 * w_L^-r = offset^-1 * w_N^(-r*wstride)
+        const fe beta = fe_mul(Fc->alpha, fe_mul(Fc->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
+        idft_small<F>(v, Fc->zinv);
+        fe acc = v[F - 1];
+#pragma unroll
+        for (int m = F - 2; m >= 0; m--) acc = fe_add(fe_mul(acc, beta), v[m]);
+        next[r] = fe_mul(acc, Fc->inv_fold);
     }
 }
 
@@ -974,8 +1009,15 @@ void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const 
                      const NttTables &TN, size_t wstride, fe *next) {
     unsigned blocks = cdiv(L / fold, 256);
     if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "fri_fold", 16.0 * L + 16.0 * (L / fold), hipLaunchKernelGGL(k_fri_fold, dim3(blocks), dim3(256), 0, st, layer, L, fold,
-                                               (const FoldConsts *)fold_consts_dev, TN.inv_lo, TN.inv_hi, wstride, next));
+    const FoldConsts *F = (const FoldConsts *)fold_consts_dev;
+#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold", 16.0 * L + 16.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, next))
+    switch (fold) {
+        case 2: ZK_FOLD(2); break;
+        case 4: ZK_FOLD(4); break;
+        case 8: ZK_FOLD(8); break;
+        default: ZK_FOLD(16); break;
+    }
+#undef ZK_FOLD
 }
 
 // ================================================================ elementwise helpers

@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
     for (int k = 0; k < fold; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
     const fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
     fe acc = fe_zero();
-    for (int mm = fold - 1; mm >= 0; mm--) {
+    for (int mm = fold - 1; mm >= 0; mm--) {  // direct form: this fold runs once per proof on 1/G of layer 0
         fe Vm = fe_zero();
         for (int k = 0; k < fold; k++) Vm = fe_add(Vm, fe_mul(v[k], F->zinv[(k * mm) & (fold - 1)]));
         acc = fe_add(fe_mul(acc, beta), Vm);
