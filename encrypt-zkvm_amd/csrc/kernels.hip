@@ -327,6 +327,32 @@ void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out) {
     hipLaunchKernelGGL(k_pow_expand, dim3(std::min<size_t>(cdiv(n, 256), 65536)), dim3(256), 0, st, lo, hi, n, out);
 }
 
+// ================================================================ grinding (proof of work)
+// nonce candidates start .. start+count: BLAKE3(seed || nonce_le64) (one 40-byte block) whose first
+// u64 has >= bits trailing zeros; the smallest such nonce wins (winterfell searches from 1 upward).
+__global__ void k_grind(const uint32_t *seed, uint64_t start, uint32_t count, int bits, unsigned long long *best) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t nonce = start + t;
+    uint32_t m[16], cv[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = seed[i];
+    m[8] = (uint32_t)nonce;
+    m[9] = (uint32_t)(nonce >> 32);
+#pragma unroll
+    for (int i = 10; i < 16; i++) m[i] = 0;
+    b3::iv(cv);
+    b3::compress(cv, m, 0, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    const uint64_t head = (uint64_t)cv[0] | ((uint64_t)cv[1] << 32);
+    const int tz = head ? __builtin_ctzll(head) : 64;
+    if (tz >= bits) atomicMin(best, (unsigned long long)nonce);
+}
+
+void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,
+                  unsigned long long *best_dev) {
+    ZK_PROF(st, "grind", 0.0, hipLaunchKernelGGL(k_grind, dim3(cdiv(count, 256)), dim3(256), 0, st, seed_dev, start, count, bits, best_dev));
+}
+
 // ================================================================ hashing and Merkle trees
 __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t h[8]) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);

@@ -472,20 +472,43 @@ int zk::remainder_step(std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R
     return ZK_OK;
 }
 
-std::vector<uint64_t> zk::grind_and_positions(Coin &coin, const zk_options *opt, size_t N, zk_record &R) {
+static bool nonce_ok(const uint8_t seed[32], uint64_t nonce, uint32_t bits) {
+    uint8_t d[32];
+    Coin::merge_with_int(seed, nonce, d);
+    uint64_t head;
+    memcpy(&head, d, 8);
+    const unsigned tz = head ? (unsigned)__builtin_ctzll(head) : 64;
+    return tz >= bits;
+}
+
+int zk::grind_and_positions(zk_prover *p, Coin &coin, const zk_options *opt, size_t N, zk_record &R,
+                            std::vector<uint64_t> &pos) {
     uint64_t nonce = 1;
-    for (;; nonce++) {
-        uint8_t d[32];
-        Coin::merge_with_int(coin.seed, nonce, d);
-        uint64_t head;
-        memcpy(&head, d, 8);
-        unsigned tz = head ? (unsigned)__builtin_ctzll(head) : 64;
-        if (tz >= opt->grinding) break;
+    if (p && opt->grinding >= 8) {
+        // ~2^grinding BLAKE3 calls: search batches of 2^22 nonces on the GPU, smallest hit wins
+        if (!p->pow_seed) {
+            ZK_CHECK_HIP(p->arena.alloc(&p->pow_seed, 8));
+            ZK_CHECK_HIP(p->arena.alloc(&p->pow_best, 1));
+        }
+        ZK_CHECK_HIP(hipMemcpyAsync(p->pow_seed, coin.seed, 32, hipMemcpyHostToDevice, p->st));
+        const unsigned long long none = ~0ULL;
+        unsigned long long best = none;
+        ZK_CHECK_HIP(hipMemcpyAsync(p->pow_best, &none, 8, hipMemcpyHostToDevice, p->st));
+        const uint32_t batch = 1u << 22;
+        for (uint64_t start = 1; best == none; start += batch) {
+            grind_launch(p->st, p->pow_seed, start, batch, (int)opt->grinding, p->pow_best);
+            ZK_CHECK_HIP(hipMemcpyAsync(&best, p->pow_best, 8, hipMemcpyDeviceToHost, p->st));
+            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        }
+        nonce = best;
+        if (!nonce_ok(coin.seed, nonce, opt->grinding)) ZK_FAIL(ZK_ERR_DEVICE, "GPU grinding returned an invalid nonce");
+    } else {
+        while (!nonce_ok(coin.seed, nonce, opt->grinding)) nonce++;
     }
     R.pow_nonce = nonce;
     Coin::merge_with_int(coin.seed, nonce, coin.seed);
     coin.counter = 0;
-    std::vector<uint64_t> pos;
+    pos.clear();
     for (uint32_t q = 0; q < opt->num_queries; q++) {
         uint8_t d[32];
         coin.next(d);
@@ -497,7 +520,7 @@ std::vector<uint64_t> zk::grind_and_positions(Coin &coin, const zk_options *opt,
     pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
     R.num_positions = (uint32_t)pos.size();
     memcpy(R.positions, pos.data(), pos.size() * 8);
-    return pos;
+    return ZK_OK;
 }
 
 std::vector<std::vector<uint64_t>> zk::fri_fold_positions(const std::vector<uint64_t> &pos, size_t N, uint32_t fold,
@@ -738,7 +761,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "fri");
 
     // S7: grinding and query positions [P10, P11]
-    const std::vector<uint64_t> pos = grind_and_positions(coin, opt, N, R);
+    std::vector<uint64_t> pos;
+    ZK_TRY(grind_and_positions(p, coin, opt, N, R, pos));
     const size_t nu = pos.size();
     const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
 

@@ -96,6 +96,8 @@ struct zk_prover {
     fe *sh_zero = nullptr;      // one zero chunk (stands in for openings another rank owns)
     uint8_t *sh_roots = nullptr;  // world subtree roots
     unsigned *sh_flags = nullptr;  // world degree flags
+    uint32_t *pow_seed = nullptr;            // grinding: the coin seed ...
+    unsigned long long *pow_best = nullptr;  // ... and the smallest nonce found
     std::map<std::pair<int, int>, std::unique_ptr<zk::Plan>> plans;
     // stage timing
     std::vector<std::pair<const char *, hipEvent_t>> stage_ev;
@@ -160,8 +162,10 @@ int fri_num_layers(size_t N, const zk_options *opt);
 FoldConsts fold_consts(fe alpha, uint32_t fold);
 // S6: interpolate the last layer (natural order, over 3 * <w_L>), keep L/B coefficients, commit [P9]
 int remainder_step(std::vector<fe> &last, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag);
-// S7: grinding nonce and the sorted unique query positions [P10, P11]
-std::vector<uint64_t> grind_and_positions(Coin &coin, const zk_options *opt, size_t N, zk_record &R);
+// S7: grinding nonce (on the GPU of `p` for grinding >= 8, else on the host) and the sorted unique
+// query positions [P10, P11]
+int grind_and_positions(zk_prover *p, Coin &coin, const zk_options *opt, size_t N, zk_record &R,
+                        std::vector<uint64_t> &pos);
 // positions folded down the FRI layers, first-occurrence order [P12]
 std::vector<std::vector<uint64_t>> fri_fold_positions(const std::vector<uint64_t> &pos, size_t N, uint32_t fold,
                                                       int nl);

@@ -499,7 +499,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     stage_mark(P0, "fri");
 
     // S7 / S8: positions, then every rank gathers the chunks it owns; all-gather; the host combines
-    const std::vector<uint64_t> pos = grind_and_positions(coin, opt, N, R);
+    std::vector<uint64_t> pos;
+    ZK_TRY(grind_and_positions(P0, coin, opt, N, R, pos));
     const size_t nu = pos.size();
     const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
     Openings O;

@@ -80,6 +80,10 @@ void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out);
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride,
          int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp);
 
+// grinding: atomicMin into *best_dev of the nonces in [start, start+count) with >= bits trailing zeros
+void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,
+                  unsigned long long *best_dev);
+
 // ---------------------------------------------------------------- hashing
 // leaf[i] = BLAKE3(row i) for natural LDE index i < N = B*n of a coset-major column set:
 // element (column c, index i) lives at base[(c*B + i%B)*n + i/B].

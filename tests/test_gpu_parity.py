@@ -97,7 +97,8 @@ CASES = [("push.5\npush.3\nadd", ProofOptions()), (LR_PROGRAM, ProofOptions()),
          (push_add_program(200), ProofOptions()), (cipher_mix_program(60)[0], ProofOptions()),
          (cipher_mix_program(60)[0], ProofOptions(num_queries=40, blowup_factor=16, fri_folding_factor=4,
                                                   fri_remainder_max_degree=31, grinding_factor=4)),
-         (ops_for_trace_len(14, "cipher"), ProofOptions())]
+         (ops_for_trace_len(14, "cipher"), ProofOptions()),
+         (LR_PROGRAM, ProofOptions(num_queries=20, grinding_factor=18))]  # GPU proof-of-work search
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
