@@ -176,6 +176,8 @@ def main():
         C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
         opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
         verified = orc.verify(proof, opub, 95)[0] == 0
+    from zkvm_amd.prover import verify as zk_verify
+    zk_verified = zk_verify(proof, pub, 95)[0] == 0
 
     if rank != 0:
         if pg is not None:
@@ -206,7 +208,7 @@ def main():
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
-        "proof_bytes": len(proof), "proof_verified_by_oracle": verified,
+        "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
     }
     print(json.dumps(out), flush=True)
     if pg is not None:

@@ -181,6 +181,13 @@ class ExecutionProver:
 
 
 # ------------------------------------------------------------------ VM harness (vm::prove)
+def verify(proof: bytes, pub: PubInputs, min_security: int = 95) -> tuple[int, str]:
+    """winterfell::verify (vm/src/lib.rs:93-98) for this library's proofs, on the host: (status, reason)."""
+    msg = C.create_string_buffer(256)
+    rc = lib().zk_verify(proof, len(proof), C.byref(pub), min_security, msg, 256)
+    return rc, msg.value.decode()
+
+
 def vm_trace(source: str, public, secret, server_key, last_row):
     """Processor::run + trace (vm/src/processor/mod.rs:61-95) via the native VM.
     Returns (trace (28, n, 2) uint64, outputs[16], program_hash[2])."""

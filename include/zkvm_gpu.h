@@ -36,6 +36,7 @@ extern "C" {
 #define ZK_ERR_STACK -11    /* StackError (vm/src/processor/errors.rs:4-42) */
 #define ZK_ERR_CHIPLETS -12 /* ChipletsError (vm/src/processor/errors.rs:44-71) */
 #define ZK_ERR_DEGREE -20   /* proof written, but the trace does not satisfy ProcessorAir */
+#define ZK_ERR_VERIFY -30   /* zk_verify: the proof is rejected (reason in msg) */
 
 #define ZK_TRACE_WIDTH 28
 #define ZK_MAX_COLS 32
@@ -162,6 +163,13 @@ void zk_comm_destroy(zk_comm *comm);
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec);
+
+/* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
+ * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required
+ * (the reference's test asks 95 for its options).  Returns ZK_OK, or ZK_ERR_VERIFY with the reason in
+ * msg. */
+int zk_verify(const uint8_t *proof, size_t proof_len, const zk_pub_inputs *pub, uint32_t min_security, char *msg,
+              size_t msg_cap);
 
 /* ---- per-stage timing of the last proof (ms), for benchmarks ---- */
 int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, int *count);

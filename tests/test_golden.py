@@ -155,6 +155,27 @@ def test_oracle_verifier_accepts_and_rejects(oracle, c):
         assert oracle.verify(proof, wrong, 0)[0] != 0
 
 
+@pytest.mark.parametrize("c", CASES, ids=IDS)
+def test_product_verifier_accepts_and_rejects(c):
+    """zk_verify (the library's host verifier) on the golden proofs, tampered copies and wrong inputs."""
+    from zkvm_amd.prover import verify
+    _, proof, pub = load_case(c)
+    assert verify(proof, pub, 0) == (0, "")
+    for off in (40, len(proof) // 3, len(proof) // 2, (2 * len(proof)) // 3, len(proof) - 12):
+        bad = bytearray(proof)
+        bad[off] ^= 0x01
+        rc, why = verify(bytes(bad), pub, 0)
+        assert rc == native.ZK_ERR_VERIFY and why, f"tampered byte {off} accepted"
+    assert verify(proof[:-1], pub, 0)[0] == native.ZK_ERR_VERIFY
+    wrong = make_pub_inputs(ints(c["program_hash"]), [1] + ints(c["stack_outputs"])[1:], c["lwe_size"], c["delta"])
+    if ints(c["stack_outputs"])[0] != 1:
+        assert verify(proof, wrong, 0)[0] == native.ZK_ERR_VERIFY
+    # conjectured security of the reference options is 95 bits (BASELINE.md)
+    if c["options"] == {"num_queries": 32, "blowup": 8, "grinding": 0, "field_extension": 1, "fri_folding": 8,
+                        "fri_rem_max_deg": 127}:
+        assert verify(proof, pub, 95)[0] == 0 and verify(proof, pub, 96)[0] == native.ZK_ERR_VERIFY
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("c", CASES, ids=IDS)
 def test_gpu_reproduces_golden_proof(c):
