@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "blake3.hpp"
+#include "ext2.hpp"
 #include "f128.hpp"
 
 namespace zk {
@@ -126,6 +127,17 @@ struct Coin {
             if (fe_canonical(v)) return v;
         }
         return fe_zero();
+    }
+    // draw::<E>: E::ELEMENT_BYTES of the next digest, retried until every component is canonical
+    // (k = 1: the first 16 bytes, identical to draw(); k = 2: both 16-byte halves)
+    fe2 draw_ext(int k) {
+        for (int i = 0; i < 1000; i++) {
+            uint8_t d[32];
+            next(d);
+            const fe a = fe_from_bytes(d), b = k == 2 ? fe_from_bytes(d + 16) : fe_zero();
+            if (fe_canonical(a) && fe_canonical(b)) return fe2{a, b};
+        }
+        return fe2_zero();
     }
 };
 

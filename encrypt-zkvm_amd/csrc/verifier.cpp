@@ -3,7 +3,8 @@
 // examples/linear_regression/src/main.rs:85), restated for ProcessorAir and the proof layout of
 // DESIGN.md "Protocol profile" (P1-P14).
 //
-// Checks: proof context and conjectured security (winter-air: min(128 - log2 N, log2(B) * q
+// Both FieldExtension::None and Quadratic (every E value is an fe2; base values carry b = 0).
+// Checks: proof context and conjectured security (winter-air: min(128*k - log2 N, log2(B) * q
 // [+ grinding when the query bound is >= 80]) - 1), the transcript, every batch Merkle opening
 // (trace, composition, FRI layers), the out-of-domain identity H(z) = sum_j z^(jn) H_j(z) against
 // ProcessorAir::evaluate_transition at z (air/src/lib.rs:104-168, constrains.rs:95-216) and the
@@ -155,67 +156,71 @@ void check_batch(const uint8_t *bytes, size_t blen, const std::vector<std::array
 }
 
 fe mds_entry(const uint64_t m[16][2], int i) { return fe_make(m[i][0], m[i][1]); }
-fe cube(fe x) { return fe_mul(fe_mul(x, x), x); }
+fe2 cube(fe2 x) { return fe2_mul(fe2_mul(x, x), x); }
 
-// ProcessorAir::evaluate_transition (air/src/lib.rs:104-168) at one frame; per = 9 periodic values
-void air_eval(const fe *cur, const fe *nxt, const fe *per, uint32_t L, fe delta, fe *out) {
-    const fe one = fe_one();
-    auto nt = [&](fe b) { return fe_sub(one, b); };
-    const fe b0 = cur[5], b1 = cur[4], b2 = cur[3], b3 = cur[2], b4 = cur[1];
-    auto sel = [&](fe a, fe b, fe c, fe d, fe e) { return fe_mul(fe_mul(fe_mul(fe_mul(a, b), c), d), e); };
-    const fe is_add = sel(nt(b0), b1, nt(b2), nt(b3), nt(b4)), is_sadd = sel(nt(b0), b1, nt(b2), b3, nt(b4));
-    const fe is_add2 = sel(nt(b0), b1, nt(b2), b3, b4), is_mul = sel(nt(b0), b1, nt(b2), nt(b3), b4);
-    const fe is_smul = sel(nt(b0), b1, b2, nt(b3), nt(b4)), is_push = sel(b0, nt(b1), nt(b2), nt(b3), nt(b4));
-    const fe is_read = sel(b0, nt(b1), nt(b2), nt(b3), b4), is_read2 = sel(b0, nt(b1), nt(b2), b3, nt(b4));
-    const fe is_noop = sel(nt(b0), nt(b1), nt(b2), nt(b3), nt(b4));
-    fe opcode = b0;
-    for (fe b : {b1, b2, b3, b4}) opcode = fe_add(fe_add(opcode, opcode), b);
-    const fe *s = cur + 12, *sn = nxt + 12;
+// ProcessorAir::evaluate_transition (air/src/lib.rs:104-168) at one frame over E (the verifier's
+// evaluate_transition<E>, E = f128 or its quadratic extension); per = 9 periodic values
+void air_eval(const fe2 *cur, const fe2 *nxt, const fe2 *per, uint32_t L, fe delta, fe2 *out) {
+    const fe2 one = fe2_one();
+    auto nt = [&](fe2 b) { return fe2_sub(one, b); };
+    auto mul = fe2_mul;
+    auto add = fe2_add;
+    auto sub = fe2_sub;
+    const fe2 b0 = cur[5], b1 = cur[4], b2 = cur[3], b3 = cur[2], b4 = cur[1];
+    auto sel = [&](fe2 a, fe2 b, fe2 c, fe2 d, fe2 e) { return mul(mul(mul(mul(a, b), c), d), e); };
+    const fe2 is_add = sel(nt(b0), b1, nt(b2), nt(b3), nt(b4)), is_sadd = sel(nt(b0), b1, nt(b2), b3, nt(b4));
+    const fe2 is_add2 = sel(nt(b0), b1, nt(b2), b3, b4), is_mul = sel(nt(b0), b1, nt(b2), nt(b3), b4);
+    const fe2 is_smul = sel(nt(b0), b1, b2, nt(b3), nt(b4)), is_push = sel(b0, nt(b1), nt(b2), nt(b3), nt(b4));
+    const fe2 is_read = sel(b0, nt(b1), nt(b2), nt(b3), b4), is_read2 = sel(b0, nt(b1), nt(b2), b3, nt(b4));
+    const fe2 is_noop = sel(nt(b0), nt(b1), nt(b2), nt(b3), nt(b4));
+    fe2 opcode = b0;
+    for (fe2 b : {b1, b2, b3, b4}) opcode = add(add(opcode, opcode), b);
+    const fe2 *s = cur + 12, *sn = nxt + 12;
     const fe four = fe_make(4);
-    out[0] = fe_sub(nxt[0], fe_add(cur[0], one));
-    out[1] = fe_add(fe_sub(fe_add(fe_sub(fe_sub(nxt[11], cur[11]), b0), b1), fe_mul(is_read2, four)), fe_mul(is_add2, four));
-    out[2] = fe_mul(b0, b1);
-    out[3] = fe_mul(is_add, fe_sub(sn[0], fe_add(s[0], s[1])));
-    fe a4 = fe_zero(), a5 = fe_zero(), a7 = fe_zero();
+    out[0] = sub(nxt[0], add(cur[0], one));
+    out[1] = add(sub(add(sub(sub(nxt[11], cur[11]), b0), b1), fe2_mulb(is_read2, four)), fe2_mulb(is_add2, four));
+    out[2] = mul(b0, b1);
+    out[3] = mul(is_add, sub(sn[0], add(s[0], s[1])));
+    fe2 a4 = fe2_zero(), a5 = fe2_zero(), a7 = fe2_zero();
     for (uint32_t i = 0; i < L; i++) {
-        const fe triv = i == L - 1 ? fe_mul(delta, s[0]) : fe_zero();  // encrypt_trivial (server_key.rs)
-        a4 = fe_add(a4, fe_sub(sn[i], fe_add(s[1 + i], triv)));
-        a5 = fe_add(a5, fe_sub(sn[i], fe_add(s[i], s[L + i])));
-        a7 = fe_add(a7, fe_sub(sn[i], fe_mul(s[1 + i], s[0])));
+        const fe2 triv = i == L - 1 ? fe2_mulb(s[0], delta) : fe2_zero();  // encrypt_trivial (server_key.rs)
+        a4 = add(a4, sub(sn[i], add(s[1 + i], triv)));
+        a5 = add(a5, sub(sn[i], add(s[i], s[L + i])));
+        a7 = add(a7, sub(sn[i], mul(s[1 + i], s[0])));
     }
-    out[4] = fe_mul(is_sadd, a4);
-    out[5] = fe_mul(is_add2, a5);
-    out[6] = fe_mul(is_mul, fe_sub(sn[0], fe_mul(s[0], s[1])));
-    out[7] = fe_mul(is_smul, a7);
-    out[8] = fe_mul(is_push, fe_sub(sn[1], s[0]));
-    out[9] = fe_mul(is_read, fe_sub(sn[1], s[0]));
-    out[10] = fe_mul(is_read2, fe_sub(sn[5], s[0]));
-    out[11] = fe_mul(is_noop, fe_sub(sn[0], s[0]));
-    const fe hf = per[0], h0 = cur[6];
-    fe x[4], m0[4], y[4];
+    out[4] = mul(is_sadd, a4);
+    out[5] = mul(is_add2, a5);
+    out[6] = mul(is_mul, sub(sn[0], mul(s[0], s[1])));
+    out[7] = mul(is_smul, a7);
+    out[8] = mul(is_push, sub(sn[1], s[0]));
+    out[9] = mul(is_read, sub(sn[1], s[0]));
+    out[10] = mul(is_read2, sub(sn[5], s[0]));
+    out[11] = mul(is_noop, sub(sn[0], s[0]));
+    const fe2 hf = per[0], h0 = cur[6];
+    fe2 x[4], m0[4], y[4];
     for (int i = 0; i < 4; i++) x[i] = cube(cur[7 + i]);
     for (int i = 0; i < 4; i++) {
-        fe t = fe_zero();
-        for (int j = 0; j < 4; j++) t = fe_add(t, fe_mul(mds_entry(ZK_MDS, 4 * i + j), x[j]));
-        m0[i] = fe_add(t, per[1 + i]);
+        fe2 t = fe2_zero();
+        for (int j = 0; j < 4; j++) t = add(t, fe2_mulb(x[j], mds_entry(ZK_MDS, 4 * i + j)));
+        m0[i] = add(t, per[1 + i]);
     }
-    m0[0] = fe_add(m0[0], opcode);
-    m0[1] = fe_add(m0[1], fe_mul(sn[0], is_push));
-    for (int i = 0; i < 4; i++) y[i] = fe_sub(nxt[7 + i], per[5 + i]);
+    m0[0] = add(m0[0], opcode);
+    m0[1] = add(m0[1], mul(sn[0], is_push));
+    for (int i = 0; i < 4; i++) y[i] = sub(nxt[7 + i], per[5 + i]);
     for (int i = 0; i < 4; i++) {
-        fe t = fe_zero();
-        for (int j = 0; j < 4; j++) t = fe_add(t, fe_mul(mds_entry(ZK_INV_MDS, 4 * i + j), y[j]));
-        out[12 + i] = fe_mul(fe_mul(fe_sub(cube(t), m0[i]), hf), h0);
+        fe2 t = fe2_zero();
+        for (int j = 0; j < 4; j++) t = add(t, fe2_mulb(y[j], mds_entry(ZK_INV_MDS, 4 * i + j)));
+        out[12 + i] = mul(mul(sub(cube(t), m0[i]), hf), h0);
     }
-    const fe nf = fe_sub(one, hf);
-    out[16] = fe_mul(fe_mul(fe_sub(nxt[7], cur[7]), nf), h0);
-    out[17] = fe_mul(fe_mul(fe_sub(nxt[8], cur[8]), nf), h0);
-    out[18] = fe_mul(fe_mul(nxt[9], nf), h0);
-    out[19] = fe_mul(fe_mul(nxt[10], nf), h0);
+    const fe2 nf = sub(one, hf);
+    out[16] = mul(mul(sub(nxt[7], cur[7]), nf), h0);
+    out[17] = mul(mul(sub(nxt[8], cur[8]), nf), h0);
+    out[18] = mul(mul(nxt[9], nf), h0);
+    out[19] = mul(mul(nxt[10], nf), h0);
 }
 
 // periodic columns (CYCLE_MASK + 8 ARK columns, air/src/lib.rs:201-225) at a point y = z^(n/16)
-void periodic_at(fe y, fe out[9]) {
+void periodic_at(fe2 y, fe2 out[9]) {
     std::vector<std::vector<fe>> cols(9, std::vector<fe>(16));
     for (int r = 0; r < 16; r++) {
         cols[0][r] = fe_make(r < 14 ? 1 : 0);
@@ -223,8 +228,31 @@ void periodic_at(fe y, fe out[9]) {
     }
     for (int j = 0; j < 9; j++) {
         h_interp_coset(cols[j], fe_one());
-        out[j] = h_poly_eval(cols[j].data(), 16, y);
+        fe2 acc = fe2_zero();
+        for (int t = 16; t-- > 0;) acc = fe2_add(fe2_mul(acc, y), fe2_lift(cols[j][t]));
+        out[j] = acc;
     }
+}
+
+// k base components per E value (the wire order), canonical or the proof is rejected
+fe2 elem_ext(const uint8_t *b, int k) { return fe2{elem(b), k == 2 ? elem(b + 16) : fe_zero()}; }
+void flatten(const fe2 *v, size_t m, int k, std::vector<fe> &out) {
+    out.clear();
+    for (size_t i = 0; i < m; i++) {
+        out.push_back(v[i].a);
+        if (k == 2) out.push_back(v[i].b);
+    }
+}
+void hash_ext(const fe2 *v, size_t m, int k, uint8_t d[32]) {
+    std::vector<fe> f;
+    flatten(v, m, k, f);
+    hash_elems(f.data(), f.size(), d);
+}
+// sum_t c[t] x^t for E coefficients at a base point
+fe2 poly_eval_ext(const fe2 *c, size_t m, fe x) {
+    fe2 acc = fe2_zero();
+    for (size_t t = m; t-- > 0;) acc = fe2_add(fe2_mulb(acc, x), c[t]);
+    return acc;
 }
 
 void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_t min_security) {
@@ -235,17 +263,18 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
     const uint8_t *mod = r.take(mlen);
     const uint8_t nq = r.u8(), B = r.u8(), grind = r.u8(), ext = r.u8(), fold = r.u8(), remdeg = r.u8();
     const uint8_t nu = r.u8();
-    if (r.bad || width != W || auxw || auxr || mlen != 16 || ext != 1 || logn < 4 || logn > 32 || B < 8 ||
-        (B & (B - 1)) || !(fold == 2 || fold == 4 || fold == 8 || fold == 16) || ((remdeg + 1) & remdeg))
+    if (r.bad || width != W || auxw || auxr || mlen != 16 || (ext != 1 && ext != 2) || logn < 4 || logn > 32 ||
+        B < 8 || (B & (B - 1)) || !(fold == 2 || fold == 4 || fold == 8 || fold == 16) || ((remdeg + 1) & remdeg))
         fail("malformed proof context");
     uint64_t pm[2] = {ZK_P_LO, ZK_P_HI};
     if (memcmp(mod, pm, 16)) fail("field modulus mismatch");
+    const int K = ext;  // FieldExtension degree: 1 = None, 2 = Quadratic
     const size_t n = (size_t)1 << logn, N = n * B;
     const int logB = ilog2z(B), logN = logn + logB;
     {
         int q_sec = logB * nq;
         if (q_sec >= 80) q_sec += grind;
-        const int sec = std::min(std::min(128 - logN, q_sec) - 1, 128);
+        const int sec = std::min(std::min(128 * K - logN, q_sec) - 1, 128);
         if (sec < (int)min_security) fail("insufficient proof security: " + std::to_string(sec));
     }
     int nl = 0;
@@ -265,11 +294,11 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
         coin.init(e);
     }
     coin.reseed(coms);
-    fe ct[NT], cb[NA];
-    for (auto &v : ct) v = coin.draw();
-    for (auto &v : cb) v = coin.draw();
+    fe2 ct[NT], cb[NA];
+    for (auto &v : ct) v = coin.draw_ext(K);
+    for (auto &v : cb) v = coin.draw_ext(K);
     coin.reseed(coms + 32);
-    const fe z = coin.draw();
+    const fe2 z = coin.draw_ext(K);
 
     if (r.u8() != 1) fail("expected one trace segment");
     const uint32_t tvl = r.u32();
@@ -284,53 +313,57 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
     const uint8_t *ts = r.take(tsl);
     const uint16_t oel = r.u16();
     const uint8_t *oe = r.take(oel);
-    if (r.bad || tsl != 1 + 2 * W * 16 || ts[0] != 2 || oel == 0 || oel % 16 || oel / 16 > ZK_MAX_CCOLS)
+    const int ES = 16 * K;  // bytes per E value
+    if (r.bad || tsl != 1 + 2 * W * ES || ts[0] != 2 || oel == 0 || oel % ES || oel / ES > ZK_MAX_CCOLS)
         fail("malformed out-of-domain frame");
-    const int C = oel / 16;
-    std::vector<fe> ood(2 * W + C);
+    const int C = oel / ES;
+    std::vector<fe2> ood(2 * W + C);
     for (int c = 0; c < W; c++) {
-        ood[c] = elem(ts + 1 + 32 * c);
-        ood[W + c] = elem(ts + 1 + 32 * c + 16);
+        ood[c] = elem_ext(ts + 1 + 2 * ES * c, K);
+        ood[W + c] = elem_ext(ts + 1 + 2 * ES * c + ES, K);
     }
-    for (int j = 0; j < C; j++) ood[2 * W + j] = elem(oe + 16 * j);
+    for (int j = 0; j < C; j++) ood[2 * W + j] = elem_ext(oe + ES * j, K);
     {
         uint8_t d[32];
-        hash_elems(ood.data(), 2 * W, d);
+        hash_ext(ood.data(), 2 * W, K, d);
         coin.reseed(d);
-        hash_elems(ood.data() + 2 * W, C, d);
+        hash_ext(ood.data() + 2 * W, C, K, d);
         coin.reseed(d);
     }
     // out-of-domain identity
     {
-        const fe g = h_root_of_unity(logn), one = fe_one();
-        fe per[9], ev[NT];
-        periodic_at(h_pow(z, n / 16), per);
+        const fe g = h_root_of_unity(logn);
+        const fe2 one = fe2_one();
+        fe2 per[9], ev[NT];
+        periodic_at(fe2_exp(z, n / 16), per);
         air_eval(ood.data(), ood.data() + W, per, pub->lwe_size, fe_make(pub->delta), ev);
-        fe t = fe_zero();
-        for (int k = 0; k < NT; k++) t = fe_add(t, fe_mul(ct[k], ev[k]));
-        const fe gl2 = h_pow(g, n - 2), gl1 = h_pow(g, n - 1), zn = h_pow(z, n);
-        fe h = fe_mul(fe_mul(t, fe_mul(fe_sub(z, gl2), fe_sub(z, gl1))), h_inv(fe_sub(zn, one)));
+        fe2 t = fe2_zero();
+        for (int k = 0; k < NT; k++) t = fe2_add(t, fe2_mul(ct[k], ev[k]));
+        const fe2 gl2 = fe2_lift(h_pow(g, n - 2)), gl1 = fe2_lift(h_pow(g, n - 1)), zn = fe2_exp(z, n);
+        fe2 h = fe2_mul(fe2_mul(t, fe2_mul(fe2_sub(z, gl2), fe2_sub(z, gl1))), fe2_inv(fe2_sub(zn, one)));
         const int fc[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
-        fe bs0 = fe_zero(), bs1 = fe_zero();
-        for (int i = 0; i < 12; i++) bs0 = fe_add(bs0, fe_mul(cb[i], ood[fc[i]]));
-        for (int i = 0; i < 2; i++) bs1 = fe_add(bs1, fe_mul(cb[12 + i], fe_sub(ood[7 + i], fe_from_bytes(pub->program_hash[i]))));
-        for (int i = 0; i < 8; i++) bs1 = fe_add(bs1, fe_mul(cb[14 + i], fe_sub(ood[12 + i], fe_from_bytes(pub->stack_outputs[i]))));
-        h = fe_add(h, fe_mul(bs0, h_inv(fe_sub(z, one))));
-        h = fe_add(h, fe_mul(bs1, h_inv(fe_sub(z, gl2))));
-        fe hc = fe_zero(), zz = one;
+        fe2 bs0 = fe2_zero(), bs1 = fe2_zero();
+        for (int i = 0; i < 12; i++) bs0 = fe2_add(bs0, fe2_mul(cb[i], ood[fc[i]]));
+        for (int i = 0; i < 2; i++)
+            bs1 = fe2_add(bs1, fe2_mul(cb[12 + i], fe2_sub(ood[7 + i], fe2_lift(fe_from_bytes(pub->program_hash[i])))));
+        for (int i = 0; i < 8; i++)
+            bs1 = fe2_add(bs1, fe2_mul(cb[14 + i], fe2_sub(ood[12 + i], fe2_lift(fe_from_bytes(pub->stack_outputs[i])))));
+        h = fe2_add(h, fe2_mul(bs0, fe2_inv(fe2_sub(z, one))));
+        h = fe2_add(h, fe2_mul(bs1, fe2_inv(fe2_sub(z, gl2))));
+        fe2 hc = fe2_zero(), zz = one;
         for (int j = 0; j < C; j++) {
-            hc = fe_add(hc, fe_mul(zz, ood[2 * W + j]));
-            zz = fe_mul(zz, zn);
+            hc = fe2_add(hc, fe2_mul(zz, ood[2 * W + j]));
+            zz = fe2_mul(zz, zn);
         }
-        if (!fe_eq(h, hc)) fail("out-of-domain constraint evaluation mismatch");
+        if (!fe2_eq(h, hc)) fail("out-of-domain constraint evaluation mismatch");
     }
-    fe at[W], ac[ZK_MAX_CCOLS];
-    for (auto &v : at) v = coin.draw();
-    for (int j = 0; j < C; j++) ac[j] = coin.draw();
-    std::vector<fe> alphas(nl);
+    fe2 at[W], ac[ZK_MAX_CCOLS];
+    for (auto &v : at) v = coin.draw_ext(K);
+    for (int j = 0; j < C; j++) ac[j] = coin.draw_ext(K);
+    std::vector<fe2> alphas(nl);
     for (int l = 0; l < nl; l++) {
         coin.reseed(coms + 64 + 32 * l);
-        alphas[l] = coin.draw();
+        alphas[l] = coin.draw_ext(K);
     }
     coin.reseed(coms + 64 + 32 * nl);
 
@@ -348,7 +381,7 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
     const uint8_t nparts = r.u8();
     const uint8_t *nonce_b = r.take(8);
     const uint8_t gkr = r.u8();
-    if (r.bad || nparts != 0 || gkr != 0 || r.off != r.len || rml % 16) fail("malformed proof tail");
+    if (r.bad || nparts != 0 || gkr != 0 || r.off != r.len || rml % ES) fail("malformed proof tail");
     {
         uint8_t d[32];
         b3::hash_bytes(rm, rml, d);
@@ -377,29 +410,36 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
     std::sort(pos.begin(), pos.end());
     pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
     if (pos.size() != nu) fail("number of unique queries mismatch");
-    if (tvl != nu * W * 16u || cvl != nu * (uint32_t)C * 16u) fail("malformed query values");
-    std::vector<fe> tvals(nu * W), cvals(nu * C);
+    const int CK = C * K;
+    if (tvl != nu * W * 16u || cvl != nu * (uint32_t)CK * 16u) fail("malformed query values");
+    std::vector<fe> tvals(nu * W), cflat(nu * CK);
     for (size_t i = 0; i < tvals.size(); i++) tvals[i] = elem(tv + 16 * i);
-    for (size_t i = 0; i < cvals.size(); i++) cvals[i] = elem(cv + 16 * i);
+    for (size_t i = 0; i < cflat.size(); i++) cflat[i] = elem(cv + 16 * i);
     std::vector<std::array<uint8_t, 32>> dig(nu);
     for (size_t q = 0; q < nu; q++) hash_elems(tvals.data() + q * W, W, dig[q].data());
     check_batch(tp, tpl, dig, pos, logN, coms, "trace query");
-    for (size_t q = 0; q < nu; q++) hash_elems(cvals.data() + q * C, C, dig[q].data());
+    for (size_t q = 0; q < nu; q++) hash_elems(cflat.data() + q * CK, CK, dig[q].data());
     check_batch(cp, cpl, dig, pos, logN, coms + 32, "constraint query");
 
-    // DEEP values at the positions
-    std::vector<fe> evals(nu);
+    // DEEP values at the positions (in E)
+    std::vector<fe2> evals(nu);
     {
-        const fe wN = h_root_of_unity(logN), zg = fe_mul(z, h_root_of_unity(logn)), three = fe_make(3);
+        const fe wN = h_root_of_unity(logN), three = fe_make(3);
+        const fe2 zg = fe2_mulb(z, h_root_of_unity(logn));
         for (size_t q = 0; q < nu; q++) {
-            const fe x = fe_mul(three, h_pow(wN, pos[q]));
-            fe s1 = fe_zero(), s2 = fe_zero();
+            const fe2 x = fe2_lift(fe_mul(three, h_pow(wN, pos[q])));
+            fe2 s1 = fe2_zero(), s2 = fe2_zero();
             for (int c = 0; c < W; c++) {
-                s1 = fe_add(s1, fe_mul(at[c], fe_sub(tvals[q * W + c], ood[c])));
-                s2 = fe_add(s2, fe_mul(at[c], fe_sub(tvals[q * W + c], ood[W + c])));
+                const fe2 v = fe2_lift(tvals[q * W + c]);
+                s1 = fe2_add(s1, fe2_mul(at[c], fe2_sub(v, ood[c])));
+                s2 = fe2_add(s2, fe2_mul(at[c], fe2_sub(v, ood[W + c])));
             }
-            for (int j = 0; j < C; j++) s1 = fe_add(s1, fe_mul(ac[j], fe_sub(cvals[q * C + j], ood[2 * W + j])));
-            evals[q] = fe_add(fe_mul(s1, h_inv(fe_sub(x, z))), fe_mul(s2, h_inv(fe_sub(x, zg))));
+            for (int j = 0; j < C; j++) {
+                const fe *hv = cflat.data() + q * CK + j * K;
+                const fe2 h = fe2{hv[0], K == 2 ? hv[1] : fe_zero()};
+                s1 = fe2_add(s1, fe2_mul(ac[j], fe2_sub(h, ood[2 * W + j])));
+            }
+            evals[q] = fe2_add(fe2_mul(s1, fe2_inv(fe2_sub(x, z))), fe2_mul(s2, fe2_inv(fe2_sub(x, zg))));
         }
     }
     // FRI [P9]
@@ -412,35 +452,44 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
         for (uint64_t p : fp)
             if (std::find(folded.begin(), folded.end(), p % target) == folded.end()) folded.push_back(p % target);
         const size_t m = folded.size();
-        if (lvl[l] != m * fold * 16) fail("malformed FRI layer " + std::to_string(l));
-        std::vector<fe> rows(m * fold);
-        for (size_t i = 0; i < rows.size(); i++) rows[i] = elem(lv[l] + 16 * i);
+        if (lvl[l] != m * fold * ES) fail("malformed FRI layer " + std::to_string(l));
+        std::vector<fe2> rows(m * fold);
+        for (size_t i = 0; i < rows.size(); i++) rows[i] = elem_ext(lv[l] + ES * i, K);
         std::vector<std::array<uint8_t, 32>> ld(m);
-        for (size_t q = 0; q < m; q++) hash_elems(rows.data() + q * fold, fold, ld[q].data());
+        for (size_t q = 0; q < m; q++) hash_ext(rows.data() + q * fold, fold, K, ld[q].data());
         check_batch(lp[l], lpl[l], ld, folded, ilog2z(target), coms + 64 + 32 * l,
                     ("FRI layer " + std::to_string(l) + " query").c_str());
         for (size_t i = 0; i < fp.size(); i++) {
             const size_t ri = std::find(folded.begin(), folded.end(), fp[i] % target) - folded.begin();
-            if (!fe_eq(rows[ri * fold + fp[i] / target], evals[i])) fail("FRI layer " + std::to_string(l) + " folding mismatch");
+            if (!fe2_eq(rows[ri * fold + fp[i] / target], evals[i])) fail("FRI layer " + std::to_string(l) + " folding mismatch");
         }
-        std::vector<fe> nxt(m);
+        std::vector<fe2> nxt(m);
         for (size_t q = 0; q < m; q++) {
-            std::vector<fe> v(rows.begin() + q * fold, rows.begin() + (q + 1) * fold);
-            h_interp_coset(v, fe_mul(fe_make(3), h_pow(dgen, folded[q])));
-            nxt[q] = h_poly_eval(v.data(), fold, alphas[l]);
+            // interpolate each E component over the coset, then evaluate the E polynomial at alpha
+            std::vector<fe> va(fold), vb(fold);
+            for (int t = 0; t < fold; t++) {
+                va[t] = rows[q * fold + t].a;
+                vb[t] = rows[q * fold + t].b;
+            }
+            const fe xo = fe_mul(fe_make(3), h_pow(dgen, folded[q]));
+            h_interp_coset(va, xo);
+            if (K == 2) h_interp_coset(vb, xo);
+            fe2 acc = fe2_zero();
+            for (int t = fold; t-- > 0;) acc = fe2_add(fe2_mul(acc, alphas[l]), fe2{va[t], K == 2 ? vb[t] : fe_zero()});
+            nxt[q] = acc;
         }
         evals = nxt;
         fp = folded;
         dgen = h_pow(dgen, fold);
         dsz = target;
     }
-    const size_t rem_len = rml / 16;
+    const size_t rem_len = rml / ES;
     if (rem_len != dsz / B) fail("remainder has the wrong size");
-    std::vector<fe> rem(rem_len);
-    for (size_t i = 0; i < rem_len; i++) rem[i] = elem(rm + 16 * i);
+    std::vector<fe2> rem(rem_len);
+    for (size_t i = 0; i < rem_len; i++) rem[i] = elem_ext(rm + ES * i, K);
     for (size_t i = 0; i < fp.size(); i++) {
         const fe x = fe_mul(fe_make(3), h_pow(dgen, fp[i]));
-        if (!fe_eq(h_poly_eval(rem.data(), rem_len, x), evals[i])) fail("FRI remainder mismatch");
+        if (!fe2_eq(poly_eval_ext(rem.data(), rem_len, x), evals[i])) fail("FRI remainder mismatch");
     }
 }
 

@@ -10,6 +10,7 @@
  * Written as a literal restatement of the reference's formulas (no algebraic shortcuts), so that
  * it can serve as the checker for the optimised GPU kernel.
  */
+#include "ext.h"
 #include "internal.h"
 #include "rescue_consts.h"
 
@@ -118,4 +119,96 @@ void or_air_eval_transition(const void *cur, const void *nxt, const void *period
     memcpy(p, periodic9, sizeof p);
     air_eval_u(c, n, p, lwe_size, (u128)delta, o);
     memcpy(out20, o, sizeof o);
+}
+
+/* The same transition evaluated over E (evaluate_transition<E> with E = QuadExtension<f128>, as the
+ * verifier calls it at the out-of-domain point, air/src/lib.rs:104-168).  Same formula order as
+ * air_eval_u, every operand lifted to e2. */
+static e2 nE(e2 b) { return e2_sub(e2_base(1), b); }
+static e2 mE(e2 x, e2 y) { return e2_mul(x, y); }
+void air_eval_e(const e2 *cur, const e2 *nxt, const e2 *per, uint32_t lwe, u128 delta, e2 *out) {
+#define S(i) cur[12 + (i)]
+#define SN(i) nxt[12 + (i)]
+#define C_(v) e2_base((u128)(v))
+    const e2 b0 = cur[5], b1 = cur[4], b2 = cur[3], b3 = cur[2], b4 = cur[1];
+    e2 is_shr = b0, is_shl = b1;
+    e2 is_add = mE(mE(mE(mE(nE(b0), b1), nE(b2)), nE(b3)), nE(b4));
+    e2 is_sadd = mE(mE(mE(mE(nE(b0), b1), nE(b2)), b3), nE(b4));
+    e2 is_add2 = mE(mE(mE(mE(nE(b0), b1), nE(b2)), b3), b4);
+    e2 is_mul = mE(mE(mE(mE(nE(b0), b1), nE(b2)), nE(b3)), b4);
+    e2 is_smul = mE(mE(mE(mE(nE(b0), b1), b2), nE(b3)), nE(b4));
+    e2 is_push = mE(mE(mE(mE(b0, nE(b1)), nE(b2)), nE(b3)), nE(b4));
+    e2 is_read = mE(mE(mE(mE(b0, nE(b1)), nE(b2)), nE(b3)), b4);
+    e2 is_read2 = mE(mE(mE(mE(b0, nE(b1)), nE(b2)), b3), nE(b4));
+    e2 is_noop = mE(mE(mE(mE(nE(b0), nE(b1)), nE(b2)), nE(b3)), nE(b4));
+    e2 opcode = e2_add(e2_add(e2_add(e2_add(e2_mulb(b0, 16), e2_mulb(b1, 8)), e2_mulb(b2, 4)), e2_mulb(b3, 2)), b4);
+
+    out[0] = e2_sub(nxt[0], e2_add(cur[0], C_(1)));
+    out[1] = e2_add(e2_sub(e2_add(e2_sub(e2_sub(nxt[11], cur[11]), is_shr), is_shl), e2_mulb(is_read2, 4)),
+                    e2_mulb(is_add2, 4));
+    out[2] = mE(is_shr, is_shl);
+    out[3] = mE(is_add, e2_sub(SN(0), e2_add(S(0), S(1))));
+    {
+        e2 acc = C_(0);
+        for (uint32_t i = 0; i < lwe; i++) {
+            e2 triv = i == lwe - 1 ? e2_mulb(S(0), delta) : C_(0);
+            acc = e2_add(acc, e2_sub(SN(i), e2_add(S(1 + i), triv)));
+        }
+        out[4] = mE(is_sadd, acc);
+    }
+    {
+        e2 acc = C_(0);
+        for (uint32_t i = 0; i < lwe; i++) acc = e2_add(acc, e2_sub(SN(i), e2_add(S(i), S(lwe + i))));
+        out[5] = mE(is_add2, acc);
+    }
+    out[6] = mE(is_mul, e2_sub(SN(0), mE(S(0), S(1))));
+    {
+        e2 acc = C_(0);
+        for (uint32_t i = 0; i < lwe; i++) acc = e2_add(acc, e2_sub(SN(i), mE(S(1 + i), S(0))));
+        out[7] = mE(is_smul, acc);
+    }
+    out[8] = mE(is_push, e2_sub(SN(1), S(0)));
+    out[9] = mE(is_read, e2_sub(SN(1), S(0)));
+    out[10] = mE(is_read2, e2_sub(SN(5), S(0)));
+    out[11] = mE(is_noop, e2_sub(SN(0), S(0)));
+    {
+        const e2 hash_flag = per[0], *ark = per + 1, h0 = cur[6];
+        e2 s0[4], s1[4], t[4];
+        for (int i = 0; i < 4; i++) s0[i] = e2_exp(cur[7 + i], 3);
+        for (int i = 0; i < 4; i++) {
+            t[i] = C_(0);
+            for (int j = 0; j < 4; j++) t[i] = e2_add(t[i], e2_mulb(s0[j], mds(OR_MDS, 4 * i + j)));
+        }
+        for (int i = 0; i < 4; i++) s0[i] = e2_add(t[i], ark[i]);
+        s0[0] = e2_add(s0[0], opcode);
+        s0[1] = e2_add(s0[1], mE(SN(0), is_push));
+        for (int i = 0; i < 4; i++) s1[i] = e2_sub(nxt[7 + i], ark[4 + i]);
+        for (int i = 0; i < 4; i++) {
+            t[i] = C_(0);
+            for (int j = 0; j < 4; j++) t[i] = e2_add(t[i], e2_mulb(s1[j], mds(OR_INV_MDS, 4 * i + j)));
+        }
+        for (int i = 0; i < 4; i++) s1[i] = e2_exp(t[i], 3);
+        for (int i = 0; i < 4; i++) out[12 + i] = mE(mE(e2_sub(s1[i], s0[i]), hash_flag), h0);
+        e2 nf = nE(hash_flag);
+        out[16] = mE(mE(e2_sub(nxt[7], cur[7]), nf), h0);
+        out[17] = mE(mE(e2_sub(nxt[8], cur[8]), nf), h0);
+        out[18] = mE(mE(nxt[9], nf), h0);
+        out[19] = mE(mE(nxt[10], nf), h0);
+    }
+#undef C_
+#undef S
+#undef SN
+}
+
+void or_e2_mul(const void *x, const void *y, void *out) {
+    const uint8_t *a = (const uint8_t *)x, *b = (const uint8_t *)y;
+    e2 r = e2_mul(e2_make(ld(a), ld(a + 16)), e2_make(ld(b), ld(b + 16)));
+    st(out, r.a);
+    st((uint8_t *)out + 16, r.b);
+}
+void or_e2_inv(const void *x, void *out) {
+    const uint8_t *a = (const uint8_t *)x;
+    e2 r = e2_inv(e2_make(ld(a), ld(a + 16)));
+    st(out, r.a);
+    st((uint8_t *)out + 16, r.b);
 }

@@ -103,6 +103,9 @@ void or_fmul(const void *a, const void *b, void *out);
 void or_finv(const void *a, void *out);
 void or_fexp(const void *a, const void *e /*u128 LE*/, void *out);
 void or_root_of_unity(uint32_t log_n, void *out);
+/* quadratic extension E = F[X]/(X^2 - X - 1): 32-byte values a || b (ext.h) */
+void or_e2_mul(const void *x, const void *y, void *out);
+void or_e2_inv(const void *x, void *out);
 
 /* ---- NTT over f128 ---- */
 /* evaluate polynomial (m coeffs) over offset * <w_size>, natural order */

@@ -71,6 +71,8 @@ def lib():
         for name in ("or_fadd", "or_fsub", "or_fmul", "or_fexp"):
             getattr(L, name).argtypes = [vp, vp, vp]
         L.or_finv.argtypes = [vp, vp]
+        L.or_e2_mul.argtypes = [vp, vp, vp]
+        L.or_e2_inv.argtypes = [vp, vp]
         L.or_root_of_unity.argtypes = [u32, vp]
         L.or_eval_coset.argtypes = [vp, sz, sz, vp, vp]
         L.or_interp_coset.argtypes = [vp, sz, vp]
@@ -125,6 +127,16 @@ def fop(name, a, b=None):
     else:
         getattr(lib(), name)(_buf([a]), _buf([b]), out)
     return from_bytes(out.raw)[0]
+
+
+def e2op(name, x, y=None):
+    """Quadratic-extension op on (a, b) pairs (a + b*X)."""
+    out = C.create_string_buffer(32)
+    if y is None:
+        getattr(lib(), name)(_buf(list(x)), out)
+    else:
+        getattr(lib(), name)(_buf(list(x)), _buf(list(y)), out)
+    return tuple(from_bytes(out.raw))
 
 
 def root_of_unity(log_n: int) -> int:

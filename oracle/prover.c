@@ -10,6 +10,7 @@
  */
 #include <stdio.h>
 
+#include "ext.h"
 #include "internal.h"
 
 #define W 28 /* ProcessorAir trace width (vm/src/processor/mod.rs:76-84) */
@@ -37,14 +38,21 @@ static void coin_next(coin_t *c, uint8_t out[32]) {
     c->counter++;
     blake3_merge_with_int(c->seed, c->counter, out);
 }
-static u128 coin_draw(coin_t *c) {
+/* DefaultRandomCoin::draw::<E>: the first E::ELEMENT_BYTES of the next digest, retried until every
+ * base component is canonical (k = 1: 16 bytes; k = 2: both 16-byte halves) */
+static e2 coin_draw_e(coin_t *c, int k) {
     for (int i = 0; i < 1000; i++) {
         uint8_t d[32];
         coin_next(c, d);
-        u128 v = ld(d);
-        if (v < F_P) return v;
+        const u128 a = ld(d);
+        if (k == 1) {
+            if (a < F_P) return e2_base(a);
+        } else {
+            const u128 b = ld(d + 16);
+            if (a < F_P && b < F_P) return e2_make(a, b);
+        }
     }
-    return 0;
+    return e2_base(0);
 }
 
 /* ----------------------------------------------------------------- byte writer */
@@ -172,7 +180,7 @@ static size_t sorted_assertions(size_t n, const or_pub_inputs *pub, assertion_t 
 int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_inputs *pub, uint8_t *proof_out,
              size_t *proof_len, or_record *rec, const or_dump *dump) {
     if (n < 16 || (n & (n - 1)) || !opt || !pub || !proof_len) return OR_ERR_INVALID_ARG;
-    if (opt->field_extension != 1 || opt->blowup < CE_BLOWUP || (opt->blowup & (opt->blowup - 1)) ||
+    if ((opt->field_extension != 1 && opt->field_extension != 2) || opt->blowup < CE_BLOWUP || (opt->blowup & (opt->blowup - 1)) ||
         (opt->fri_folding != 2 && opt->fri_folding != 4 && opt->fri_folding != 8 && opt->fri_folding != 16) ||
         ((opt->fri_rem_max_deg + 1) & opt->fri_rem_max_deg) || opt->num_queries == 0 ||
         opt->num_queries > OR_MAX_QUERIES || pub->lwe_size == 0 || pub->lwe_size > 5)
@@ -181,6 +189,7 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
     const size_t B = opt->blowup, N = B * n, CE = CE_BLOWUP * n, fold = opt->fri_folding;
     if (opt->num_queries >= N) return OR_ERR_INVALID_ARG;
     const size_t C = num_comp_cols(n);
+    const int K = (int)opt->field_extension; /* 1: FieldExtension::None, 2: Quadratic */
     const u128 offset = F_GENERATOR; /* StarkDomain offset = GENERATOR [P1] */
     const u128 g_n = f_root_of_unity(ilog2_sz(n));
     or_record R;
@@ -227,13 +236,13 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
     memcpy(R.trace_root, tnodes + 32, 32);
     coin_reseed(&coin, R.trace_root);
 
-    /* S3: composition coefficients (transition then boundary) [P4] and evaluation */
-    u128 ct[NUM_TCONS], cb[NUM_ASSERTS];
-    for (int k = 0; k < NUM_TCONS; k++) st(R.coeff_t[k], ct[k] = coin_draw(&coin));
-    for (int k = 0; k < NUM_ASSERTS; k++) st(R.coeff_b[k], cb[k] = coin_draw(&coin));
+    /* S3: composition coefficients (transition then boundary) [P4], drawn in E, and evaluation */
+    e2 ct[NUM_TCONS], cb[NUM_ASSERTS];
+    for (int k = 0; k < NUM_TCONS; k++) st(R.coeff_t[k], (ct[k] = coin_draw_e(&coin, K)).a);
+    for (int k = 0; k < NUM_ASSERTS; k++) st(R.coeff_b[k], (cb[k] = coin_draw_e(&coin, K)).a);
     assertion_t as[NUM_ASSERTS];
     sorted_assertions(n, pub, as);
-    u128 *comp = (u128 *)malloc(CE * 16);
+    e2 *comp = (e2 *)malloc(CE * sizeof(e2));
     {
         const size_t lde_shift = N / CE;
         const u128 w_ce = f_root_of_unity(ilog2_sz(CE));
@@ -253,149 +262,182 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
             u128 xp = f_exp(x, n / 16);
             for (int j = 0; j < 9; j++) per[j] = poly_eval(pcoef[j], 16, xp);
             air_eval_u(cur, nxt, per, pub->lwe_size, pub->delta, ev);
-            u128 t = 0;
-            for (int k = 0; k < NUM_TCONS; k++) t = f_add(t, f_mul(ct[k], ev[k]));
+            e2 t = e2_base(0);
+            for (int k = 0; k < NUM_TCONS; k++) t = e2_add(t, e2_mulb(ct[k], ev[k]));
             /* transition divisor (x^n - 1) / ((x - g^(n-2)) (x - g^(n-1))) [P6] */
             u128 zt = f_mul(f_sub(f_exp(x, n), 1), f_inv(f_mul(f_sub(x, g_last2), f_sub(x, g_last1))));
-            u128 acc = f_mul(t, f_inv(zt));
+            e2 acc = e2_mulb(t, f_inv(zt));
             /* boundary groups keyed by (stride, step): (0,0) then (0,n-2) [P3] */
-            u128 b0 = 0, b1 = 0;
+            e2 b0 = e2_base(0), b1 = e2_base(0);
             for (int k = 0; k < NUM_ASSERTS; k++) {
-                u128 v = f_mul(cb[k], f_sub(cur[as[k].col], as[k].value));
-                if (as[k].step == 0) b0 = f_add(b0, v);
-                else b1 = f_add(b1, v);
+                e2 v = e2_mulb(cb[k], f_sub(cur[as[k].col], as[k].value));
+                if (as[k].step == 0) b0 = e2_add(b0, v);
+                else b1 = e2_add(b1, v);
             }
-            acc = f_add(acc, f_mul(b0, f_inv(f_sub(x, 1))));
-            acc = f_add(acc, f_mul(b1, f_inv(f_sub(x, g_last2))));
+            acc = e2_add(acc, e2_mulb(b0, f_inv(f_sub(x, 1))));
+            acc = e2_add(acc, e2_mulb(b1, f_inv(f_sub(x, g_last2))));
             comp[i] = acc;
             x = f_mul(x, w_ce);
         }
     }
-    if (dump && dump->composition) memcpy(dump->composition, comp, CE * 16);
+    if (dump && dump->composition)
+        for (size_t i = 0; i < CE; i++) st((uint8_t *)dump->composition + 16 * i, comp[i].a);
 
-    /* S4: constraint commitment: interpolate over the CE coset, segment into C columns [P5] */
-    u128 *cpolys = (u128 *)calloc(C * n, 16);
-    u128 *clde = (u128 *)malloc(N * C * 16);
+    /* S4: constraint commitment: interpolate each E component over the CE coset, segment into C
+     * columns of E polynomials (base polys (col, j) at cpolys[(col*K + j)*n]) [P5]; a leaf is the row
+     * of C E values, i.e. C*K base elements */
+    const size_t CK = C * K;
+    u128 *cpolys = (u128 *)calloc(CK * n, 16);
+    u128 *clde = (u128 *)malloc(N * CK * 16);
     uint8_t *cleaves = (uint8_t *)malloc(N * 32);
     int degree_ok = 1;
     {
         u128 *coef = (u128 *)malloc(CE * 16);
-        memcpy(coef, comp, CE * 16);
-        interp_coset_u(coef, CE, offset);
-        for (size_t k = C * n; k < CE; k++)
-            if (coef[k]) degree_ok = 0; /* composition degree must be < C*n */
         u128 *col = (u128 *)malloc(N * 16);
-        for (size_t j = 0; j < C; j++) {
-            memcpy(cpolys + j * n, coef + j * n, n * 16);
-            eval_coset_u(cpolys + j * n, n, N, offset, col);
-            for (size_t i = 0; i < N; i++) clde[i * C + j] = col[i];
+        for (int j = 0; j < K; j++) {
+            for (size_t i = 0; i < CE; i++) coef[i] = j ? comp[i].b : comp[i].a;
+            interp_coset_u(coef, CE, offset);
+            for (size_t k = C * n; k < CE; k++)
+                if (coef[k]) degree_ok = 0; /* composition degree must be < C*n */
+            for (size_t c = 0; c < C; c++) {
+                u128 *pc = cpolys + (c * K + j) * n;
+                memcpy(pc, coef + c * n, n * 16);
+                eval_coset_u(pc, n, N, offset, col);
+                for (size_t i = 0; i < N; i++) clde[i * CK + c * K + j] = col[i];
+            }
         }
         free(col);
         free(coef);
-        for (size_t i = 0; i < N; i++) blake3_hash_elems(clde + i * C, C, cleaves + 32 * i);
+        for (size_t i = 0; i < N; i++) blake3_hash_elems(clde + i * CK, CK, cleaves + 32 * i);
     }
     uint8_t *cnodes = merkle_build(cleaves, N);
     memcpy(R.constraint_root, cnodes + 32, 32);
     coin_reseed(&coin, R.constraint_root);
 
-    /* S5: OOD point and frame [P7] */
-    u128 z = coin_draw(&coin), zg = f_mul(z, g_n);
-    st(R.z, z);
-    u128 ood[2 * W], oodc[OR_MAX_CCOLS];
+    /* S5: OOD point (in E) and frame [P7] */
+    const e2 z = coin_draw_e(&coin, K), zg = e2_mulb(z, g_n);
+    st(R.z, z.a);
+    e2 ood[2 * W], oodc[OR_MAX_CCOLS];
     for (int c = 0; c < W; c++) {
-        ood[c] = poly_eval(polys + c * n, n, z);
-        ood[W + c] = poly_eval(polys + c * n, n, zg);
-        st(R.ood_trace_z[c], ood[c]);
-        st(R.ood_trace_zg[c], ood[W + c]);
+        ood[c] = poly_eval_e(polys + c * n, n, z);
+        ood[W + c] = poly_eval_e(polys + c * n, n, zg);
+        st(R.ood_trace_z[c], ood[c].a);
+        st(R.ood_trace_zg[c], ood[W + c].a);
     }
     {
         uint8_t h[32];
-        blake3_hash_elems(ood, 2 * W, h);
+        e2_hash(ood, 2 * W, K, h);
         coin_reseed(&coin, h);
     }
-    for (size_t j = 0; j < C; j++) st(R.ood_constraints[j], oodc[j] = poly_eval(cpolys + j * n, n, z));
+    for (size_t c = 0; c < C; c++) {
+        oodc[c] = poly_eval_e(cpolys + c * K * n, n, z);
+        if (K == 2) oodc[c] = e2_add(oodc[c], e2_mulX(poly_eval_e(cpolys + (c * K + 1) * n, n, z)));
+        st(R.ood_constraints[c], oodc[c].a);
+    }
     {
         uint8_t h[32];
-        blake3_hash_elems(oodc, C, h);
+        e2_hash(oodc, C, K, h);
         coin_reseed(&coin, h);
     }
     /* DEEP coefficients [P8] and DEEP evaluations over the LDE domain (evaluation form) */
-    u128 at[W], ac[OR_MAX_CCOLS];
-    for (int c = 0; c < W; c++) st(R.deep_t[c], at[c] = coin_draw(&coin));
-    for (size_t j = 0; j < C; j++) st(R.deep_c[j], ac[j] = coin_draw(&coin));
-    u128 *deep = (u128 *)malloc(N * 16);
+    e2 at[W], ac[OR_MAX_CCOLS];
+    for (int c = 0; c < W; c++) st(R.deep_t[c], (at[c] = coin_draw_e(&coin, K)).a);
+    for (size_t c = 0; c < C; c++) st(R.deep_c[c], (ac[c] = coin_draw_e(&coin, K)).a);
+    e2 *deep = (e2 *)malloc(N * sizeof(e2));
     {
         const u128 w_n = f_root_of_unity(ilog2_sz(N));
         u128 x = offset;
         for (size_t i = 0; i < N; i++) {
-            u128 s1 = 0, s2 = 0;
+            e2 s1 = e2_base(0), s2 = e2_base(0);
             for (int c = 0; c < W; c++) {
-                s1 = f_add(s1, f_mul(at[c], f_sub(lde[i * W + c], ood[c])));
-                s2 = f_add(s2, f_mul(at[c], f_sub(lde[i * W + c], ood[W + c])));
+                const e2 v = e2_base(lde[i * W + c]);
+                s1 = e2_add(s1, e2_mul(at[c], e2_sub(v, ood[c])));
+                s2 = e2_add(s2, e2_mul(at[c], e2_sub(v, ood[W + c])));
             }
-            for (size_t j = 0; j < C; j++) s1 = f_add(s1, f_mul(ac[j], f_sub(clde[i * C + j], oodc[j])));
-            deep[i] = f_add(f_mul(s1, f_inv(f_sub(x, z))), f_mul(s2, f_inv(f_sub(x, zg))));
+            for (size_t c = 0; c < C; c++) {
+                const e2 h = e2_make(clde[i * CK + c * K], K == 2 ? clde[i * CK + c * K + 1] : 0);
+                s1 = e2_add(s1, e2_mul(ac[c], e2_sub(h, oodc[c])));
+            }
+            const e2 xe = e2_base(x);
+            deep[i] = e2_add(e2_mul(s1, e2_inv(e2_sub(xe, z))), e2_mul(s2, e2_inv(e2_sub(xe, zg))));
             x = f_mul(x, w_n);
         }
     }
-    if (dump && dump->deep) memcpy(dump->deep, deep, N * 16);
+    if (dump && dump->deep)
+        for (size_t i = 0; i < N; i++) st((uint8_t *)dump->deep + 16 * i, deep[i].a);
 
-    /* S6: FRI [P9, P10] */
+    /* S6: FRI over E [P9, P10] */
     size_t max_rem = (size_t)(opt->fri_rem_max_deg + 1) * B, nl = 0;
     for (size_t s = N; s > max_rem; s /= fold) nl++;
     if (nl > OR_MAX_FRI_LAYERS) return OR_ERR_INVALID_ARG;
     R.num_fri_layers = (uint32_t)nl;
-    u128 *layer_vals[OR_MAX_FRI_LAYERS];   /* transposed: row r = [e[r + k*L/fold]] */
+    e2 *layer_vals[OR_MAX_FRI_LAYERS]; /* transposed: row r = [e[r + k*L/fold]] */
     uint8_t *layer_leaves[OR_MAX_FRI_LAYERS], *layer_nodes[OR_MAX_FRI_LAYERS];
     size_t layer_rows[OR_MAX_FRI_LAYERS];
-    u128 *ev = deep;
+    e2 *ev = deep;
     size_t L = N;
     for (size_t l = 0; l < nl; l++) {
         size_t rows = L / fold;
-        u128 *tv = (u128 *)malloc(L * 16);
+        e2 *tv = (e2 *)malloc(L * sizeof(e2));
         for (size_t r = 0; r < rows; r++)
             for (size_t k = 0; k < fold; k++) tv[r * fold + k] = ev[r + k * rows];
         uint8_t *lv = (uint8_t *)malloc(rows * 32);
-        for (size_t r = 0; r < rows; r++) blake3_hash_elems(tv + r * fold, fold, lv + 32 * r);
+        for (size_t r = 0; r < rows; r++) e2_hash(tv + r * fold, fold, K, lv + 32 * r);
         uint8_t *nodes = merkle_build(lv, rows);
         memcpy(R.fri_roots[l], nodes + 32, 32);
         coin_reseed(&coin, R.fri_roots[l]);
-        u128 alpha = coin_draw(&coin);
-        st(R.fri_alphas[l], alpha);
+        const e2 alpha = coin_draw_e(&coin, K);
+        st(R.fri_alphas[l], alpha.a);
         /* degree-respecting projection: p_r interpolates (offset*w_L^r*zeta^k, tv[r][k]); next[r] = p_r(alpha) */
-        u128 *nx = (u128 *)malloc(rows * 16);
-        const u128 w_l = f_root_of_unity(ilog2_sz(L)), zeta = f_root_of_unity(ilog2_sz(fold));
+        e2 *nx = (e2 *)malloc(rows * sizeof(e2));
+        const u128 w_l = f_root_of_unity(ilog2_sz(L));
         u128 xr = offset;
         for (size_t r = 0; r < rows; r++) {
-            u128 vals[16];
-            memcpy(vals, tv + r * fold, fold * 16);
-            interp_coset_u(vals, fold, xr); /* coefficients of p_r in x */
-            (void)zeta;
-            nx[r] = poly_eval(vals, fold, alpha);
+            u128 va[16], vb[16];
+            for (size_t k = 0; k < fold; k++) {
+                va[k] = tv[r * fold + k].a;
+                vb[k] = tv[r * fold + k].b;
+            }
+            interp_coset_u(va, fold, xr); /* coefficients of p_r in x, per E component */
+            if (K == 2) interp_coset_u(vb, fold, xr);
+            e2 acc = e2_base(0);
+            for (size_t m = fold; m-- > 0;) acc = e2_add(e2_mul(acc, alpha), e2_make(va[m], K == 2 ? vb[m] : 0));
+            nx[r] = acc;
             xr = f_mul(xr, w_l);
         }
         layer_vals[l] = tv;
         layer_leaves[l] = lv;
         layer_nodes[l] = nodes;
         layer_rows[l] = rows;
-        if (l == 0 && dump && dump->fri_layer1) memcpy(dump->fri_layer1, nx, rows * 16);
+        if (l == 0 && dump && dump->fri_layer1)
+            for (size_t r = 0; r < rows; r++) st((uint8_t *)dump->fri_layer1 + 16 * r, nx[r].a);
         if (ev != deep) free(ev);
         ev = nx;
         L = rows;
     }
-    /* remainder: interpolate over offset*<w_L>, keep L/blowup coefficients, commit by hash */
+    /* remainder: interpolate over offset*<w_L>, keep L/blowup coefficients (in E), commit by hash */
+    e2 rem[OR_MAX_REMAINDER];
+    size_t rl = L / B;
     {
-        u128 *rc = (u128 *)malloc(L * 16);
-        memcpy(rc, ev, L * 16);
-        interp_coset_u(rc, L, offset);
-        size_t rl = L / B;
+        if (rl > OR_MAX_REMAINDER) return OR_ERR_INVALID_ARG;
+        u128 *ra = (u128 *)malloc(L * 16), *rb = (u128 *)calloc(L, 16);
+        for (size_t i = 0; i < L; i++) {
+            ra[i] = ev[i].a;
+            rb[i] = ev[i].b;
+        }
+        interp_coset_u(ra, L, offset);
+        if (K == 2) interp_coset_u(rb, L, offset);
         R.remainder_len = (uint32_t)rl;
-        for (size_t k = 0; k < rl && k < OR_MAX_REMAINDER; k++) st(R.remainder[k], rc[k]);
+        for (size_t k = 0; k < rl; k++) {
+            rem[k] = e2_make(ra[k], rb[k]);
+            st(R.remainder[k], ra[k]);
+        }
         for (size_t k = rl; k < L; k++)
-            if (rc[k]) degree_ok = 0;
-        blake3_hash_elems(rc, rl, R.remainder_commitment);
+            if (ra[k] || rb[k]) degree_ok = 0;
+        e2_hash(rem, rl, K, R.remainder_commitment);
         coin_reseed(&coin, R.remainder_commitment);
-        free(rc);
+        free(ra);
+        free(rb);
     }
     if (ev != deep) free(ev);
 
@@ -475,26 +517,30 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
         free(vals);
         free(paths.p);
     }
-    /* constraint queries */
+    /* constraint queries: rows of C E values */
     {
         buf_t paths = {0};
         prove_batch(cleaves, cnodes, N, pos, nu, &paths);
-        uint8_t *vals = (uint8_t *)malloc(nu * C * 16);
-        for (size_t q = 0; q < nu; q++) memcpy(vals + q * C * 16, clde + pos[q] * C, C * 16);
-        write_queries(&pf, vals, nu * C * 16, &paths);
+        uint8_t *vals = (uint8_t *)malloc(nu * CK * 16);
+        for (size_t q = 0; q < nu; q++) memcpy(vals + q * CK * 16, clde + pos[q] * CK, CK * 16);
+        write_queries(&pf, vals, nu * CK * 16, &paths);
         free(vals);
         free(paths.p);
     }
     /* OOD frame: trace states (frame size 2, interleaved per column), constraint evaluations [P7] */
     {
-        bw_u16(&pf, (uint16_t)(1 + 2 * W * 16));
+        u128 flat[2 * OR_MAX_CCOLS + 4];
+        bw_u16(&pf, (uint16_t)(1 + 2 * W * 16 * K));
         bw_u8(&pf, 2);
         for (int c = 0; c < W; c++) {
-            bw(&pf, &ood[c], 16);
-            bw(&pf, &ood[W + c], 16);
+            e2_flatten(&ood[c], 1, K, flat);
+            bw(&pf, flat, 16 * K);
+            e2_flatten(&ood[W + c], 1, K, flat);
+            bw(&pf, flat, 16 * K);
         }
-        bw_u16(&pf, (uint16_t)(C * 16));
-        bw(&pf, oodc, C * 16);
+        bw_u16(&pf, (uint16_t)(C * 16 * K));
+        e2_flatten(oodc, C, K, flat);
+        bw(&pf, flat, C * 16 * K);
     }
     /* FRI proof: per layer, fold positions (first-occurrence order), rows + batch proof */
     {
@@ -516,17 +562,19 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
             }
             buf_t paths = {0};
             prove_batch(layer_leaves[l], layer_nodes[l], layer_rows[l], nfpv, m, &paths);
-            uint8_t *vals = (uint8_t *)malloc(m * fold * 16);
-            for (size_t q = 0; q < m; q++) memcpy(vals + q * fold * 16, layer_vals[l] + nfpv[q] * fold, fold * 16);
-            write_queries(&pf, vals, m * fold * 16, &paths);
+            u128 *vals = (u128 *)malloc(m * fold * K * 16);
+            for (size_t q = 0; q < m; q++) e2_flatten(layer_vals[l] + nfpv[q] * fold, fold, K, vals + q * fold * K);
+            write_queries(&pf, (const uint8_t *)vals, m * fold * K * 16, &paths);
             free(vals);
             free(paths.p);
             memcpy(fp, nfpv, m * 8);
             nfp = m;
             dsz = target;
         }
-        bw_u16(&pf, (uint16_t)(R.remainder_len * 16));
-        bw(&pf, R.remainder, R.remainder_len * 16);
+        u128 flat[2 * OR_MAX_REMAINDER];
+        e2_flatten(rem, rl, K, flat);
+        bw_u16(&pf, (uint16_t)(rl * 16 * K));
+        bw(&pf, flat, rl * 16 * K);
         bw_u8(&pf, 0); /* num_partitions = 1, stored as log2 */
     }
     bw_u64(&pf, nonce);
@@ -539,8 +587,8 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
         if (dump->trace_polys) memcpy(dump->trace_polys, polys, W * n * 16);
         if (dump->trace_lde) memcpy(dump->trace_lde, lde, N * W * 16);
         if (dump->trace_leaves) memcpy(dump->trace_leaves, leaves, N * 32);
-        if (dump->comp_polys) memcpy(dump->comp_polys, cpolys, C * n * 16);
-        if (dump->comp_lde) memcpy(dump->comp_lde, clde, N * C * 16);
+        if (dump->comp_polys) memcpy(dump->comp_polys, cpolys, CK * n * 16);
+        if (dump->comp_lde) memcpy(dump->comp_lde, clde, N * CK * 16);
     }
     if (proof_out && *proof_len >= pf.len)
         memcpy(proof_out, pf.p, pf.len);

@@ -10,6 +10,7 @@
  */
 #include <stdio.h>
 
+#include "ext.h"
 #include "internal.h"
 
 #define W 28
@@ -55,15 +56,25 @@ static void vc_reseed(vcoin_t *c, const uint8_t d[32]) {
     memcpy(c->seed, o, 32);
     c->counter = 0;
 }
-static u128 vc_draw(vcoin_t *c) {
+/* draw::<E> (see coin_draw_e in prover.c) */
+static e2 vc_draw(vcoin_t *c, int k) {
     for (int i = 0; i < 1000; i++) {
         uint8_t d[32];
         c->counter++;
         blake3_merge_with_int(c->seed, c->counter, d);
-        u128 v = ld(d);
-        if (v < F_P) return v;
+        const u128 a = ld(d), b = k == 2 ? ld(d + 16) : 0;
+        if (a < F_P && b < F_P) return e2_make(a, b);
     }
-    return 0;
+    return e2_base(0);
+}
+/* n E values of k base components each from bytes; 0 when a component is not canonical */
+static int rd_e(const uint8_t *p, size_t n, int k, e2 *out) {
+    for (size_t i = 0; i < n; i++) {
+        const u128 a = ld(p + 16 * k * i), b = k == 2 ? ld(p + 16 * k * i + 16) : 0;
+        if (a >= F_P || b >= F_P) return 0;
+        out[i] = e2_make(a, b);
+    }
+    return 1;
 }
 
 #define FAIL(...)                                   \
@@ -189,7 +200,8 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
     int rc = 0;
     rd_t r = {proof, proof_len, 0, 0};
     uint64_t pos[OR_MAX_QUERIES + 1], fp[OR_MAX_QUERIES + 1];
-    u128 *tvals = NULL, *cvals = NULL, evals[OR_MAX_QUERIES + 1];
+    u128 *tvals = NULL, *cvals = NULL;
+    e2 evals[OR_MAX_QUERIES + 1];
     /* ---- context */
     uint8_t width = rd_u8(&r), auxw = rd_u8(&r), auxr = rd_u8(&r), logn = rd_u8(&r);
     uint16_t meta = rd_u16(&r);
@@ -199,7 +211,7 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
     uint8_t nq = rd_u8(&r), B = rd_u8(&r), grind = rd_u8(&r), ext = rd_u8(&r), fold = rd_u8(&r),
             remdeg = rd_u8(&r);
     uint8_t nu = rd_u8(&r);
-    if (r.bad || width != W || auxw || auxr || mlen != 16 || ext != 1 || logn < 4 || logn > 32 || B < 8 ||
+    if (r.bad || width != W || auxw || auxr || mlen != 16 || (ext != 1 && ext != 2) || logn < 4 || logn > 32 || B < 8 ||
         (B & (B - 1)) || !(fold == 2 || fold == 4 || fold == 8 || fold == 16))
         FAIL("malformed proof context");
     {
@@ -207,10 +219,11 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
         if (memcmp(mod, &p, 16)) FAIL("field modulus mismatch");
     }
     const size_t n = (size_t)1 << logn, N = n * B;
+    const int K = ext;
     /* conjectured security */
     {
         unsigned logN = logn + ilog2_sz(B);
-        int field_sec = 128 - (int)logN;
+        int field_sec = 128 * K - (int)logN;
         int q_sec = (int)ilog2_sz(B) * nq;
         if (q_sec >= 80) q_sec += grind;
         int sec = (field_sec < q_sec ? field_sec : q_sec) - 1;
@@ -242,11 +255,11 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
         coin.counter = 0;
     }
     vc_reseed(&coin, coms);
-    u128 ct[NUM_TCONS], cb[NUM_ASSERTS];
-    for (int i = 0; i < NUM_TCONS; i++) ct[i] = vc_draw(&coin);
-    for (int i = 0; i < NUM_ASSERTS; i++) cb[i] = vc_draw(&coin);
+    e2 ct[NUM_TCONS], cb[NUM_ASSERTS];
+    for (int i = 0; i < NUM_TCONS; i++) ct[i] = vc_draw(&coin, K);
+    for (int i = 0; i < NUM_ASSERTS; i++) cb[i] = vc_draw(&coin, K);
     vc_reseed(&coin, coms + 32);
-    u128 z = vc_draw(&coin);
+    const e2 z = vc_draw(&coin, K);
     /* ---- read the remaining sections in proof order */
     uint8_t nseg = rd_u8(&r);
     if (nseg != 1) FAIL("expected one trace segment");
@@ -262,66 +275,70 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
     const uint8_t *ts = rd(&r, tsl);
     uint16_t oel = rd_u16(&r);
     const uint8_t *oe = rd(&r, oel);
-    if (r.bad || tsl != 1 + 2 * W * 16 || ts[0] != 2 || oel % 16 || oel / 16 > OR_MAX_CCOLS || oel == 0)
+    if (r.bad || tsl != 1 + 2 * W * 16 * K || ts[0] != 2 || oel % (16 * K) || oel / (16 * K) > OR_MAX_CCOLS ||
+        oel == 0)
         FAIL("malformed OOD frame");
-    const size_t C = oel / 16;
-    u128 oz[W], ozg[W], oc[OR_MAX_CCOLS];
-    for (int c = 0; c < W; c++) {
-        oz[c] = ld(ts + 1 + 32 * c);
-        ozg[c] = ld(ts + 1 + 32 * c + 16);
-        if (oz[c] >= F_P || ozg[c] >= F_P) FAIL("non-canonical OOD value");
-    }
-    for (size_t j = 0; j < C; j++) oc[j] = ld(oe + 16 * j);
+    const size_t C = oel / (16 * K);
+    e2 oz[W], ozg[W], oc[OR_MAX_CCOLS];
+    for (int c = 0; c < W; c++)
+        if (!rd_e(ts + 1 + 32 * K * c, 1, K, &oz[c]) || !rd_e(ts + 1 + 32 * K * c + 16 * K, 1, K, &ozg[c]))
+            FAIL("non-canonical OOD value");
+    if (!rd_e(oe, C, K, oc)) FAIL("non-canonical OOD value");
     {
-        u128 flat[2 * W];
-        memcpy(flat, oz, sizeof oz);
-        memcpy(flat + W, ozg, sizeof ozg);
+        e2 both[2 * W];
+        memcpy(both, oz, sizeof oz);
+        memcpy(both + W, ozg, sizeof ozg);
         uint8_t h[32];
-        blake3_hash_elems(flat, 2 * W, h);
+        e2_hash(both, 2 * W, K, h);
         vc_reseed(&coin, h);
-        blake3_hash_elems(oc, C, h);
+        e2_hash(oc, C, K, h);
         vc_reseed(&coin, h);
     }
     /* ---- OOD consistency: H(z) from the AIR at z vs sum_j z^(jn) H_j(z) */
     {
         const u128 g = f_root_of_unity(logn);
-        u128 per[9], pc[9][16], ev[NUM_TCONS];
+        e2 per[9], ev[NUM_TCONS];
+        u128 pc[9][16];
         for (unsigned s = 0; s < 16; s++) {
             u128 row[9];
             air_periodic_u(s, row);
             for (int j = 0; j < 9; j++) pc[j][s] = row[j];
         }
-        u128 zp = f_exp(z, n / 16);
+        const e2 zp = e2_exp(z, n / 16);
         for (int j = 0; j < 9; j++) {
             interp_coset_u(pc[j], 16, 1);
-            per[j] = poly_eval(pc[j], 16, zp);
+            per[j] = poly_eval_e(pc[j], 16, zp);
         }
-        air_eval_u(oz, ozg, per, pub->lwe_size, pub->delta, ev);
-        u128 t = 0;
-        for (int k = 0; k < NUM_TCONS; k++) t = f_add(t, f_mul(ct[k], ev[k]));
-        u128 gl2 = f_exp(g, n - 2), gl1 = f_exp(g, n - 1);
-        u128 h = f_mul(f_mul(t, f_mul(f_sub(z, gl2), f_sub(z, gl1))), f_inv(f_sub(f_exp(z, n), 1)));
+        air_eval_e(oz, ozg, per, pub->lwe_size, pub->delta, ev);
+        e2 t = e2_base(0);
+        for (int k = 0; k < NUM_TCONS; k++) t = e2_add(t, e2_mul(ct[k], ev[k]));
+        const e2 gl2 = e2_base(f_exp(g, n - 2)), gl1 = e2_base(f_exp(g, n - 1)), one = e2_base(1);
+        const e2 zn = e2_exp(z, n);
+        e2 h = e2_mul(e2_mul(t, e2_mul(e2_sub(z, gl2), e2_sub(z, gl1))), e2_inv(e2_sub(zn, one)));
         const int fc[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
-        u128 b0 = 0, b1 = 0;
-        for (int i = 0; i < 12; i++) b0 = f_add(b0, f_mul(cb[i], oz[fc[i]]));
-        for (int i = 0; i < 2; i++) b1 = f_add(b1, f_mul(cb[12 + i], f_sub(oz[7 + i], ld(pub->program_hash[i]))));
-        for (int i = 0; i < 8; i++) b1 = f_add(b1, f_mul(cb[14 + i], f_sub(oz[12 + i], ld(pub->stack_outputs[i]))));
-        h = f_add(h, f_mul(b0, f_inv(f_sub(z, 1))));
-        h = f_add(h, f_mul(b1, f_inv(f_sub(z, gl2))));
-        u128 hc = 0, zn = f_exp(z, n), zz = 1;
+        e2 b0 = e2_base(0), b1 = e2_base(0);
+        for (int i = 0; i < 12; i++) b0 = e2_add(b0, e2_mul(cb[i], oz[fc[i]]));
+        for (int i = 0; i < 2; i++)
+            b1 = e2_add(b1, e2_mul(cb[12 + i], e2_sub(oz[7 + i], e2_base(ld(pub->program_hash[i])))));
+        for (int i = 0; i < 8; i++)
+            b1 = e2_add(b1, e2_mul(cb[14 + i], e2_sub(oz[12 + i], e2_base(ld(pub->stack_outputs[i])))));
+        h = e2_add(h, e2_mul(b0, e2_inv(e2_sub(z, one))));
+        h = e2_add(h, e2_mul(b1, e2_inv(e2_sub(z, gl2))));
+        /* H(z) = sum_j z^(jn) H_j(z); with k = 2, H_j(z) = oc[j] as the E-valued column */
+        e2 hc = e2_base(0), zz = one;
         for (size_t j = 0; j < C; j++) {
-            hc = f_add(hc, f_mul(zz, oc[j]));
-            zz = f_mul(zz, zn);
+            hc = e2_add(hc, e2_mul(zz, oc[j]));
+            zz = e2_mul(zz, zn);
         }
-        if (h != hc) FAIL("out-of-domain constraint evaluation mismatch");
+        if (!e2_eq(h, hc)) FAIL("out-of-domain constraint evaluation mismatch");
     }
-    u128 at[W], ac[OR_MAX_CCOLS];
-    for (int c = 0; c < W; c++) at[c] = vc_draw(&coin);
-    for (size_t j = 0; j < C; j++) ac[j] = vc_draw(&coin);
-    u128 alphas[OR_MAX_FRI_LAYERS];
+    e2 at[W], ac[OR_MAX_CCOLS];
+    for (int c = 0; c < W; c++) at[c] = vc_draw(&coin, K);
+    for (size_t j = 0; j < C; j++) ac[j] = vc_draw(&coin, K);
+    e2 alphas[OR_MAX_FRI_LAYERS];
     for (size_t l = 0; l < nl; l++) {
         vc_reseed(&coin, coms + 64 + 32 * l);
-        alphas[l] = vc_draw(&coin);
+        alphas[l] = vc_draw(&coin, K);
     }
     vc_reseed(&coin, coms + 64 + 32 * nl);
     /* ---- FRI section (parsed now, checked after the queries) */
@@ -341,7 +358,7 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
     const uint8_t *nonce_b = rd(&r, 8);
     uint8_t gkr = rd_u8(&r);
     if (r.bad || nparts != 0 || gkr != 0 || r.off != r.len) FAIL("malformed proof tail");
-    const size_t rem_len = rml / 16;
+    const size_t rem_len = rml / (16 * K);
     {
         uint8_t h[32];
         or_blake3(rm, rml, h);
@@ -380,9 +397,10 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
         if (nuq == 0 || pos[nuq - 1] != pos[i]) pos[nuq++] = pos[i];
     if (nuq != nu) FAIL("number of unique queries mismatch");
     /* ---- trace and constraint openings */
-    if (tvl != nu * W * 16 || cvl != nu * C * 16) FAIL("malformed query values");
+    const size_t CK = C * K;
+    if (tvl != nu * W * 16 || cvl != nu * CK * 16) FAIL("malformed query values");
     tvals = (u128 *)malloc(nu * W * 16);
-    cvals = (u128 *)malloc(nu * C * 16);
+    cvals = (u128 *)malloc(nu * CK * 16);
     memcpy(tvals, tv, tvl);
     memcpy(cvals, cv, cvl);
     {
@@ -394,23 +412,27 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
             free(dig);
             FAIL("trace query does not match the commitment");
         }
-        for (size_t q = 0; q < nu; q++) blake3_hash_elems(cvals + q * C, C, dig + 32 * q);
+        for (size_t q = 0; q < nu; q++) blake3_hash_elems(cvals + q * CK, CK, dig + 32 * q);
         rd_t pc2 = {cp, cpl, 0, 0};
         e = batch_root(&pc2, dig, pos, nu, logn + ilog2_sz(B), root);
         free(dig);
         if (e || pc2.off != pc2.len || memcmp(root, coms + 32, 32)) FAIL("constraint query does not match the commitment");
     }
-    /* ---- DEEP values at the query positions */
+    /* ---- DEEP values at the query positions (in E) */
     {
-        const u128 wN = f_root_of_unity(logn + ilog2_sz(B)), zg = f_mul(z, f_root_of_unity(logn));
+        const u128 wN = f_root_of_unity(logn + ilog2_sz(B));
+        const e2 zg = e2_mulb(z, f_root_of_unity(logn));
         for (size_t q = 0; q < nu; q++) {
-            u128 x = f_mul(F_GENERATOR, f_exp(wN, pos[q])), s1 = 0, s2 = 0;
+            const e2 x = e2_base(f_mul(F_GENERATOR, f_exp(wN, pos[q])));
+            e2 s1 = e2_base(0), s2 = e2_base(0), hv[OR_MAX_CCOLS];
             for (int c = 0; c < W; c++) {
-                s1 = f_add(s1, f_mul(at[c], f_sub(tvals[q * W + c], oz[c])));
-                s2 = f_add(s2, f_mul(at[c], f_sub(tvals[q * W + c], ozg[c])));
+                const e2 v = e2_base(tvals[q * W + c]);
+                s1 = e2_add(s1, e2_mul(at[c], e2_sub(v, oz[c])));
+                s2 = e2_add(s2, e2_mul(at[c], e2_sub(v, ozg[c])));
             }
-            for (size_t j = 0; j < C; j++) s1 = f_add(s1, f_mul(ac[j], f_sub(cvals[q * C + j], oc[j])));
-            evals[q] = f_add(f_mul(s1, f_inv(f_sub(x, z))), f_mul(s2, f_inv(f_sub(x, zg))));
+            if (!rd_e((const uint8_t *)(cvals + q * CK), C, K, hv)) FAIL("non-canonical constraint value");
+            for (size_t j = 0; j < C; j++) s1 = e2_add(s1, e2_mul(ac[j], e2_sub(hv[j], oc[j])));
+            evals[q] = e2_add(e2_mul(s1, e2_inv(e2_sub(x, z))), e2_mul(s2, e2_inv(e2_sub(x, zg))));
         }
     }
     /* ---- FRI layers */
@@ -418,7 +440,6 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
         size_t dsz = N, ncur = nu;
         memcpy(fp, pos, nu * 8);
         u128 dgen = f_root_of_unity(ilog2_sz(N));
-        const u128 zeta = f_root_of_unity(ilog2_sz(fold));
         for (size_t l = 0; l < nl; l++) {
             size_t target = dsz / fold;
             uint64_t folded[OR_MAX_QUERIES + 1];
@@ -429,11 +450,14 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
                 for (size_t j = 0; j < m; j++) seen |= folded[j] == p;
                 if (!seen) folded[m++] = p;
             }
-            if (lvl[l] != m * fold * 16) FAIL("malformed FRI layer %zu", l);
-            u128 *rows = (u128 *)malloc(m * fold * 16);
-            memcpy(rows, lv[l], lvl[l]);
+            if (lvl[l] != m * fold * 16 * K) FAIL("malformed FRI layer %zu", l);
+            e2 *rows = (e2 *)malloc(m * fold * sizeof(e2));
+            if (!rd_e(lv[l], m * fold, K, rows)) {
+                free(rows);
+                FAIL("non-canonical FRI value in layer %zu", l);
+            }
             uint8_t *dig = (uint8_t *)malloc(m * 32), root[32];
-            for (size_t q = 0; q < m; q++) blake3_hash_elems(rows + q * fold, fold, dig + 32 * q);
+            for (size_t q = 0; q < m; q++) blake3_hash_elems((const u128 *)(lv[l] + 16 * K * fold * q), fold * K, dig + 32 * q);
             rd_t pr = {lp[l], lpl[l], 0, 0};
             int e = batch_root(&pr, dig, folded, m, ilog2_sz(target), root);
             free(dig);
@@ -445,33 +469,43 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
             for (size_t i = 0; i < ncur; i++) {
                 size_t ri = 0;
                 while (folded[ri] != fp[i] % target) ri++;
-                if (rows[ri * fold + fp[i] / target] != evals[i]) {
+                if (!e2_eq(rows[ri * fold + fp[i] / target], evals[i])) {
                     free(rows);
                     FAIL("FRI layer %zu folding mismatch", l);
                 }
             }
-            u128 nxt[OR_MAX_QUERIES + 1];
+            e2 nxt[OR_MAX_QUERIES + 1];
             for (size_t q = 0; q < m; q++) {
-                u128 xe = f_mul(f_exp(dgen, folded[q]), F_GENERATOR), v[16];
-                (void)zeta;
-                memcpy(v, rows + q * fold, fold * 16);
-                interp_coset_u(v, fold, xe);
-                nxt[q] = poly_eval(v, fold, alphas[l]);
+                u128 xe = f_mul(f_exp(dgen, folded[q]), F_GENERATOR), va[16], vb[16];
+                for (size_t t = 0; t < fold; t++) {
+                    va[t] = rows[q * fold + t].a;
+                    vb[t] = rows[q * fold + t].b;
+                }
+                interp_coset_u(va, fold, xe);
+                if (K == 2) interp_coset_u(vb, fold, xe);
+                e2 acc = e2_base(0);
+                for (size_t t = fold; t-- > 0;) acc = e2_add(e2_mul(acc, alphas[l]), e2_make(va[t], K == 2 ? vb[t] : 0));
+                nxt[q] = acc;
             }
             free(rows);
-            memcpy(evals, nxt, m * 16);
+            memcpy(evals, nxt, m * sizeof(e2));
             memcpy(fp, folded, m * 8);
             ncur = m;
             dgen = f_exp(dgen, fold);
             dsz = target;
         }
-        /* remainder */
-        if (rem_len != dsz / B) FAIL("remainder has wrong size");
-        u128 *rp = (u128 *)malloc(rml + 16);
-        memcpy(rp, rm, rml);
+        /* remainder: an E polynomial with rem_len coefficients, evaluated at base points */
+        if (rem_len != dsz / B || rml != rem_len * 16 * K) FAIL("remainder has wrong size");
+        e2 *rp = (e2 *)malloc((rem_len + 1) * sizeof(e2));
+        if (!rd_e(rm, rem_len, K, rp)) {
+            free(rp);
+            FAIL("non-canonical remainder coefficient");
+        }
         for (size_t i = 0; i < ncur; i++) {
-            u128 x = f_mul(F_GENERATOR, f_exp(dgen, fp[i]));
-            if (poly_eval(rp, rem_len, x) != evals[i]) {
+            const e2 x = e2_base(f_mul(F_GENERATOR, f_exp(dgen, fp[i])));
+            e2 acc = e2_base(0);
+            for (size_t t = rem_len; t-- > 0;) acc = e2_add(e2_mul(acc, x), rp[t]);
+            if (!e2_eq(acc, evals[i])) {
                 free(rp);
                 FAIL("FRI remainder mismatch");
             }

@@ -117,6 +117,21 @@ def test_full_proof_matches_oracle(gpu, oracle, case):
     assert oracle.verify(proof, opub, 0) == (0, "")
 
 
+def test_config1_pushadd_2_16_bit_exact(gpu, oracle):
+    """BASELINE.json configs[1]: a 2^16-step Push/Add program, full prove on one GPU, proof bytes
+    identical to the CPU prover (the oracle, ~10 s)."""
+    src = ops_for_trace_len(16, "pushadd")
+    trace, pub = workload_trace(src, seed=16)
+    assert trace.shape[1] == 1 << 16
+    proof, rec, _, rc = gpu.prove(trace, pub, ProofOptions(), record=True)
+    assert rc == 0
+    opub = oracle_pub(oracle, pub)
+    oproof, orec, _ = oracle.prove(trace, opub)
+    compare_records(rec, orec)
+    assert proof == oproof
+    assert oracle.verify(proof, opub, 95) == (0, "")
+
+
 def test_stage_dumps_match_oracle(gpu, oracle):
     trace, pub = workload_trace(cipher_mix_program(30)[0], seed=11)
     names = ("trace_polys", "trace_lde", "trace_leaves", "composition", "comp_polys", "comp_lde", "deep", "fri_layer1")

@@ -83,3 +83,24 @@ def test_merkle_root(oracle):
     while len(lvl) > 1:
         lvl = [oracle.blake3(lvl[2 * i] + lvl[2 * i + 1]) for i in range(len(lvl) // 2)]
     assert oracle.merkle_root(b"".join(leaves)) == lvl[0]
+
+
+def test_quadratic_extension_against_bigint(oracle):
+    """E = F[X]/(X^2 - X - 1) (winter-math ExtensibleField<2> for f128): X^2 - X - 1 is irreducible
+    (its discriminant 5 is a non-residue mod p) and the oracle's mul / inv agree with polynomial
+    arithmetic mod (p, X^2 - X - 1) in Python big ints."""
+    P = 2**128 - 45 * 2**40 + 1
+    assert pow(5, (P - 1) // 2, P) == P - 1
+
+    def mul(x, y):  # (a0 + a1 X)(b0 + b1 X), X^2 = X + 1
+        c0, c1, c2 = x[0] * y[0], x[0] * y[1] + x[1] * y[0], x[1] * y[1]
+        return ((c0 + c2) % P, (c1 + c2) % P)
+
+    rng = random.Random(11)
+    for _ in range(50):
+        x = tuple(rng.randrange(P) for _ in range(2))
+        y = tuple(rng.randrange(P) for _ in range(2))
+        assert oracle.e2op("or_e2_mul", x, y) == mul(x, y)
+        xi = oracle.e2op("or_e2_inv", x)
+        assert mul(x, xi) == (1, 0)
+    assert oracle.e2op("or_e2_mul", (0, 1), (0, 1)) == (1, 1)  # X^2 = 1 + X

@@ -37,6 +37,12 @@ CASES = [
     ("cipher20", cipher_mix_program(20)[0], 4, {"num_queries": 40}),
     ("pushadd12_f2_r7", push_add_program(12), 6, {"fri_folding": 2, "fri_rem_max_deg": 7, "num_queries": 50}),
     ("lr_f16_r15", LR_PROGRAM, 7, {"fri_folding": 16, "fri_rem_max_deg": 15, "blowup": 32}),
+    # FieldExtension::Quadratic: E-valued coefficients, OOD, DEEP, FRI
+    ("lr_quad", LR_PROGRAM, 8, {"field_extension": 2}),
+    ("pushadd12_quad_q43_f4", push_add_program(12), 9,
+     {"field_extension": 2, "num_queries": 43, "fri_folding": 4, "fri_rem_max_deg": 31}),
+    ("cipher8_quad_f2_g9", cipher_mix_program(8)[0], 10,
+     {"field_extension": 2, "fri_folding": 2, "fri_rem_max_deg": 7, "grinding": 9}),
 ]
 
 
