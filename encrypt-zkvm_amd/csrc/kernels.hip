@@ -1046,6 +1046,251 @@ void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const 
 #undef ZK_FOLD
 }
 
+// ================================================================ FieldExtension::Quadratic (K5-K7 over E)
+// OOD over E points: the same wave layout as k_ood_eval with E-valued Horner steps.
+__global__ void k_ood_tables_ext(fe2 z, fe2 zg, uint64_t chunk, int nw, fe2 *tab) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 128 + 2 * nw) return;
+    fe2 x;
+    uint64_t e;
+    if (t < 128) {
+        x = t < 64 ? z : zg;
+        e = t & 63;
+    } else {
+        const int u = t - 128;
+        x = u < nw ? z : zg;
+        e = chunk * (uint64_t)(u < nw ? u : u - nw);
+    }
+    tab[t] = fe2_exp(x, e);
+}
+
+__device__ __forceinline__ fe2 horner_ext(const fe *v, int E, fe2 y) {
+    fe2 h = fe2_lift(v[E - 1]);
+    for (int e = E - 2; e >= 0; e--) {
+        h = fe2_mul(h, y);
+        h.a = fe_add(h.a, v[e]);
+    }
+    return h;
+}
+
+template <int E>
+__global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, const fe *cpolys, int C, size_t n,
+                                                      const fe2 *tab, int nw, fe *partials) {
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (gw >= nw) return;
+    const int np = 2 * W + C;
+    const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
+    const int g = blockIdx.y;
+    const bool comp = g >= tgroups;
+    const int p0 = comp ? 0 : g * OOD_GROUP;
+    const int p1 = comp ? C : min(W, p0 + OOD_GROUP);
+    const size_t base = (size_t)gw * 64 * E + lane;
+    const fe2 y0 = fe2_mul(tab[63], tab[1]), y1 = fe2_mul(tab[127], tab[65]);  // x^64
+    const fe2 wz = fe2_mul(tab[lane], tab[128 + gw]);
+    const fe2 wzg = comp ? fe2_zero() : fe2_mul(tab[64 + lane], tab[128 + nw + gw]);
+    for (int p = p0; p < p1; p++) {
+        const fe *c = (comp ? cpolys : tpolys) + (size_t)p * n;
+        fe v[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const size_t k = base + 64 * (size_t)e;
+            v[e] = k < n ? c[k] : fe_zero();
+        }
+        const fe2 hz = fe2_mul(horner_ext(v, E, y0), wz);
+        const fe sa = wave_sum(hz.a), sb = wave_sum(hz.b);
+        const int slot = comp ? 2 * W + p : p;
+        if (lane == 0) {
+            partials[(size_t)slot * nw + gw] = sa;
+            partials[(size_t)(np + slot) * nw + gw] = sb;
+        }
+        if (!comp) {
+            const fe2 hg = fe2_mul(horner_ext(v, E, y1), wzg);
+            const fe ga = wave_sum(hg.a), gb = wave_sum(hg.b);
+            if (lane == 0) {
+                partials[(size_t)(W + p) * nw + gw] = ga;
+                partials[(size_t)(np + W + p) * nw + gw] = gb;
+            }
+        }
+    }
+}
+
+void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
+                  fe *tab, fe *partials, fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    const int E = n >= 1024 ? 16 : std::max<int>(1, (int)(n / 64));
+    const int nw = (int)((n + 64 * E - 1) / (64 * E));
+    fe2 *t2 = reinterpret_cast<fe2 *>(tab);
+    hipLaunchKernelGGL(k_ood_tables_ext, dim3(cdiv(128 + 2 * nw, 256)), dim3(256), 0, st, z, zg, (uint64_t)64 * E, nw, t2);
+    const dim3 grid(cdiv(nw, 4), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
+#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval_ext<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, t2, nw, partials)
+    const double bytes = 16.0 * (W + C) * n;
+    switch (E) {
+        case 16: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(16)); break;
+        case 8: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(8)); break;
+        case 4: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(4)); break;
+        case 2: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(2)); break;
+        default: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(1)); break;
+    }
+#undef ZK_OOD
+    sum_partials(st, partials, 2 * (2 * W + C), nw, out);
+}
+
+// 1 / (N(x - z) N(x - zg)): N(x - z) = (x - z.a)(x - z.a - z.b) - z.b^2 (the norm of x - z, X^2 = X + 1)
+__device__ __forceinline__ fe norm_pair_denominator(const fe *xr, const fe *wlo, const fe *whi, size_t i, int log_n,
+                                                    fe2 z, fe2 zg, fe zb2, fe zgb2) {
+    const fe x = fe_mul(xr[i >> log_n], pow_split(wlo, whi, i & (((size_t)1 << log_n) - 1)));
+    const fe xa = fe_sub(x, z.a), ga = fe_sub(x, zg.a);
+    const fe d1 = fe_sub(fe_mul(xa, fe_sub(xa, z.b)), zb2);
+    const fe d2 = fe_sub(fe_mul(ga, fe_sub(ga, zg.b)), zgb2);
+    return fe_mul(d1, d2);
+}
+
+__global__ void __launch_bounds__(256) k_batch_inv_norm_pairs(const fe *xr, int log_b, int log_n, const fe *wlo,
+                                                              const fe *whi, fe2 z, fe2 zg, fe zb2, fe zgb2, fe *out,
+                                                              size_t total_threads) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    const size_t T = total_threads;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    fe acc = fe_one();
+#pragma unroll 4
+    for (int k = 0; k < INV_K; k++) {
+        const size_t i = t + (size_t)k * T;
+        if (i < N) {
+            acc = fe_mul(acc, norm_pair_denominator(xr, wlo, whi, i, log_n, z, zg, zb2, zgb2));
+            out[i] = acc;
+        }
+    }
+    fe inv = fe_inv(acc);
+#pragma unroll 4
+    for (int k = INV_K - 1; k >= 0; k--) {
+        const size_t i = t + (size_t)k * T;
+        if (i >= N) continue;
+        const fe d = norm_pair_denominator(xr, wlo, whi, i, log_n, z, zg, zb2, zgb2);
+        out[i] = k > 0 ? fe_mul(inv, out[i - T]) : inv;
+        inv = fe_mul(inv, d);
+    }
+}
+
+void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,
+                          fe *out) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    const size_t threads = (N + INV_K - 1) / INV_K;
+    const fe zb2 = fe_mul(z.b, z.b), zgb2 = fe_mul(zg.b, zg.b);
+    ZK_PROF(st, "batch_inv_ext", 16.0 * N, hipLaunchKernelGGL(k_batch_inv_norm_pairs, dim3(cdiv(threads, 256)), dim3(256), 0, st, xr,
+                                                    log_b, log_n, Tn.fwd_lo, Tn.fwd_hi, z, zg, zb2, zgb2, out, threads));
+}
+
+// DEEP over E at x (natural index i):
+//   s1 = sum_c at_c T_c(x) + sum_j ac_j H_j(x) - k1,  s2 = sum_c at_c T_c(x) - k2
+//   deep = s1 / (x - z) + s2 / (x - zg) = (s1 u1 d2 + s2 u2 d1) / (d1 d2)
+// with (x - z)^-1 = u1 / d1, u1 = (x - z.a - z.b) + z.b X, d1 = N(x - z).
+__global__ void __launch_bounds__(256) k_deep_ext(const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                                                  const DeepConstsE *D, const fe *wN_lo, const fe *wN_hi, fe three,
+                                                  const fe *inv_d, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i & (B - 1), q = i >> log_b;
+        const fe *p = lde + r * n + q;
+        acc288 aA = acc288_zero(), aB = acc288_zero();
+#pragma unroll 4
+        for (int c = 0; c < 28; c++) {
+            const fe v = p[(size_t)c * B * n];
+            acc288_madd(aA, D->alpha_t[c].a, v);
+            acc288_madd(aB, D->alpha_t[c].b, v);
+        }
+        const fe2 sT = fe2{acc288_reduce(aA), acc288_reduce(aB)};
+        const fe *pc = clde + r * n + q;
+        acc288 hA = acc288_zero(), hB = acc288_zero();
+        for (int j = 0; j < ccols; j++) {
+            const fe h0 = pc[(size_t)(2 * j) * B * n], h1 = pc[(size_t)(2 * j + 1) * B * n];
+            const fe2 ac = D->alpha_c[j];
+            acc288_madd(hA, ac.a, h0);  // (ac.a + ac.b X)(h0 + h1 X) = (ac.a h0 + ac.b h1) + (ac.a h1 + ac.b (h0 + h1)) X
+            acc288_madd(hA, ac.b, h1);
+            acc288_madd(hB, ac.a, h1);
+            acc288_madd(hB, ac.b, fe_add(h0, h1));
+        }
+        const fe2 sH = fe2{acc288_reduce(hA), acc288_reduce(hB)};
+        const fe2 s1 = fe2_sub(fe2_add(sT, sH), D->k1), s2 = fe2_sub(sT, D->k2);
+        const fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));
+        const fe xa = fe_sub(x, D->z.a), ga = fe_sub(x, D->zg.a);
+        const fe u1 = fe_sub(xa, D->z.b), u2 = fe_sub(ga, D->zg.b);
+        const fe d1 = fe_sub(fe_mul(xa, u1), D->zb2), d2 = fe_sub(fe_mul(ga, u2), D->zgb2);
+        const fe2 t1 = fe2_mul(s1, fe2{u1, D->z.b}), t2 = fe2_mul(s2, fe2{u2, D->zg.b});
+        const fe2 num = fe2_add(fe2_mulb(t1, d2), fe2_mulb(t2, d1));
+        const fe2 res = fe2_mulb(num, inv_d[r * n + q]);
+        out[i] = res.a;
+        out[N + i] = res.b;
+    }
+}
+
+void deep_eval_ext_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                          const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    unsigned blocks = cdiv(N, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "deep_ext", (448.0 + 32.0 * ccols + 48.0) * N, hipLaunchKernelGGL(k_deep_ext, dim3(blocks), dim3(256), 0, st, lde, log_n, log_b,
+                                                   clde, ccols, (const DeepConstsE *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi,
+                                                   three, inv_d, out));
+}
+
+// FRI row r over E: [e(r + k rows)]_k, each value hashed as (a, b)
+__global__ void __launch_bounds__(256) k_hash_fri_rows_ext(const fe *layer, size_t L, int fold, uint8_t *leaves) {
+    const size_t rows = L / fold;
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h[8];
+        b3::hash_elements(2 * fold, [&](int t) { return layer[(size_t)(t & 1) * L + r + (size_t)(t >> 1) * rows]; }, h);
+        store_digest(leaves + 32 * r, h);
+    }
+}
+
+void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes) {
+    const size_t rows = L / fold;
+    ZK_PROF(st, "hash_fri_rows_ext", 32.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows_ext, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, leaves));
+    merkle_tree(st, leaves, rows, nodes);
+}
+
+// FRI fold over E: the interpolation is F-linear, so each component goes through idft_small and the
+// resulting E coefficients are evaluated at beta = alpha / x_r by an E Horner.
+template <int F>
+__global__ void __launch_bounds__(256) k_fri_fold_ext(const fe *layer, size_t L, const FoldConstsE *Fc, const fe *wi_lo,
+                                                      const fe *wi_hi, size_t wstride, fe *next) {
+    const size_t rows = L / F;
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
+        fe va[F], vb[F];
+#pragma unroll
+        for (int k = 0; k < F; k++) {
+            va[k] = layer[r + (size_t)k * rows];
+            vb[k] = layer[L + r + (size_t)k * rows];
+        }
+        const fe2 beta = fe2_mulb(Fc->alpha, fe_mul(Fc->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
+        idft_small<F>(va, Fc->zinv);
+        idft_small<F>(vb, Fc->zinv);
+        fe2 acc = fe2{va[F - 1], vb[F - 1]};
+#pragma unroll
+        for (int m = F - 2; m >= 0; m--) acc = fe2_add(fe2_mul(acc, beta), fe2{va[m], vb[m]});
+        acc = fe2_mulb(acc, Fc->inv_fold);
+        next[r] = acc.a;
+        next[rows + r] = acc.b;
+    }
+}
+
+void fri_fold_ext_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
+                         const NttTables &TN, size_t wstride, fe *next) {
+    unsigned blocks = cdiv(L / fold, 256);
+    if (blocks > 65536) blocks = 65536;
+    const FoldConstsE *F = (const FoldConstsE *)fold_consts_dev;
+#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold_ext", 32.0 * L + 32.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold_ext<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, next))
+    switch (fold) {
+        case 2: ZK_FOLD(2); break;
+        case 4: ZK_FOLD(4); break;
+        case 8: ZK_FOLD(8); break;
+        default: ZK_FOLD(16); break;
+    }
+#undef ZK_FOLD
+}
+
 // ================================================================ elementwise helpers
 __global__ void k_coset_major_to_natural(const fe *src, int log_n, int log_b, fe *dst) {
     size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;

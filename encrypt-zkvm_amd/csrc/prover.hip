@@ -329,7 +329,7 @@ BatchPlan zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
 // ---------------------------------------------------------------- protocol steps (host side)
 int zk::check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_options *o, const zk_pub_inputs *pub) {
     if (!o || !pub) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
-    if (o->field_extension != 1 || o->blowup < 8 || (o->blowup & (o->blowup - 1)) ||
+    if ((o->field_extension != 1 && o->field_extension != 2) || o->blowup < 8 || (o->blowup & (o->blowup - 1)) ||
         (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) ||
         ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) || o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
@@ -406,6 +406,28 @@ void zk::draw_air_consts(Coin &coin, const zk_pub_inputs *pub, size_t n, AirCons
     for (int k = 0; k < NUM_TCONS; k++) fe_to_bytes(K.coeff_t[k] = coin.draw(), R.coeff_t[k]);
     for (int k = 0; k < NUM_ASSERTS; k++) fe_to_bytes(K.coeff_b[k] = coin.draw(), R.coeff_b[k]);
     air_static_consts(pub, n, K);
+}
+
+void zk::draw_air_consts_ext(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &Ka, AirConsts &Kb,
+                             zk_record &R) {
+    memset(&Ka, 0, sizeof Ka);
+    for (int k = 0; k < NUM_TCONS; k++) {
+        const fe2 v = coin.draw_ext(2);
+        Ka.coeff_t[k] = v.a;
+        Kb.coeff_t[k] = v.b;
+        fe_to_bytes(v.a, R.coeff_t[k]);
+    }
+    for (int k = 0; k < NUM_ASSERTS; k++) {
+        const fe2 v = coin.draw_ext(2);
+        Ka.coeff_b[k] = v.a;
+        Kb.coeff_b[k] = v.b;
+        fe_to_bytes(v.a, R.coeff_b[k]);
+    }
+    air_static_consts(pub, n, Ka);
+    const AirConsts tmp = Kb;
+    Kb = Ka;
+    memcpy(Kb.coeff_t, tmp.coeff_t, sizeof Kb.coeff_t);
+    memcpy(Kb.coeff_b, tmp.coeff_b, sizeof Kb.coeff_b);
 }
 
 void zk::ood_reseed(Coin &coin, const fe *h, int C, zk_record &R) {
@@ -543,8 +565,9 @@ std::vector<std::vector<uint64_t>> zk::fri_fold_positions(const std::vector<uint
 }
 
 std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood,
-                                         const Openings &O) {
+                                         const Openings &O, const std::vector<fe> *rem_flat) {
     const int nl = (int)R.num_fri_layers;
+    const int K = (int)opt->field_extension, ES = 16 * K;
     const size_t nu = R.num_positions;
     Bytes pf;
     pf.u8(W);
@@ -583,19 +606,20 @@ std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C,
     };
     pf.u8(1);
     write_queries(O.trace_rows.data(), nu * W * 16, 0);
-    write_queries(O.comp_rows.data(), nu * C * 16, 1);
-    pf.u16((uint16_t)(1 + 2 * W * 16));
+    write_queries(O.comp_rows.data(), nu * C * ES, 1);
+    pf.u16((uint16_t)(1 + 2 * W * ES));
     pf.u8(2);
     for (int c = 0; c < W; c++) {
-        pf.put(&ood[c], 16);
-        pf.put(&ood[W + c], 16);
+        pf.put(&ood[c * K], ES);
+        pf.put(&ood[(W + c) * K], ES);
     }
-    pf.u16((uint16_t)(C * 16));
-    pf.put(ood + 2 * W, C * 16);
+    pf.u16((uint16_t)(C * ES));
+    pf.put(ood + 2 * W * K, C * ES);
     pf.u8((uint8_t)nl);
     for (int l = 0; l < nl; l++) write_queries(O.fri_rows[l].data(), O.fri_rows[l].size() * 16, 2 + l);
-    pf.u16((uint16_t)(R.remainder_len * 16));
-    pf.put(R.remainder, R.remainder_len * 16);
+    pf.u16((uint16_t)(R.remainder_len * ES));
+    if (rem_flat) pf.put(rem_flat->data(), R.remainder_len * ES);
+    else pf.put(R.remainder, R.remainder_len * 16);
     pf.u8(0);
     pf.u64(R.pow_nonce);
     pf.u8(0);
@@ -646,6 +670,25 @@ static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, si
         for (size_t i = 0; i < N; i++) o[i * ncols + c] = h[((size_t)c * B + (i % B)) * n + i / B];
 }
 
+// FieldExtension::Quadratic buffers (planar E): composition 2 x 8n, its inverse NTT, the composition LDE
+// (up to 2 x 8 base columns), DEEP 2N, FRI layers 2(N + 16), OOD tables and partial sums.
+static int ensure_ext(zk_prover *p) {
+    if (p->x_comp) return ZK_OK;
+    const size_t n = p->max_n, N = n * p->max_b, CE = 8 * n;
+    DeviceArena &A = p->arena;
+    ZK_CHECK_HIP(A.alloc(&p->x_comp, 2 * CE));
+    ZK_CHECK_HIP(A.alloc(&p->x_ctmp, 2 * CE));
+    ZK_CHECK_HIP(A.alloc(&p->x_clde, (size_t)2 * 8 * N));  // C <= 8 E columns
+    ZK_CHECK_HIP(A.alloc(&p->x_deep, 2 * N));
+    ZK_CHECK_HIP(A.alloc(&p->x_fri, 2 * (N + 16)));
+    ZK_CHECK_HIP(A.alloc(&p->x_partials, (size_t)2 * (2 * ZK_MAX_COLS + ZK_MAX_CCOLS) * ood_waves(n)));
+    ZK_CHECK_HIP(A.alloc(&p->x_tab, (size_t)2 * (128 + 2 * ood_waves(n))));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_air, 2 * sizeof(AirConsts)));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_deep_consts, sizeof(DeepConstsE)));
+    ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_fold_consts, sizeof(FoldConstsE)));
+    return ZK_OK;
+}
+
 int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                     uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     if (!p || !d_trace_v || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
@@ -679,46 +722,124 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "trace_commit");
     coin.reseed(R.trace_root);
 
-    // S3: constraint composition coefficients [P4] and evaluation over the CE domain
-    AirConsts K;
-    draw_air_consts(coin, pub, n, K, R);
-    ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
-    batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), K.g_last2, p->inv);
-    eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->air_consts,
-                     p->comp);
+    // S3: constraint composition coefficients [P4] and evaluation over the CE domain.  With
+    // FieldExtension::Quadratic the coefficients are E values and the composition has two planes
+    // (a, b): the evaluator runs once per plane with that component of every coefficient.
+    const int KX = (int)opt->field_extension, CK = C * KX;
+    if (KX == 2) ZK_TRY(ensure_ext(p));
+    fe *comp = KX == 2 ? p->x_comp : p->comp, *ctmp = KX == 2 ? p->x_ctmp : p->ctmp;
+    fe *clde = KX == 2 ? p->x_clde : p->clde, *deep = KX == 2 ? p->x_deep : p->deep;
+    fe *fri = KX == 2 ? p->x_fri : p->fri;
+    if (KX == 1) {
+        AirConsts K;
+        draw_air_consts(coin, pub, n, K, R);
+        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), K.g_last2, p->inv);
+        eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->air_consts,
+                         comp);
+    } else {
+        AirConsts Kp[2];
+        draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
+        ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
+        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), Kp[0].g_last2, p->inv);
+        for (int j = 0; j < 2; j++)
+            eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->x_air + j,
+                             comp + j * CE);
+    }
     stage_mark(p, "constraints");
 
-    // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit
-    ntt(p->st, pl->Tn, p->comp, n, p->ctmp, n, 8, true, nullptr, nullptr, p->tmp);
+    // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit.
+    // Base column (c, j) of the E column c lives at cpolys[(c*k + j)*n]: a leaf is C E values.
+    ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
     ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
-    comp_cross_coset(p->st, p->ctmp, log_n, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
-                     h_inv(h_pow(three, n)), C, p->cpolys, p->flag);
+    for (int j = 0; j < KX; j++) {
+        CrossMap m;
+        for (int r = 0; r < 8; r++) m.c[r] = ctmp + (size_t)(8 * j + r) * n;
+        m.k0 = 0;
+        m.kcount = n;
+        m.pstride = (size_t)KX * n;
+        comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
+                          h_inv(h_pow(three, n)), C, p->cpolys + (size_t)j * n, p->flag);
+    }
     for (uint32_t r = 0; r < B; r++)
-        ntt(p->st, pl->Tn, p->cpolys, n, p->clde + r * n, B * n, C, false, &pl->coset[r], nullptr, p->tmp);
-    ZK_TRY(commit_rows(p, p->clde, C, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
+        ntt(p->st, pl->Tn, p->cpolys, n, clde + r * n, B * n, CK, false, &pl->coset[r], nullptr, p->tmp);
+    ZK_TRY(commit_rows(p, clde, CK, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
     ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
     coin.reseed(R.constraint_root);
 
-    // S5: OOD frame [P7], DEEP coefficients [P8] and evaluations
-    const fe z = coin.draw(), zg = fe_mul(z, g);
-    fe_to_bytes(z, R.z);
-    fe h[2 * W + ZK_MAX_CCOLS];
-    ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
-    ZK_CHECK_HIP(hipMemcpyAsync(h, p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    ood_reseed(coin, h, C, R);
-    stage_mark(p, "ood");
-    {
-        const DeepConsts D = draw_deep_consts(coin, h, C, z, zg, R);
+    // S5: OOD frame [P7], DEEP coefficients [P8] and evaluations.  h holds the frame flattened
+    // (k base elements per E value): [T(z)]_W ++ [T(zg)]_W ++ [H(z)]_C.
+    std::vector<fe> h((2 * W + C) * KX);
+    if (KX == 1) {
+        const fe z = coin.draw(), zg = fe_mul(z, g);
+        fe_to_bytes(z, R.z);
+        ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
+        ZK_CHECK_HIP(hipMemcpyAsync(h.data(), p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        ood_reseed(coin, h.data(), C, R);
+        stage_mark(p, "ood");
+        const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         batch_inv_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
-        deep_eval_launch(p->st, p->lde, log_n, log_b, p->clde, C, p->deep_consts, pl->TN, three, p->inv, p->deep);
+        deep_eval_launch(p->st, p->lde, log_n, log_b, clde, C, p->deep_consts, pl->TN, three, p->inv, deep);
+    } else {
+        const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
+        fe_to_bytes(z.a, R.z);
+        const int np = 2 * W + CK;  // E values of the trace polys at z, zg and of the C*k base composition polys at z
+        ood_eval_ext(p->st, p->polys, W, p->cpolys, CK, log_n, z, zg, p->x_tab, p->x_partials, p->ood);
+        std::vector<fe> hv(2 * np);
+        ZK_CHECK_HIP(hipMemcpyAsync(hv.data(), p->ood, hv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        std::vector<fe2> e(2 * W + C);
+        for (int c = 0; c < 2 * W; c++) e[c] = fe2{hv[c], hv[np + c]};
+        for (int c = 0; c < C; c++) {  // H_c(z) = P_c0(z) + X * P_c1(z)
+            const int s0 = 2 * W + 2 * c;
+            e[2 * W + c] = fe2_add(fe2{hv[s0], hv[np + s0]}, fe2_mulX(fe2{hv[s0 + 1], hv[np + s0 + 1]}));
+        }
+        for (size_t i = 0; i < e.size(); i++) {
+            h[2 * i] = e[i].a;
+            h[2 * i + 1] = e[i].b;
+        }
+        for (int c = 0; c < W; c++) {
+            fe_to_bytes(e[c].a, R.ood_trace_z[c]);
+            fe_to_bytes(e[W + c].a, R.ood_trace_zg[c]);
+        }
+        for (int j = 0; j < C; j++) fe_to_bytes(e[2 * W + j].a, R.ood_constraints[j]);
+        uint8_t d[32];
+        hash_elems(h.data(), 4 * W, d);
+        coin.reseed(d);
+        hash_elems(h.data() + 4 * W, 2 * C, d);
+        coin.reseed(d);
+        stage_mark(p, "ood");
+        DeepConstsE D;
+        memset(&D, 0, sizeof D);
+        fe2 k1 = fe2_zero(), k2 = fe2_zero();
+        for (int c = 0; c < W; c++) {
+            D.alpha_t[c] = coin.draw_ext(2);
+            fe_to_bytes(D.alpha_t[c].a, R.deep_t[c]);
+            k1 = fe2_add(k1, fe2_mul(D.alpha_t[c], e[c]));
+            k2 = fe2_add(k2, fe2_mul(D.alpha_t[c], e[W + c]));
+        }
+        for (int j = 0; j < C; j++) {
+            D.alpha_c[j] = coin.draw_ext(2);
+            fe_to_bytes(D.alpha_c[j].a, R.deep_c[j]);
+            k1 = fe2_add(k1, fe2_mul(D.alpha_c[j], e[2 * W + j]));
+        }
+        D.k1 = k1;
+        D.k2 = k2;
+        D.z = z;
+        D.zg = zg;
+        D.zb2 = fe_mul(z.b, z.b);
+        D.zgb2 = fe_mul(zg.b, zg.b);
+        ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+        batch_inv_norm_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
+        deep_eval_ext_launch(p->st, p->lde, log_n, log_b, clde, C, p->x_deep_consts, pl->TN, three, p->inv, deep);
     }
     stage_mark(p, "deep");
 
-    // S6: FRI [P9, P10]
+    // S6: FRI [P9, P10]; E layers are planar (k planes of L values)
     const int nl = fri_num_layers(N, opt);
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
@@ -730,33 +851,68 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     std::vector<const fe *> layer_vals(nl + 1);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
-    layer_vals[0] = p->deep;
+    std::vector<fe> rem_flat;
+    layer_vals[0] = deep;
     layer_len[0] = N;
     {
-        fe *next = p->fri;
+        fe *next = fri;
         uint8_t *dig = p->fri_dig;
         for (int l = 0; l < nl; l++) {
             const size_t L = layer_len[l], rows = L / fold;
             layer_leaves[l] = dig;
             layer_nodes[l] = dig + 32 * rows;
             dig += 64 * rows;
-            commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+            if (KX == 1) commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+            else commit_fri_layer_ext(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
             ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
             ZK_CHECK_HIP(hipStreamSynchronize(p->st));
             coin.reseed(R.fri_roots[l]);
-            const fe alpha = coin.draw();
-            fe_to_bytes(alpha, R.fri_alphas[l]);
-            const FoldConsts F = fold_consts(alpha, fold);
-            ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
-            fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
+            if (KX == 1) {
+                const fe alpha = coin.draw();
+                fe_to_bytes(alpha, R.fri_alphas[l]);
+                const FoldConsts F = fold_consts(alpha, fold);
+                ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+                fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
+            } else {
+                const fe2 alpha = coin.draw_ext(2);
+                fe_to_bytes(alpha.a, R.fri_alphas[l]);
+                const FoldConsts F1 = fold_consts(fe_zero(), fold);
+                FoldConstsE F;
+                memcpy(F.zinv, F1.zinv, sizeof F.zinv);
+                F.alpha = alpha;
+                F.inv_offset = F1.inv_offset;
+                F.inv_fold = F1.inv_fold;
+                ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+                fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
+            }
             layer_vals[l + 1] = next;
             layer_len[l + 1] = rows;
-            next += rows;
+            next += KX * rows;
         }
-        std::vector<fe> rv(layer_len[nl]);
+        const size_t L = layer_len[nl];
+        std::vector<fe> rv(KX * L);
         ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
+        if (KX == 1) {
+            ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
+        } else {
+            // per component: interpolate over 3 * <w_L>, keep L/B coefficients; commit to the E coefficients
+            std::vector<fe> va(rv.begin(), rv.begin() + L), vb(rv.begin() + L, rv.end());
+            h_interp_coset(va, three);
+            h_interp_coset(vb, three);
+            const size_t rl = L / B;
+            if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
+            for (size_t k = rl; k < L; k++)
+                if (!fe_is_zero(va[k]) || !fe_is_zero(vb[k])) degree_flag = 1;
+            R.remainder_len = (uint32_t)rl;
+            for (size_t k = 0; k < rl; k++) {
+                fe_to_bytes(va[k], R.remainder[k]);
+                rem_flat.push_back(va[k]);
+                rem_flat.push_back(vb[k]);
+            }
+            hash_elems(rem_flat.data(), rem_flat.size(), R.remainder_commitment);
+            coin.reseed(R.remainder_commitment);
+        }
     }
     stage_mark(p, "fri");
 
@@ -778,11 +934,12 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         for (int c = 0; c < ncols; c++) fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
     };
     for (size_t q = 0; q < nu; q++) row_at(p->lde, W, pos[q]);
-    for (size_t q = 0; q < nu; q++) row_at(p->clde, C, pos[q]);
+    for (size_t q = 0; q < nu; q++) row_at(clde, CK, pos[q]);
     for (int l = 0; l < nl; l++) {
         const size_t rows = layer_len[l] / fold;
         for (uint64_t r : fri_pos[l])
-            for (uint32_t k = 0; k < fold; k++) fe_at(layer_vals[l], r + k * rows);
+            for (uint32_t k = 0; k < fold; k++)
+                for (int j = 0; j < KX; j++) fe_at(layer_vals[l], j * layer_len[l] + r + k * rows);
     }
     const size_t off_dig = addr.size();
     for (int b = 0; b < 2 + nl; b++) {
@@ -805,11 +962,11 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         size_t off = 0;
         O.trace_rows.assign(got.begin(), got.begin() + nu * W);
         off += nu * W;
-        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * C);
-        off += nu * C;
+        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * CK);
+        off += nu * CK;
         for (int l = 0; l < nl; l++) {
-            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold);
-            off += fri_pos[l].size() * fold;
+            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold * KX);
+            off += fri_pos[l].size() * fold * KX;
         }
         const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
         for (int b = 0; b < 2 + nl; b++) {
@@ -821,21 +978,21 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "queries");
 
     // S9: proof bytes [P13, P14]
-    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h, O);
+    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h.data(), O, KX == 2 ? &rem_flat : nullptr);
     stage_mark(p, "serialize");
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     stage_collect(p);
     collect_kernel_stats(p);
 
     if (rec) *rec = R;
-    if (dump) {
+    if (dump) {  // E-valued stages dump their a component (as the oracle does)
         if (dump->trace_polys) ZK_CHECK_HIP(hipMemcpy(dump->trace_polys, p->polys, (size_t)W * n * 16, hipMemcpyDeviceToHost));
         if (dump->trace_lde) coset_major_rows_to_host(p, p->lde, W, n, B, dump->trace_lde);
         if (dump->trace_leaves) ZK_CHECK_HIP(hipMemcpy(dump->trace_leaves, p->leaves, 32 * N, hipMemcpyDeviceToHost));
-        if (dump->composition) coset_major_rows_to_host(p, p->comp, 1, n, 8, dump->composition);
-        if (dump->comp_polys) ZK_CHECK_HIP(hipMemcpy(dump->comp_polys, p->cpolys, (size_t)C * n * 16, hipMemcpyDeviceToHost));
-        if (dump->comp_lde) coset_major_rows_to_host(p, p->clde, C, n, B, dump->comp_lde);
-        if (dump->deep) ZK_CHECK_HIP(hipMemcpy(dump->deep, p->deep, N * 16, hipMemcpyDeviceToHost));
+        if (dump->composition) coset_major_rows_to_host(p, comp, 1, n, 8, dump->composition);
+        if (dump->comp_polys) ZK_CHECK_HIP(hipMemcpy(dump->comp_polys, p->cpolys, (size_t)CK * n * 16, hipMemcpyDeviceToHost));
+        if (dump->comp_lde) coset_major_rows_to_host(p, clde, CK, n, B, dump->comp_lde);
+        if (dump->deep) ZK_CHECK_HIP(hipMemcpy(dump->deep, deep, N * 16, hipMemcpyDeviceToHost));
         if (dump->fri_layer1 && nl > 0)
             ZK_CHECK_HIP(hipMemcpy(dump->fri_layer1, layer_vals[1], layer_len[1] * 16, hipMemcpyDeviceToHost));
     }

@@ -96,6 +96,10 @@ struct zk_prover {
     fe *sh_zero = nullptr;      // one zero chunk (stands in for openings another rank owns)
     uint8_t *sh_roots = nullptr;  // world subtree roots
     unsigned *sh_flags = nullptr;  // world degree flags
+    // FieldExtension::Quadratic working set (planar E buffers), allocated on first use
+    fe *x_comp = nullptr, *x_ctmp = nullptr, *x_clde = nullptr, *x_deep = nullptr, *x_fri = nullptr,
+       *x_partials = nullptr, *x_tab = nullptr;
+    void *x_air = nullptr, *x_deep_consts = nullptr, *x_fold_consts = nullptr;
     uint32_t *pow_seed = nullptr;            // grinding: the coin seed ...
     unsigned long long *pow_best = nullptr;  // ... and the smallest nonce found
     std::map<std::pair<int, int>, std::unique_ptr<zk::Plan>> plans;
@@ -153,6 +157,9 @@ int num_comp_cols(size_t n);
 Coin seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub);
 // S3: composition coefficients (20 transition, 22 boundary) and the evaluator's constants [P3, P4]
 void draw_air_consts(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &K, zk_record &R);
+// FieldExtension::Quadratic: the coefficients are E values (a + bX); the composition is linear in them, so
+// the evaluator runs once with the a components (Ka) and once with the b components (Kb)
+void draw_air_consts_ext(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &Ka, AirConsts &Kb, zk_record &R);
 // S5: record the OOD frame h = T(z) || T(zg) || H(z) and reseed the coin with its two hashes [P7]
 void ood_reseed(Coin &coin, const fe *h, int C, zk_record &R);
 // S5: DEEP coefficients and the combined constants k1, k2 [P8]
@@ -178,9 +185,11 @@ struct Openings {
     std::vector<BatchPlan> plans;                // 2 + nl
     std::vector<std::vector<uint8_t>> digests;   // 2 + nl, 32 B each, plan order
 };
-// S9: Proof::to_bytes [P13, P14]
-std::vector<uint8_t> serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood,
-                                     const Openings &O);
+// S9: Proof::to_bytes [P13, P14].  E values are k = opt->field_extension base elements each:
+// ood_flat = [T(z)]_W ++ [T(zg)]_W ++ [H(z)]_C flattened, comp_rows nu x C*k, fri_rows |pos| x fold*k;
+// the remainder is R.remainder (k = 1) or rem_flat (rem_len x k).
+std::vector<uint8_t> serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood_flat,
+                                     const Openings &O, const std::vector<fe> *rem_flat = nullptr);
 // copy the proof out (proof_len in/out) and fold the degree flag into the status
 int deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, uint8_t *proof_out, size_t *proof_len);
 

@@ -663,6 +663,7 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
         X.rank.push_back(comm->loopback() ? l : comm->rank);
     }
     if (opt->blowup != 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "the sharded prover needs blowup 8 (LDE cosets = CE cosets)");
+    if (opt->field_extension != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "the sharded prover supports FieldExtension::None only");
     const size_t m = n / opt->fri_folding;
     if (m < 8 * (size_t)X.G || n / X.G < 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace too short to shard over this many ranks");
     X.log_n = ilog2(n);

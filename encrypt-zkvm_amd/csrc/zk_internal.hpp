@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "ext2.hpp"
 #include "f128.hpp"
 
 namespace zk {
@@ -168,6 +169,34 @@ struct FoldConsts {
 void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
                      const NttTables &TN, size_t wstride, fe *next);
 void coset_major_to_natural(hipStream_t st, const fe *src, int log_n, int log_b, fe *dst);
+
+// ---------------------------------------------------------------- FieldExtension::Quadratic (ext2.hpp)
+// Every E-valued buffer is planar: component a at [0, M), component b at [M, 2M).
+// OOD frame over E points: out[j*np + P], np = 2W + C, component j of poly P's value (T(z), T(zg), H(z));
+// tab: 2 * (128 + 2 * ood_waves(n)) fe, partials: 2 * np * ood_waves(n) fe.
+void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
+                  fe *tab, fe *partials, fe *out);
+// out[i] = 1 / (N(x_i - z) N(x_i - zg)), N the norm E -> F (coset-major like batch_inv_pairs)
+void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,
+                          fe *out);
+struct DeepConstsE {
+    fe2 alpha_t[32];
+    fe2 alpha_c[16];
+    fe2 k1, k2, z, zg;
+    fe zb2, zgb2;  // z.b^2, zg.b^2
+};
+// DEEP over E: ccols E columns = base columns (2j, 2j+1) of clde; out planar (2N)
+void deep_eval_ext_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
+                          const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
+struct FoldConstsE {
+    fe zinv[16];
+    fe2 alpha;
+    fe inv_offset, inv_fold;
+};
+// layer planar (2L), next planar (2 L/fold); leaves hash rows of fold E values (a, b per value)
+void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes);
+void fri_fold_ext_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
+                         const NttTables &TN, size_t wstride, fe *next);
 // out[k] = src[idx[k]] for field elements
 void gather_fe(hipStream_t st, const fe *src, const uint64_t *idx, size_t k, fe *out);
 

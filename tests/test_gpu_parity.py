@@ -148,6 +148,43 @@ def test_stage_dumps_match_oracle(gpu, oracle):
             assert np.array_equal(dumps[name][:k], odumps[name][:k]), name
 
 
+def test_quadratic_stage_dumps_match_oracle(gpu, oracle):
+    """FieldExtension::Quadratic: every stage (a components of the E-valued ones, both planes of the
+    composition columns) equals the oracle's."""
+    trace, pub = workload_trace(cipher_mix_program(30)[0], seed=12)
+    names = ("composition", "comp_polys", "comp_lde", "deep", "fri_layer1")
+    opts = ProofOptions(32, 8, 0, 2, 8, 127)
+    proof, _, dumps, rc = gpu.prove(trace, pub, opts, dump=names)
+    assert rc == 0
+    oproof, orec, odumps = oracle.prove(trace, oracle_pub(oracle, pub), oracle.default_options(field_extension=2),
+                                        want=names)
+    n = trace.shape[1]
+    ck = 2 * orec.num_ccols
+    trim = {"comp_polys": ck * n, "comp_lde": 8 * n * ck}
+    for name in names:
+        k = trim.get(name, len(odumps[name]))
+        assert np.array_equal(dumps[name][:k], odumps[name][:k]), name
+    assert proof == oproof
+
+
+def test_config5_quadratic_128_bit(gpu, oracle):
+    """SURVEY config 5 at 2^14: FieldExtension::Quadratic with 43 queries reaches 128-bit conjectured
+    security; proof bytes identical to the oracle's and accepted by both verifiers at 128 bits."""
+    from zkvm_amd.prover import verify
+    src = ops_for_trace_len(14, "pushadd")
+    trace, pub = workload_trace(src, seed=14)
+    opts = ProofOptions(43, 8, 0, 2, 8, 127)
+    proof, rec, _, rc = gpu.prove(trace, pub, opts, record=True)
+    assert rc == 0
+    opub = oracle_pub(oracle, pub)
+    oproof, orec, _ = oracle.prove(trace, opub, oracle.default_options(num_queries=43, field_extension=2))
+    compare_records(rec, orec)
+    assert proof == oproof
+    assert oracle.verify(proof, opub, 128) == (0, "")
+    assert verify(proof, pub, 128) == (0, "")
+    assert verify(proof, pub, 129)[0] == native.ZK_ERR_VERIFY
+
+
 def test_plug_points(gpu, oracle):
     """zk_lde_new / read_frame / query / eval_constraints against the oracle's stages."""
     trace, pub = workload_trace(LR_PROGRAM, seed=2)

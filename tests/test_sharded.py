@@ -14,7 +14,8 @@ from zkvm_amd.prover import GpuProver, ProofOptions, make_pub_inputs
 from zkvm_amd.sharded import ShardedProver
 
 GOLD = Path(__file__).resolve().parent / "golden"
-CASES = [c for c in json.loads((GOLD / "cases.json").read_text())["cases"] if c["options"]["blowup"] == 8]
+CASES = [c for c in json.loads((GOLD / "cases.json").read_text())["cases"]
+         if c["options"]["blowup"] == 8 and c["options"]["field_extension"] == 1]
 
 
 def ints(hs):
