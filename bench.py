@@ -11,6 +11,9 @@ Multi-GPU (one process per GPU, torchrun): every rank proves its own independent
 scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
 whole-job rate.  rank 0 prints one JSON line.
 
+--config5 (BASELINE.json configs[4]): the same workload at 128-bit conjectured security,
+ProofOptions(43, 8, 0, Quadratic, 8, 127): composition, OOD, DEEP and FRI over the quadratic extension.
+
 --sharded (BASELINE.json configs[3], e.g. --log-n 22): ONE proof per step with the LDE domain sharded
 by coset over all ranks (zk_prove_sharded, RCCL over xGMI: all-to-all of leaf digests and composition
 coefficient slices, all-gathers of subtree roots, FRI layer 1 and openings); strong scaling.
@@ -88,7 +91,7 @@ def timed_loop(step, steps: int, warmup: int, pg, local: int) -> float:
     return max_over_ranks(pg, time.perf_counter() - t0, local)
 
 
-def cpu_baseline(log_n: int):
+def cpu_baseline(log_n: int, config5: bool = False):
     """The oracle's single-threaded CPU prove (the build's restatement of the reference path; the
     reference Rust prover cannot be built here) on a bounded sample of the same generator."""
     from oracle import oracle as orc
@@ -99,13 +102,14 @@ def cpu_baseline(log_n: int):
     w = make_workload(src, seed=77)
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
     pub = orc.make_pub(h, outputs)
+    opts = orc.default_options(num_queries=43, field_extension=2) if config5 else orc.default_options()
     t0 = time.perf_counter()
-    orc.prove(trace, pub)
+    orc.prove(trace, pub, opts)
     dt = time.perf_counter() - t0
     n = trace.shape[1]
     return {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle or_prove (C, 1 thread) on one 2^{log_n}-step trace of the same cipher-mix "
-                      f"generator, reference options: {dt:.1f} s"}
+                      f"generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s"}
 
 
 def pmc_traffic(kernel: str):
@@ -130,6 +134,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
+    ap.add_argument("--config5", action="store_true",
+                    help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
     if args.sharded:
         return run_sharded(args)
@@ -147,7 +153,9 @@ def main():
     n = trace.shape[1]
     log(f"[rank {rank}] VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
-    opts = ProofOptions()
+    opts = ProofOptions(43, 8, 0, 2, 8, 127) if args.config5 else ProofOptions()
+    min_sec = 128 if args.config5 else 95
+    opts_str = "ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5 else "ProofOptions(32, 8, 0, None, 8, 127)"
     gpu = GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor)
     d_trace, _ = gpu.upload_trace(trace)
 
@@ -175,9 +183,9 @@ def main():
         C.memmove(opub.program_hash, bytes(pub.program_hash), 32)
         C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
         opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
-        verified = orc.verify(proof, opub, 95)[0] == 0
+        verified = orc.verify(proof, opub, min_sec)[0] == 0
     from zkvm_amd.prover import verify as zk_verify
-    zk_verified = zk_verify(proof, pub, 95)[0] == 0
+    zk_verified = zk_verify(proof, pub, min_sec)[0] == 0
 
     if rank != 0:
         if pg is not None:
@@ -196,15 +204,17 @@ def main():
                 "kernel_share_of_device_time": round(tot_ms / prove_total_ms, 3)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_log_n)
+        cpu = cpu_baseline(args.cpu_log_n, args.config5)
     value = world * n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f128", "data": "synthetic (seeded VM trace)",
-        "config": {"workload": f"configs[2]: 2^{args.log_n}-step READ2/ADD2/SMUL cipher-mix program, full prove",
+        "config": {"workload": f"configs[{4 if args.config5 else 2}]: 2^{args.log_n}-step READ2/ADD2/SMUL cipher-mix program, "
+                               f"full prove" + (" at 128-bit conjectured security" if args.config5 else ""),
                    "trace_len": n, "trace_width": 28, "lde_len": n * opts.blowup_factor,
-                   "options": "ProofOptions(32, 8, 0, None, 8, 127)", "parallelism": f"independent proof per GPU x{world}"},
+                   "options": opts_str, "parallelism": f"independent proof per GPU x{world}"},
+        "security_bits_checked": min_sec,
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},

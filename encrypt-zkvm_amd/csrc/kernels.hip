@@ -558,20 +558,30 @@ __device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
 // Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
 // SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
 struct EvalShared {
-    fe ct[20], cb[22], v1[10], xr[8], inv_zn[8], inv_mds[16];
+    fe ct[20], cb[22], ct2[20], cb2[22], v1[10], xr[8], inv_zn[8], inv_mds[16];
     fe g_last2, g_last1, delta;
 };
 
 #ifndef ZK_EVAL_WAVES
 #define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
 #endif
-__global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *wn_lo,
+#ifndef ZK_EVAL_WAVES_EXT
+#define ZK_EVAL_WAVES_EXT 4  // the two-plane (quadratic extension) variant (4: 128 VGPRs, 9 spills; 3: 142, 0)
+#endif
+// KE coefficient planes: KE = 2 for FieldExtension::Quadratic, where the composition coefficients are
+// E values; the composition is linear in them, so each constraint value is folded into two
+// accumulators (K = a components, K2 = b components) and two planes comp[t], comp[plane + t] are written.
+template <int KE>
+__global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_EXT) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *wn_lo,
                                                           const fe *wn_hi, const fe *periodic, const fe *inv_bd,
-                                                          const AirConsts *K, fe *comp) {
+                                                          const AirConsts *K, const AirConsts *K2, size_t plane,
+                                                          fe *comp) {
     __shared__ EvalShared S;
     {
         const int t = threadIdx.x;
-        if (t < 20) S.ct[t] = K->coeff_t[t];
+        if (KE == 2 && t >= 128 && t < 148) S.ct2[t - 128] = K2->coeff_t[t - 128];
+        else if (KE == 2 && t >= 148 && t < 170) S.cb2[t - 148] = K2->coeff_b[t - 148];
+        else if (t < 20) S.ct[t] = K->coeff_t[t];
         else if (t < 42) S.cb[t - 20] = K->coeff_b[t - 20];
         else if (t < 52) S.v1[t - 42] = K->assert_val[12 + t - 42];
         else if (t < 60) S.xr[t - 52] = K->xr[t - 52];
@@ -601,6 +611,16 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
     const fe one = fe_one();
     const fe s0n = NXT(12);
     fe t = fe_zero();  // sum of coeff_t[k] * C_k (kept reduced: a lazy 288-bit sum here costs 130 spills)
+    fe t2 = fe_zero();  // the b-plane sum (KE = 2)
+#define ZK_ACC(k, val)                                                    \
+    do {                                                                  \
+        const fe v_ = (val);                                              \
+        t = fe_add(t, fe_mul(S.ct[k], v_));                               \
+        if (KE == 2) {                                                    \
+            t2 = fe_add(t2, fe_mul(S.ct2[k], v_));                        \
+            asm volatile("" : "+v"(t2.lo), "+v"(t2.hi));                  \
+        }                                                                 \
+    } while (0)
     // 12..19 Rescue round / copy (constrains.rs:182-216) first: it needs only the opcode value and
     // is_push from the flags, so the ten selectors below are never live across it.
     {
@@ -637,13 +657,13 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
 #pragma unroll
             for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
             const fe acc = acc288_reduce(am);
-            t = fe_add(t, fe_mul(S.ct[12 + r2], fe_mul(fe_sub(cube(acc), m0[r2]), fh)));
+            ZK_ACC(12 + r2, fe_mul(fe_sub(cube(acc), m0[r2]), fh));
         }
         ZK_SEQ(cb, t.lo);
-        t = fe_add(t, fe_mul(S.ct[16], fe_mul(fe_sub(NXT(7), CUR(7)), nfh)));
-        t = fe_add(t, fe_mul(S.ct[17], fe_mul(fe_sub(NXT(8), CUR(8)), nfh)));
-        t = fe_add(t, fe_mul(S.ct[18], fe_mul(NXT(9), nfh)));
-        t = fe_add(t, fe_mul(S.ct[19], fe_mul(NXT(10), nfh)));
+        ZK_ACC(16, fe_mul(fe_sub(NXT(7), CUR(7)), nfh));
+        ZK_ACC(17, fe_mul(fe_sub(NXT(8), CUR(8)), nfh));
+        ZK_ACC(18, fe_mul(NXT(9), nfh));
+        ZK_ACC(19, fe_mul(NXT(10), nfh));
     }
     ZK_SEQ(cb, t.lo);
     // 0..11: degree-5 selectors (flags.rs:45-79) with shared prefixes, each consumed right away
@@ -653,12 +673,12 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
                  nb4 = fe_sub(one, b4);
         const fe s0 = CUR(12), s1 = CUR(13);
         // 0 clock, 2 shift
-        t = fe_add(t, fe_mul(S.ct[0], fe_sub(NXT(0), fe_add(CUR(0), one))));
-        t = fe_add(t, fe_mul(S.ct[2], fe_mul(b0, b1)));
+        ZK_ACC(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
+        ZK_ACC(2, fe_mul(b0, b1));
         // 11 noop
         {
             const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
-            t = fe_add(t, fe_mul(S.ct[11], fe_mul(is_noop, fe_sub(s0n, s0))));
+            ZK_ACC(11, fe_mul(is_noop, fe_sub(s0n, s0)));
         }
         ZK_SEQ(cb, t.lo);
         const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
@@ -666,8 +686,8 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
         {
             const fe n0_1_n2_n3 = fe_mul(n0_1_n2, nb3);
             // 3 add, 6 mul
-            t = fe_add(t, fe_mul(S.ct[3], fe_mul(fe_mul(n0_1_n2_n3, nb4), fe_sub(s0n, fe_add(s0, s1)))));
-            t = fe_add(t, fe_mul(S.ct[6], fe_mul(fe_mul(n0_1_n2_n3, b4), fe_sub(s0n, fe_mul(s0, s1)))));
+            ZK_ACC(3, fe_mul(fe_mul(n0_1_n2_n3, nb4), fe_sub(s0n, fe_add(s0, s1))));
+            ZK_ACC(6, fe_mul(fe_mul(n0_1_n2_n3, b4), fe_sub(s0n, fe_mul(s0, s1))));
         }
         ZK_SEQ(cb, t.lo);
         {
@@ -688,9 +708,9 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
             }
             const fe acc7 = fe_sub(sum_sn, fe_mul(sum_s1, s0));
             acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
-            t = fe_add(t, fe_mul(S.ct[4], fe_mul(is_sadd, acc4)));
-            t = fe_add(t, fe_mul(S.ct[5], fe_mul(is_add2, acc5)));
-            t = fe_add(t, fe_mul(S.ct[7], fe_mul(is_smul, acc7)));
+            ZK_ACC(4, fe_mul(is_sadd, acc4));
+            ZK_ACC(5, fe_mul(is_add2, acc5));
+            ZK_ACC(7, fe_mul(is_smul, acc7));
         }
         ZK_SEQ(cb, t.lo);
         {
@@ -699,9 +719,9 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
             const fe p0n3 = fe_mul(p0, nb3);
             is_read2 = fe_mul(fe_mul(p0, b3), nb4);
             const fe d1 = fe_sub(NXT(13), s0);
-            t = fe_add(t, fe_mul(S.ct[8], fe_mul(fe_mul(p0n3, nb4), d1)));
-            t = fe_add(t, fe_mul(S.ct[9], fe_mul(fe_mul(p0n3, b4), d1)));
-            t = fe_add(t, fe_mul(S.ct[10], fe_mul(is_read2, fe_sub(NXT(17), s0))));
+            ZK_ACC(8, fe_mul(fe_mul(p0n3, nb4), d1));
+            ZK_ACC(9, fe_mul(fe_mul(p0n3, b4), d1));
+            ZK_ACC(10, fe_mul(is_read2, fe_sub(NXT(17), s0)));
         }
         // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
         {
@@ -709,7 +729,7 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
             fe d = fe_sub(is_add2, is_read2);
             d = fe_add(d, d);
             d = fe_add(d, d);
-            t = fe_add(t, fe_mul(S.ct[1], fe_add(v, d)));
+            ZK_ACC(1, fe_add(v, d));
         }
     }
     ZK_SEQ(cb, t.lo);
@@ -733,9 +753,30 @@ __global__ void __launch_bounds__(256, ZK_EVAL_WAVES) k_eval_constraints(const f
         acc288_madd(a1, S.cb[14 + k], fe_sub(c, S.v1[2 + k]));
     }
     const fe bs0 = acc288_reduce(a0), bs1 = acc288_reduce(a1);
+    const fe ibd = inv_bd[t_id];
     fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
-    res = fe_add(res, fe_mul(num, inv_bd[t_id]));  // coset-major, like comp
+    res = fe_add(res, fe_mul(num, ibd));  // coset-major, like comp
     comp[t_id] = res;
+    if (KE == 2) {
+        ZK_SEQ(cb, res.lo);
+        fe res2 = fe_mul(fe_mul(fe_mul(t2, xa), fe_sub(x, S.g_last1)), S.inv_zn[rc]);
+        acc288 c0 = acc288_zero(), c1 = acc288_zero();
+        acc288_madd(c0, S.cb2[0], CUR(0));
+        acc288_madd(c0, S.cb2[1], CUR(7));
+        acc288_madd(c0, S.cb2[2], CUR(8));
+        acc288_madd(c0, S.cb2[3], CUR(11));
+        acc288_madd(c1, S.cb2[12], fe_sub(CUR(7), S.v1[0]));
+        acc288_madd(c1, S.cb2[13], fe_sub(CUR(8), S.v1[1]));
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            fe c = CUR(12 + k);
+            acc288_madd(c0, S.cb2[4 + k], c);
+            acc288_madd(c1, S.cb2[14 + k], fe_sub(c, S.v1[2 + k]));
+        }
+        const fe num2 = fe_add(fe_mul(acc288_reduce(c0), xa), fe_mul(acc288_reduce(c1), fe_sub(x, one)));
+        comp[plane + t_id] = fe_add(res2, fe_mul(num2, ibd));
+    }
+#undef ZK_ACC
 #undef CUR
 #undef NXT
 }
@@ -764,8 +805,17 @@ void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap m
                              const fe *periodic, const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
     upload_rescue(st);
     const size_t CE = (size_t)map.nce << log_n;
-    ZK_PROF(st, "eval_constraints", (448.0 * (map.lshift == 0 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL(k_eval_constraints, dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts_dev, comp));
+    ZK_PROF(st, "eval_constraints", (448.0 * (map.lshift == 0 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL((k_eval_constraints<1>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
+                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts_dev, consts_dev, (size_t)0, comp));
+}
+
+void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
+                          const fe *inv_bd, const AirConsts *consts2_dev, fe *comp) {
+    upload_rescue(st);
+    const EvalMap map{8, 0, 1, log_b - 3, 1 << log_b};
+    const size_t CE = (size_t)map.nce << log_n;
+    ZK_PROF(st, "eval_constraints_ext", (448.0 + 48.0) * CE, hipLaunchKernelGGL((k_eval_constraints<2>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
+                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts2_dev, consts2_dev + 1, CE, comp));
 }
 
 // ================================================================ composition interpolation (K4)

@@ -742,9 +742,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
         batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), Kp[0].g_last2, p->inv);
-        for (int j = 0; j < 2; j++)
-            eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->x_air + j,
-                             comp + j * CE);
+        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->x_air,
+                             comp);
     }
     stage_mark(p, "constraints");
 
