@@ -40,6 +40,9 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 #ifndef ZK_NTT_TILE
 #define ZK_NTT_TILE 4096
 #endif
+#ifndef ZK_NTT_PASS_TABLE
+#define ZK_NTT_PASS_TABLE 1  // inter-pass twiddles from a full table (0: split tables, one multiply more)
+#endif
 constexpr int NTT_THREADS = ZK_NTT_THREADS;
 
 template <int LOGM>
@@ -136,6 +139,7 @@ struct NttArgs {
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
     const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
     const fe *pre_full;           // ... or the same from a full table (preferred when present)
+    const fe *pass_tw;            // inter-pass twiddles [k1 * n2 + j2] (replaces big_lo/hi when present)
     fe post;                      // post-scale constant
     int has_post;
     int log_n;
@@ -199,8 +203,12 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a) {
         int line = e >> LOGM, j2 = e & (M - 1);
         size_t k1 = k1_0 + line;
         fe v = s[lds_idx<LOGM>(line, j2)];
-        size_t t = ((size_t)j2 * k1) & (n - 1);
-        v = fe_mul(v, pow_split(a.big_lo, a.big_hi, t));
+        if (a.pass_tw) {
+            v = fe_mul(v, a.pass_tw[k1_0 * M + e]);  // = w^(j2 k1), contiguous over the block
+        } else {
+            size_t t = ((size_t)j2 * k1) & (n - 1);
+            v = fe_mul(v, pow_split(a.big_lo, a.big_hi, t));
+        }
         out[k1 * M + j2] = v;
     }
 }
@@ -296,6 +304,11 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.pre_lo = pre ? pre->lo : nullptr;
     a.pre_hi = pre ? pre->hi : nullptr;
     a.pre_full = pre ? pre->full : nullptr;
+#if ZK_NTT_PASS_TABLE
+    a.pass_tw = inverse ? T.inv_pass : T.fwd_pass;
+#else
+    a.pass_tw = nullptr;
+#endif
     a.has_post = post_scale != nullptr;
     a.post = post_scale ? *post_scale : fe_zero();
     a.log_n = T.log_n;
@@ -316,6 +329,22 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a2.in_stride = (size_t)1 << L;
     a2.pre_lo = a2.pre_hi = a2.pre_full = nullptr;
     ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
+}
+
+__global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n2, fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t k1 = idx >> log_n2, j2 = idx & (((size_t)1 << log_n2) - 1);
+        out[idx] = pow_split(lo, hi, (j2 * k1) & (n - 1));
+    }
+}
+
+void make_pass_twiddles(hipStream_t st, NttTables &T) {
+    const size_t n = (size_t)1 << T.log_n;
+    const int log_n2 = (T.log_n + 1) / 2;  // pass-1 line length, as in ntt()
+    const unsigned blocks = std::min<size_t>(cdiv(n, 256), 65536);
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.fwd_lo, T.fwd_hi, T.log_n, log_n2, T.fwd_pass);
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.inv_lo, T.inv_hi, T.log_n, log_n2, T.inv_pass);
 }
 
 __global__ void k_pow_expand(const fe *lo, const fe *hi, size_t n, fe *out) {

@@ -117,6 +117,11 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     pl->log_n = key.first;
     pl->log_b = key.second;
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n, &pl->Tn));
+    if (pl->log_n > 12) {  // four-step NTTs: inter-pass twiddle tables (2n elements)
+        ZK_CHECK_HIP(p->arena.alloc(&pl->Tn.fwd_pass, n));
+        ZK_CHECK_HIP(p->arena.alloc(&pl->Tn.inv_pass, n));
+        make_pass_twiddles(p->st, pl->Tn);
+    }
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + 3, &pl->Tce));
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + pl->log_b, &pl->TN));
     fe wN = h_root_of_unity(pl->log_n + pl->log_b), wce = h_root_of_unity(pl->log_n + 3);
@@ -1158,6 +1163,11 @@ extern "C" int zk_diag_ntt(int device, const uint8_t *in, size_t n, int batch, i
     std::unique_ptr<zk_prover, void (*)(zk_prover *)> guard(p, zk_prover_destroy);
     NttTables T;
     ZK_CHECK_HIP(make_ntt_tables(p, ilog2(n), &T));
+    if (T.log_n > 12) {
+        ZK_CHECK_HIP(p->arena.alloc(&T.fwd_pass, n));
+        ZK_CHECK_HIP(p->arena.alloc(&T.inv_pass, n));
+        make_pass_twiddles(p->st, T);
+    }
     PowTable pre;
     fe off = offset ? fe_from_bytes(offset) : fe_one();
     bool use_pre = !inverse && !fe_eq(off, fe_one());

@@ -63,7 +63,12 @@ struct NttTables {
     int log_n = 0;
     fe *dft_fwd = nullptr, *dft_inv = nullptr;
     fe *fwd_lo = nullptr, *fwd_hi = nullptr, *inv_lo = nullptr, *inv_hi = nullptr;
+    // four-step inter-pass twiddles w^(j2*k1) laid out as pass 1 consumes them, [k1 * n2 + j2]
+    // (n elements each; only for log_n > 12, else null)
+    fe *fwd_pass = nullptr, *inv_pass = nullptr;
 };
+// fill NttTables::fwd_pass / inv_pass (allocated by the caller, n elements each)
+void make_pass_twiddles(hipStream_t st, NttTables &T);
 
 // A power series s^k, k < n, as split tables (s^k = lo[k & 2047] * hi[k >> 11])
 struct PowTable {
