@@ -21,6 +21,7 @@ from .native import Dump, Options, PubInputs, Record, ZkError, check, lib
 
 P = 2**128 - 45 * 2**40 + 1
 FIELD_EXTENSION_NONE = 1
+FIELD_EXTENSION_QUADRATIC = 2
 
 
 @dataclass(frozen=True)
