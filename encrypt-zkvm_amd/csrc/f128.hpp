@@ -273,22 +273,20 @@ __host__ static inline fe fe_from_u128(unsigned __int128 v) { return fe{(uint64_
 __host__ static inline unsigned __int128 fe_to_u128(fe a) { return ((unsigned __int128)a.hi << 64) | a.lo; }
 __host__ static inline fe fe_mul(fe a, fe b) {
     typedef unsigned __int128 u128;
-    const u128 M = (u128)UINT64_MAX, C = (u128)ZK_C;
     const u128 P = ((u128)ZK_P_HI << 64) | ZK_P_LO;
-    u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
-    u128 mid = (p00 >> 64) + (p01 & M) + (p10 & M);
-    u128 lo = (p00 & M) | (mid << 64);
-    u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
-    while (hi) {
-        u128 q00 = (hi & M) * C, q10 = (hi >> 64) * C;
-        u128 add_lo = q00 + (q10 << 64);
-        u128 add_hi = (q10 >> 64) + (add_lo < q00);
-        u128 s = lo + add_lo;
-        hi = add_hi + (s < lo);
-        lo = s;
-    }
-    if (lo >= P) lo -= P;
-    return fe_from_u128(lo);
+    const u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
+    const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+    const u128 lo = (mid << 64) | (uint64_t)p00;
+    const u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);  // product = hi * 2^128 + lo
+    // 2^128 = C (mod p), C < 2^46: lo + hi*C = s2 + top * 2^128 with top < 2^47, then fold once more
+    const u128 t0 = (u128)(uint64_t)hi * ZK_C, t1 = (u128)(uint64_t)(hi >> 64) * ZK_C;
+    const u128 s1 = lo + t0;
+    const u128 s2 = s1 + (t1 << 64);
+    const uint64_t top = (uint64_t)(t1 >> 64) + (uint64_t)(s1 < lo) + (uint64_t)(s2 < s1);
+    u128 r = s2 + (u128)top * ZK_C;
+    if (r < s2) r += ZK_C;  // wrapped past 2^128: + 2^128 = + C (mod p); cannot wrap again
+    if (r >= P) r -= P;
+    return fe_from_u128(r);
 }
 
 ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }

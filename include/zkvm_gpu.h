@@ -182,7 +182,9 @@ int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, in
 /* ---- VM trace generator (harness; vm::Processor::run + trace, vm/src/processor/mod.rs:61-95) ----
  * source: assembly text (Program::compile); public: u8 inputs; secret: ciphertexts of lwe_size
  * elements; last_row: the 28 values the reference draws from thread_rng().  trace_out receives
- * 28 x n column-major with n <= cap_rows; outputs = 16 stack values; hash = program hash. */
+ * 28 x n column-major with n <= cap_rows; outputs = 16 stack values; hash = program hash.
+ * trace_out = NULL is a size query: *n_out is set from the compiled program alone (the VM does not
+ * run) and ZK_ERR_BUFFER_TOO_SMALL is returned. */
 int zk_vm_trace(const char *source, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
                 size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, uint8_t *trace_out,
                 size_t cap_rows, size_t *n_out, uint8_t *outputs, uint8_t *program_hash);
