@@ -112,9 +112,10 @@ def cpu_baseline(log_n: int, config5: bool = False):
                       f"generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s"}
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (tools/pmc_traffic.py), if any."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
+def pmc_traffic(kernel: str, config5: bool = False):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary of the same configuration
+    (tools/pmc_traffic.py), if any."""
+    f = ROOT / "profiles" / ("pmc_traffic_config5.json" if config5 else "pmc_traffic.json")
     if not f.exists():
         return None
     try:
@@ -198,7 +199,7 @@ def main():
     achieved = tot_bytes / (tot_ms / 1e3) / 1e9
     prove_total_ms = sum(v[0] for v in kstats.values())
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name, args.config5),
                 "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
                 "alg_bytes_per_launch": tot_bytes / launches,
                 "kernel_share_of_device_time": round(tot_ms / prove_total_ms, 3)}

@@ -178,15 +178,19 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_single(NttArgs a, int batch) 
 // Four-step, pass 1.  n = n1 * n2, input index k = k1 + n1*k2.  A block takes LPB consecutive k1
 // (lines of length n2 = 2^LOGM read at stride n1 -> LPB contiguous elements per row), runs the
 // size-n2 DFT over k2, multiplies by w_n^(j2*k1) and writes X[k1*n2 + j2] (contiguous runs).
+// Grid: one dimension over (line group, column) with the column fastest, remapped per XCD, so an XCD
+// runs one line group for every column back to back and its slice of the pass twiddle table stays
+// in that XCD's L2 (columns outermost re-fetched the table once per column).
 template <int LOGM, int TILE>
-__global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a) {
+__global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a, int batch) {
     extern __shared__ fe s[];
     constexpr int M = 1 << LOGM;  // n2
     constexpr int LPB = TILE / M;
     const size_t n = (size_t)1 << a.log_n;
     const size_t n1 = n >> LOGM;
-    const size_t k1_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
-    const size_t b = blockIdx.y;
+    const size_t lin = xcd_block(blockIdx.x, gridDim.x);
+    const size_t k1_0 = (lin / batch) * LPB;
+    const size_t b = lin % batch;
     const fe *in = a.in + b * a.in_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k2 = e / LPB;
@@ -261,7 +265,7 @@ static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
     size_t sh = lds_bytes<TILE>(LOGM);
     hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    ZK_PROF(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+    ZK_PROF(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB) * batch), dim3(NTT_THREADS), sh, st, a, batch));
 }
 
 template <int LOGM, int TILE>

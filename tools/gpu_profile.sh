@@ -29,4 +29,10 @@ cp "$O/pmc_traffic_$TAG.json" "$R/profiles/pmc_traffic.json"
 find "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
 (cd "$R" && timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err")
 echo "bench ok"
+# config 5 (128-bit options, quadratic extension): kernel trace + bench line
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c5_$TAG" -o "c5_$TAG" -- \
+  python3 "$R/bench.py" --config5 $BENCH_ARGS > "$O/prof_bench_c5_$TAG.json" 2> "$O/prof_bench_c5_$TAG.err"
+echo "config5 kernel trace ok"
+(cd "$R" && timeout -k 10 600 python3 bench.py --config5 > "$O/bench_c5_$TAG.json" 2> "$O/bench_c5_$TAG.err")
+echo "config5 bench ok"
 cat "$O/bench_$TAG.json"
