@@ -33,6 +33,11 @@ for p in (ROOT, ROOT / "encrypt-zkvm_amd"):
         sys.path.insert(0, str(p))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+# f128 operation throughput of this build's field arithmetic, whole chip, measured by
+# tools/ubench/mul_ubench.hip (profiles/r01_ubench_field_ops.txt): the VALU ceiling of the NTT
+FE_MUL_PEAK = 536.78e9
+FE_ADD_PEAK = 2922.68e9
+FE_SUB_PEAK = 3251.22e9
 METRIC = "STARK prove: trace-steps/sec at 2^20 steps; achieved HBM GB/s vs 8 TB/s peak"
 
 
@@ -173,6 +178,7 @@ def main():
     gpu.profile(True)
     gpu.prove_device(d_trace, n, pub, opts)
     kstats = gpu.kernel_stats()
+    kops = gpu.kernel_ops()
     gpu.profile(False)
 
     verified = None
@@ -203,6 +209,14 @@ def main():
                 "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
                 "alg_bytes_per_launch": tot_bytes / launches,
                 "kernel_share_of_device_time": round(tot_ms / prove_total_ms, 3)}
+    if name in kops:
+        # the NTT is integer-VALU bound: its algorithmic f128 multiplies and add/subs priced at the
+        # measured field-op throughput give the compute floor of the same launches
+        muls, addsubs = kops[name]
+        floor_ms = 1e3 * (muls / FE_MUL_PEAK + addsubs / (0.5 * FE_ADD_PEAK + 0.5 * FE_SUB_PEAK))
+        roofline["valu"] = {"bound": "valu", "fe_mul_per_launch": muls / launches, "fe_addsub_per_launch": addsubs / launches,
+                            "achieved_fe_mul_per_s": round(muls / (tot_ms / 1e3), 1), "peak_fe_mul_per_s": FE_MUL_PEAK,
+                            "floor_ms_per_launch": round(floor_ms / launches, 4), "frac": round(floor_ms / tot_ms, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_log_n, args.config5)

@@ -245,6 +245,14 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass2(NttArgs a) {
     }
 }
 
+// Algorithmic operation counts of lds_dft per element (for the profiler): the first radix-4 round
+// multiplies one of four elements, every further radix-4 round one per element, a trailing radix-2
+// stage one per two; every stage adds or subtracts once per element.
+static double dft_muls_per_elem(int logm) {
+    if (logm < 2) return 0.5;
+    return 0.25 + (double)((logm - 2) / 2) + ((logm & 1) ? 0.5 : 0.0);
+}
+
 template <int TILE>
 static size_t lds_bytes(int logm) {
     int M = 1 << logm;
@@ -256,7 +264,9 @@ static void launch_single(hipStream_t st, const NttArgs &a, int batch) {
     constexpr int LPB = TILE / (1 << LOGM);
     size_t sh = lds_bytes<TILE>(LOGM);
     hipFuncSetAttribute((const void *)ntt_single<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    ZK_PROF(st, "ntt_single", 32.0 * batch * (1 << LOGM), hipLaunchKernelGGL((ntt_single<LOGM, TILE>), dim3(cdiv(batch, LPB)), dim3(NTT_THREADS), sh, st, a, batch));
+    const double el = (double)batch * (1 << LOGM);
+    ZK_PROF_OPS(st, "ntt_single", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.pre_full || a.pre_lo ? 1 : 0) + (a.has_post ? 1 : 0)),
+                el * LOGM, hipLaunchKernelGGL((ntt_single<LOGM, TILE>), dim3(cdiv(batch, LPB)), dim3(NTT_THREADS), sh, st, a, batch));
 }
 
 template <int LOGM, int TILE>
@@ -265,7 +275,10 @@ static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
     size_t sh = lds_bytes<TILE>(LOGM);
     hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    ZK_PROF(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB) * batch), dim3(NTT_THREADS), sh, st, a, batch));
+    const double el = (double)batch * ((size_t)1 << a.log_n);
+    ZK_PROF_OPS(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * el,
+                el * (dft_muls_per_elem(LOGM) + 1.0 + (a.pre_full || a.pre_lo ? 1 : 0) + (a.pass_tw ? 0 : 1)), el * LOGM,
+                hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB) * batch), dim3(NTT_THREADS), sh, st, a, batch));
 }
 
 template <int LOGM, int TILE>
@@ -274,7 +287,9 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     size_t n2 = ((size_t)1 << a.log_n) >> LOGM;
     size_t sh = lds_bytes<TILE>(LOGM);
     hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    ZK_PROF(st, "ntt_pass2", 32.0 * batch * ((size_t)1 << a.log_n), hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+    const double el = (double)batch * ((size_t)1 << a.log_n);
+    ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.has_post ? 1 : 0)), el * LOGM,
+                hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
 }
 
 #define ZK_DISPATCH_LOGM(logm, FN, ...)           \

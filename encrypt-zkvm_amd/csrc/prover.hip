@@ -273,10 +273,14 @@ void zk::collect_kernel_stats(zk_prover *p) {
             p->kstat_ms.push_back(0);
             p->kstat_n.push_back(0);
             p->kstat_bytes.push_back(0);
+            p->kstat_muls.push_back(0);
+            p->kstat_addsubs.push_back(0);
         }
         p->kstat_ms[i] += ms;
         p->kstat_n[i] += 1;
         p->kstat_bytes[i] += r.bytes;
+        p->kstat_muls[i] += r.muls;
+        p->kstat_addsubs[i] += r.addsubs;
     }
     P.reset();
 }
@@ -297,7 +301,20 @@ int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, in
         p->kstat_ms.clear();
         p->kstat_n.clear();
         p->kstat_bytes.clear();
+        p->kstat_muls.clear();
+        p->kstat_addsubs.clear();
     }
+    return ZK_OK;
+}
+
+int zk_prover_kernel_ops(zk_prover *p, double *total_muls, double *total_addsubs, int cap, int *count) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    const int k = (int)p->kstat_names.size();
+    for (int i = 0; i < k && i < cap; i++) {
+        if (total_muls) total_muls[i] = p->kstat_muls[i];
+        if (total_addsubs) total_addsubs[i] = p->kstat_addsubs[i];
+    }
+    if (count) *count = k;
     return ZK_OK;
 }
 

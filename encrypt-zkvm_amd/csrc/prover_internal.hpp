@@ -111,6 +111,7 @@ struct zk_prover {
     std::vector<float> kstat_ms;
     std::vector<int> kstat_n;
     std::vector<double> kstat_bytes;
+    std::vector<double> kstat_muls, kstat_addsubs;
     size_t last_n = 0;
     uint32_t last_b = 0;
 };

@@ -20,6 +20,7 @@ struct KernelProfiler {
         const char *name;
         hipEvent_t a, b;
         double bytes;  // algorithmic HBM bytes of this launch (DESIGN.md "Roofline accounting")
+        double muls, addsubs;  // algorithmic f128 multiplies / additions+subtractions (0 = not modelled)
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
@@ -32,8 +33,8 @@ struct KernelProfiler {
         }
         return pool[used++];
     }
-    void begin(hipStream_t st, const char *name, double bytes) {
-        Rec r{name, get(), nullptr, bytes};
+    void begin(hipStream_t st, const char *name, double bytes, double muls = 0, double addsubs = 0) {
+        Rec r{name, get(), nullptr, bytes, muls, addsubs};
         hipEventRecord(r.a, st);
         recs.push_back(r);
     }
@@ -47,6 +48,14 @@ struct KernelProfiler {
     }
 };
 KernelProfiler &profiler();
+// ZK_PROF with the launch's algorithmic f128 operation counts (for the VALU roofline)
+#define ZK_PROF_OPS(st, name, bytes, muls, addsubs, ...)                               \
+    do {                                                                             \
+        ::zk::KernelProfiler &P_ = ::zk::profiler();                                 \
+        if (P_.on) P_.begin(st, name, (double)(bytes), (double)(muls), (double)(addsubs)); \
+        __VA_ARGS__;                                                                 \
+        if (P_.on) P_.end(st);                                                       \
+    } while (0)
 #define ZK_PROF(st, name, bytes, ...)        \
     do {                                     \
         ::zk::KernelProfiler &P_ = ::zk::profiler(); \

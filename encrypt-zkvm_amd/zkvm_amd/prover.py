@@ -146,6 +146,20 @@ class GpuProver:
         check(lib().zk_prover_kernel_stats(self.handle, names, ms, nl, by, 64, C.byref(cnt)))
         return {names[i].decode(): (ms[i], nl[i], by[i]) for i in range(min(cnt.value, 64))}
 
+    def kernel_ops(self) -> dict:
+        """{kernel: (f128 multiplies, f128 additions/subtractions)} for the kernels whose operation
+        count the library models (the NTT passes), accumulated like kernel_stats."""
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        nl = (C.c_int * 64)()
+        by = (C.c_double * 64)()
+        mu = (C.c_double * 64)()
+        ad = (C.c_double * 64)()
+        cnt = C.c_int(0)
+        check(lib().zk_prover_kernel_stats(self.handle, names, ms, nl, by, 64, C.byref(cnt)))
+        check(lib().zk_prover_kernel_ops(self.handle, mu, ad, 64, C.byref(cnt)))
+        return {names[i].decode(): (mu[i], ad[i]) for i in range(min(cnt.value, 64)) if mu[i] or ad[i]}
+
 
 _hip_lib = None
 

@@ -178,6 +178,9 @@ int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, 
 int zk_prover_profile(zk_prover *p, int enable);
 int zk_prover_kernel_stats(zk_prover *p, const char **names, float *total_ms, int *launches, double *total_bytes,
                            int cap, int *count);
+/* the same kernels (same order) with their algorithmic f128 multiplies and additions/subtractions
+ * (0 where a kernel's operation count is not modelled; the NTT passes are) */
+int zk_prover_kernel_ops(zk_prover *p, double *total_muls, double *total_addsubs, int cap, int *count);
 
 /* ---- VM trace generator (harness; vm::Processor::run + trace, vm/src/processor/mod.rs:61-95) ----
  * source: assembly text (Program::compile); public: u8 inputs; secret: ciphertexts of lwe_size
