@@ -40,6 +40,9 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 #ifndef ZK_NTT_TILE
 #define ZK_NTT_TILE 4096
 #endif
+#ifndef ZK_NTT_WAVES
+#define ZK_NTT_WAVES 4  // waves per SIMD: two 512-thread blocks per CU (the LDS limit) need <= 128 VGPRs
+#endif
 #ifndef ZK_NTT_PASS_TABLE
 #define ZK_NTT_PASS_TABLE 1  // inter-pass twiddles from a full table (0: split tables, one multiply more)
 #endif
@@ -147,7 +150,7 @@ struct NttArgs {
 
 // Single pass: whole polynomial (n = M <= TILE) per line, LPB = TILE / n polys per block.
 template <int LOGM, int TILE>
-__global__ void __launch_bounds__(NTT_THREADS) ntt_single(NttArgs a, int batch) {
+__global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs a, int batch) {
     extern __shared__ fe s[];
     constexpr int M = 1 << LOGM;
     constexpr int LPB = TILE / M;
@@ -182,7 +185,7 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_single(NttArgs a, int batch) 
 // runs one line group for every column back to back and its slice of the pass twiddle table stays
 // in that XCD's L2 (columns outermost re-fetched the table once per column).
 template <int LOGM, int TILE>
-__global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a, int batch) {
+__global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a, int batch) {
     extern __shared__ fe s[];
     constexpr int M = 1 << LOGM;  // n2
     constexpr int LPB = TILE / M;
@@ -220,7 +223,7 @@ __global__ void __launch_bounds__(NTT_THREADS) ntt_pass1(NttArgs a, int batch) {
 // Four-step, pass 2.  Lines over k1 (length n1 = 2^LOGM, stride n2) for LPB consecutive j2;
 // output A[n2*j1 + j2] (LPB contiguous per j1).
 template <int LOGM, int TILE>
-__global__ void __launch_bounds__(NTT_THREADS) ntt_pass2(NttArgs a) {
+__global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a) {
     extern __shared__ fe s[];
     constexpr int M = 1 << LOGM;  // n1
     constexpr int LPB = TILE / M;
