@@ -255,7 +255,8 @@ def run_sharded(args):
     n = trace.shape[1]
     log(f"[rank {rank}] VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
-    opts = ProofOptions()
+    opts = ProofOptions(43, 8, 0, 2, 8, 127) if args.config5 else ProofOptions()
+    min_sec = 128 if args.config5 else 95
     uid = ShardedProver.unique_id() if rank == 0 else None
     if pg is not None:
         box = [uid]
@@ -280,7 +281,7 @@ def run_sharded(args):
         C.memmove(opub.program_hash, bytes(pub.program_hash), 32)
         C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
         opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
-        verified = orc.verify(last["proof"], opub, 95)[0] == 0
+        verified = orc.verify(last["proof"], opub, min_sec)[0] == 0
     sp.close()
     if rank == 0:
         out = {
@@ -288,9 +289,11 @@ def run_sharded(args):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f128",
             "data": "synthetic (seeded VM trace)",
-            "config": {"workload": f"configs[3]: one 2^{args.log_n}-step cipher-mix proof, LDE domain sharded by coset",
+            "config": {"workload": f"configs[{4 if args.config5 else 3}]: one 2^{args.log_n}-step cipher-mix proof, "
+                                   f"LDE domain sharded by coset",
                        "trace_len": n, "trace_width": 28, "lde_len": 8 * n,
-                       "options": "ProofOptions(32, 8, 0, None, 8, 127)",
+                       "options": ("ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5
+                                   else "ProofOptions(32, 8, 0, None, 8, 127)"),
                        "parallelism": f"coset-sharded x{world} (RCCL all-to-all / all-gather)"},
             "roofline": None, "cpu_baseline": None,
             "stage_ms": {k: round(v, 3) for k, v in stages.items()},

@@ -860,13 +860,19 @@ void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap m
                                                        map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts_dev, consts_dev, (size_t)0, comp));
 }
 
+void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
+                                 const fe *periodic, const fe *inv_bd, const AirConsts *consts2_dev, size_t plane,
+                                 fe *comp) {
+    upload_rescue(st);
+    const size_t CE = (size_t)map.nce << log_n;
+    ZK_PROF(st, "eval_constraints_ext", (448.0 * (map.lshift == 0 ? 1 : 2) + 48.0) * CE, hipLaunchKernelGGL((k_eval_constraints<2>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
+                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts2_dev, consts2_dev + 1, plane, comp));
+}
+
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
                           const fe *inv_bd, const AirConsts *consts2_dev, fe *comp) {
-    upload_rescue(st);
-    const EvalMap map{8, 0, 1, log_b - 3, 1 << log_b};
-    const size_t CE = (size_t)map.nce << log_n;
-    ZK_PROF(st, "eval_constraints_ext", (448.0 + 48.0) * CE, hipLaunchKernelGGL((k_eval_constraints<2>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts2_dev, consts2_dev + 1, CE, comp));
+    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, Tn, periodic, inv_bd,
+                                consts2_dev, (size_t)8 << log_n, comp);
 }
 
 // ================================================================ composition interpolation (K4)

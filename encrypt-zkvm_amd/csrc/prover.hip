@@ -516,6 +516,94 @@ int zk::remainder_step(std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R
     return ZK_OK;
 }
 
+// ---- FieldExtension::Quadratic host steps (shared by the single-GPU and sharded paths)
+// hv = ood_eval_ext output (2 planes of np = 2W + C*2 values): E values of T(z), T(zg) and of the 2C base
+// composition columns at z.  Builds the E frame e = T(z) ++ T(zg) ++ H(z) (H_c = P_c0 + X P_c1), its
+// flattened form h (the serialization order), records the a components, reseeds the coin [P7, P15].
+void zk::ood_reseed_ext(Coin &coin, const std::vector<fe> &hv, int C, zk_record &R, std::vector<fe2> &e,
+                        std::vector<fe> &h) {
+    const int np = 2 * W + 2 * C;
+    e.assign(2 * W + C, fe2_zero());
+    for (int c = 0; c < 2 * W; c++) e[c] = fe2{hv[c], hv[np + c]};
+    for (int c = 0; c < C; c++) {
+        const int s0 = 2 * W + 2 * c;
+        e[2 * W + c] = fe2_add(fe2{hv[s0], hv[np + s0]}, fe2_mulX(fe2{hv[s0 + 1], hv[np + s0 + 1]}));
+    }
+    h.assign(2 * e.size(), fe_zero());
+    for (size_t i = 0; i < e.size(); i++) {
+        h[2 * i] = e[i].a;
+        h[2 * i + 1] = e[i].b;
+    }
+    for (int c = 0; c < W; c++) {
+        fe_to_bytes(e[c].a, R.ood_trace_z[c]);
+        fe_to_bytes(e[W + c].a, R.ood_trace_zg[c]);
+    }
+    for (int j = 0; j < C; j++) fe_to_bytes(e[2 * W + j].a, R.ood_constraints[j]);
+    uint8_t d[32];
+    hash_elems(h.data(), 4 * W, d);
+    coin.reseed(d);
+    hash_elems(h.data() + 4 * W, 2 * C, d);
+    coin.reseed(d);
+}
+
+DeepConstsE zk::draw_deep_consts_ext(Coin &coin, const std::vector<fe2> &e, int C, fe2 z, fe2 zg, zk_record &R) {
+    DeepConstsE D;
+    memset(&D, 0, sizeof D);
+    fe2 k1 = fe2_zero(), k2 = fe2_zero();
+    for (int c = 0; c < W; c++) {
+        D.alpha_t[c] = coin.draw_ext(2);
+        fe_to_bytes(D.alpha_t[c].a, R.deep_t[c]);
+        k1 = fe2_add(k1, fe2_mul(D.alpha_t[c], e[c]));
+        k2 = fe2_add(k2, fe2_mul(D.alpha_t[c], e[W + c]));
+    }
+    for (int j = 0; j < C; j++) {
+        D.alpha_c[j] = coin.draw_ext(2);
+        fe_to_bytes(D.alpha_c[j].a, R.deep_c[j]);
+        k1 = fe2_add(k1, fe2_mul(D.alpha_c[j], e[2 * W + j]));
+    }
+    D.k1 = k1;
+    D.k2 = k2;
+    D.z = z;
+    D.zg = zg;
+    D.zb2 = fe_mul(z.b, z.b);
+    D.zgb2 = fe_mul(zg.b, zg.b);
+    return D;
+}
+
+FoldConstsE zk::fold_consts_ext(fe2 alpha, uint32_t fold) {
+    const FoldConsts F1 = fold_consts(fe_zero(), fold);
+    FoldConstsE F;
+    memset(&F, 0, sizeof F);
+    memcpy(F.zinv, F1.zinv, sizeof F.zinv);
+    F.alpha = alpha;
+    F.inv_offset = F1.inv_offset;
+    F.inv_fold = F1.inv_fold;
+    return F;
+}
+
+// rv: the last layer, planar (a plane then b plane, L values each, natural order over 3 * <w_L>)
+int zk::remainder_step_ext(const std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag,
+                           std::vector<fe> &rem_flat) {
+    const size_t L = rv.size() / 2;
+    std::vector<fe> va(rv.begin(), rv.begin() + L), vb(rv.begin() + L, rv.end());
+    h_interp_coset(va, fe_make(3));
+    h_interp_coset(vb, fe_make(3));
+    const size_t rl = L / B;
+    if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
+    for (size_t k = rl; k < L; k++)
+        if (!fe_is_zero(va[k]) || !fe_is_zero(vb[k])) degree_flag = 1;
+    R.remainder_len = (uint32_t)rl;
+    rem_flat.clear();
+    for (size_t k = 0; k < rl; k++) {
+        fe_to_bytes(va[k], R.remainder[k]);
+        rem_flat.push_back(va[k]);
+        rem_flat.push_back(vb[k]);
+    }
+    hash_elems(rem_flat.data(), rem_flat.size(), R.remainder_commitment);
+    coin.reseed(R.remainder_commitment);
+    return ZK_OK;
+}
+
 static bool nonce_ok(const uint8_t seed[32], uint64_t nonce, uint32_t bits) {
     uint8_t d[32];
     Coin::merge_with_int(seed, nonce, d);
@@ -694,7 +782,7 @@ static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, si
 
 // FieldExtension::Quadratic buffers (planar E): composition 2 x 8n, its inverse NTT, the composition LDE
 // (up to 2 x 8 base columns), DEEP 2N, FRI layers 2(N + 16), OOD tables and partial sums.
-static int ensure_ext(zk_prover *p) {
+int zk::ensure_ext(zk_prover *p) {
     if (p->x_comp) return ZK_OK;
     const size_t n = p->max_n, N = n * p->max_b, CE = 8 * n;
     DeviceArena &A = p->arena;
@@ -813,47 +901,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         std::vector<fe> hv(2 * np);
         ZK_CHECK_HIP(hipMemcpyAsync(hv.data(), p->ood, hv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        std::vector<fe2> e(2 * W + C);
-        for (int c = 0; c < 2 * W; c++) e[c] = fe2{hv[c], hv[np + c]};
-        for (int c = 0; c < C; c++) {  // H_c(z) = P_c0(z) + X * P_c1(z)
-            const int s0 = 2 * W + 2 * c;
-            e[2 * W + c] = fe2_add(fe2{hv[s0], hv[np + s0]}, fe2_mulX(fe2{hv[s0 + 1], hv[np + s0 + 1]}));
-        }
-        for (size_t i = 0; i < e.size(); i++) {
-            h[2 * i] = e[i].a;
-            h[2 * i + 1] = e[i].b;
-        }
-        for (int c = 0; c < W; c++) {
-            fe_to_bytes(e[c].a, R.ood_trace_z[c]);
-            fe_to_bytes(e[W + c].a, R.ood_trace_zg[c]);
-        }
-        for (int j = 0; j < C; j++) fe_to_bytes(e[2 * W + j].a, R.ood_constraints[j]);
-        uint8_t d[32];
-        hash_elems(h.data(), 4 * W, d);
-        coin.reseed(d);
-        hash_elems(h.data() + 4 * W, 2 * C, d);
-        coin.reseed(d);
+        std::vector<fe2> e;
+        ood_reseed_ext(coin, hv, C, R, e, h);
         stage_mark(p, "ood");
-        DeepConstsE D;
-        memset(&D, 0, sizeof D);
-        fe2 k1 = fe2_zero(), k2 = fe2_zero();
-        for (int c = 0; c < W; c++) {
-            D.alpha_t[c] = coin.draw_ext(2);
-            fe_to_bytes(D.alpha_t[c].a, R.deep_t[c]);
-            k1 = fe2_add(k1, fe2_mul(D.alpha_t[c], e[c]));
-            k2 = fe2_add(k2, fe2_mul(D.alpha_t[c], e[W + c]));
-        }
-        for (int j = 0; j < C; j++) {
-            D.alpha_c[j] = coin.draw_ext(2);
-            fe_to_bytes(D.alpha_c[j].a, R.deep_c[j]);
-            k1 = fe2_add(k1, fe2_mul(D.alpha_c[j], e[2 * W + j]));
-        }
-        D.k1 = k1;
-        D.k2 = k2;
-        D.z = z;
-        D.zg = zg;
-        D.zb2 = fe_mul(z.b, z.b);
-        D.zgb2 = fe_mul(zg.b, zg.b);
+        const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         batch_inv_norm_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
         deep_eval_ext_launch(p->st, p->lde, log_n, log_b, clde, C, p->x_deep_consts, pl->TN, three, p->inv, deep);
@@ -897,12 +948,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             } else {
                 const fe2 alpha = coin.draw_ext(2);
                 fe_to_bytes(alpha.a, R.fri_alphas[l]);
-                const FoldConsts F1 = fold_consts(fe_zero(), fold);
-                FoldConstsE F;
-                memcpy(F.zinv, F1.zinv, sizeof F.zinv);
-                F.alpha = alpha;
-                F.inv_offset = F1.inv_offset;
-                F.inv_fold = F1.inv_fold;
+                const FoldConstsE F = fold_consts_ext(alpha, fold);
                 ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
                 fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
             }
@@ -914,26 +960,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         std::vector<fe> rv(KX * L);
         ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        if (KX == 1) {
-            ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
-        } else {
-            // per component: interpolate over 3 * <w_L>, keep L/B coefficients; commit to the E coefficients
-            std::vector<fe> va(rv.begin(), rv.begin() + L), vb(rv.begin() + L, rv.end());
-            h_interp_coset(va, three);
-            h_interp_coset(vb, three);
-            const size_t rl = L / B;
-            if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
-            for (size_t k = rl; k < L; k++)
-                if (!fe_is_zero(va[k]) || !fe_is_zero(vb[k])) degree_flag = 1;
-            R.remainder_len = (uint32_t)rl;
-            for (size_t k = 0; k < rl; k++) {
-                fe_to_bytes(va[k], R.remainder[k]);
-                rem_flat.push_back(va[k]);
-                rem_flat.push_back(vb[k]);
-            }
-            hash_elems(rem_flat.data(), rem_flat.size(), R.remainder_commitment);
-            coin.reseed(R.remainder_commitment);
-        }
+        if (KX == 1) ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
+        else ZK_TRY(remainder_step_ext(rv, B, coin, R, degree_flag, rem_flat));
     }
     stage_mark(p, "fri");
 

@@ -165,6 +165,15 @@ void draw_air_consts_ext(Coin &coin, const zk_pub_inputs *pub, size_t n, AirCons
 void ood_reseed(Coin &coin, const fe *h, int C, zk_record &R);
 // S5: DEEP coefficients and the combined constants k1, k2 [P8]
 DeepConsts draw_deep_consts(Coin &coin, const fe *h, int C, fe z, fe zg, zk_record &R);
+// FieldExtension::Quadratic versions [P15] (prover.hip): E working set on first use, OOD frame from the
+// two-plane ood_eval_ext output, DEEP and fold constants, remainder from a planar last layer
+int ensure_ext(zk_prover *p);
+void ood_reseed_ext(Coin &coin, const std::vector<fe> &hv, int C, zk_record &R, std::vector<fe2> &e,
+                    std::vector<fe> &h);
+DeepConstsE draw_deep_consts_ext(Coin &coin, const std::vector<fe2> &e, int C, fe2 z, fe2 zg, zk_record &R);
+FoldConstsE fold_consts_ext(fe2 alpha, uint32_t fold);
+int remainder_step_ext(const std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag,
+                       std::vector<fe> &rem_flat);
 // S6: number of FRI layers for an LDE domain of N points [P9]
 int fri_num_layers(size_t N, const zk_options *opt);
 FoldConsts fold_consts(fe alpha, uint32_t fold);

@@ -96,14 +96,16 @@ __global__ void __launch_bounds__(256) k_sh_hash_fri0(const fe *deep, int log_n,
     st_digest(send + 32 * a2a_slot(j, q0, Bl, log_mg), h);
 }
 
-// received chunks [s][j][q'] -> natural order of this rank's range: item (s + G*j) + 8*q'
-__global__ void k_sh_permute(const uint8_t *recv, int G, int Bl, int log_mg, int esize, uint8_t *out) {
+// received chunks [s][j][q'] (source chunk s at item s * src_stride) -> natural order of this rank's
+// range: item (s + G*j) + 8*q'.  src_stride > Bl << log_mg when each source sent several planes.
+__global__ void k_sh_permute(const uint8_t *recv, int G, int Bl, int log_mg, int esize, size_t src_stride,
+                             uint8_t *out) {
     const size_t per = (size_t)Bl << log_mg;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= per * G) return;
     const size_t s = t / per, rem = t % per, j = rem >> log_mg, qp = rem & (((size_t)1 << log_mg) - 1);
     const size_t idx = (s + (size_t)G * j) + 8 * qp;
-    const uint4 *src = reinterpret_cast<const uint4 *>(recv + t * esize);
+    const uint4 *src = reinterpret_cast<const uint4 *>(recv + (s * src_stride + rem) * esize);
     uint4 *dst = reinterpret_cast<uint4 *>(out + idx * esize);
     for (int w = 0; w < esize / 16; w++) dst[w] = src[w];
 }
@@ -161,6 +163,87 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
         acc = fe_add(fe_mul(acc, beta), Vm);
     }
     out[t] = fe_mul(acc, F->inv_fold);
+}
+
+// ---- FieldExtension::Quadratic versions: E buffers are planar with plane stride Bl*n (DEEP) / Bl*m (fold)
+__global__ void __launch_bounds__(256) k_sh_deep_ext(const fe *lde, int log_n, int Bl, int g, int G, const fe *clde,
+                                                     int ccols, const DeepConstsE *D, const fe *wN_lo, const fe *wN_hi,
+                                                     fe three, const fe *inv_d, fe *out) {
+    const size_t n = (size_t)1 << log_n, cs = (size_t)Bl * n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= cs) return;
+    const size_t j = t >> log_n, q = t & (n - 1);
+    const size_t i = (size_t)(g + G * (int)j) + 8 * q;
+    const fe *p = lde + j * n + q;
+    acc288 aA = acc288_zero(), aB = acc288_zero();
+#pragma unroll 4
+    for (int c = 0; c < 28; c++) {
+        const fe v = p[(size_t)c * cs];
+        acc288_madd(aA, D->alpha_t[c].a, v);
+        acc288_madd(aB, D->alpha_t[c].b, v);
+    }
+    const fe2 sT = fe2{acc288_reduce(aA), acc288_reduce(aB)};
+    const fe *pc = clde + j * n + q;
+    acc288 hA = acc288_zero(), hB = acc288_zero();
+    for (int k = 0; k < ccols; k++) {  // E column k = base columns (2k, 2k+1)
+        const fe h0 = pc[(size_t)(2 * k) * cs], h1 = pc[(size_t)(2 * k + 1) * cs];
+        const fe2 ac = D->alpha_c[k];
+        acc288_madd(hA, ac.a, h0);
+        acc288_madd(hA, ac.b, h1);
+        acc288_madd(hB, ac.a, h1);
+        acc288_madd(hB, ac.b, fe_add(h0, h1));
+    }
+    const fe2 sH = fe2{acc288_reduce(hA), acc288_reduce(hB)};
+    const fe2 s1 = fe2_sub(fe2_add(sT, sH), D->k1), s2 = fe2_sub(sT, D->k2);
+    const fe x = fe_mul(three, fe_mul(wN_lo[i & 2047], wN_hi[i >> 11]));
+    const fe xa = fe_sub(x, D->z.a), ga = fe_sub(x, D->zg.a);
+    const fe u1 = fe_sub(xa, D->z.b), u2 = fe_sub(ga, D->zg.b);
+    const fe d1 = fe_sub(fe_mul(xa, u1), D->zb2), d2 = fe_sub(fe_mul(ga, u2), D->zgb2);
+    const fe2 num = fe2_add(fe2_mulb(fe2_mul(s1, fe2{u1, D->z.b}), d2), fe2_mulb(fe2_mul(s2, fe2{u2, D->zg.b}), d1));
+    const fe2 res = fe2_mulb(num, inv_d[t]);
+    out[t] = res.a;
+    out[cs + t] = res.b;
+}
+
+__global__ void __launch_bounds__(256) k_sh_hash_fri0_ext(const fe *deep, int log_n, int Bl, int fold, int log_m,
+                                                          int log_mg, uint8_t *send) {
+    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)Bl << log_m)) return;
+    const size_t j = t >> log_m, q0 = t & (m - 1);
+    const fe *p = deep + j * n + q0;
+    uint32_t h[8];
+    b3::hash_elements(2 * fold, [&](int e) { return p[(size_t)(e & 1) * cs + ((size_t)(e >> 1) << log_m)]; }, h);
+    st_digest(send + 32 * a2a_slot(j, q0, Bl, log_mg), h);
+}
+
+__global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int G, int fold,
+                                                          int log_m, const FoldConstsE *F, const fe *wi_lo,
+                                                          const fe *wi_hi, fe *out) {
+    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n, om = (size_t)Bl * m;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= om) return;
+    const size_t j = t >> log_m, q0 = t & (m - 1);
+    const size_t rp = (size_t)(g + G * (int)j) + 8 * q0;
+    fe va[16], vb[16];
+    for (int k = 0; k < fold; k++) {
+        va[k] = deep[j * n + q0 + ((size_t)k << log_m)];
+        vb[k] = deep[cs + j * n + q0 + ((size_t)k << log_m)];
+    }
+    const fe2 beta = fe2_mulb(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    fe2 acc = fe2_zero();
+    for (int mm = fold - 1; mm >= 0; mm--) {  // direct form per component, Horner in E
+        fe Va = fe_zero(), Vb = fe_zero();
+        for (int k = 0; k < fold; k++) {
+            const fe z = F->zinv[(k * mm) & (fold - 1)];
+            Va = fe_add(Va, fe_mul(va[k], z));
+            Vb = fe_add(Vb, fe_mul(vb[k], z));
+        }
+        acc = fe2_add(fe2_mul(acc, beta), fe2{Va, Vb});
+    }
+    acc = fe2_mulb(acc, F->inv_fold);
+    out[t] = acc.a;
+    out[om + t] = acc.b;
 }
 
 // ---------------------------------------------------------------- a Merkle tree split over G ranks
@@ -227,7 +310,7 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
         zk_prover *p = X.P[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
         hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr, 256)), dim3(256), 0, p->st, (const uint8_t *)rcv[l], X.G, X.Bl,
-                           log_mg, 32, leaves[l]);
+                           log_mg, 32, (size_t)X.Bl << log_mg, leaves[l]);
         merkle_tree(p->st, leaves[l], T.Mr, nodes[l]);
         rs[l] = T.Mr >= 2 ? nodes[l] + 32 : leaves[l];
         rr[l] = p->sh_roots;
@@ -251,6 +334,13 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
 int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out,
                   size_t *proof_len, zk_record *rec) {
     const int G = X.G, Bl = X.Bl, log_n = X.log_n, C = X.C, nlp = (int)X.P.size();
+    // FieldExtension: KX = 1 (None) or 2 (Quadratic, every E-valued buffer planar: plane stride Bl*n per rank)
+    const int KX = (int)opt->field_extension, CK = C * KX;
+    auto COMP = [&](zk_prover *p) { return KX == 2 ? p->x_comp : p->comp; };
+    auto CTMP = [&](zk_prover *p) { return KX == 2 ? p->x_ctmp : p->ctmp; };
+    auto CLDE = [&](zk_prover *p) { return KX == 2 ? p->x_clde : p->clde; };
+    auto DEEP = [&](zk_prover *p) { return KX == 2 ? p->x_deep : p->deep; };
+    auto FRI = [&](zk_prover *p) { return KX == 2 ? p->x_fri : p->fri; };
     const size_t n = X.n, N = 8 * n, CE = 8 * n;
     const uint32_t fold = opt->fri_folding;
     const size_t m = n / fold;          // FRI layer-0 positions per coset
@@ -297,8 +387,13 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     coin.reseed(R.trace_root);
 
     // S3: constraint evaluation over the local CE cosets (CE domain = LDE domain at blowup 8)
-    AirConsts K;
-    draw_air_consts(coin, pub, n, K, R);
+    AirConsts K, Kp[2];
+    if (KX == 1) {
+        draw_air_consts(coin, pub, n, K, R);
+    } else {
+        draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
+        K = Kp[0];
+    }
     for (int l = 0; l < nlp; l++) {
         zk_prover *p = X.P[l];
         Plan *pl = X.pl[l];
@@ -306,10 +401,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         fe xr[8];
         for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] + G * j];
         ZK_CHECK_HIP(hipMemcpyAsync(p->sh_xr, xr, Bl * sizeof(fe), hipMemcpyHostToDevice, p->st));
-        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
         batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, fe_one(), K.g_last2, p->inv);
-        eval_constraints_mapped(p->st, p->lde, log_n, EvalMap{Bl, X.rank[l], G, 0, Bl}, pl->Tn, pl->periodic, p->inv,
-                                (const AirConsts *)p->air_consts, p->comp);
+        const EvalMap em{Bl, X.rank[l], G, 0, Bl};
+        if (KX == 1) {
+            ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+            eval_constraints_mapped(p->st, p->lde, log_n, em, pl->Tn, pl->periodic, p->inv,
+                                    (const AirConsts *)p->air_consts, p->comp);
+        } else {
+            ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
+            eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->Tn, pl->periodic, p->inv,
+                                        (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp);
+        }
     }
     stage_mark(P0, "constraints");
 
@@ -322,34 +424,38 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ntt(p->st, X.pl[l]->Tn, p->comp, n, p->ctmp, n, Bl, true, nullptr, nullptr, p->tmp);
-            hipLaunchKernelGGL(k_sh_pack, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->ctmp, log_n, Bl,
-                               ilog2(kg), p->tmp);
+            // planes are Bl columns each and contiguous: KX*Bl columns, sent as [d][plane*Bl + j][k']
+            ntt(p->st, X.pl[l]->Tn, COMP(p), n, CTMP(p), n, KX * Bl, true, nullptr, nullptr, p->tmp);
+            hipLaunchKernelGGL(k_sh_pack, dim3(cdiv((size_t)KX * Bl * n, 256)), dim3(256), 0, p->st, CTMP(p), log_n,
+                               KX * Bl, ilog2(kg), p->tmp);
             snd[l] = p->tmp;
-            rcv[l] = p->comp;
+            rcv[l] = COMP(p);
         }
-        ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, (size_t)Bl * kg * sizeof(fe)));
+        ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe)));
         const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
         std::vector<const void *> fs(nlp);
         std::vector<void *> fr(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            CrossMap cm;
-            for (int r = 0; r < 8; r++) cm.c[r] = p->comp + ((size_t)(r % G) * Bl + r / G) * kg;
-            cm.k0 = (size_t)X.rank[l] * kg;
-            cm.kcount = kg;
-            cm.pstride = kg;
             ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
-            comp_cross_mapped(p->st, cm, X.pl[l]->Tce, X.pl[l]->inv3, scale, w8inv, inv3n, C, p->ctmp, p->flag);
+            for (int pln = 0; pln < KX; pln++) {  // base column (c, pln) of E column c -> CTMP slice c*KX + pln
+                CrossMap cm;
+                for (int r = 0; r < 8; r++) cm.c[r] = COMP(p) + ((size_t)(r % G) * KX * Bl + pln * Bl + r / G) * kg;
+                cm.k0 = (size_t)X.rank[l] * kg;
+                cm.kcount = kg;
+                cm.pstride = (size_t)KX * kg;
+                comp_cross_mapped(p->st, cm, X.pl[l]->Tce, X.pl[l]->inv3, scale, w8inv, inv3n, C, CTMP(p) + pln * kg,
+                                  p->flag);
+            }
             fs[l] = p->flag;
             fr[l] = p->sh_flags;
         }
-        for (int c = 0; c < C; c++) {
+        for (int c = 0; c < CK; c++) {
             std::vector<const void *> s2(nlp);
             std::vector<void *> r2(nlp);
             for (int l = 0; l < nlp; l++) {
-                s2[l] = X.P[l]->ctmp + c * kg;
+                s2[l] = CTMP(X.P[l]) + c * kg;
                 r2[l] = X.P[l]->cpolys + (size_t)c * n;
             }
             ZK_TRY(X.comm->all_gather(X.P, s2, r2, kg * sizeof(fe)));
@@ -359,7 +465,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             for (int j = 0; j < Bl; j++)
-                ntt(p->st, X.pl[l]->Tn, p->cpolys, n, p->clde + j * n, (size_t)Bl * n, C, false,
+                ntt(p->st, X.pl[l]->Tn, p->cpolys, n, CLDE(p) + j * n, (size_t)Bl * n, CK, false,
                     &X.pl[l]->coset[X.rank[l] + G * j], nullptr, p->tmp);
         }
     }
@@ -370,7 +476,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     DistTree Tcomp;
     ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_mg) {
         zk_prover *p = X.P[l];
-        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->clde, C, log_n, Bl,
+        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, CLDE(p), CK, log_n, Bl,
                            log_mg, send);
     }, scratch, lv, nd));
     memcpy(R.constraint_root, Tcomp.root, 32);
@@ -384,25 +490,50 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     coin.reseed(R.constraint_root);
 
     // S5: OOD frame (every process evaluates the replicated polynomials), DEEP over the local cosets
-    const fe z = coin.draw(), zg = fe_mul(z, g);
-    fe_to_bytes(z, R.z);
-    fe h[2 * W + ZK_MAX_CCOLS];
+    std::vector<fe> h;  // the OOD frame, flattened (k base elements per E value)
     ZK_CHECK_HIP(hipSetDevice(P0->device));
-    ood_eval(P0->st, P0->polys, W, P0->cpolys, C, log_n, z, zg, P0->ood_tab, P0->partials, P0->ood);
-    ZK_CHECK_HIP(hipMemcpyAsync(h, P0->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
-    ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
-    ood_reseed(coin, h, C, R);
-    stage_mark(P0, "ood");
-    const DeepConsts D = draw_deep_consts(coin, h, C, z, zg, R);
-    for (int l = 0; l < nlp; l++) {
-        zk_prover *p = X.P[l];
-        Plan *pl = X.pl[l];
-        ZK_CHECK_HIP(hipSetDevice(p->device));
-        ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-        batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
-        hipLaunchKernelGGL(k_sh_deep, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl, X.rank[l],
-                           G, p->clde, C, (const DeepConsts *)p->deep_consts, pl->TN.fwd_lo, pl->TN.fwd_hi, three,
-                           p->inv, p->deep);
+    if (KX == 1) {
+        const fe z = coin.draw(), zg = fe_mul(z, g);
+        fe_to_bytes(z, R.z);
+        h.resize(2 * W + C);
+        ood_eval(P0->st, P0->polys, W, P0->cpolys, C, log_n, z, zg, P0->ood_tab, P0->partials, P0->ood);
+        ZK_CHECK_HIP(hipMemcpyAsync(h.data(), P0->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        ood_reseed(coin, h.data(), C, R);
+        stage_mark(P0, "ood");
+        const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            Plan *pl = X.pl[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+            batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
+            hipLaunchKernelGGL(k_sh_deep, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl,
+                               X.rank[l], G, p->clde, C, (const DeepConsts *)p->deep_consts, pl->TN.fwd_lo,
+                               pl->TN.fwd_hi, three, p->inv, p->deep);
+        }
+    } else {
+        const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
+        fe_to_bytes(z.a, R.z);
+        const int np = 2 * W + CK;
+        ood_eval_ext(P0->st, P0->polys, W, P0->cpolys, CK, log_n, z, zg, P0->x_tab, P0->x_partials, P0->ood);
+        std::vector<fe> hv(2 * np);
+        ZK_CHECK_HIP(hipMemcpyAsync(hv.data(), P0->ood, hv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        std::vector<fe2> e;
+        ood_reseed_ext(coin, hv, C, R, e, h);
+        stage_mark(P0, "ood");
+        const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            Plan *pl = X.pl[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+            batch_inv_norm_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
+            hipLaunchKernelGGL(k_sh_deep_ext, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl,
+                               X.rank[l], G, p->x_clde, C, (const DeepConstsE *)p->x_deep_consts, pl->TN.fwd_lo,
+                               pl->TN.fwd_hi, three, p->inv, p->x_deep);
+        }
     }
     stage_mark(P0, "deep");
 
@@ -416,24 +547,31 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     std::vector<const fe *> layer_vals(nl + 1);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
+    std::vector<fe> rem_flat;
     layer_len[0] = N;
     DistTree Tfri0;
+    auto remainder = [&](std::vector<fe> &rv) -> int {  // rv: KX planes of the last layer
+        if (KX == 1) return remainder_step(rv, 8, coin, R, degree_flag);
+        return remainder_step_ext(rv, 8, coin, R, degree_flag, rem_flat);
+    };
     if (nl == 0) {
-        // no folding: the remainder is the whole DEEP layer, all-gathered into natural order
+        // no folding: the remainder is the whole DEEP layer, all-gathered into natural order per plane
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
-            snd[l] = X.P[l]->deep;
-            rcv[l] = X.P[l]->comp;
+            snd[l] = DEEP(X.P[l]);
+            rcv[l] = COMP(X.P[l]);
         }
-        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)Bl * n * sizeof(fe)));
+        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)KX * Bl * n * sizeof(fe)));
         ZK_CHECK_HIP(hipSetDevice(P0->device));
-        hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(N, 256)), dim3(256), 0, P0->st, (const uint8_t *)P0->comp, G, Bl,
-                           log_n, 16, (uint8_t *)P0->fri);
-        std::vector<fe> rv(N);
-        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), P0->fri, N * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
+        for (int pln = 0; pln < KX; pln++)
+            hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(N, 256)), dim3(256), 0, P0->st,
+                               (const uint8_t *)(COMP(P0) + (size_t)pln * Bl * n), G, Bl, log_n, 16,
+                               (size_t)KX * Bl * n, (uint8_t *)(FRI(P0) + pln * N));
+        std::vector<fe> rv(KX * N);
+        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), FRI(P0), rv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
         ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
-        ZK_TRY(remainder_step(rv, 8, coin, R, degree_flag));
+        ZK_TRY(remainder(rv));
     } else {
         for (int l = 0; l < nlp; l++) {
             f0l[l] = (uint8_t *)X.P[l]->tmp;
@@ -441,59 +579,91 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
         ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_mg) {
             zk_prover *p = X.P[l];
-            hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n, Bl,
-                               (int)fold, log_m, log_mg, send);
+            if (KX == 1)
+                hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n,
+                                   Bl, (int)fold, log_m, log_mg, send);
+            else
+                hipLaunchKernelGGL(k_sh_hash_fri0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->x_deep,
+                                   log_n, Bl, (int)fold, log_m, log_mg, send);
         }, scratch, f0l, f0n));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
-        fe alpha = coin.draw();
-        fe_to_bytes(alpha, R.fri_alphas[0]);
         {
-            const FoldConsts F = fold_consts(alpha, fold);
             std::vector<const void *> snd(nlp);
             std::vector<void *> rcv(nlp);
+            FoldConsts F;
+            FoldConstsE FE;
+            if (KX == 1) {
+                const fe alpha = coin.draw();
+                fe_to_bytes(alpha, R.fri_alphas[0]);
+                F = fold_consts(alpha, fold);
+            } else {
+                const fe2 alpha = coin.draw_ext(2);
+                fe_to_bytes(alpha.a, R.fri_alphas[0]);
+                FE = fold_consts_ext(alpha, fold);
+            }
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
-                hipLaunchKernelGGL(k_sh_fri_fold0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n, Bl,
-                                   X.rank[l], G, (int)fold, log_m, (const FoldConsts *)p->fold_consts, X.pl[l]->TN.inv_lo,
-                                   X.pl[l]->TN.inv_hi, p->ctmp);
-                snd[l] = p->ctmp;
-                rcv[l] = p->comp;
+                if (KX == 1) {
+                    ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+                    hipLaunchKernelGGL(k_sh_fri_fold0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n,
+                                       Bl, X.rank[l], G, (int)fold, log_m, (const FoldConsts *)p->fold_consts,
+                                       X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, p->ctmp);
+                } else {
+                    ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &FE, sizeof FE, hipMemcpyHostToDevice, p->st));
+                    hipLaunchKernelGGL(k_sh_fri_fold0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st,
+                                       p->x_deep, log_n, Bl, X.rank[l], G, (int)fold, log_m,
+                                       (const FoldConstsE *)p->x_fold_consts, X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi,
+                                       p->x_ctmp);
+                }
+                snd[l] = CTMP(p);
+                rcv[l] = COMP(p);
             }
-            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)Bl * m * sizeof(fe)));
+            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
             ZK_CHECK_HIP(hipSetDevice(P0->device));
-            hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st, (const uint8_t *)P0->comp, G, Bl,
-                               log_m, 16, (uint8_t *)P0->fri);
+            for (int pln = 0; pln < KX; pln++)
+                hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st,
+                                   (const uint8_t *)(COMP(P0) + (size_t)pln * Bl * m), G, Bl, log_m, 16,
+                                   (size_t)KX * Bl * m, (uint8_t *)(FRI(P0) + pln * rows0));
         }
-        layer_vals[1] = P0->fri;
+        layer_vals[1] = FRI(P0);
         layer_len[1] = rows0;
         {
-            fe *next = P0->fri + rows0;
+            fe *next = FRI(P0) + KX * rows0;
             uint8_t *dig = P0->fri_dig;  // the all-to-all scratch is free once layer 0 is committed
             for (int l = 1; l < nl; l++) {
                 const size_t L = layer_len[l], rows = L / fold;
                 layer_leaves[l] = dig;
                 layer_nodes[l] = dig + 32 * rows;
                 dig += 64 * rows;
-                commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+                if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+                else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
                 ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, P0->st));
                 ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
                 coin.reseed(R.fri_roots[l]);
-                alpha = coin.draw();
-                fe_to_bytes(alpha, R.fri_alphas[l]);
-                const FoldConsts F = fold_consts(alpha, fold);
-                ZK_CHECK_HIP(hipMemcpyAsync(P0->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
-                fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
+                if (KX == 1) {
+                    const fe alpha = coin.draw();
+                    fe_to_bytes(alpha, R.fri_alphas[l]);
+                    const FoldConsts F = fold_consts(alpha, fold);
+                    ZK_CHECK_HIP(hipMemcpyAsync(P0->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
+                    fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
+                } else {
+                    const fe2 alpha = coin.draw_ext(2);
+                    fe_to_bytes(alpha.a, R.fri_alphas[l]);
+                    const FoldConstsE F = fold_consts_ext(alpha, fold);
+                    ZK_CHECK_HIP(hipMemcpyAsync(P0->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
+                    fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L,
+                                        next);
+                }
                 layer_vals[l + 1] = next;
                 layer_len[l + 1] = rows;
-                next += rows;
+                next += KX * rows;
             }
-            std::vector<fe> rv(layer_len[nl]);
+            std::vector<fe> rv(KX * layer_len[nl]);
             ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
             ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
-            ZK_TRY(remainder_step(rv, 8, coin, R, degree_flag));
+            ZK_TRY(remainder(rv));
         }
     }
     stage_mark(P0, "fri");
@@ -521,18 +691,23 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         for (int c = 0; c < ncols; c++) req.push_back({own, buf, 16 * (((size_t)c * Bl + j) * n + q), nullptr});
     };
     for (size_t q = 0; q < nu; q++) lde_row(B_LDE, W, pos[q]);
-    for (size_t q = 0; q < nu; q++) lde_row(B_CLDE, C, pos[q]);
+    for (size_t q = 0; q < nu; q++) lde_row(B_CLDE, CK, pos[q]);
     for (uint64_t rp : (nl > 0 ? fri_pos[0] : std::vector<uint64_t>())) {
         const int r = (int)(rp & 7), own = r % G, j = r / G;
         const size_t q0 = rp >> 3;
-        for (uint32_t k = 0; k < fold; k++) req.push_back({own, B_DEEP, 16 * (j * n + q0 + k * m), nullptr});
+        for (uint32_t k = 0; k < fold; k++)
+            for (int pln = 0; pln < KX; pln++)
+                req.push_back({own, B_DEEP, 16 * ((size_t)pln * Bl * n + j * n + q0 + k * m), nullptr});
     }
     for (int l = 1; l < nl; l++) {
-        const size_t rows = layer_len[l] / fold;
+        const size_t L = layer_len[l], rows = L / fold;
         for (uint64_t r : fri_pos[l])
             for (uint32_t k = 0; k < fold; k++)
-                req.push_back({0, B_FRI,
-                               (size_t)((const uint8_t *)(layer_vals[l] + r + k * rows) - (const uint8_t *)P0->fri), nullptr});
+                for (int pln = 0; pln < KX; pln++)
+                    req.push_back({0, B_FRI,
+                                   (size_t)((const uint8_t *)(layer_vals[l] + pln * L + r + k * rows) -
+                                            (const uint8_t *)FRI(P0)),
+                                   nullptr});
     }
     const size_t off_dig = req.size();
     const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
@@ -564,9 +739,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
-            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)p->clde, (const uint8_t *)p->deep,
+            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
                                         p->leaves, p->nodes, p->cleaves, p->cnodes, f0l[l], f0n[l],
-                                        (const uint8_t *)p->fri, p->fri_dig};
+                                        (const uint8_t *)FRI(p), p->fri_dig};
             std::vector<uint64_t> addr(NK);
             for (size_t t = 0; t < NK; t++) {
                 const Req &q = req[t];
@@ -595,11 +770,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         size_t off = 0;
         O.trace_rows.assign(got.begin(), got.begin() + nu * W);
         off += nu * W;
-        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * C);
-        off += nu * C;
+        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * CK);
+        off += nu * CK;
         for (int l = 0; l < nl; l++) {
-            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold);
-            off += fri_pos[l].size() * fold;
+            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold * KX);
+            off += fri_pos[l].size() * fold * KX;
         }
         const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
         for (int b = 0; b < 2 + nl; b++) {
@@ -609,7 +784,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
     }
     stage_mark(P0, "queries");
-    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h, O);
+    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h.data(), O, KX == 2 ? &rem_flat : nullptr);
     stage_mark(P0, "serialize");
     ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
     stage_collect(P0);
@@ -663,7 +838,6 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
         X.rank.push_back(comm->loopback() ? l : comm->rank);
     }
     if (opt->blowup != 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "the sharded prover needs blowup 8 (LDE cosets = CE cosets)");
-    if (opt->field_extension != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "the sharded prover supports FieldExtension::None only");
     const size_t m = n / opt->fri_folding;
     if (m < 8 * (size_t)X.G || n / X.G < 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace too short to shard over this many ranks");
     X.log_n = ilog2(n);
@@ -674,6 +848,7 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
         Plan *pl = nullptr;
         ZK_TRY(get_plan(p, n, 8, &pl));
         X.pl.push_back(pl);
+        if (opt->field_extension == 2) ZK_TRY(ensure_ext(p));
         if (!p->sh_buf) {
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_buf, (size_t)8 * ZK_GATHER_CAP));
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_xr, 8));

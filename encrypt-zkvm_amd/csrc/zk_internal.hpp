@@ -193,6 +193,10 @@ void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
                           const fe *inv_bd, const AirConsts *consts2_dev, fe *comp);
+// ... over the CE cosets of `map` (see eval_constraints_mapped), b plane at comp + plane
+void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
+                                 const fe *periodic, const fe *inv_bd, const AirConsts *consts2_dev, size_t plane,
+                                 fe *comp);
 // out[i] = 1 / (N(x_i - z) N(x_i - zg)), N the norm E -> F (coset-major like batch_inv_pairs)
 void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,
                           fe *out);

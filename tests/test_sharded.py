@@ -14,8 +14,7 @@ from zkvm_amd.prover import GpuProver, ProofOptions, make_pub_inputs
 from zkvm_amd.sharded import ShardedProver
 
 GOLD = Path(__file__).resolve().parent / "golden"
-CASES = [c for c in json.loads((GOLD / "cases.json").read_text())["cases"]
-         if c["options"]["blowup"] == 8 and c["options"]["field_extension"] == 1]
+CASES = [c for c in json.loads((GOLD / "cases.json").read_text())["cases"] if c["options"]["blowup"] == 8]
 
 
 def ints(hs):
@@ -57,22 +56,24 @@ def test_sharded_matches_golden(c, world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 8])
-def test_sharded_matches_single_gpu_2_14(world):
+@pytest.mark.parametrize("ext", [1, 2])
+def test_sharded_matches_single_gpu_2_14(world, ext):
     from zkvm_amd.prover import vm_trace
     from zkvm_amd.workloads import make_workload, ops_for_trace_len
     src = ops_for_trace_len(14, "cipher")
     w = make_workload(src, seed=21)
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    opts = ProofOptions(field_extension=ext)
     g = GpuProver(0, max_trace_len=trace.shape[1])
     try:
-        single, _, _, rc = g.prove(trace, pub)
+        single, _, _, rc = g.prove(trace, pub, opts)
     finally:
         g.close()
     assert rc == 0
     sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
     try:
-        got, _ = sp.prove(trace, pub)
+        got, _ = sp.prove(trace, pub, opts)
     finally:
         sp.close()
     assert hashlib.sha256(got).hexdigest() == hashlib.sha256(single).hexdigest()
