@@ -33,6 +33,13 @@ echo "bench ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c5_$TAG" -o "c5_$TAG" -- \
   python3 "$R/bench.py" --config5 $BENCH_ARGS > "$O/prof_bench_c5_$TAG.json" 2> "$O/prof_bench_c5_$TAG.err"
 echo "config5 kernel trace ok"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_c5_$TAG" -o f -- \
+  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_fetch_c5_$TAG.err"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write_c5_$TAG" -o w -- \
+  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_write_c5_$TAG.err"
+python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" -o "$O/pmc_traffic_c5_$TAG.json"
+find "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
+echo "config5 pmc ok"
 (cd "$R" && timeout -k 10 600 python3 bench.py --config5 > "$O/bench_c5_$TAG.json" 2> "$O/bench_c5_$TAG.err")
 echo "config5 bench ok"
 cat "$O/bench_$TAG.json"
