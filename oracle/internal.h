@@ -35,19 +35,20 @@ static inline void mul_wide(u128 a, u128 b, u128 *hi, u128 *lo) {
     *hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
 }
 
-/* a * b mod p by repeated folding of the high half with 2^128 = C (mod p). */
+/* a * b mod p: fold the high half with 2^128 = C (mod p), C < 2^46.  lo + hi*C = s + top*2^128 with
+ * top < 2^47; one more fold of top, whose carry (at most one) is again worth C. */
 static inline u128 f_mul(u128 a, u128 b) {
     u128 hi, lo;
     mul_wide(a, b, &hi, &lo);
-    while (hi) {
-        u128 h2, l2;
-        mul_wide(hi, F_C, &h2, &l2);
-        u128 s = lo + l2;
-        hi = h2 + (s < lo);
-        lo = s;
-    }
-    if (lo >= F_P) lo -= F_P;
-    return lo;
+    const uint64_t C64 = (uint64_t)F_C;
+    const u128 t0 = (u128)(uint64_t)hi * C64, t1 = (u128)(uint64_t)(hi >> 64) * C64;
+    const u128 s1 = lo + t0;
+    const u128 s2 = s1 + (t1 << 64);
+    const uint64_t top = (uint64_t)(t1 >> 64) + (uint64_t)(s1 < lo) + (uint64_t)(s2 < s1);
+    u128 r = s2 + (u128)top * C64;
+    if (r < s2) r += F_C;
+    if (r >= F_P) r -= F_P;
+    return r;
 }
 
 static inline u128 f_exp(u128 b, u128 e) {
@@ -60,6 +61,23 @@ static inline u128 f_exp(u128 b, u128 e) {
     return r;
 }
 static inline u128 f_inv(u128 a) { return f_exp(a, F_P - 2); } /* inv(0) = 0 like winterfell */
+/* in-place Montgomery batch inversion (winter-math batch_inversion): one f_inv for n values (all nonzero) */
+static inline void f_batch_inv(u128 *v, size_t n) {
+    if (!n) return;
+    u128 *pre = (u128 *)malloc(n * sizeof(u128));
+    u128 acc = 1;
+    for (size_t i = 0; i < n; i++) {
+        pre[i] = acc;
+        acc = f_mul(acc, v[i]);
+    }
+    u128 inv = f_inv(acc);
+    for (size_t i = n; i-- > 0;) {
+        const u128 vi = v[i];
+        v[i] = f_mul(inv, pre[i]);
+        inv = f_mul(inv, vi);
+    }
+    free(pre);
+}
 
 static inline u128 f_root_of_unity(unsigned log_n) {
     u128 r = f_exp(F_GENERATOR, (F_P - 1) >> F_TWO_ADICITY);

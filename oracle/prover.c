@@ -38,6 +38,22 @@ static void coin_next(coin_t *c, uint8_t out[32]) {
     c->counter++;
     blake3_merge_with_int(c->seed, c->counter, out);
 }
+/* coefficients of the degree < f polynomial through (x0 * zeta^k, v[k]), zeta = w_f (interp_coset_u over
+ * x0 * <w_f> with the inverses precomputed): c_m = (1/f) x0^-m sum_k v_k zeta^-km */
+static void interp_small(u128 *v, size_t f, u128 inv_x0, const u128 *zinv, u128 inv_f) {
+    u128 c[16];
+    for (size_t m = 0; m < f; m++) {
+        u128 acc = 0;
+        for (size_t k = 0; k < f; k++) acc = f_add(acc, f_mul(v[k], zinv[(k * m) & (f - 1)]));
+        c[m] = acc;
+    }
+    u128 sc = inv_f;
+    for (size_t m = 0; m < f; m++) {
+        v[m] = f_mul(c[m], sc);
+        sc = f_mul(sc, inv_x0);
+    }
+}
+
 /* DefaultRandomCoin::draw::<E>: the first E::ELEMENT_BYTES of the next digest, retried until every
  * base component is canonical (k = 1: 16 bytes; k = 2: both 16-byte halves) */
 static e2 coin_draw_e(coin_t *c, int k) {
@@ -255,18 +271,47 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
             for (int j = 0; j < 9; j++) pcoef[j][r] = row[j];
         }
         for (int j = 0; j < 9; j++) interp_coset_u(pcoef[j], 16, 1);
+        /* x^(n/16) = offset^(n/16) * w_128^i depends on i mod 128 only (winterfell evaluates the periodic
+         * polynomials once per distinct point): a 128-row table */
+        u128(*pertab)[9] = (u128(*)[9])malloc(128 * sizeof(*pertab));
+        {
+            u128 y = f_exp(offset, n / 16);
+            const u128 w128 = f_root_of_unity(7);
+            for (int r = 0; r < 128; r++) {
+                for (int j = 0; j < 9; j++) pertab[r][j] = poly_eval(pcoef[j], 16, y);
+                y = f_mul(y, w128);
+            }
+        }
+        /* divisor inverses: x^n = offset^n * w_8^i takes 8 values; the boundary denominators
+         * (x - 1)(x - g^(n-2)) are batch-inverted over the CE domain (winter-math batch_inversion) */
+        u128 inv_xn[8];
+        {
+            u128 y = f_exp(offset, n);
+            const u128 w8 = f_root_of_unity(3);
+            for (int r = 0; r < 8; r++) {
+                inv_xn[r] = f_inv(f_sub(y, 1));
+                y = f_mul(y, w8);
+            }
+        }
+        u128 *bden = (u128 *)malloc(CE * sizeof(u128));
+        {
+            u128 x = offset;
+            for (size_t i = 0; i < CE; i++) {
+                bden[i] = f_mul(f_sub(x, 1), f_sub(x, g_last2));
+                x = f_mul(x, w_ce);
+            }
+            f_batch_inv(bden, CE);
+        }
         u128 x = offset;
         for (size_t i = 0; i < CE; i++) {
             const u128 *cur = lde + (i * lde_shift) * W, *nxt = lde + ((i * lde_shift + B) % N) * W;
-            u128 per[9], ev[NUM_TCONS];
-            u128 xp = f_exp(x, n / 16);
-            for (int j = 0; j < 9; j++) per[j] = poly_eval(pcoef[j], 16, xp);
-            air_eval_u(cur, nxt, per, pub->lwe_size, pub->delta, ev);
+            u128 ev[NUM_TCONS];
+            air_eval_u(cur, nxt, pertab[i & 127], pub->lwe_size, pub->delta, ev);
             e2 t = e2_base(0);
             for (int k = 0; k < NUM_TCONS; k++) t = e2_add(t, e2_mulb(ct[k], ev[k]));
-            /* transition divisor (x^n - 1) / ((x - g^(n-2)) (x - g^(n-1))) [P6] */
-            u128 zt = f_mul(f_sub(f_exp(x, n), 1), f_inv(f_mul(f_sub(x, g_last2), f_sub(x, g_last1))));
-            e2 acc = e2_mulb(t, f_inv(zt));
+            /* transition divisor (x^n - 1) / ((x - g^(n-2)) (x - g^(n-1))) [P6]: multiply by its inverse */
+            const u128 xa = f_sub(x, g_last2);
+            e2 acc = e2_mulb(t, f_mul(f_mul(xa, f_sub(x, g_last1)), inv_xn[i & 7]));
             /* boundary groups keyed by (stride, step): (0,0) then (0,n-2) [P3] */
             e2 b0 = e2_base(0), b1 = e2_base(0);
             for (int k = 0; k < NUM_ASSERTS; k++) {
@@ -274,11 +319,13 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
                 if (as[k].step == 0) b0 = e2_add(b0, v);
                 else b1 = e2_add(b1, v);
             }
-            acc = e2_add(acc, e2_mulb(b0, f_inv(f_sub(x, 1))));
-            acc = e2_add(acc, e2_mulb(b1, f_inv(f_sub(x, g_last2))));
+            acc = e2_add(acc, e2_mulb(b0, f_mul(bden[i], xa)));                 /* / (x - 1) */
+            acc = e2_add(acc, e2_mulb(b1, f_mul(bden[i], f_sub(x, 1))));        /* / (x - g^(n-2)) */
             comp[i] = acc;
             x = f_mul(x, w_ce);
         }
+        free(bden);
+        free(pertab);
     }
     if (dump && dump->composition)
         for (size_t i = 0; i < CE; i++) st((uint8_t *)dump->composition + 16 * i, comp[i].a);
@@ -346,6 +393,26 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
     e2 *deep = (e2 *)malloc(N * sizeof(e2));
     {
         const u128 w_n = f_root_of_unity(ilog2_sz(N));
+        /* 1/((x - z)(x - zg)) for all x: batch inversion of the E products via their base norms
+         * (N(a + bX) = a^2 + ab - b^2; a base value is its own norm's square root case b = 0) */
+        e2 *dden = (e2 *)malloc(N * sizeof(e2));
+        u128 *nrm = (u128 *)malloc(N * sizeof(u128));
+        {
+            u128 x = offset;
+            for (size_t i = 0; i < N; i++) {
+                const e2 xe = e2_base(x);
+                const e2 d = e2_mul(e2_sub(xe, z), e2_sub(xe, zg));
+                dden[i] = d;
+                nrm[i] = d.b ? f_sub(f_add(f_mul(d.a, d.a), f_mul(d.a, d.b)), f_mul(d.b, d.b)) : d.a;
+                x = f_mul(x, w_n);
+            }
+            f_batch_inv(nrm, N);
+            for (size_t i = 0; i < N; i++) {  /* d^-1 = conj(d) / N(d), conj(a + bX) = (a + b) - bX */
+                const e2 d = dden[i];
+                dden[i] = d.b ? e2_make(f_mul(f_add(d.a, d.b), nrm[i]), f_neg(f_mul(d.b, nrm[i]))) : e2_base(nrm[i]);
+            }
+            free(nrm);
+        }
         u128 x = offset;
         for (size_t i = 0; i < N; i++) {
             e2 s1 = e2_base(0), s2 = e2_base(0);
@@ -359,9 +426,11 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
                 s1 = e2_add(s1, e2_mul(ac[c], e2_sub(h, oodc[c])));
             }
             const e2 xe = e2_base(x);
-            deep[i] = e2_add(e2_mul(s1, e2_inv(e2_sub(xe, z))), e2_mul(s2, e2_inv(e2_sub(xe, zg))));
+            /* s1/(x - z) + s2/(x - zg) = (s1 (x - zg) + s2 (x - z)) / ((x - z)(x - zg)) */
+            deep[i] = e2_mul(e2_add(e2_mul(s1, e2_sub(xe, zg)), e2_mul(s2, e2_sub(xe, z))), dden[i]);
             x = f_mul(x, w_n);
         }
+        free(dden);
     }
     if (dump && dump->deep)
         for (size_t i = 0; i < N; i++) st((uint8_t *)dump->deep + 16 * i, deep[i].a);
@@ -390,20 +459,24 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
         st(R.fri_alphas[l], alpha.a);
         /* degree-respecting projection: p_r interpolates (offset*w_L^r*zeta^k, tv[r][k]); next[r] = p_r(alpha) */
         e2 *nx = (e2 *)malloc(rows * sizeof(e2));
-        const u128 w_l = f_root_of_unity(ilog2_sz(L));
-        u128 xr = offset;
+        /* x_r = offset * w_L^r; x_r^-1 advances by w_L^-1; the fold-point DFT uses zeta^-t, zeta = w_fold */
+        const u128 wl_inv = f_inv(f_root_of_unity(ilog2_sz(L))), inv_f = f_inv((u128)fold);
+        u128 zinv[16];
+        zinv[0] = 1;
+        for (size_t t = 1; t < fold; t++) zinv[t] = f_mul(zinv[t - 1], f_inv(f_root_of_unity(ilog2_sz(fold))));
+        u128 xr_inv = f_inv(offset);
         for (size_t r = 0; r < rows; r++) {
             u128 va[16], vb[16];
             for (size_t k = 0; k < fold; k++) {
                 va[k] = tv[r * fold + k].a;
                 vb[k] = tv[r * fold + k].b;
             }
-            interp_coset_u(va, fold, xr); /* coefficients of p_r in x, per E component */
-            if (K == 2) interp_coset_u(vb, fold, xr);
+            interp_small(va, fold, xr_inv, zinv, inv_f); /* coefficients of p_r in x, per E component */
+            if (K == 2) interp_small(vb, fold, xr_inv, zinv, inv_f);
             e2 acc = e2_base(0);
             for (size_t m = fold; m-- > 0;) acc = e2_add(e2_mul(acc, alpha), e2_make(va[m], K == 2 ? vb[m] : 0));
             nx[r] = acc;
-            xr = f_mul(xr, w_l);
+            xr_inv = f_mul(xr_inv, wl_inv);
         }
         layer_vals[l] = tv;
         layer_leaves[l] = lv;
