@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-n", type=int, default=20)
-    ap.add_argument("--cpu-log-n", type=int, default=16)
+    ap.add_argument("--cpu-log-n", type=int, default=18)  # ~20 s of single-core oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
