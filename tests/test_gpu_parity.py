@@ -233,3 +233,21 @@ def test_bench_size_proof_verifies(gpu, oracle):
     # proof is deterministic for a fixed trace
     proof2, _, _, _ = gpu.prove(trace, pub, ProofOptions())
     assert proof2 == proof
+
+
+def test_reference_vm_prove_and_verify(gpu):
+    """vm/src/lib.rs:47-99 (test_prove) through the GPU prover: the same program, inputs and LWE
+    parameters; the decrypted output is (a + x) * 3 and the proof verifies at 95 bits (zk_verify, and
+    the oracle's verifier)."""
+    from zkvm_amd.prover import prove, verify
+    from zkvm_amd.workloads import LweParameters, ServerKey, rand_field
+    import numpy as np
+    src = "read2\nread\nsadd\npush.1\npush.2\nadd\nsmul\n"
+    a, b, clear_x = 1, 3, 2
+    sk = ServerKey(LweParameters(8, 128, 4, 2.412_390_240_121_573e-5), seed=99)
+    x = sk.encrypt(clear_x)
+    last_row = [rand_field(np.random.default_rng(5), lo=1) for _ in range(28)]
+    h, output, proof = prove(src, [a, b], [x], sk, last_row, gpu=gpu)
+    assert sk.decrypt(output[:5]) == (a + clear_x) * 3
+    pub = make_pub_inputs(h, output, sk.lwe_size(), sk.parameters.delta)
+    assert verify(proof, pub, 95) == (0, "")

@@ -96,3 +96,15 @@ def test_vm_errors_match_oracle(oracle, source, code):
         codes, values, _ = oracle.program_compile(source)
         oracle.processor_trace(codes, values)
     assert str(oe.value) in str(e.value)
+
+
+def test_reference_vm_program_output():
+    """The VM half of vm/src/lib.rs:47-99 (test_prove): read2 / read / sadd / push.1 / push.2 / add / smul
+    with a = 1, x = Enc(2) decrypts to (a + x) * 3 on the top of the stack."""
+    from zkvm_amd.workloads import LweParameters, rand_field
+    src = "read2\nread\nsadd\npush.1\npush.2\nadd\nsmul\n"
+    sk = ServerKey(LweParameters(8, 128, 4, 2.412_390_240_121_573e-5), seed=99)
+    x = sk.encrypt(2)
+    last_row = [rand_field(np.random.default_rng(5), lo=1) for _ in range(28)]
+    trace, output, h = vm_trace(src, [1, 3], [x], sk, last_row)
+    assert trace.shape[0] == 28 and sk.decrypt(output[:5]) == 9
