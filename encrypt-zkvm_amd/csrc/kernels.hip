@@ -48,11 +48,42 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 #endif
 constexpr int NTT_THREADS = ZK_NTT_THREADS;
 
-template <int LOGM>
-__device__ __forceinline__ int lds_idx(int line, int pos) {
-    constexpr int PAD = LOGM >= 4 ? 1 : 0;
-    return line * ((1 << LOGM) + PAD) + pos;
-}
+#ifndef ZK_NTT_SWZ
+#define ZK_NTT_SWZ 1  // XOR-swizzled LDS tiles (0: one pad element per line)
+#endif
+
+// LDS layout of a tile: LPB lines of M = 2^LOGM elements (16 B, i.e. 4 banks, each).  With 64 banks a
+// 16-lane quarter-wave is conflict-free when its elements differ in the low 4 index bits.
+//   swizzled (M >= 64): element (line, pos) at line*M + (sw(pos) ^ ((line & LMASK) << R)), where
+//   sw(x) = x ^ 5*((x >> 4) & 3) folds index bits 4-5 into bits 0-3 (the radix-4 rounds with h = 1 and
+//   h = 4 stride through exactly those bits) and the line goes above the R = log2(16/LPB) bits that 16
+//   lanes vary in the load and pass-2 store phases.  sw is linear over XOR, so an element at pos + d
+//   (d's bits zero in pos) is idx ^ sw(d).
+//   padded (small M): line*(M + 1) + pos.
+template <int LOGM, int TILE>
+struct Lds {
+    static constexpr int M = 1 << LOGM, LPB = TILE >> LOGM;
+    static constexpr bool SWZ = ZK_NTT_SWZ && LOGM >= 6;
+    static constexpr int LLPB = LPB >= 16 ? 4 : LPB >= 8 ? 3 : LPB >= 4 ? 2 : LPB >= 2 ? 1 : 0;
+    static constexpr int R = 4 - LLPB;
+    static constexpr int LMASK = (1 << LLPB) - 1;
+    __device__ __forceinline__ static int sw(int x) { return SWZ ? x ^ (((x >> 4) & 3) * 5) : x; }
+    __device__ __forceinline__ static int idx(int line, int pos) {
+        if constexpr (SWZ) return line * M + (sw(pos) ^ ((line & LMASK) << R));
+        else return line * (M + (LOGM >= 4 ? 1 : 0)) + pos;
+    }
+    __device__ __forceinline__ static int at(int p, int d) {
+        if constexpr (SWZ) return p ^ sw(d);
+        else return p + d;
+    }
+    // load phase: the v-th element of a line (in lane order) is DFT input k = v rotated right by R bits,
+    // so that after the bit reversal the R low lane bits land in the low position bits
+    __device__ __forceinline__ static int load_k(int v) {
+        if constexpr (SWZ && R > 0) return ((v & ((1 << R) - 1)) << (LOGM - R)) | (v >> R);
+        else return v;
+    }
+    static constexpr size_t bytes() { return (size_t)(SWZ ? TILE : TILE + (LOGM >= 4 ? LPB : 0)) * sizeof(fe); }
+};
 
 // Radix-4 rounds: each radix-4 butterfly performs DIT stages lg and lg+1 (half h = 2^(lg-1)) on
 // positions p0 + {0, h, 2h, 3h}, p0 = grp*4h + j, j < h:
@@ -71,14 +102,15 @@ __device__ void lds_dft(fe *s, const fe *tw4096) {
 #pragma unroll
         for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
             int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
-            int p = lds_idx<LOGM>(line, local * 4);
-            fe x0 = s[p], x1 = s[p + 1], x2 = s[p + 2], x3 = s[p + 3];
+            using L = Lds<LOGM, TILE>;
+            const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
+            fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
             fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
             fe a3 = fe_mul(fe_sub(x2, x3), w4);
             s[p] = fe_add(a0, a2);
-            s[p + 2] = fe_sub(a0, a2);
-            s[p + 1] = fe_add(a1, a3);
-            s[p + 3] = fe_sub(a1, a3);
+            s[p2] = fe_sub(a0, a2);
+            s[p1] = fe_add(a1, a3);
+            s[p3] = fe_sub(a1, a3);
         }
         __syncthreads();
         lg0 = 3;
@@ -89,18 +121,20 @@ __device__ void lds_dft(fe *s, const fe *tw4096) {
             for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
                 int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
                 int j = local & (h - 1), grp = local >> (lg - 1);
-                int p = lds_idx<LOGM>(line, grp * 4 * h + j);
+                using L = Lds<LOGM, TILE>;
+                const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h),
+                          p3h = L::at(p, 3 * h);
                 fe w1 = tw4096[j << (12 - lg)];
                 fe w2 = tw4096[j << (11 - lg)];
                 fe w3 = tw4096[(j + h) << (11 - lg)];
-                fe x0 = s[p], x1 = s[p + h], x2 = s[p + 2 * h], x3 = s[p + 3 * h];
+                fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
                 fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
                 fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
                 fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
                 s[p] = fe_add(a0, u2);
-                s[p + 2 * h] = fe_sub(a0, u2);
-                s[p + h] = fe_add(a1, u3);
-                s[p + 3 * h] = fe_sub(a1, u3);
+                s[p2h] = fe_sub(a0, u2);
+                s[ph] = fe_add(a1, u3);
+                s[p3h] = fe_sub(a1, u3);
             }
             __syncthreads();
             lg0 = lg + 2;
@@ -115,8 +149,8 @@ __device__ void lds_dft(fe *s, const fe *tw4096) {
             int local = bf & (M / 2 - 1);
             int j = local & (half - 1);
             int grp = local >> (lg - 1);
-            int i0 = lds_idx<LOGM>(line, grp * 2 * half + j);
-            int i1 = i0 + half;
+            int i0 = Lds<LOGM, TILE>::idx(line, grp * 2 * half + j);
+            int i1 = Lds<LOGM, TILE>::at(i0, half);
             fe w = tw4096[j << twshift];
             fe u = s[i0];
             fe v = fe_mul(s[i1], w);
@@ -164,7 +198,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
             if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
             else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
         }
-        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
     lds_dft<LOGM, TILE>(s, a.tw4096);
@@ -172,7 +206,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         int line = e >> LOGM, j = e & (M - 1);
         int b = b0 + line;
         if (b >= batch) continue;
-        fe v = s[lds_idx<LOGM>(line, j)];
+        fe v = s[Lds<LOGM, TILE>::idx(line, j)];
         if (a.has_post) v = fe_mul(v, a.post);
         a.out[(size_t)b * a.out_stride + j] = v;
     }
@@ -196,12 +230,12 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     const size_t b = lin % batch;
     const fe *in = a.in + b * a.in_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
-        int line = e % LPB, k2 = e / LPB;
+        int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
         size_t k = k1_0 + line + n1 * (size_t)k2;
         fe v = in[k];
         if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
         else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
-        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
     lds_dft<LOGM, TILE>(s, a.tw4096);
@@ -209,7 +243,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j2 = e & (M - 1);
         size_t k1 = k1_0 + line;
-        fe v = s[lds_idx<LOGM>(line, j2)];
+        fe v = s[Lds<LOGM, TILE>::idx(line, j2)];
         if (a.pass_tw) {
             v = fe_mul(v, a.pass_tw[k1_0 * M + e]);  // = w^(j2 k1), contiguous over the block
         } else {
@@ -233,16 +267,16 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const size_t b = blockIdx.y;
     const fe *in = a.in + b * a.in_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
-        int line = e % LPB, k1 = e / LPB;
+        int line = e % LPB, k1 = Lds<LOGM, TILE>::load_k(e / LPB);
         fe v = in[(size_t)k1 * n2 + j2_0 + line];
-        s[lds_idx<LOGM>(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = v;
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
     lds_dft<LOGM, TILE>(s, a.tw4096);
     fe *out = a.out + b * a.out_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, j1 = e / LPB;
-        fe v = s[lds_idx<LOGM>(line, j1)];
+        fe v = s[Lds<LOGM, TILE>::idx(line, j1)];
         if (a.has_post) v = fe_mul(v, a.post);
         out[n2 * (size_t)j1 + j2_0 + line] = v;
     }
@@ -256,16 +290,10 @@ static double dft_muls_per_elem(int logm) {
     return 0.25 + (double)((logm - 2) / 2) + ((logm & 1) ? 0.5 : 0.0);
 }
 
-template <int TILE>
-static size_t lds_bytes(int logm) {
-    int M = 1 << logm;
-    return (size_t)(TILE + (logm >= 4 ? TILE / M : 0)) * sizeof(fe);
-}
-
 template <int LOGM, int TILE>
 static void launch_single(hipStream_t st, const NttArgs &a, int batch) {
     constexpr int LPB = TILE / (1 << LOGM);
-    size_t sh = lds_bytes<TILE>(LOGM);
+    size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_single<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * (1 << LOGM);
     ZK_PROF_OPS(st, "ntt_single", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.pre_full || a.pre_lo ? 1 : 0) + (a.has_post ? 1 : 0)),
@@ -276,7 +304,7 @@ template <int LOGM, int TILE>
 static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     constexpr int LPB = TILE / (1 << LOGM);
     size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
-    size_t sh = lds_bytes<TILE>(LOGM);
+    size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
     ZK_PROF_OPS(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * el,
@@ -288,7 +316,7 @@ template <int LOGM, int TILE>
 static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     constexpr int LPB = TILE / (1 << LOGM);
     size_t n2 = ((size_t)1 << a.log_n) >> LOGM;
-    size_t sh = lds_bytes<TILE>(LOGM);
+    size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
     ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.has_post ? 1 : 0)), el * LOGM,
