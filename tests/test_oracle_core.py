@@ -104,3 +104,14 @@ def test_quadratic_extension_against_bigint(oracle):
         xi = oracle.e2op("or_e2_inv", x)
         assert mul(x, xi) == (1, 0)
     assert oracle.e2op("or_e2_mul", (0, 1), (0, 1)) == (1, 1)  # X^2 = 1 + X
+
+
+def test_two_adic_root_matches_winter_math(oracle):
+    """winter-math 0.9.0 f128 (`src/field/f128/mod.rs`, not vendored; constant recalled from the published
+    crate): TWO_ADIC_ROOT_OF_UNITY = 23953097886125630542083529559205016746, of order 2^40.  The oracle and
+    the library derive it as GENERATOR^((p-1)/2^40) with GENERATOR = 3; both must give this constant."""
+    P = 2**128 - 45 * 2**40 + 1
+    G40 = 23953097886125630542083529559205016746
+    assert pow(3, (P - 1) >> 40, P) == G40
+    assert pow(G40, 2**40, P) == 1 and pow(G40, 2**39, P) != 1
+    assert oracle.root_of_unity(40) == G40
