@@ -85,79 +85,90 @@ struct Lds {
     static constexpr size_t bytes() { return (size_t)(SWZ ? TILE : TILE + (LOGM >= 4 ? LPB : 0)) * sizeof(fe); }
 };
 
+// One radix-4 round (stages lg, lg+1), compile-time lg so every shift and mask is an immediate.
+template <int LOGM, int TILE, int LG>
+__device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
+    constexpr int M = 1 << LOGM;
+    constexpr int Q = TILE / 4;
+    constexpr int h = 1 << (LG - 1);
+    using L = Lds<LOGM, TILE>;
+#pragma unroll
+    for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
+        const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+        const int j = local & (h - 1), grp = local >> (LG - 1);
+        const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+        const fe w1 = tw4096[j << (12 - LG)];
+        const fe w2 = tw4096[j << (11 - LG)];
+        const fe w3 = tw4096[(j + h) << (11 - LG)];
+        const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+        const fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
+        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        const fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
+        s[p] = fe_add(a0, u2);
+        s[p2h] = fe_sub(a0, u2);
+        s[ph] = fe_add(a1, u3);
+        s[p3h] = fe_sub(a1, u3);
+    }
+    __syncthreads();
+}
+
+// rounds LG, LG+2, ... while LG + 1 <= LOGM, then the trailing radix-2 stage of an odd LOGM
+template <int LOGM, int TILE, int LG>
+__device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
+    if constexpr (LG + 1 <= LOGM) {
+        r4_round<LOGM, TILE, LG>(s, tw4096);
+        r4_rounds<LOGM, TILE, LG + 2>(s, tw4096);
+    } else if constexpr (LG == LOGM) {
+        constexpr int M = 1 << LOGM;
+        constexpr int half = 1 << (LG - 1);
+        using L = Lds<LOGM, TILE>;
+#pragma unroll
+        for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
+            const int line = bf >> (LOGM - 1), local = bf & (M / 2 - 1);
+            const int j = local & (half - 1), grp = local >> (LG - 1);
+            const int i0 = L::idx(line, grp * 2 * half + j), i1 = L::at(i0, half);
+            const fe w = tw4096[j << (12 - LG)];  // w_len^j = w_4096^(j * 4096/len)
+            const fe u = s[i0];
+            const fe v = fe_mul(s[i1], w);
+            s[i0] = fe_add(u, v);
+            s[i1] = fe_sub(u, v);
+        }
+        __syncthreads();
+    }
+}
+
 // Radix-4 rounds: each radix-4 butterfly performs DIT stages lg and lg+1 (half h = 2^(lg-1)) on
 // positions p0 + {0, h, 2h, 3h}, p0 = grp*4h + j, j < h:
 //   stage lg   : (x0, x1), (x2, x3) with w_2h^j
 //   stage lg+1 : (x0, x2) with w_4h^j, (x1, x3) with w_4h^(j+h)
 // so a round reads and writes each LDS element once for two stages.  The first round (h = 1, j = 0)
 // has w_2 = w_4^0 = 1 and needs a single multiply by w_4.  An odd log2(M) ends with one radix-2 stage.
+// Inlined into each kernel: `s` stays an LDS pointer (ds_read/ds_write) and the twiddle table a
+// global one (global_load, counted by vmcnt only; as a called function both were flat accesses
+// and every LDS wait also waited for the twiddle loads).
 template <int LOGM, int TILE>
-__device__ void lds_dft(fe *s, const fe *tw4096) {
+__device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096) {
     constexpr int M = 1 << LOGM;
-    constexpr int BFLY = TILE / 2;
     constexpr int Q = TILE / 4;
-    int lg0 = 1;
     if constexpr (LOGM >= 2) {
         const fe w4 = tw4096[1024];
+        using L = Lds<LOGM, TILE>;
 #pragma unroll
         for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
-            int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
-            using L = Lds<LOGM, TILE>;
+            const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
             const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
-            fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
-            fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
-            fe a3 = fe_mul(fe_sub(x2, x3), w4);
+            const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
+            const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+            const fe a3 = fe_mul(fe_sub(x2, x3), w4);
             s[p] = fe_add(a0, a2);
             s[p2] = fe_sub(a0, a2);
             s[p1] = fe_add(a1, a3);
             s[p3] = fe_sub(a1, a3);
         }
         __syncthreads();
-        lg0 = 3;
-#pragma unroll 1
-        for (int lg = 3; lg + 1 <= LOGM; lg += 2) {
-            const int h = 1 << (lg - 1);
-#pragma unroll
-            for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
-                int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
-                int j = local & (h - 1), grp = local >> (lg - 1);
-                using L = Lds<LOGM, TILE>;
-                const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h),
-                          p3h = L::at(p, 3 * h);
-                fe w1 = tw4096[j << (12 - lg)];
-                fe w2 = tw4096[j << (11 - lg)];
-                fe w3 = tw4096[(j + h) << (11 - lg)];
-                fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-                fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
-                fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
-                fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
-                s[p] = fe_add(a0, u2);
-                s[p2h] = fe_sub(a0, u2);
-                s[ph] = fe_add(a1, u3);
-                s[p3h] = fe_sub(a1, u3);
-            }
-            __syncthreads();
-            lg0 = lg + 2;
-        }
-    }
-#pragma unroll 1
-    for (int lg = lg0; lg <= LOGM; lg++) {
-        const int half = 1 << (lg - 1);
-        const int twshift = 12 - lg;  // w_len^j = w_4096^(j * 4096/len)
-        for (int bf = threadIdx.x; bf < BFLY; bf += NTT_THREADS) {
-            int line = bf >> (LOGM - 1);
-            int local = bf & (M / 2 - 1);
-            int j = local & (half - 1);
-            int grp = local >> (lg - 1);
-            int i0 = Lds<LOGM, TILE>::idx(line, grp * 2 * half + j);
-            int i1 = Lds<LOGM, TILE>::at(i0, half);
-            fe w = tw4096[j << twshift];
-            fe u = s[i0];
-            fe v = fe_mul(s[i1], w);
-            s[i0] = fe_add(u, v);
-            s[i1] = fe_sub(u, v);
-        }
-        __syncthreads();
+        r4_rounds<LOGM, TILE, 3>(s, tw4096);
+    } else {
+        r4_rounds<LOGM, TILE, 1>(s, tw4096);
     }
 }
 
