@@ -152,6 +152,16 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     return ZK_OK;
 }
 
+const fe *zk::boundary_inverses(zk_prover *p, Plan *pl) {
+    if (!pl->bnd_inv) {
+        const size_t CE = (size_t)8 << pl->log_n;
+        if (p->arena.alloc(&pl->bnd_inv, CE) != hipSuccess) return nullptr;
+        const fe g_last2 = h_pow(h_root_of_unity(pl->log_n), ((size_t)1 << pl->log_n) - 2);
+        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, fe_one(), g_last2, pl->bnd_inv);
+    }
+    return pl->bnd_inv;
+}
+
 // ---------------------------------------------------------------- prover object
 int zk_device_count(int *count) {
     int c = 0;
@@ -844,15 +854,17 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         AirConsts K;
         draw_air_consts(coin, pub, n, K, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
-        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), K.g_last2, p->inv);
-        eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->air_consts,
+        const fe *binv = boundary_inverses(p, pl);
+        if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
+        eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, binv, (const AirConsts *)p->air_consts,
                          comp);
     } else {
         AirConsts Kp[2];
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
-        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, log_n, fe_one(), Kp[0].g_last2, p->inv);
-        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, p->inv, (const AirConsts *)p->x_air,
+        const fe *binv = boundary_inverses(p, pl);
+        if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
+        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, binv, (const AirConsts *)p->x_air,
                              comp);
     }
     stage_mark(p, "constraints");
@@ -1144,8 +1156,9 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
     for (int k = 0; k < NUM_ASSERTS; k++) K.coeff_b[k] = fe_from_bytes(coeff_b + 16 * k);
     air_static_consts(pub, n, K);
     ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
-    batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, fe_one(), K.g_last2, p->inv);
-    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->Tn, pl->periodic, p->inv,
+    const fe *binv = boundary_inverses(p, pl);
+    if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
+    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->Tn, pl->periodic, binv,
                      (const AirConsts *)p->air_consts, p->comp);
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     coset_major_rows_to_host(p, p->comp, 1, n, 8, out);

@@ -73,7 +73,12 @@ struct Plan {  // everything that depends only on (n, B)
     PowTable inv3;                // 3^-k, k < n
     fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)
     fe *periodic = nullptr;               // 128 x 9
+    // 1 / ((x - 1)(x - g^(n-2))) over the CE domain (coset-major): the two boundary divisors
+    // depend only on n, so they are inverted once per plan (first proof) and reused
+    fe *bnd_inv = nullptr;
 };
+// the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
+const fe *boundary_inverses(zk_prover *p, Plan *pl);
 
 }  // namespace zk
 
