@@ -35,13 +35,13 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 // decimation-in-time stages; the result is in natural order.  Lines are padded by one element
 // so that LPB lanes writing the same position of consecutive lines hit different banks.
 #ifndef ZK_NTT_THREADS
-#define ZK_NTT_THREADS 512
+#define ZK_NTT_THREADS 1024
 #endif
 #ifndef ZK_NTT_TILE
 #define ZK_NTT_TILE 4096
 #endif
 #ifndef ZK_NTT_WAVES
-#define ZK_NTT_WAVES 4  // waves per SIMD: two 512-thread blocks per CU (the LDS limit) need <= 128 VGPRs
+#define ZK_NTT_WAVES 8  // waves per SIMD: two 1024-thread blocks per CU (the LDS limit) need <= 64 VGPRs
 #endif
 #ifndef ZK_NTT_PASS_TABLE
 #define ZK_NTT_PASS_TABLE 1  // inter-pass twiddles from a full table (0: split tables, one multiply more)
@@ -525,10 +525,45 @@ __global__ void __launch_bounds__(256) k_merge_top(const uint8_t *src, size_t cn
     }
 }
 
+// Three Merkle levels per launch: thread t merges the 8 child digests src[8t .. 8t+8) into
+// nodes[cnt + 4t .. +4), their pairs into nodes[cnt/2 + 2t .. +2) and those into nodes[cnt/4 + t].
+// One compression per thread per level-launch left every wave with a single dependent compression
+// behind its loads (and 14 launches per tree); seven per thread keep the VALU busy.
+__global__ void __launch_bounds__(256) k_merge_level3(const uint8_t *src, uint8_t *nodes, size_t cnt) {
+    const size_t q = cnt / 4;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < q; t += (size_t)gridDim.x * blockDim.x) {
+        uint32_t l[8], r[8], h0[8], h1[8], g0[8];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const size_t c0 = 4 * t + 2 * half;
+            load_digest(src + 64 * c0, l);
+            load_digest(src + 64 * c0 + 32, r);
+            b3::merge(l, r, h0);
+            store_digest(nodes + 32 * (cnt + c0), h0);
+            load_digest(src + 64 * (c0 + 1), l);
+            load_digest(src + 64 * (c0 + 1) + 32, r);
+            b3::merge(l, r, h1);
+            store_digest(nodes + 32 * (cnt + c0 + 1), h1);
+            b3::merge(h0, h1, half ? r : g0);
+            store_digest(nodes + 32 * (cnt / 2 + 2 * t + half), half ? r : g0);
+        }
+        b3::merge(g0, r, h0);
+        store_digest(nodes + 32 * (cnt / 4 + t), h0);
+    }
+}
+
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes) {
     // invariant: src holds 2*cnt digests whose parents go to nodes[cnt .. 2cnt)
     size_t cnt = nl / 2;
     const uint8_t *src = leaves;
+    while (cnt >= 2048) {
+        unsigned blocks = cdiv(cnt / 4, 256);
+        if (blocks > 65536) blocks = 65536;
+        ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
+                hipLaunchKernelGGL(k_merge_level3, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
+        src = nodes + 32 * (cnt / 4);
+        cnt /= 8;
+    }
     while (cnt > 256) {
         unsigned blocks = cdiv(cnt, 256);
         if (blocks > 65536) blocks = 65536;
@@ -756,36 +791,53 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         ZK_ACC(19, fe_mul(NXT(10), nfh));
     }
     ZK_SEQ(cb, t.lo);
-    // 0..11: degree-5 selectors (flags.rs:45-79) with shared prefixes, each consumed right away
+    // 0..11: degree-5 selectors (flags.rs:45-79) with shared prefixes, each consumed right away.
+    // Sibling selectors share one multiply: P*(1 - b) = P - P*b.  Two pairs of constraints are folded
+    // before their coefficient (3/6 and 8/9 differ only in the last bit b4):
+    //   ct3*(X(1-b4))*d3 + ct6*(X b4)*d6 = X*(ct3 d3 + b4 (ct6 d6 - ct3 d3))
+    //   ct8*(Z(1-b4))*d1 + ct9*(Z b4)*d1 = Z d1 * (ct8 + b4 (ct9 - ct8))
+    // (exact field identities: the composition values are unchanged).
     {
         const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
-        const fe nb0 = fe_sub(one, b0), nb1 = fe_sub(one, b1), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3),
-                 nb4 = fe_sub(one, b4);
+        const fe nb0 = fe_sub(one, b0), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3), nb4 = fe_sub(one, b4);
         const fe s0 = CUR(12), s1 = CUR(13);
         // 0 clock, 2 shift
         ZK_ACC(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
-        ZK_ACC(2, fe_mul(b0, b1));
+        const fe b01 = fe_mul(b0, b1);
+        ZK_ACC(2, b01);
+        const fe b0n1 = fe_sub(b0, b01);   // b0 (1-b1)
+        const fe n0_1 = fe_sub(b1, b01);   // (1-b0) b1
+        const fe n01 = fe_sub(nb0, n0_1);  // (1-b0)(1-b1)
         // 11 noop
         {
-            const fe is_noop = fe_mul(fe_mul(fe_mul(fe_mul(nb0, nb1), nb2), nb3), nb4);
+            const fe is_noop = fe_mul(fe_mul(fe_mul(n01, nb2), nb3), nb4);
             ZK_ACC(11, fe_mul(is_noop, fe_sub(s0n, s0)));
         }
         ZK_SEQ(cb, t.lo);
-        const fe n0_1 = fe_mul(nb0, b1), n0_1_n2 = fe_mul(n0_1, nb2);
+        const fe n0_1_b2 = fe_mul(n0_1, b2);
+        const fe n0_1_n2 = fe_sub(n0_1, n0_1_b2);
+        const fe Y = fe_mul(n0_1_n2, b3);  // (1-b0) b1 (1-b2) b3
         fe is_add2, is_read2;
         {
-            const fe n0_1_n2_n3 = fe_mul(n0_1_n2, nb3);
-            // 3 add, 6 mul
-            ZK_ACC(3, fe_mul(fe_mul(n0_1_n2_n3, nb4), fe_sub(s0n, fe_add(s0, s1))));
-            ZK_ACC(6, fe_mul(fe_mul(n0_1_n2_n3, b4), fe_sub(s0n, fe_mul(s0, s1))));
+            // 3 add, 6 mul: X = (1-b0) b1 (1-b2)(1-b3)
+            const fe X = fe_sub(n0_1_n2, Y);
+            const fe e3 = fe_mul(S.ct[3], fe_sub(s0n, fe_add(s0, s1)));
+            const fe e6 = fe_mul(S.ct[6], fe_sub(s0n, fe_mul(s0, s1)));
+            const fe v36 = fe_mul(X, fe_add(e3, fe_mul(b4, fe_sub(e6, e3))));
+            t = fe_add(t, v36);
+            if (KE == 2) {
+                const fe f3 = fe_mul(S.ct2[3], fe_sub(s0n, fe_add(s0, s1)));
+                const fe f6 = fe_mul(S.ct2[6], fe_sub(s0n, fe_mul(s0, s1)));
+                t2 = fe_add(t2, fe_mul(X, fe_add(f3, fe_mul(b4, fe_sub(f6, f3)))));
+                asm volatile("" : "+v"(t2.lo), "+v"(t2.hi));
+            }
         }
         ZK_SEQ(cb, t.lo);
         {
             // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs (fhe/src/server_key.rs:89-124)
-            const fe n0_1_n2_3 = fe_mul(n0_1_n2, b3);
-            const fe is_sadd = fe_mul(n0_1_n2_3, nb4);
-            is_add2 = fe_mul(n0_1_n2_3, b4);
-            const fe is_smul = fe_mul(fe_mul(fe_mul(n0_1, b2), nb3), nb4);
+            is_add2 = fe_mul(Y, b4);
+            const fe is_sadd = fe_sub(Y, is_add2);
+            const fe is_smul = fe_mul(fe_mul(n0_1_b2, nb3), nb4);
             // sum_k (sn_k - s1_k * s0) = sum sn_k - s0 * sum s1_k  (one multiply instead of L)
             fe acc4 = fe_zero(), acc5 = fe_zero(), sum_sn = fe_zero(), sum_s1 = fe_zero();
             for (int k = 0; k < L; k++) {
@@ -805,12 +857,16 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         ZK_SEQ(cb, t.lo);
         {
             // 8 push / 9 read / 10 read2
-            const fe p0 = fe_mul(fe_mul(b0, nb1), nb2);
-            const fe p0n3 = fe_mul(p0, nb3);
-            is_read2 = fe_mul(fe_mul(p0, b3), nb4);
-            const fe d1 = fe_sub(NXT(13), s0);
-            ZK_ACC(8, fe_mul(fe_mul(p0n3, nb4), d1));
-            ZK_ACC(9, fe_mul(fe_mul(p0n3, b4), d1));
+            const fe p0 = fe_mul(b0n1, nb2);     // b0 (1-b1)(1-b2)
+            const fe p0b3 = fe_mul(p0, b3);
+            const fe p0n3 = fe_sub(p0, p0b3);
+            is_read2 = fe_mul(p0b3, nb4);
+            const fe zd1 = fe_mul(p0n3, fe_sub(NXT(13), s0));
+            t = fe_add(t, fe_mul(zd1, fe_add(S.ct[8], fe_mul(b4, fe_sub(S.ct[9], S.ct[8])))));
+            if (KE == 2) {
+                t2 = fe_add(t2, fe_mul(zd1, fe_add(S.ct2[8], fe_mul(b4, fe_sub(S.ct2[9], S.ct2[8])))));
+                asm volatile("" : "+v"(t2.lo), "+v"(t2.hi));
+            }
             ZK_ACC(10, fe_mul(is_read2, fe_sub(NXT(17), s0)));
         }
         // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
