@@ -187,6 +187,7 @@ struct NttArgs {
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
     const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
     const fe *pre_full;           // ... or the same from a full table (preferred when present)
+    size_t pre_stride;            // batch entry b uses pre_full + b * pre_stride (0: one table for all)
     const fe *pass_tw;            // inter-pass twiddles [k1 * n2 + j2] (replaces big_lo/hi when present)
     fe post;                      // post-scale constant
     int has_post;
@@ -206,7 +207,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         fe v = fe_zero();
         if (b < batch) {
             v = a.in[(size_t)b * a.in_stride + k];
-            if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
+            if (a.pre_full) v = fe_mul(v, a.pre_full[(size_t)b * a.pre_stride + k]);
             else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
         }
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
         size_t k = k1_0 + line + n1 * (size_t)k2;
         fe v = in[k];
-        if (a.pre_full) v = fe_mul(v, a.pre_full[k]);
+        if (a.pre_full) v = fe_mul(v, a.pre_full[b * a.pre_stride + k]);
         else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
@@ -352,7 +353,7 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     }
 
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
-         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
+         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, size_t pre_stride) {
     constexpr int TILE = ZK_NTT_TILE;
     NttArgs a;
     a.in = in;
@@ -365,6 +366,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.pre_lo = pre ? pre->lo : nullptr;
     a.pre_hi = pre ? pre->hi : nullptr;
     a.pre_full = pre ? pre->full : nullptr;
+    a.pre_stride = pre_stride;
 #if ZK_NTT_PASS_TABLE
     a.pass_tw = inverse ? T.inv_pass : T.fwd_pass;
 #else
@@ -1178,6 +1180,73 @@ void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const
     if (blocks > 65536) blocks = 65536;
     ZK_PROF(st, "deep", (448.0 + 16.0 * ccols + 32.0) * N, hipLaunchKernelGGL(k_deep, dim3(blocks), dim3(256), 0, st, lde, log_n, log_b, clde, ccols,
                                            (const DeepConsts *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi, three, inv_d, out));
+}
+
+// ---- DEEP through coefficient form.  With the shared trace coefficients alpha (z and zg terms) and
+// composition coefficients gamma, the DEEP numerator is one polynomial of degree n:
+//   num(x) = (x - zg)(S(x) - k1) + (x - z)(A(x) - k2),  A = sum alpha_i T_i,  S = A + sum gamma_j H_j
+//          = x (S + A)(x) - (zg S + z A)(x) - (k1 + k2) x + (k1 zg + k2 z)
+// so U = num has coefficients U_k = P_{k-1} - Q_k (P = S + A, Q = zg S + z A) plus the two constant
+// corrections, and U_n = P_{n-1}.  Its values on coset r are LDE(U_0..U_{n-1}) + U_n s_r^n (x^n = s_r^n
+// on the whole coset).  DEEP(x) = num(x) / ((x - z)(x - zg)) -- the same field values as summing the 35
+// LDE columns point by point, from one n-coefficient combination and one B-coset LDE: the 28 + 7 LDE
+// columns (3.7 GB at 2^20) are never read.
+__global__ void __launch_bounds__(256) k_deep_combine(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
+                                                      const DeepConsts *D, fe *P, fe *Q) {
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+        acc288 aA = acc288_zero(), aH = acc288_zero();
+#pragma unroll 4
+        for (int c = 0; c < 28; c++) acc288_madd(aA, D->alpha_t[c], ld_fe(tpolys + (size_t)c * n + k));
+        for (int j = 0; j < ccols; j++) acc288_madd(aH, D->alpha_c[j], ld_fe(cpolys + (size_t)j * n + k));
+        const fe A = acc288_reduce(aA);
+        const fe S = fe_add(A, acc288_reduce(aH));
+        P[k] = fe_add(S, A);
+        Q[k] = fe_add(fe_mul(D->zg, S), fe_mul(D->z, A));
+    }
+}
+
+__global__ void __launch_bounds__(256) k_deep_shift(const fe *P, const fe *Q, size_t n, const DeepConsts *D,
+                                                    const fe *xn, int B, fe *U, fe *un) {
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+        fe u = fe_sub(k ? P[k - 1] : fe_zero(), Q[k]);
+        if (k == 0) u = fe_add(u, fe_add(fe_mul(D->k1, D->zg), fe_mul(D->k2, D->z)));
+        if (k == 1) u = fe_sub(u, fe_add(D->k1, D->k2));
+        U[k] = u;
+        if (k == 0)
+            for (int r = 0; r < B; r++) un[r] = fe_mul(P[n - 1], xn[r]);
+    }
+}
+
+// out[i] (natural order) = (ulde[coset-major i] + un[coset]) * inv[coset-major i]
+__global__ void __launch_bounds__(256) k_deep_point(const fe *ulde, const fe *un, int log_n, int log_b, const fe *inv,
+                                                    fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i & (B - 1), cm = r * n + (i >> log_b);
+        out[i] = fe_mul(fe_add(ld_fe(ulde + cm), un[r]), ld_fe(inv + cm));
+    }
+}
+
+void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                       int log_b, const void *deep_consts_dev, const fe *coset_full, const fe *xn, const fe *inv_d,
+                       fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    const DeepConsts *D = (const DeepConsts *)deep_consts_dev;
+    fe *P = scratch, *Q = scratch + n, *U = scratch + 2 * n, *un = scratch + 3 * n;
+    unsigned blocks = cdiv(n, 256);
+    if (blocks > 65536) blocks = 65536;
+    ZK_PROF(st, "deep_combine", (16.0 * (28 + ccols) + 32.0) * n,
+            hipLaunchKernelGGL(k_deep_combine, dim3(blocks), dim3(256), 0, st, tpolys, cpolys, ccols, n, D, P, Q));
+    ZK_PROF(st, "deep_shift", 48.0 * n, hipLaunchKernelGGL(k_deep_shift, dim3(blocks), dim3(256), 0, st, P, Q, n, D, xn, (int)B, U, un));
+    // the B coset NTTs in launches of up to 8 (ntt_tmp holds 8n)
+    for (size_t r0 = 0; r0 < B; r0 += 8) {
+        PowTable cosets;
+        cosets.full = const_cast<fe *>(coset_full) + r0 * n;
+        ntt(st, Tn, U, 0, ulde + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets, nullptr, ntt_tmp, n);
+    }
+    unsigned pb = cdiv(N, 256);
+    if (pb > 65536) pb = 65536;
+    ZK_PROF(st, "deep", 48.0 * N, hipLaunchKernelGGL(k_deep_point, dim3(pb), dim3(256), 0, st, ulde, un, log_n, log_b, inv_d, out));
 }
 
 // ================================================================ FRI fold (K7)

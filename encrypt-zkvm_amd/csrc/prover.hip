@@ -125,14 +125,17 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + 3, &pl->Tce));
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + pl->log_b, &pl->TN));
     fe wN = h_root_of_unity(pl->log_n + pl->log_b), wce = h_root_of_unity(pl->log_n + 3);
-    std::vector<fe> xrN(B), xrce(8);
+    std::vector<fe> xrN(B), xrce(8), xnN(B);
     fe s = fe_make(3);
+    // full tables for the LDE pre-scale (B * n elements: 128 MiB at n = 2^20, B = 8), contiguous so
+    // one launch can run every coset (pre_stride n)
+    ZK_CHECK_HIP(p->arena.alloc(&pl->coset_full, (size_t)B * n));
     for (uint32_t r = 0; r < B; r++) {
         xrN[r] = s;
+        xnN[r] = h_pow(s, n);
         PowTable t;
         ZK_CHECK_HIP(make_pow_table(p, s, n, &t));
-        // full table for the LDE pre-scale (B * n elements: 128 MiB at n = 2^20, B = 8)
-        ZK_CHECK_HIP(p->arena.alloc(&t.full, n));
+        t.full = pl->coset_full + (size_t)r * n;
         pow_expand(p->st, t.lo, t.hi, n, t.full);
         pl->coset.push_back(t);
         s = fe_mul(s, wN);
@@ -143,6 +146,7 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
         s = fe_mul(s, wce);
     }
     ZK_CHECK_HIP(upload(p, &pl->xr_N, xrN));
+    ZK_CHECK_HIP(upload(p, &pl->xn_N, xnN));
     ZK_CHECK_HIP(upload(p, &pl->xr_ce, xrce));
     ZK_CHECK_HIP(make_pow_table(p, h_inv(fe_make(3)), n, &pl->inv3));
     ZK_CHECK_HIP(upload(p, &pl->periodic, periodic_table(n)));
@@ -195,6 +199,7 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * N));
     ZK_CHECK_HIP(A.alloc(&p->inv, std::max(N, CE)));
     ZK_CHECK_HIP(A.alloc(&p->deep, N));
+    ZK_CHECK_HIP(A.alloc(&p->ulde, N));
     // FRI layers: sum over layers of L/fold values and 2*L/fold digests; worst case fold = 2
     ZK_CHECK_HIP(A.alloc(&p->fri, N + 16));
     ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * N));
@@ -904,7 +909,9 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         batch_inv_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
-        deep_eval_launch(p->st, p->lde, log_n, log_b, clde, C, p->deep_consts, pl->TN, three, p->inv, deep);
+        // scratch: ctmp (3n + B; the composition iNTT output, dead after the cross-coset step)
+        deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, pl->coset_full, pl->xn_N,
+                          p->inv, p->ctmp, p->ulde, p->tmp, deep);
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
         fe_to_bytes(z.a, R.z);

@@ -69,7 +69,9 @@ struct DeviceArena {
 struct Plan {  // everything that depends only on (n, B)
     int log_n = 0, log_b = 0;
     NttTables Tn, Tce, TN;        // sizes n, 8n, B*n
-    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B
+    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B (full tables contiguous from coset_full)
+    fe *coset_full = nullptr;     // B x n: coset[r].full = coset_full + r * n
+    fe *xn_N = nullptr;           // (3 * w_N^r)^n, r < B: x^n on LDE coset r
     PowTable inv3;                // 3^-k, k < n
     fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)
     fe *periodic = nullptr;               // 128 x 9
@@ -90,6 +92,7 @@ struct zk_prover {
     zk::DeviceArena arena;
     fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
        *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
+    fe *ulde = nullptr;  // LDE of the DEEP numerator polynomial (B*n, coset-major)
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
     fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;

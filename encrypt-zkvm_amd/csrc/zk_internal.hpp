@@ -93,7 +93,7 @@ void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out);
 //   post_scale  : optional constant multiplied into every output (e.g. 1/n)
 // in and out must not alias.  tmp must hold batch * n elements when log_n > 12.
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride,
-         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp);
+         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, size_t pre_stride = 0);
 
 // grinding: atomicMin into *best_dev of the nonces in [start, start+count) with >= bits trailing zeros
 void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,
@@ -175,6 +175,12 @@ struct DeepConsts {
 };
 void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
                       const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
+// DEEP through coefficient form (kernels.hip): combine the trace and composition polynomials into the
+// numerator polynomial, LDE it over the B cosets (coset_full: B contiguous (3 w_N^r)^k tables, xn[r] =
+// (3 w_N^r)^n), divide point-wise.  scratch: 3n + B elements; ulde: B*n; ntt_tmp: 8n.
+void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                       int log_b, const void *deep_consts_dev, const fe *coset_full, const fe *xn, const fe *inv_d,
+                       fe *scratch, fe *ulde, fe *ntt_tmp, fe *out);
 // FRI fold: next[r] = p_r(alpha) over rows r < L/fold (consts: FoldConsts in device memory)
 struct FoldConsts {
     fe zinv[16];  // zeta^-t, t < fold
