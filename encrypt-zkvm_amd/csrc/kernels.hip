@@ -1182,71 +1182,189 @@ void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const
                                            (const DeepConsts *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi, three, inv_d, out));
 }
 
-// ---- DEEP through coefficient form.  With the shared trace coefficients alpha (z and zg terms) and
-// composition coefficients gamma, the DEEP numerator is one polynomial of degree n:
-//   num(x) = (x - zg)(S(x) - k1) + (x - z)(A(x) - k2),  A = sum alpha_i T_i,  S = A + sum gamma_j H_j
-//          = x (S + A)(x) - (zg S + z A)(x) - (k1 + k2) x + (k1 zg + k2 z)
-// so U = num has coefficients U_k = P_{k-1} - Q_k (P = S + A, Q = zg S + z A) plus the two constant
-// corrections, and U_n = P_{n-1}.  Its values on coset r are LDE(U_0..U_{n-1}) + U_n s_r^n (x^n = s_r^n
-// on the whole coset).  DEEP(x) = num(x) / ((x - z)(x - zg)) -- the same field values as summing the 35
-// LDE columns point by point, from one n-coefficient combination and one B-coset LDE: the 28 + 7 LDE
-// columns (3.7 GB at 2^20) are never read.
-__global__ void __launch_bounds__(256) k_deep_combine(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
-                                                      const DeepConsts *D, fe *P, fe *Q) {
-    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+// ---- DEEP through coefficient form.  The trace coefficients alpha are shared by the z and zg terms
+// and gamma weighs the composition columns, so with A = sum alpha_i T_i and S = A + sum gamma_j H_j
+// (k1 = S(z), k2 = A(zg) exactly, since the OOD values are evaluations of the same polynomials):
+//   DEEP(x) = (S(x) - S(z)) / (x - z) + (A(x) - A(zg)) / (x - zg)
+// is a polynomial of degree n - 2, and (F(x) - F(c)) / (x - c) has coefficients
+//   q_k = sum_{m > k} f_m c^(m-k-1) = c^-(k+1) * sum_{m > k} f_m c^m      (a suffix sum).
+// So: g1_m = S_m z^m, g2_m = A_m zg^m (one pass over the 28 + 7 coefficient columns), suffix sums
+// (block totals, one scan of the totals, local scans), D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k, and one
+// B-coset LDE of D gives the DEEP values: the same field values as the point-wise quotient of the 35
+// LDE columns, without reading those columns (3.7 GB at 2^20) or inverting 8n denominators.
+constexpr int DIV_T = 256, DIV_E = 8, DIV_CH = DIV_T * DIV_E;
+
+// base^e for e < 2048 (lo) and base^(2048 u) for u < H (hi), 4 bases: z, zg, 1/z, 1/zg
+struct DeepPowBases {
+    fe b[4];
+};
+__global__ void k_deep_pow_tables(DeepPowBases pb, size_t H, fe *out) {
+    const size_t per = 2048 + H;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= 4 * per) return;
+    const size_t b = t / per, e = t % per;
+    const uint64_t ex = e < 2048 ? e : 2048 * (uint64_t)(e - 2048);
+    out[t] = fe_exp(pb.b[b], ex, 0);
+}
+
+__device__ __forceinline__ fe block_sum256(fe v, fe *red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    fe r = red[0];
+    for (int i = 1; i < DIV_T / 64; i++) r = fe_add(r, red[i]);
+    __syncthreads();
+    return r;
+}
+
+// phase 1: g1, g2 and per-256 totals (one coefficient per thread)
+__global__ void __launch_bounds__(DIV_T) k_deep_div_g(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
+                                                     const DeepConsts *D, const fe *pw, size_t H, fe *g1, fe *g2,
+                                                     fe *bs) {
+    __shared__ fe red[DIV_T / 64];
+    const size_t per = 2048 + H;
+    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    fe v1 = fe_zero(), v2 = fe_zero();
+    if (k < n) {
         acc288 aA = acc288_zero(), aH = acc288_zero();
 #pragma unroll 4
         for (int c = 0; c < 28; c++) acc288_madd(aA, D->alpha_t[c], ld_fe(tpolys + (size_t)c * n + k));
         for (int j = 0; j < ccols; j++) acc288_madd(aH, D->alpha_c[j], ld_fe(cpolys + (size_t)j * n + k));
         const fe A = acc288_reduce(aA);
         const fe S = fe_add(A, acc288_reduce(aH));
-        P[k] = fe_add(S, A);
-        Q[k] = fe_add(fe_mul(D->zg, S), fe_mul(D->z, A));
+        v1 = fe_mul(S, pow_split(pw, pw + 2048, k));
+        v2 = fe_mul(A, pow_split(pw + per, pw + per + 2048, k));
+        g1[k] = v1;
+        g2[k] = v2;
+    }
+    v1 = block_sum256(v1, red);
+    v2 = block_sum256(v2, red);
+    if (threadIdx.x == 0) {
+        bs[2 * blockIdx.x] = v1;
+        bs[2 * blockIdx.x + 1] = v2;
     }
 }
 
-__global__ void __launch_bounds__(256) k_deep_shift(const fe *P, const fe *Q, size_t n, const DeepConsts *D,
-                                                    const fe *xn, int B, fe *U, fe *un) {
-    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-        fe u = fe_sub(k ? P[k - 1] : fe_zero(), Q[k]);
-        if (k == 0) u = fe_add(u, fe_add(fe_mul(D->k1, D->zg), fe_mul(D->k2, D->z)));
-        if (k == 1) u = fe_sub(u, fe_add(D->k1, D->k2));
-        U[k] = u;
-        if (k == 0)
-            for (int r = 0; r < B; r++) un[r] = fe_mul(P[n - 1], xn[r]);
+// phase 2 (one block): carry[j] = sum of the totals of blocks after j (exclusive suffix), both sums
+__global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
+    __shared__ fe t1[1024], t2[1024];
+    const int per = (nb + 1023) / 1024, lo = threadIdx.x * per, hi = min(lo + per, nb);
+    fe a = fe_zero(), b = fe_zero();
+    for (int j = lo; j < hi; j++) {
+        a = fe_add(a, bs[2 * j]);
+        b = fe_add(b, bs[2 * j + 1]);
+    }
+    t1[threadIdx.x] = a;
+    t2[threadIdx.x] = b;
+    __syncthreads();
+    // inclusive suffix scan over the 1024 thread totals (Hillis-Steele)
+    for (int d = 1; d < 1024; d <<= 1) {
+        fe x = t1[threadIdx.x], y = t2[threadIdx.x];
+        if (threadIdx.x + d < 1024) {
+            x = fe_add(x, t1[threadIdx.x + d]);
+            y = fe_add(y, t2[threadIdx.x + d]);
+        }
+        __syncthreads();
+        t1[threadIdx.x] = x;
+        t2[threadIdx.x] = y;
+        __syncthreads();
+    }
+    fe c1 = threadIdx.x + 1 < 1024 ? t1[threadIdx.x + 1] : fe_zero();
+    fe c2 = threadIdx.x + 1 < 1024 ? t2[threadIdx.x + 1] : fe_zero();
+    for (int j = hi - 1; j >= lo; j--) {  // exclusive suffix within this thread's entries
+        const fe x = bs[2 * j], y = bs[2 * j + 1];
+        bs[2 * j] = c1;
+        bs[2 * j + 1] = c2;
+        c1 = fe_add(c1, x);
+        c2 = fe_add(c2, y);
     }
 }
 
-// out[i] (natural order) = (ulde[coset-major i] + un[coset]) * inv[coset-major i]
-__global__ void __launch_bounds__(256) k_deep_point(const fe *ulde, const fe *un, int log_n, int log_b, const fe *inv,
-                                                    fe *out) {
+// phase 3: thread owns 8 consecutive coefficients; D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k
+__global__ void __launch_bounds__(DIV_T) k_deep_div_q(const fe *g1, const fe *g2, const fe *carry, int nb1, size_t n,
+                                                     fe z, fe zg, const fe *pw, size_t H, fe *Dk) {
+    __shared__ fe t1[DIV_T], t2[DIV_T];
+    const size_t per = 2048 + H;
+    const fe *ilo = pw + 2 * per, *ihi = ilo + 2048, *jlo = pw + 3 * per, *jhi = jlo + 2048;
+    const size_t k0 = blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
+    fe a[DIV_E], b[DIV_E];
+    fe s1 = fe_zero(), s2 = fe_zero();
+#pragma unroll
+    for (int e = 0; e < DIV_E; e++) {
+        const size_t k = k0 + e;
+        a[e] = k < n ? ld_fe(g1 + k) : fe_zero();
+        b[e] = k < n ? ld_fe(g2 + k) : fe_zero();
+        s1 = fe_add(s1, a[e]);
+        s2 = fe_add(s2, b[e]);
+    }
+    t1[threadIdx.x] = s1;
+    t2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int d = 1; d < DIV_T; d <<= 1) {
+        fe x = t1[threadIdx.x], y = t2[threadIdx.x];
+        if (threadIdx.x + d < DIV_T) {
+            x = fe_add(x, t1[threadIdx.x + d]);
+            y = fe_add(y, t2[threadIdx.x + d]);
+        }
+        __syncthreads();
+        t1[threadIdx.x] = x;
+        t2[threadIdx.x] = y;
+        __syncthreads();
+    }
+    // R = sum of g over m >= k0 + 8: later threads of this chunk + the phase-1 blocks after it
+    const int cb = min((int)blockIdx.x * (DIV_CH / DIV_T) + DIV_CH / DIV_T - 1, nb1 - 1);
+    fe r1 = fe_add(carry[2 * cb], threadIdx.x + 1 < DIV_T ? t1[threadIdx.x + 1] : fe_zero());
+    fe r2 = fe_add(carry[2 * cb + 1], threadIdx.x + 1 < DIV_T ? t2[threadIdx.x + 1] : fe_zero());
+    fe pz = pow_split(ilo, ihi, k0 + DIV_E), pg = pow_split(jlo, jhi, k0 + DIV_E);  // z^-(k+1) at k = k0 + 7
+#pragma unroll
+    for (int e = DIV_E - 1; e >= 0; e--) {
+        const size_t k = k0 + e;
+        if (k < n) Dk[k] = fe_add(fe_mul(pz, r1), fe_mul(pg, r2));
+        r1 = fe_add(r1, a[e]);
+        r2 = fe_add(r2, b[e]);
+        pz = fe_mul(pz, z);
+        pg = fe_mul(pg, zg);
+    }
+}
+
+// coset-major LDE -> natural order
+__global__ void __launch_bounds__(256) k_coset_to_natural(const fe *src, int log_n, int log_b, fe *out) {
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i & (B - 1), cm = r * n + (i >> log_b);
-        out[i] = fe_mul(fe_add(ld_fe(ulde + cm), un[r]), ld_fe(inv + cm));
-    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = ld_fe(src + (i & (B - 1)) * n + (i >> log_b));
 }
 
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                       int log_b, const void *deep_consts_dev, const fe *coset_full, const fe *xn, const fe *inv_d,
-                       fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
+                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
+                       fe *ulde, fe *ntt_tmp, fe *out) {
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
     const DeepConsts *D = (const DeepConsts *)deep_consts_dev;
-    fe *P = scratch, *Q = scratch + n, *U = scratch + 2 * n, *un = scratch + 3 * n;
-    unsigned blocks = cdiv(n, 256);
-    if (blocks > 65536) blocks = 65536;
+    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH;  // hi[] covers every t < nb * 2048 + 8
+    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *Dk = g2 + n, *bs = Dk + n;
+    DeepPowBases pb;
+    pb.b[0] = z;
+    pb.b[1] = zg;
+    pb.b[2] = fe_inv(z);
+    pb.b[3] = fe_inv(zg);
+    hipLaunchKernelGGL(k_deep_pow_tables, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, pw);
+    const size_t nb1 = (n + DIV_T - 1) / DIV_T;
     ZK_PROF(st, "deep_combine", (16.0 * (28 + ccols) + 32.0) * n,
-            hipLaunchKernelGGL(k_deep_combine, dim3(blocks), dim3(256), 0, st, tpolys, cpolys, ccols, n, D, P, Q));
-    ZK_PROF(st, "deep_shift", 48.0 * n, hipLaunchKernelGGL(k_deep_shift, dim3(blocks), dim3(256), 0, st, P, Q, n, D, xn, (int)B, U, un));
-    // the B coset NTTs in launches of up to 8 (ntt_tmp holds 8n)
+            hipLaunchKernelGGL(k_deep_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, cpolys, ccols, n, D, pw, H,
+                               g1, g2, bs));
+    hipLaunchKernelGGL(k_deep_div_scan, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
+    ZK_PROF(st, "deep_divide", 48.0 * n,
+            hipLaunchKernelGGL(k_deep_div_q, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw, H,
+                               Dk));
+    // the B coset LDEs of D in launches of up to 8 (ntt_tmp holds 8n)
     for (size_t r0 = 0; r0 < B; r0 += 8) {
         PowTable cosets;
         cosets.full = const_cast<fe *>(coset_full) + r0 * n;
-        ntt(st, Tn, U, 0, ulde + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets, nullptr, ntt_tmp, n);
+        ntt(st, Tn, Dk, 0, ulde + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets, nullptr, ntt_tmp, n);
     }
-    unsigned pb = cdiv(N, 256);
-    if (pb > 65536) pb = 65536;
-    ZK_PROF(st, "deep", 48.0 * N, hipLaunchKernelGGL(k_deep_point, dim3(pb), dim3(256), 0, st, ulde, un, log_n, log_b, inv_d, out));
+    unsigned pb2 = cdiv(N, 256);
+    if (pb2 > 65536) pb2 = 65536;
+    ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
 }
 
 // ================================================================ FRI fold (K7)

@@ -200,6 +200,7 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->inv, std::max(N, CE)));
     ZK_CHECK_HIP(A.alloc(&p->deep, N));
     ZK_CHECK_HIP(A.alloc(&p->ulde, N));
+    ZK_CHECK_HIP(A.alloc(&p->dscratch, 4 * (2048 + n / 2048 + 2) + 3 * n + 2 * (n / 256 + 1)));
     // FRI layers: sum over layers of L/fold values and 2*L/fold digests; worst case fold = 2
     ZK_CHECK_HIP(A.alloc(&p->fri, N + 16));
     ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * N));
@@ -908,10 +909,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         stage_mark(p, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-        batch_inv_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
-        // scratch: ctmp (3n + B; the composition iNTT output, dead after the cross-coset step)
-        deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, pl->coset_full, pl->xn_N,
-                          p->inv, p->ctmp, p->ulde, p->tmp, deep);
+        deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->coset_full,
+                          p->dscratch, p->ulde, p->tmp, deep);
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
         fe_to_bytes(z.a, R.z);

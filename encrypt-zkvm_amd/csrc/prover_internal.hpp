@@ -92,7 +92,8 @@ struct zk_prover {
     zk::DeviceArena arena;
     fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
        *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
-    fe *ulde = nullptr;  // LDE of the DEEP numerator polynomial (B*n, coset-major)
+    fe *ulde = nullptr;      // LDE of the DEEP polynomial (B*n, coset-major)
+    fe *dscratch = nullptr;  // DEEP division scratch (power tables, suffix-sum inputs, coefficients)
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
     fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;

@@ -175,12 +175,13 @@ struct DeepConsts {
 };
 void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
                       const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
-// DEEP through coefficient form (kernels.hip): combine the trace and composition polynomials into the
-// numerator polynomial, LDE it over the B cosets (coset_full: B contiguous (3 w_N^r)^k tables, xn[r] =
-// (3 w_N^r)^n), divide point-wise.  scratch: 3n + B elements; ulde: B*n; ntt_tmp: 8n.
+// DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
+// by suffix sums over the combined coefficients, one LDE over the B cosets (coset_full: B contiguous
+// (3 w_N^r)^k tables), natural-order output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
+// elements; ulde: B*n; ntt_tmp: 8n.
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                       int log_b, const void *deep_consts_dev, const fe *coset_full, const fe *xn, const fe *inv_d,
-                       fe *scratch, fe *ulde, fe *ntt_tmp, fe *out);
+                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
+                       fe *ulde, fe *ntt_tmp, fe *out);
 // FRI fold: next[r] = p_r(alpha) over rows r < L/fold (consts: FoldConsts in device memory)
 struct FoldConsts {
     fe zinv[16];  // zeta^-t, t < fold
