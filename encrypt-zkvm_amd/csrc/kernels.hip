@@ -1150,38 +1150,6 @@ void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *
 }
 
 // ================================================================ DEEP composition (K6)
-__global__ void __launch_bounds__(256) k_deep(const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                                              const DeepConsts *D, const fe *wN_lo, const fe *wN_hi, fe three,
-                                              const fe *inv_d, fe *out) {
-    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i & (B - 1), q = i >> log_b;
-        const fe *p = lde + r * n + q;
-        acc288 aT = acc288_zero();
-#pragma unroll 4
-        for (int c = 0; c < 28; c++) acc288_madd(aT, D->alpha_t[c], p[(size_t)c * B * n]);
-        const fe sT = acc288_reduce(aT);
-        const fe *pc = clde + r * n + q;
-        acc288 aH = acc288_zero();
-        for (int j = 0; j < ccols; j++) acc288_madd(aH, D->alpha_c[j], pc[(size_t)j * B * n]);
-        const fe sH = acc288_reduce(aH);
-        fe s1 = fe_sub(fe_add(sT, sH), D->k1);
-        fe s2 = fe_sub(sT, D->k2);
-        fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));
-        fe num = fe_add(fe_mul(s1, fe_sub(x, D->zg)), fe_mul(s2, fe_sub(x, D->z)));
-        out[i] = fe_mul(num, inv_d[r * n + q]);  // inverses are coset-major
-    }
-}
-
-void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                      const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out) {
-    size_t N = (size_t)1 << (log_n + log_b);
-    unsigned blocks = cdiv(N, 256);
-    if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "deep", (448.0 + 16.0 * ccols + 32.0) * N, hipLaunchKernelGGL(k_deep, dim3(blocks), dim3(256), 0, st, lde, log_n, log_b, clde, ccols,
-                                           (const DeepConsts *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi, three, inv_d, out));
-}
-
 // ---- DEEP through coefficient form.  The trace coefficients alpha are shared by the z and zg terms
 // and gamma weighs the composition columns, so with A = sum alpha_i T_i and S = A + sum gamma_j H_j
 // (k1 = S(z), k2 = A(zg) exactly, since the OOD values are evaluations of the same polynomials):

@@ -173,8 +173,6 @@ struct DeepConsts {
     fe alpha_c[16];
     fe k1, k2, z, zg;
 };
-void deep_eval_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                      const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
 // DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
 // by suffix sums over the combined coefficients, one LDE over the B cosets (coset_full: B contiguous
 // (3 w_N^r)^k tables), natural-order output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
