@@ -1335,6 +1335,40 @@ void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, co
     ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
 }
 
+// ================================================================ FRI transcript on the device
+// DefaultRandomCoin<Blake3_256> for the FRI commit phase without a host round trip per layer:
+// seed = merge(seed, root) (the layer root is nodes[1]), then draw: counter = 1, 2, ...,
+// merge_with_int(seed, counter) = BLAKE3(seed || counter_le64) until the first 16 bytes (k = 1) or
+// both 16-byte halves (k = 2) are canonical.  alpha goes to *alpha_out (the fold kernel's constants).
+// The host replays the same transcript from the downloaded roots (same alphas, checked).
+__device__ __forceinline__ bool fe_canon_dev(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+    return !(hi == ZK_P_HI && lo >= ZK_P_LO);
+}
+__global__ void k_fri_coin(uint32_t *seed, const uint8_t *root, int k, fe *alpha_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t s[8], r[8], h[8];
+    for (int i = 0; i < 8; i++) s[i] = seed[i];
+    load_digest(root, r);
+    b3::merge(s, r, h);
+    for (int i = 0; i < 8; i++) seed[i] = h[i];
+    for (uint32_t ctr = 1; ctr < 1000; ctr++) {
+        uint32_t m[16] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], ctr, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t d[8];
+        b3::iv(d);
+        b3::compress(d, m, 0, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+        if (fe_canon_dev(d[0], d[1], d[2], d[3]) && (k == 1 || fe_canon_dev(d[4], d[5], d[6], d[7]))) {
+            alpha_out[0] = fe{(uint64_t)d[0] | ((uint64_t)d[1] << 32), (uint64_t)d[2] | ((uint64_t)d[3] << 32)};
+            if (k == 2) alpha_out[1] = fe{(uint64_t)d[4] | ((uint64_t)d[5] << 32), (uint64_t)d[6] | ((uint64_t)d[7] << 32)};
+            return;
+        }
+    }
+}
+
+void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev, int k, fe *alpha_dev) {
+    hipLaunchKernelGGL(k_fri_coin, dim3(1), dim3(64), 0, st, seed_dev, root_dev, k, alpha_dev);
+}
+
 // ================================================================ FRI fold (K7)
 // next[r] = p_r(alpha), p_r of degree < fold interpolating the layer values at x_r * zeta^k:
 //   p_r(alpha) = (1/fold) * sum_m V_m (alpha / x_r)^m,  V_m = sum_k v_k zeta^(-k m)

@@ -217,6 +217,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->fold_consts, sizeof(FoldConsts)));
+    ZK_CHECK_HIP(A.alloc(&p->fri_seed, 32));
+    ZK_CHECK_HIP(A.alloc(&p->fri_alphas, 2 * ZK_MAX_FRI_LAYERS));
     *out = p.release();
     return ZK_OK;
 }
@@ -945,8 +947,21 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     layer_vals[0] = deep;
     layer_len[0] = N;
     {
+        // The layer coins run on the device (fri_coin_launch): no host round trip per layer.  The
+        // constant part of the fold constants is uploaded once; each layer's coin writes alpha into it.
         fe *next = fri;
         uint8_t *dig = p->fri_dig;
+        fe *alpha_dev = nullptr;
+        if (KX == 1) {
+            const FoldConsts F = fold_consts(fe_zero(), fold);
+            ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+            alpha_dev = &((FoldConsts *)p->fold_consts)->alpha;
+        } else {
+            const FoldConstsE F = fold_consts_ext(fe2_zero(), fold);
+            ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+            alpha_dev = &((FoldConstsE *)p->x_fold_consts)->alpha.a;
+        }
+        ZK_CHECK_HIP(hipMemcpyAsync(p->fri_seed, coin.seed, 32, hipMemcpyHostToDevice, p->st));
         for (int l = 0; l < nl; l++) {
             const size_t L = layer_len[l], rows = L / fold;
             layer_leaves[l] = dig;
@@ -954,30 +969,30 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             dig += 64 * rows;
             if (KX == 1) commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
             else commit_fri_layer_ext(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-            ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
-            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-            coin.reseed(R.fri_roots[l]);
-            if (KX == 1) {
-                const fe alpha = coin.draw();
-                fe_to_bytes(alpha, R.fri_alphas[l]);
-                const FoldConsts F = fold_consts(alpha, fold);
-                ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
-                fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
-            } else {
-                const fe2 alpha = coin.draw_ext(2);
-                fe_to_bytes(alpha.a, R.fri_alphas[l]);
-                const FoldConstsE F = fold_consts_ext(alpha, fold);
-                ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
-                fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
-            }
+            fri_coin_launch(p->st, (uint32_t *)p->fri_seed, layer_nodes[l] + 32, KX, alpha_dev);
+            ZK_CHECK_HIP(hipMemcpyAsync(p->fri_alphas + 2 * l, alpha_dev, KX * sizeof(fe), hipMemcpyDeviceToDevice, p->st));
+            if (KX == 1) fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
+            else fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
             layer_vals[l + 1] = next;
             layer_len[l + 1] = rows;
             next += KX * rows;
         }
+        // one round trip for the whole commit phase: roots, device alphas, the last layer
         const size_t L = layer_len[nl];
-        std::vector<fe> rv(KX * L);
+        std::vector<fe> rv(KX * L), dalpha(2 * nl);
+        for (int l = 0; l < nl; l++)
+            ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
+        if (nl) ZK_CHECK_HIP(hipMemcpyAsync(dalpha.data(), p->fri_alphas, 2 * nl * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        // host replay of the same transcript (it continues into the remainder, grinding and queries)
+        for (int l = 0; l < nl; l++) {
+            coin.reseed(R.fri_roots[l]);
+            const fe2 alpha = KX == 1 ? fe2{coin.draw(), fe_zero()} : coin.draw_ext(2);
+            fe_to_bytes(alpha.a, R.fri_alphas[l]);
+            if (!fe_eq(alpha.a, dalpha[2 * l]) || (KX == 2 && !fe_eq(alpha.b, dalpha[2 * l + 1])))
+                ZK_FAIL(ZK_ERR_DEVICE, "device FRI transcript diverged from the host transcript");
+        }
         if (KX == 1) ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
         else ZK_TRY(remainder_step_ext(rv, B, coin, R, degree_flag, rem_flat));
     }

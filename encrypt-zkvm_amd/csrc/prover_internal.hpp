@@ -99,6 +99,8 @@ struct zk_prover {
     uint64_t *gather_idx = nullptr;
     unsigned *flag = nullptr;
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
+    uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
+    fe *fri_alphas = nullptr;     // the alphas the device coin drew (2 per layer)
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
