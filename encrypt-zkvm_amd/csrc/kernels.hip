@@ -1214,39 +1214,43 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_g(const fe *tpolys, const fe
     }
 }
 
-// phase 2 (one block): carry[j] = sum of the totals of blocks after j (exclusive suffix), both sums
+// phase 2 (one block): carry[j] = sum of the totals of blocks after j (exclusive suffix), NC components
+// per block entry (2: the two sums over F; 4: the two sums over E)
+template <int NC>
 __global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
-    __shared__ fe t1[1024], t2[1024];
+    __shared__ fe t[NC][1024];
     const int per = (nb + 1023) / 1024, lo = threadIdx.x * per, hi = min(lo + per, nb);
-    fe a = fe_zero(), b = fe_zero();
-    for (int j = lo; j < hi; j++) {
-        a = fe_add(a, bs[2 * j]);
-        b = fe_add(b, bs[2 * j + 1]);
-    }
-    t1[threadIdx.x] = a;
-    t2[threadIdx.x] = b;
+    fe a[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) a[c] = fe_zero();
+    for (int j = lo; j < hi; j++)
+#pragma unroll
+        for (int c = 0; c < NC; c++) a[c] = fe_add(a[c], bs[NC * j + c]);
+#pragma unroll
+    for (int c = 0; c < NC; c++) t[c][threadIdx.x] = a[c];
     __syncthreads();
     // inclusive suffix scan over the 1024 thread totals (Hillis-Steele)
     for (int d = 1; d < 1024; d <<= 1) {
-        fe x = t1[threadIdx.x], y = t2[threadIdx.x];
-        if (threadIdx.x + d < 1024) {
-            x = fe_add(x, t1[threadIdx.x + d]);
-            y = fe_add(y, t2[threadIdx.x + d]);
+        fe x[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            x[c] = t[c][threadIdx.x];
+            if (threadIdx.x + d < 1024) x[c] = fe_add(x[c], t[c][threadIdx.x + d]);
         }
         __syncthreads();
-        t1[threadIdx.x] = x;
-        t2[threadIdx.x] = y;
+#pragma unroll
+        for (int c = 0; c < NC; c++) t[c][threadIdx.x] = x[c];
         __syncthreads();
     }
-    fe c1 = threadIdx.x + 1 < 1024 ? t1[threadIdx.x + 1] : fe_zero();
-    fe c2 = threadIdx.x + 1 < 1024 ? t2[threadIdx.x + 1] : fe_zero();
-    for (int j = hi - 1; j >= lo; j--) {  // exclusive suffix within this thread's entries
-        const fe x = bs[2 * j], y = bs[2 * j + 1];
-        bs[2 * j] = c1;
-        bs[2 * j + 1] = c2;
-        c1 = fe_add(c1, x);
-        c2 = fe_add(c2, y);
-    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) a[c] = threadIdx.x + 1 < 1024 ? t[c][threadIdx.x + 1] : fe_zero();
+    for (int j = hi - 1; j >= lo; j--)  // exclusive suffix within this thread's entries
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const fe x = bs[NC * j + c];
+            bs[NC * j + c] = a[c];
+            a[c] = fe_add(a[c], x);
+        }
 }
 
 // phase 3: thread owns 8 consecutive coefficients; D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k
@@ -1320,7 +1324,7 @@ void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, co
     ZK_PROF(st, "deep_combine", (16.0 * (28 + ccols) + 32.0) * n,
             hipLaunchKernelGGL(k_deep_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, cpolys, ccols, n, D, pw, H,
                                g1, g2, bs));
-    hipLaunchKernelGGL(k_deep_div_scan, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
+    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
     ZK_PROF(st, "deep_divide", 48.0 * n,
             hipLaunchKernelGGL(k_deep_div_q, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw, H,
                                Dk));
@@ -1333,6 +1337,146 @@ void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, co
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
+}
+
+// ---- the same over E (FieldExtension::Quadratic): alpha_t, alpha_c, z, zg are E values; the
+// composition column c is the E polynomial P_c0 + X P_c1 (base columns 2c, 2c + 1).  D is E-valued:
+// its two base planes are LDE'd separately and written planar (a plane, then b plane).
+struct DeepPowBasesE {
+    fe2 b[4];
+};
+__global__ void k_deep_pow_tables_ext(DeepPowBasesE pb, size_t H, fe2 *out) {
+    const size_t per = 2048 + H;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= 4 * per) return;
+    const size_t b = t / per, e = t % per;
+    out[t] = fe2_exp(pb.b[b], e < 2048 ? e : 2048 * (uint64_t)(e - 2048));
+}
+__device__ __forceinline__ fe2 pow_split2(const fe2 *lo, const fe2 *hi, size_t t) {
+    return fe2_mul(lo[t & 2047], hi[t >> 11]);
+}
+
+__global__ void __launch_bounds__(DIV_T) k_deep_div_g_ext(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
+                                                         const DeepConstsE *D, const fe2 *pw, size_t H, fe2 *g1,
+                                                         fe2 *g2, fe *bs) {
+    __shared__ fe red[DIV_T / 64];
+    const size_t per = 2048 + H;
+    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    fe2 v1 = fe2_zero(), v2 = fe2_zero();
+    if (k < n) {
+        acc288 aA = acc288_zero(), aB = acc288_zero();
+#pragma unroll 4
+        for (int c = 0; c < 28; c++) {
+            const fe v = ld_fe(tpolys + (size_t)c * n + k);
+            acc288_madd(aA, D->alpha_t[c].a, v);
+            acc288_madd(aB, D->alpha_t[c].b, v);
+        }
+        acc288 hA = acc288_zero(), hB = acc288_zero();
+        for (int j = 0; j < ccols; j++) {
+            const fe h0 = ld_fe(cpolys + (size_t)(2 * j) * n + k), h1 = ld_fe(cpolys + (size_t)(2 * j + 1) * n + k);
+            const fe2 ac = D->alpha_c[j];
+            acc288_madd(hA, ac.a, h0);  // (ac.a + ac.b X)(h0 + h1 X) = (ac.a h0 + ac.b h1) + (ac.a h1 + ac.b (h0 + h1)) X
+            acc288_madd(hA, ac.b, h1);
+            acc288_madd(hB, ac.a, h1);
+            acc288_madd(hB, ac.b, fe_add(h0, h1));
+        }
+        const fe2 A = fe2{acc288_reduce(aA), acc288_reduce(aB)};
+        const fe2 S = fe2_add(A, fe2{acc288_reduce(hA), acc288_reduce(hB)});
+        v1 = fe2_mul(S, pow_split2(pw, pw + 2048, k));
+        v2 = fe2_mul(A, pow_split2(pw + per, pw + per + 2048, k));
+        g1[k] = v1;
+        g2[k] = v2;
+    }
+    const fe s0 = block_sum256(v1.a, red), s1 = block_sum256(v1.b, red), s2 = block_sum256(v2.a, red),
+             s3 = block_sum256(v2.b, red);
+    if (threadIdx.x == 0) {
+        bs[4 * blockIdx.x] = s0;
+        bs[4 * blockIdx.x + 1] = s1;
+        bs[4 * blockIdx.x + 2] = s2;
+        bs[4 * blockIdx.x + 3] = s3;
+    }
+}
+
+__global__ void __launch_bounds__(DIV_T) k_deep_div_q_ext(const fe2 *g1, const fe2 *g2, const fe *carry, int nb1,
+                                                         size_t n, fe2 z, fe2 zg, const fe2 *pw, size_t H, fe *Da,
+                                                         fe *Db) {
+    __shared__ fe2 t1[DIV_T], t2[DIV_T];
+    const size_t per = 2048 + H;
+    const fe2 *ilo = pw + 2 * per, *ihi = ilo + 2048, *jlo = pw + 3 * per, *jhi = jlo + 2048;
+    const size_t k0 = blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
+    fe2 s1 = fe2_zero(), s2 = fe2_zero();
+    for (int e = 0; e < DIV_E; e++) {
+        const size_t k = k0 + e;
+        if (k < n) {
+            s1 = fe2_add(s1, g1[k]);
+            s2 = fe2_add(s2, g2[k]);
+        }
+    }
+    t1[threadIdx.x] = s1;
+    t2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int d = 1; d < DIV_T; d <<= 1) {
+        fe2 x = t1[threadIdx.x], y = t2[threadIdx.x];
+        if (threadIdx.x + d < DIV_T) {
+            x = fe2_add(x, t1[threadIdx.x + d]);
+            y = fe2_add(y, t2[threadIdx.x + d]);
+        }
+        __syncthreads();
+        t1[threadIdx.x] = x;
+        t2[threadIdx.x] = y;
+        __syncthreads();
+    }
+    const int cb = min((int)blockIdx.x * (DIV_CH / DIV_T) + DIV_CH / DIV_T - 1, nb1 - 1);
+    fe2 r1 = fe2_add(fe2{carry[4 * cb], carry[4 * cb + 1]}, threadIdx.x + 1 < DIV_T ? t1[threadIdx.x + 1] : fe2_zero());
+    fe2 r2 = fe2_add(fe2{carry[4 * cb + 2], carry[4 * cb + 3]}, threadIdx.x + 1 < DIV_T ? t2[threadIdx.x + 1] : fe2_zero());
+    fe2 pz = pow_split2(ilo, ihi, k0 + DIV_E), pg = pow_split2(jlo, jhi, k0 + DIV_E);
+    for (int e = DIV_E - 1; e >= 0; e--) {
+        const size_t k = k0 + e;
+        if (k < n) {
+            const fe2 d = fe2_add(fe2_mul(pz, r1), fe2_mul(pg, r2));
+            Da[k] = d.a;
+            Db[k] = d.b;
+            r1 = fe2_add(r1, g1[k]);
+            r2 = fe2_add(r2, g2[k]);
+        }
+        pz = fe2_mul(pz, z);
+        pg = fe2_mul(pg, zg);
+    }
+}
+
+void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
+                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
+                           fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    const DeepConstsE *D = (const DeepConstsE *)deep_consts_dev;
+    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH, nb1 = (n + DIV_T - 1) / DIV_T;
+    fe2 *pw = (fe2 *)scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n;
+    fe *Da = (fe *)(g2 + n), *Db = Da + n, *bs = Db + n;
+    DeepPowBasesE pb;
+    pb.b[0] = z;
+    pb.b[1] = zg;
+    pb.b[2] = fe2_inv(z);
+    pb.b[3] = fe2_inv(zg);
+    hipLaunchKernelGGL(k_deep_pow_tables_ext, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, pw);
+    ZK_PROF(st, "deep_combine", (16.0 * (28 + 2 * ccols) + 64.0) * n,
+            hipLaunchKernelGGL(k_deep_div_g_ext, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, cpolys, ccols, n, D, pw,
+                               H, g1, g2, bs));
+    hipLaunchKernelGGL(k_deep_div_scan<4>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
+    ZK_PROF(st, "deep_divide", 96.0 * n,
+            hipLaunchKernelGGL(k_deep_div_q_ext, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg,
+                               pw, H, Da, Db));
+    for (int plane = 0; plane < 2; plane++)
+        for (size_t r0 = 0; r0 < B; r0 += 8) {
+            PowTable cosets;
+            cosets.full = const_cast<fe *>(coset_full) + r0 * n;
+            ntt(st, Tn, plane ? Db : Da, 0, ulde + plane * N + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets,
+                nullptr, ntt_tmp, n);
+        }
+    unsigned pb2 = cdiv(N, 256);
+    if (pb2 > 65536) pb2 = 65536;
+    for (int plane = 0; plane < 2; plane++)
+        ZK_PROF(st, "deep", 32.0 * N,
+                hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde + plane * N, log_n, log_b, out + plane * N));
 }
 
 // ================================================================ FRI transcript on the device
@@ -1571,59 +1715,6 @@ void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int
     const fe zb2 = fe_mul(z.b, z.b), zgb2 = fe_mul(zg.b, zg.b);
     ZK_PROF(st, "batch_inv_ext", 16.0 * N, hipLaunchKernelGGL(k_batch_inv_norm_pairs, dim3(cdiv(threads, 256)), dim3(256), 0, st, xr,
                                                     log_b, log_n, Tn.fwd_lo, Tn.fwd_hi, z, zg, zb2, zgb2, out, threads));
-}
-
-// DEEP over E at x (natural index i):
-//   s1 = sum_c at_c T_c(x) + sum_j ac_j H_j(x) - k1,  s2 = sum_c at_c T_c(x) - k2
-//   deep = s1 / (x - z) + s2 / (x - zg) = (s1 u1 d2 + s2 u2 d1) / (d1 d2)
-// with (x - z)^-1 = u1 / d1, u1 = (x - z.a - z.b) + z.b X, d1 = N(x - z).
-__global__ void __launch_bounds__(256) k_deep_ext(const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                                                  const DeepConstsE *D, const fe *wN_lo, const fe *wN_hi, fe three,
-                                                  const fe *inv_d, fe *out) {
-    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i & (B - 1), q = i >> log_b;
-        const fe *p = lde + r * n + q;
-        acc288 aA = acc288_zero(), aB = acc288_zero();
-#pragma unroll 4
-        for (int c = 0; c < 28; c++) {
-            const fe v = p[(size_t)c * B * n];
-            acc288_madd(aA, D->alpha_t[c].a, v);
-            acc288_madd(aB, D->alpha_t[c].b, v);
-        }
-        const fe2 sT = fe2{acc288_reduce(aA), acc288_reduce(aB)};
-        const fe *pc = clde + r * n + q;
-        acc288 hA = acc288_zero(), hB = acc288_zero();
-        for (int j = 0; j < ccols; j++) {
-            const fe h0 = pc[(size_t)(2 * j) * B * n], h1 = pc[(size_t)(2 * j + 1) * B * n];
-            const fe2 ac = D->alpha_c[j];
-            acc288_madd(hA, ac.a, h0);  // (ac.a + ac.b X)(h0 + h1 X) = (ac.a h0 + ac.b h1) + (ac.a h1 + ac.b (h0 + h1)) X
-            acc288_madd(hA, ac.b, h1);
-            acc288_madd(hB, ac.a, h1);
-            acc288_madd(hB, ac.b, fe_add(h0, h1));
-        }
-        const fe2 sH = fe2{acc288_reduce(hA), acc288_reduce(hB)};
-        const fe2 s1 = fe2_sub(fe2_add(sT, sH), D->k1), s2 = fe2_sub(sT, D->k2);
-        const fe x = fe_mul(three, pow_split(wN_lo, wN_hi, i));
-        const fe xa = fe_sub(x, D->z.a), ga = fe_sub(x, D->zg.a);
-        const fe u1 = fe_sub(xa, D->z.b), u2 = fe_sub(ga, D->zg.b);
-        const fe d1 = fe_sub(fe_mul(xa, u1), D->zb2), d2 = fe_sub(fe_mul(ga, u2), D->zgb2);
-        const fe2 t1 = fe2_mul(s1, fe2{u1, D->z.b}), t2 = fe2_mul(s2, fe2{u2, D->zg.b});
-        const fe2 num = fe2_add(fe2_mulb(t1, d2), fe2_mulb(t2, d1));
-        const fe2 res = fe2_mulb(num, inv_d[r * n + q]);
-        out[i] = res.a;
-        out[N + i] = res.b;
-    }
-}
-
-void deep_eval_ext_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                          const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out) {
-    const size_t N = (size_t)1 << (log_n + log_b);
-    unsigned blocks = cdiv(N, 256);
-    if (blocks > 65536) blocks = 65536;
-    ZK_PROF(st, "deep_ext", (448.0 + 32.0 * ccols + 48.0) * N, hipLaunchKernelGGL(k_deep_ext, dim3(blocks), dim3(256), 0, st, lde, log_n, log_b,
-                                                   clde, ccols, (const DeepConstsE *)deep_consts_dev, TN.fwd_lo, TN.fwd_hi,
-                                                   three, inv_d, out));
 }
 
 // FRI row r over E: [e(r + k rows)]_k, each value hashed as (a, b)

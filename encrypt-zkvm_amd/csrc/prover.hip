@@ -814,6 +814,8 @@ int zk::ensure_ext(zk_prover *p) {
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_air, 2 * sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_deep_consts, sizeof(DeepConstsE)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_fold_consts, sizeof(FoldConstsE)));
+    ZK_CHECK_HIP(A.alloc(&p->x_ulde, 2 * N));
+    ZK_CHECK_HIP(A.alloc(&p->x_dscratch, 8 * (2048 + n / 2048 + 2) + 6 * n + 4 * (n / 256 + 1)));
     return ZK_OK;
 }
 
@@ -926,8 +928,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         stage_mark(p, "ood");
         const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-        batch_inv_norm_pairs(p->st, pl->Tn, pl->xr_N, log_b, log_n, z, zg, p->inv);
-        deep_eval_ext_launch(p->st, p->lde, log_n, log_b, clde, C, p->x_deep_consts, pl->TN, three, p->inv, deep);
+        deep_coeff_ext_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->x_deep_consts, z, zg,
+                              pl->coset_full, p->x_dscratch, p->x_ulde, p->tmp, deep);
     }
     stage_mark(p, "deep");
 

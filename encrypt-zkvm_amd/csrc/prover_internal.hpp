@@ -94,6 +94,7 @@ struct zk_prover {
        *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
     fe *ulde = nullptr;      // LDE of the DEEP polynomial (B*n, coset-major)
     fe *dscratch = nullptr;  // DEEP division scratch (power tables, suffix-sum inputs, coefficients)
+    fe *x_ulde = nullptr, *x_dscratch = nullptr;  // the same for FieldExtension::Quadratic
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
     fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;

@@ -180,6 +180,11 @@ struct DeepConsts {
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
                        int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
                        fe *ulde, fe *ntt_tmp, fe *out);
+// the same over E (FieldExtension::Quadratic; DeepConstsE): scratch 8 (2048 + n/2048 + 2) + 6n + 4 ceil(n/256)
+// elements; ulde: 2*B*n; out planar (2N)
+void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
+                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
+                           fe *scratch, fe *ulde, fe *ntt_tmp, fe *out);
 // FRI fold: next[r] = p_r(alpha) over rows r < L/fold (consts: FoldConsts in device memory)
 struct FoldConsts {
     fe zinv[16];  // zeta^-t, t < fold
@@ -214,9 +219,6 @@ struct DeepConstsE {
     fe2 k1, k2, z, zg;
     fe zb2, zgb2;  // z.b^2, zg.b^2
 };
-// DEEP over E: ccols E columns = base columns (2j, 2j+1) of clde; out planar (2N)
-void deep_eval_ext_launch(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *clde, int ccols,
-                          const void *deep_consts_dev, const NttTables &TN, fe three, const fe *inv_d, fe *out);
 struct FoldConstsE {
     fe zinv[16];
     fe2 alpha;
