@@ -1307,10 +1307,20 @@ __global__ void __launch_bounds__(256) k_coset_to_natural(const fe *src, int log
         out[i] = ld_fe(src + (i & (B - 1)) * n + (i >> log_b));
 }
 
-void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
-                       fe *ulde, fe *ntt_tmp, fe *out) {
-    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+// LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j: out[j*n ..] (coset-major)
+void lde_cosets(hipStream_t st, const NttTables &Tn, const fe *coeffs, size_t n, const fe *coset_full, size_t r0,
+                size_t stride, int count, fe *out, fe *ntt_tmp) {
+    for (int j0 = 0; j0 < count; j0 += 8) {  // launches of up to 8 cosets (ntt_tmp holds 8n)
+        PowTable cosets;
+        cosets.full = const_cast<fe *>(coset_full) + (r0 + stride * j0) * n;
+        ntt(st, Tn, coeffs, 0, out + (size_t)j0 * n, n, std::min(8, count - j0), false, &cosets, nullptr, ntt_tmp,
+            stride * n);
+    }
+}
+
+const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                    const void *deep_consts_dev, fe z, fe zg, fe *scratch) {
+    const size_t n = (size_t)1 << log_n;
     const DeepConsts *D = (const DeepConsts *)deep_consts_dev;
     const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH;  // hi[] covers every t < nb * 2048 + 8
     fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *Dk = g2 + n, *bs = Dk + n;
@@ -1328,12 +1338,15 @@ void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, co
     ZK_PROF(st, "deep_divide", 48.0 * n,
             hipLaunchKernelGGL(k_deep_div_q, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw, H,
                                Dk));
-    // the B coset LDEs of D in launches of up to 8 (ntt_tmp holds 8n)
-    for (size_t r0 = 0; r0 < B; r0 += 8) {
-        PowTable cosets;
-        cosets.full = const_cast<fe *>(coset_full) + r0 * n;
-        ntt(st, Tn, Dk, 0, ulde + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets, nullptr, ntt_tmp, n);
-    }
+    return Dk;
+}
+
+void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
+                       fe *ulde, fe *ntt_tmp, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    const fe *Dk = deep_poly(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
+    lde_cosets(st, Tn, Dk, n, coset_full, 0, 1, (int)B, ulde, ntt_tmp);
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
@@ -1444,10 +1457,9 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_q_ext(const fe2 *g1, const f
     }
 }
 
-void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
-                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
-                           fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
-    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                        const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch) {
+    const size_t n = (size_t)1 << log_n;
     const DeepConstsE *D = (const DeepConstsE *)deep_consts_dev;
     const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH, nb1 = (n + DIV_T - 1) / DIV_T;
     fe2 *pw = (fe2 *)scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n;
@@ -1465,13 +1477,15 @@ void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys
     ZK_PROF(st, "deep_divide", 96.0 * n,
             hipLaunchKernelGGL(k_deep_div_q_ext, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg,
                                pw, H, Da, Db));
-    for (int plane = 0; plane < 2; plane++)
-        for (size_t r0 = 0; r0 < B; r0 += 8) {
-            PowTable cosets;
-            cosets.full = const_cast<fe *>(coset_full) + r0 * n;
-            ntt(st, Tn, plane ? Db : Da, 0, ulde + plane * N + r0 * n, n, (int)std::min<size_t>(8, B - r0), false, &cosets,
-                nullptr, ntt_tmp, n);
-        }
+    return Da;  // planes Da, Da + n
+}
+
+void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
+                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
+                           fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
+    const fe *Dk = deep_poly_ext(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
+    for (int plane = 0; plane < 2; plane++) lde_cosets(st, Tn, Dk + plane * n, n, coset_full, 0, 1, (int)B, ulde + plane * N, ntt_tmp);
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     for (int plane = 0; plane < 2; plane++)

@@ -119,31 +119,6 @@ __global__ void k_sh_pack(const fe *c, int log_n, int Bl, int log_kg, fe *send) 
     send[((((k >> log_kg) * Bl) + j) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[t];
 }
 
-// DEEP composition over the local cosets: out[j*n + q] at natural LDE index i = (g + G*j) + 8*q
-__global__ void __launch_bounds__(256) k_sh_deep(const fe *lde, int log_n, int Bl, int g, int G, const fe *clde,
-                                                 int ccols, const DeepConsts *D, const fe *wN_lo, const fe *wN_hi,
-                                                 fe three, const fe *inv_d, fe *out) {
-    const size_t n = (size_t)1 << log_n;
-    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << log_n)) return;
-    const size_t j = t >> log_n, q = t & (n - 1);
-    const size_t i = (size_t)(g + G * (int)j) + 8 * q;
-    const size_t cs = (size_t)Bl * n;
-    const fe *p = lde + j * n + q;
-    acc288 aT = acc288_zero();
-#pragma unroll 4
-    for (int c = 0; c < 28; c++) acc288_madd(aT, D->alpha_t[c], p[(size_t)c * cs]);
-    const fe sT = acc288_reduce(aT);
-    const fe *pc = clde + j * n + q;
-    acc288 aH = acc288_zero();
-    for (int k = 0; k < ccols; k++) acc288_madd(aH, D->alpha_c[k], pc[(size_t)k * cs]);
-    const fe sH = acc288_reduce(aH);
-    const fe s1 = fe_sub(fe_add(sT, sH), D->k1), s2 = fe_sub(sT, D->k2);
-    const fe x = fe_mul(three, fe_mul(wN_lo[i & 2047], wN_hi[i >> 11]));
-    const fe num = fe_add(fe_mul(s1, fe_sub(x, D->zg)), fe_mul(s2, fe_sub(x, D->z)));
-    out[t] = fe_mul(num, inv_d[t]);
-}
-
 // first FRI fold over the local cosets: row r' = r + 8*q0 (values deep[j][q0 + k*m]) -> out[j*m + q0]
 __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n, int Bl, int g, int G, int fold,
                                                       int log_m, const FoldConsts *F, const fe *wi_lo,
@@ -166,45 +141,6 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
 }
 
 // ---- FieldExtension::Quadratic versions: E buffers are planar with plane stride Bl*n (DEEP) / Bl*m (fold)
-__global__ void __launch_bounds__(256) k_sh_deep_ext(const fe *lde, int log_n, int Bl, int g, int G, const fe *clde,
-                                                     int ccols, const DeepConstsE *D, const fe *wN_lo, const fe *wN_hi,
-                                                     fe three, const fe *inv_d, fe *out) {
-    const size_t n = (size_t)1 << log_n, cs = (size_t)Bl * n;
-    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= cs) return;
-    const size_t j = t >> log_n, q = t & (n - 1);
-    const size_t i = (size_t)(g + G * (int)j) + 8 * q;
-    const fe *p = lde + j * n + q;
-    acc288 aA = acc288_zero(), aB = acc288_zero();
-#pragma unroll 4
-    for (int c = 0; c < 28; c++) {
-        const fe v = p[(size_t)c * cs];
-        acc288_madd(aA, D->alpha_t[c].a, v);
-        acc288_madd(aB, D->alpha_t[c].b, v);
-    }
-    const fe2 sT = fe2{acc288_reduce(aA), acc288_reduce(aB)};
-    const fe *pc = clde + j * n + q;
-    acc288 hA = acc288_zero(), hB = acc288_zero();
-    for (int k = 0; k < ccols; k++) {  // E column k = base columns (2k, 2k+1)
-        const fe h0 = pc[(size_t)(2 * k) * cs], h1 = pc[(size_t)(2 * k + 1) * cs];
-        const fe2 ac = D->alpha_c[k];
-        acc288_madd(hA, ac.a, h0);
-        acc288_madd(hA, ac.b, h1);
-        acc288_madd(hB, ac.a, h1);
-        acc288_madd(hB, ac.b, fe_add(h0, h1));
-    }
-    const fe2 sH = fe2{acc288_reduce(hA), acc288_reduce(hB)};
-    const fe2 s1 = fe2_sub(fe2_add(sT, sH), D->k1), s2 = fe2_sub(sT, D->k2);
-    const fe x = fe_mul(three, fe_mul(wN_lo[i & 2047], wN_hi[i >> 11]));
-    const fe xa = fe_sub(x, D->z.a), ga = fe_sub(x, D->zg.a);
-    const fe u1 = fe_sub(xa, D->z.b), u2 = fe_sub(ga, D->zg.b);
-    const fe d1 = fe_sub(fe_mul(xa, u1), D->zb2), d2 = fe_sub(fe_mul(ga, u2), D->zgb2);
-    const fe2 num = fe2_add(fe2_mulb(fe2_mul(s1, fe2{u1, D->z.b}), d2), fe2_mulb(fe2_mul(s2, fe2{u2, D->zg.b}), d1));
-    const fe2 res = fe2_mulb(num, inv_d[t]);
-    out[t] = res.a;
-    out[cs + t] = res.b;
-}
-
 __global__ void __launch_bounds__(256) k_sh_hash_fri0_ext(const fe *deep, int log_n, int Bl, int fold, int log_m,
                                                           int log_mg, uint8_t *send) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n;
@@ -507,10 +443,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-            batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
-            hipLaunchKernelGGL(k_sh_deep, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl,
-                               X.rank[l], G, p->clde, C, (const DeepConsts *)p->deep_consts, pl->TN.fwd_lo,
-                               pl->TN.fwd_hi, three, p->inv, p->deep);
+            // DEEP as an exact polynomial (kernels.hip): replicated coefficients, local cosets g + G j
+            const fe *Dk = deep_poly(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch);
+            lde_cosets(p->st, pl->Tn, Dk, n, pl->coset_full, X.rank[l], G, Bl, p->deep, p->tmp);
         }
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
@@ -529,10 +464,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-            batch_inv_norm_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, z, zg, p->inv);
-            hipLaunchKernelGGL(k_sh_deep_ext, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, log_n, Bl,
-                               X.rank[l], G, p->x_clde, C, (const DeepConstsE *)p->x_deep_consts, pl->TN.fwd_lo,
-                               pl->TN.fwd_hi, three, p->inv, p->x_deep);
+            const fe *Dk = deep_poly_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch);
+            for (int plane = 0; plane < 2; plane++)  // planar per rank: plane stride Bl * n
+                lde_cosets(p->st, pl->Tn, Dk + plane * n, n, pl->coset_full, X.rank[l], G, Bl,
+                           p->x_deep + (size_t)plane * Bl * n, p->tmp);
         }
     }
     stage_mark(P0, "deep");

@@ -173,6 +173,15 @@ struct DeepConsts {
     fe alpha_c[16];
     fe k1, k2, z, zg;
 };
+// LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j (coset_full: B contiguous
+// (3 w_N^r)^k tables): out[j*n ..], coset-major.  ntt_tmp: 8n.
+void lde_cosets(hipStream_t st, const NttTables &Tn, const fe *coeffs, size_t n, const fe *coset_full, size_t r0,
+                size_t stride, int count, fe *out, fe *ntt_tmp);
+// The DEEP polynomial's coefficients (n; over E two planes of n) computed into scratch (returned)
+const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                    const void *deep_consts_dev, fe z, fe zg, fe *scratch);
+const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                        const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch);
 // DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
 // by suffix sums over the combined coefficients, one LDE over the B cosets (coset_full: B contiguous
 // (3 w_N^r)^k tables), natural-order output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
