@@ -86,7 +86,9 @@ struct Lds {
 };
 
 // One radix-4 round (stages lg, lg+1), compile-time lg so every shift and mask is an immediate.
-template <int LOGM, int TILE, int LG>
+// CT (coset-table mode): tw is a per-line-set stage table, tw[h + j] = the stage twiddle for half-size h
+// and butterfly index j (a DFT evaluated on a coset c<w_M>: c^(M/2h) w_2h^j), instead of w_4096 powers.
+template <int LOGM, int TILE, int LG, bool CT>
 __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
@@ -97,9 +99,9 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
         const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
         const int j = local & (h - 1), grp = local >> (LG - 1);
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
-        const fe w1 = tw4096[j << (12 - LG)];
-        const fe w2 = tw4096[j << (11 - LG)];
-        const fe w3 = tw4096[(j + h) << (11 - LG)];
+        const fe w1 = CT ? tw4096[h + j] : tw4096[j << (12 - LG)];
+        const fe w2 = CT ? tw4096[2 * h + j] : tw4096[j << (11 - LG)];
+        const fe w3 = CT ? tw4096[3 * h + j] : tw4096[(j + h) << (11 - LG)];
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
         const fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
         const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
@@ -113,11 +115,11 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
 }
 
 // rounds LG, LG+2, ... while LG + 1 <= LOGM, then the trailing radix-2 stage of an odd LOGM
-template <int LOGM, int TILE, int LG>
+template <int LOGM, int TILE, int LG, bool CT>
 __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
     if constexpr (LG + 1 <= LOGM) {
-        r4_round<LOGM, TILE, LG>(s, tw4096);
-        r4_rounds<LOGM, TILE, LG + 2>(s, tw4096);
+        r4_round<LOGM, TILE, LG, CT>(s, tw4096);
+        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096);
     } else if constexpr (LG == LOGM) {
         constexpr int M = 1 << LOGM;
         constexpr int half = 1 << (LG - 1);
@@ -127,7 +129,7 @@ __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
             const int line = bf >> (LOGM - 1), local = bf & (M / 2 - 1);
             const int j = local & (half - 1), grp = local >> (LG - 1);
             const int i0 = L::idx(line, grp * 2 * half + j), i1 = L::at(i0, half);
-            const fe w = tw4096[j << (12 - LG)];  // w_len^j = w_4096^(j * 4096/len)
+            const fe w = CT ? tw4096[half + j] : tw4096[j << (12 - LG)];  // w_len^j = w_4096^(j * 4096/len)
             const fe u = s[i0];
             const fe v = fe_mul(s[i1], w);
             s[i0] = fe_add(u, v);
@@ -146,11 +148,14 @@ __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
 // Inlined into each kernel: `s` stays an LDS pointer (ds_read/ds_write) and the twiddle table a
 // global one (global_load, counted by vmcnt only; as a called function both were flat accesses
 // and every LDS wait also waited for the twiddle loads).
-template <int LOGM, int TILE>
+// CT: coset-table mode (every round generic, the first one included: 4 multiplies per 4 points).
+template <int LOGM, int TILE, bool CT = false>
 __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
-    if constexpr (LOGM >= 2) {
+    if constexpr (CT) {
+        r4_rounds<LOGM, TILE, 1, true>(s, tw4096);
+    } else if constexpr (LOGM >= 2) {
         const fe w4 = tw4096[1024];
         using L = Lds<LOGM, TILE>;
 #pragma unroll
@@ -166,9 +171,9 @@ __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096) {
             s[p3] = fe_sub(a1, a3);
         }
         __syncthreads();
-        r4_rounds<LOGM, TILE, 3>(s, tw4096);
+        r4_rounds<LOGM, TILE, 3, false>(s, tw4096);
     } else {
-        r4_rounds<LOGM, TILE, 1>(s, tw4096);
+        r4_rounds<LOGM, TILE, 1, false>(s, tw4096);
     }
 }
 
@@ -187,11 +192,19 @@ struct NttArgs {
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
     const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
     const fe *pre_full;           // ... or the same from a full table (preferred when present)
-    size_t pre_stride;            // batch entry b uses pre_full + b * pre_stride (0: one table for all)
+    size_t pre_stride;            // coset r uses pre_full + r * pre_stride
     const fe *pass_tw;            // inter-pass twiddles [k1 * n2 + j2] (replaces big_lo/hi when present)
     fe post;                      // post-scale constant
     int has_post;
     int log_n;
+    // batch entry b = column c * ncos + coset slot j (coset r = cos_r0 + j * cos_rstride): input column c at
+    // in + c * in_stride, output at out + c * out_stride + j * out_jstride.  ncos = 1 for plain batches.
+    int ncos, cos_r0, cos_rstride;
+    size_t out_jstride;
+    const fe *cos_stage;  // coset LDE (four-step): per-coset stage tables, 4096 apart (CosetTables::stage)
+    const fe *cos_pass;   // ... and per-coset pass-1 twiddles (s_r w_n^j2)^k1, n apart (CosetTables::pass)
+    __device__ __forceinline__ int coset_of(size_t b) const { return cos_r0 + (int)(b % ncos) * cos_rstride; }
+    __device__ __forceinline__ fe *out_of(size_t b) const { return out + (b / ncos) * out_stride + (b % ncos) * out_jstride; }
 };
 
 // Single pass: whole polynomial (n = M <= TILE) per line, LPB = TILE / n polys per block.
@@ -206,8 +219,8 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         int b = b0 + line;
         fe v = fe_zero();
         if (b < batch) {
-            v = a.in[(size_t)b * a.in_stride + k];
-            if (a.pre_full) v = fe_mul(v, a.pre_full[(size_t)b * a.pre_stride + k]);
+            v = a.in[(size_t)(b / a.ncos) * a.in_stride + k];
+            if (a.pre_full) v = fe_mul(v, a.pre_full[(size_t)a.coset_of(b) * a.pre_stride + k]);
             else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, (size_t)k));
         }
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
@@ -220,7 +233,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         if (b >= batch) continue;
         fe v = s[Lds<LOGM, TILE>::idx(line, j)];
         if (a.has_post) v = fe_mul(v, a.post);
-        a.out[(size_t)b * a.out_stride + j] = v;
+        a.out_of(b)[j] = v;
     }
 }
 
@@ -230,7 +243,12 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
 // Grid: one dimension over (line group, column) with the column fastest, remapped per XCD, so an XCD
 // runs one line group for every column back to back and its slice of the pass twiddle table stays
 // in that XCD's L2 (columns outermost re-fetched the table once per column).
-template <int LOGM, int TILE>
+// CT (coset LDE): no input pre-scale -- the coset shift s_r^k = s_r^(k1) (s_r^n1)^(k2) is split into a DFT
+// over the coset s_r^n1 <w_n2> (per-coset stage table, lds_dft<CT>: the first radix-4 round costs 4
+// multiplies per 4 points instead of 1, the pre-scale's 4 are gone) and the line constant s_r^k1, folded
+// into the per-coset pass twiddle (s_r w_n^j2)^k1.  Same outputs, 0.25 multiplies and one 16-B table read
+// fewer per element.
+template <int LOGM, int TILE, bool CT>
 __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a, int batch) {
     extern __shared__ fe s[];
     constexpr int M = 1 << LOGM;  // n2
@@ -240,23 +258,29 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     const size_t lin = xcd_block(blockIdx.x, gridDim.x);
     const size_t k1_0 = (lin / batch) * LPB;
     const size_t b = lin % batch;
-    const fe *in = a.in + b * a.in_stride;
+    const fe *in = a.in + (b / a.ncos) * a.in_stride;
+    const int r = a.coset_of(b);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
         size_t k = k1_0 + line + n1 * (size_t)k2;
-        fe v = in[k];
-        if (a.pre_full) v = fe_mul(v, a.pre_full[b * a.pre_stride + k]);
-        else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
+        fe v = ld_fe(in + k);
+        if (!CT) {
+            if (a.pre_full) v = fe_mul(v, a.pre_full[(size_t)r * a.pre_stride + k]);
+            else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
+        }
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    lds_dft<LOGM, TILE>(s, a.tw4096);
+    if constexpr (CT) lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096);
+    else lds_dft<LOGM, TILE>(s, a.tw4096);
     fe *out = a.out + b * a.out_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j2 = e & (M - 1);
         size_t k1 = k1_0 + line;
         fe v = s[Lds<LOGM, TILE>::idx(line, j2)];
-        if (a.pass_tw) {
+        if (CT) {
+            v = fe_mul(v, a.cos_pass[(size_t)r * n + k1_0 * M + e]);
+        } else if (a.pass_tw) {
             v = fe_mul(v, a.pass_tw[k1_0 * M + e]);  // = w^(j2 k1), contiguous over the block
         } else {
             size_t t = ((size_t)j2 * k1) & (n - 1);
@@ -285,7 +309,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     }
     __syncthreads();
     lds_dft<LOGM, TILE>(s, a.tw4096);
-    fe *out = a.out + b * a.out_stride;
+    fe *out = a.out_of(b);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, j1 = e / LPB;
         fe v = s[Lds<LOGM, TILE>::idx(line, j1)];
@@ -317,11 +341,18 @@ static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     constexpr int LPB = TILE / (1 << LOGM);
     size_t n1 = ((size_t)1 << a.log_n) >> LOGM;
     size_t sh = Lds<LOGM, TILE>::bytes();
-    hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
+    const dim3 grid(cdiv(n1, LPB) * batch);
+    if (a.cos_stage) {
+        hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        ZK_PROF_OPS(st, "ntt_pass1", 32.0 * el, el * ((double)LOGM / 2.0 + 1.0), el * LOGM,
+                    hipLaunchKernelGGL((ntt_pass1<LOGM, TILE, true>), grid, dim3(NTT_THREADS), sh, st, a, batch));
+        return;
+    }
+    hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     ZK_PROF_OPS(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * el,
                 el * (dft_muls_per_elem(LOGM) + 1.0 + (a.pre_full || a.pre_lo ? 1 : 0) + (a.pass_tw ? 0 : 1)), el * LOGM,
-                hipLaunchKernelGGL((ntt_pass1<LOGM, TILE>), dim3(cdiv(n1, LPB) * batch), dim3(NTT_THREADS), sh, st, a, batch));
+                hipLaunchKernelGGL((ntt_pass1<LOGM, TILE, false>), grid, dim3(NTT_THREADS), sh, st, a, batch));
 }
 
 template <int LOGM, int TILE>
@@ -352,9 +383,10 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     default: break;                               \
     }
 
+void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp);
+
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
-         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, size_t pre_stride) {
-    constexpr int TILE = ZK_NTT_TILE;
+         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
     NttArgs a;
     a.in = in;
     a.out = out;
@@ -366,7 +398,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.pre_lo = pre ? pre->lo : nullptr;
     a.pre_hi = pre ? pre->hi : nullptr;
     a.pre_full = pre ? pre->full : nullptr;
-    a.pre_stride = pre_stride;
+    a.pre_stride = 0;
 #if ZK_NTT_PASS_TABLE
     a.pass_tw = inverse ? T.inv_pass : T.fwd_pass;
 #else
@@ -375,7 +407,18 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.has_post = post_scale != nullptr;
     a.post = post_scale ? *post_scale : fe_zero();
     a.log_n = T.log_n;
-    const int L = T.log_n;
+    a.ncos = 1;
+    a.cos_r0 = 0;
+    a.cos_rstride = 0;
+    a.out_jstride = 0;
+    a.cos_stage = a.cos_pass = nullptr;
+    ntt_run(st, a, batch, tmp);
+}
+
+// the passes of one NTT call (single pass for n <= 4096, else four-step through tmp)
+void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
+    constexpr int TILE = ZK_NTT_TILE;
+    const int L = a.log_n;
     if (L <= 12) {
         ZK_DISPATCH_LOGM(L, launch_single, st, a, batch);
         return;
@@ -391,7 +434,36 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a2.in = tmp;
     a2.in_stride = (size_t)1 << L;
     a2.pre_lo = a2.pre_hi = a2.pre_full = nullptr;
+    a2.cos_stage = a2.cos_pass = nullptr;
     ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
+}
+
+void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
+             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp) {
+    NttArgs a;
+    memset(&a, 0, sizeof a);
+    a.in = in;
+    a.out = out;
+    a.in_stride = in_stride;
+    a.out_stride = out_cstride;
+    a.out_jstride = out_jstride;
+    a.tw4096 = T.dft_fwd;
+    a.big_lo = T.fwd_lo;
+    a.big_hi = T.fwd_hi;
+    a.pass_tw = T.fwd_pass;
+    a.log_n = T.log_n;
+    a.ncos = ncos;
+    a.cos_r0 = r0;
+    a.cos_rstride = rstride;
+    const size_t n = (size_t)1 << T.log_n;
+    if (T.log_n <= 12) {  // single pass: pre-scale from the full (3 w_N^r)^k tables
+        a.pre_full = CT.full;
+        a.pre_stride = n;
+    } else {
+        a.cos_stage = CT.stage;
+        a.cos_pass = CT.pass;
+    }
+    ntt_run(st, a, ncols * ncos, tmp);
 }
 
 __global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n2, fe *out) {
@@ -400,6 +472,20 @@ __global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n
         const size_t k1 = idx >> log_n2, j2 = idx & (((size_t)1 << log_n2) - 1);
         out[idx] = pow_split(lo, hi, (j2 * k1) & (n - 1));
     }
+}
+
+// out[k1 * n2 + j2] = s^k1 * pass[k1 * n2 + j2]  (= (s w_n^j2)^k1): the per-coset pass-1 twiddles
+__global__ void k_coset_pass(const fe *lo, const fe *hi, const fe *pass, int log_n, int log_n2, fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x)
+        out[idx] = fe_mul(pow_split(lo, hi, idx >> log_n2), pass[idx]);
+}
+
+void coset_pass_tables(hipStream_t st, const fe *s_lo, const fe *s_hi, const fe *fwd_pass, int log_n, int log_n2,
+                       fe *out) {
+    const size_t n = (size_t)1 << log_n;
+    hipLaunchKernelGGL(k_coset_pass, dim3(std::min<size_t>(cdiv(n, 256), 65536)), dim3(256), 0, st, s_lo, s_hi, fwd_pass,
+                       log_n, log_n2, out);
 }
 
 void make_pass_twiddles(hipStream_t st, NttTables &T) {
@@ -1308,14 +1394,11 @@ __global__ void __launch_bounds__(256) k_coset_to_natural(const fe *src, int log
 }
 
 // LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j: out[j*n ..] (coset-major)
-void lde_cosets(hipStream_t st, const NttTables &Tn, const fe *coeffs, size_t n, const fe *coset_full, size_t r0,
+void lde_cosets(hipStream_t st, const NttTables &Tn, const CosetTables &CT, const fe *coeffs, size_t n, size_t r0,
                 size_t stride, int count, fe *out, fe *ntt_tmp) {
-    for (int j0 = 0; j0 < count; j0 += 8) {  // launches of up to 8 cosets (ntt_tmp holds 8n)
-        PowTable cosets;
-        cosets.full = const_cast<fe *>(coset_full) + (r0 + stride * j0) * n;
-        ntt(st, Tn, coeffs, 0, out + (size_t)j0 * n, n, std::min(8, count - j0), false, &cosets, nullptr, ntt_tmp,
-            stride * n);
-    }
+    for (int j0 = 0; j0 < count; j0 += 8)  // launches of up to 8 cosets (ntt_tmp holds 8n)
+        ntt_lde(st, Tn, CT, coeffs, 0, 1, (int)(r0 + stride * j0), (int)stride, std::min(8, count - j0),
+                out + (size_t)j0 * n, 0, n, ntt_tmp);
 }
 
 const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
@@ -1342,11 +1425,11 @@ const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccol
 }
 
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
+                       int log_b, const void *deep_consts_dev, fe z, fe zg, const CosetTables &CT, fe *scratch,
                        fe *ulde, fe *ntt_tmp, fe *out) {
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
     const fe *Dk = deep_poly(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
-    lde_cosets(st, Tn, Dk, n, coset_full, 0, 1, (int)B, ulde, ntt_tmp);
+    lde_cosets(st, Tn, CT, Dk, n, 0, 1, (int)B, ulde, ntt_tmp);
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
@@ -1481,11 +1564,11 @@ const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int 
 }
 
 void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
-                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
+                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const CosetTables &CT,
                            fe *scratch, fe *ulde, fe *ntt_tmp, fe *out) {
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
     const fe *Dk = deep_poly_ext(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
-    for (int plane = 0; plane < 2; plane++) lde_cosets(st, Tn, Dk + plane * n, n, coset_full, 0, 1, (int)B, ulde + plane * N, ntt_tmp);
+    for (int plane = 0; plane < 2; plane++) lde_cosets(st, Tn, CT, Dk + plane * n, n, 0, 1, (int)B, ulde + plane * N, ntt_tmp);
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     for (int plane = 0; plane < 2; plane++)

@@ -127,19 +127,41 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     fe wN = h_root_of_unity(pl->log_n + pl->log_b), wce = h_root_of_unity(pl->log_n + 3);
     std::vector<fe> xrN(B), xrce(8), xnN(B);
     fe s = fe_make(3);
-    // full tables for the LDE pre-scale (B * n elements: 128 MiB at n = 2^20, B = 8), contiguous so
-    // one launch can run every coset (pre_stride n)
-    ZK_CHECK_HIP(p->arena.alloc(&pl->coset_full, (size_t)B * n));
+    // coset-LDE tables (CosetTables, B * n elements: 128 MiB at n = 2^20, B = 8)
+    if (pl->log_n <= 12) {
+        ZK_CHECK_HIP(p->arena.alloc(&pl->ct.full, (size_t)B * n));
+    } else {
+        ZK_CHECK_HIP(p->arena.alloc(&pl->ct.pass, (size_t)B * n));
+        ZK_CHECK_HIP(p->arena.alloc(&pl->ct.stage, (size_t)B * 4096));
+    }
+    const int log_n2 = (pl->log_n + 1) / 2;  // pass-1 line length of the four-step split (as in ntt())
+    const size_t n2 = (size_t)1 << log_n2, n1 = n >> log_n2;
+    std::vector<fe> stage(pl->log_n > 12 ? (size_t)B * 4096 : 0);
     for (uint32_t r = 0; r < B; r++) {
         xrN[r] = s;
         xnN[r] = h_pow(s, n);
         PowTable t;
         ZK_CHECK_HIP(make_pow_table(p, s, n, &t));
-        t.full = pl->coset_full + (size_t)r * n;
-        pow_expand(p->st, t.lo, t.hi, n, t.full);
+        if (pl->log_n <= 12) {
+            pow_expand(p->st, t.lo, t.hi, n, pl->ct.full + (size_t)r * n);
+        } else {
+            // pass[r][k1 n2 + j2] = s^k1 w_n^(j2 k1); stage[r][h + j] = c^(n2/2h) w_2h^j with c = s^n1
+            coset_pass_tables(p->st, t.lo, t.hi, pl->Tn.fwd_pass, pl->log_n, log_n2, pl->ct.pass + (size_t)r * n);
+            const fe c = h_pow(s, n1);
+            for (size_t h = 1; h < n2; h *= 2) {
+                const fe w = h_root_of_unity(ilog2(2 * h));
+                fe v = h_pow(c, n2 / (2 * h));
+                for (size_t j = 0; j < h; j++) {
+                    stage[(size_t)r * 4096 + h + j] = v;
+                    v = fe_mul(v, w);
+                }
+            }
+        }
         pl->coset.push_back(t);
         s = fe_mul(s, wN);
     }
+    if (pl->log_n > 12)
+        ZK_CHECK_HIP(hipMemcpy(pl->ct.stage, stage.data(), stage.size() * sizeof(fe), hipMemcpyHostToDevice));
     s = fe_make(3);
     for (int r = 0; r < 8; r++) {
         xrce[r] = s;
@@ -775,7 +797,7 @@ static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, 
     ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
     // coset r of the LDE domain: NTT of the coefficients scaled by (3 w_N^r)^k
     for (uint32_t r = 0; r < B; r++)
-        ntt(p->st, pl->Tn, p->polys, n, p->lde + r * n, B * n, W, false, &pl->coset[r], nullptr, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, (int)r, 0, 1, p->lde + r * n, B * n, 0, p->tmp);
     (void)N;
     return ZK_OK;
 }
@@ -893,7 +915,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
                           h_inv(h_pow(three, n)), C, p->cpolys + (size_t)j * n, p->flag);
     }
     for (uint32_t r = 0; r < B; r++)
-        ntt(p->st, pl->Tn, p->cpolys, n, clde + r * n, B * n, CK, false, &pl->coset[r], nullptr, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, (int)r, 0, 1, clde + r * n, B * n, 0, p->tmp);
     ZK_TRY(commit_rows(p, clde, CK, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
@@ -913,7 +935,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         stage_mark(p, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
-        deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->coset_full,
+        deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->ct,
                           p->dscratch, p->ulde, p->tmp, deep);
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
@@ -929,7 +951,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         deep_coeff_ext_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->x_deep_consts, z, zg,
-                              pl->coset_full, p->x_dscratch, p->x_ulde, p->tmp, deep);
+                              pl->ct, p->x_dscratch, p->x_ulde, p->tmp, deep);
     }
     stage_mark(p, "deep");
 

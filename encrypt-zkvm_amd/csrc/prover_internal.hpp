@@ -69,8 +69,8 @@ struct DeviceArena {
 struct Plan {  // everything that depends only on (n, B)
     int log_n = 0, log_b = 0;
     NttTables Tn, Tce, TN;        // sizes n, 8n, B*n
-    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B (full tables contiguous from coset_full)
-    fe *coset_full = nullptr;     // B x n: coset[r].full = coset_full + r * n
+    std::vector<PowTable> coset;  // (3 * w_N^r)^k, r < B (split tables)
+    CosetTables ct;               // coset-LDE tables (zk_internal.hpp)
     fe *xn_N = nullptr;           // (3 * w_N^r)^n, r < B: x^n on LDE coset r
     PowTable inv3;                // 3^-k, k < n
     fe *xr_ce = nullptr, *xr_N = nullptr;  // 3 * w_CE^r (8), 3 * w_N^r (B)

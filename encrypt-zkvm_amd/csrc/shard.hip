@@ -302,8 +302,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         if (trace) ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
         ntt(p->st, pl->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
         for (int j = 0; j < Bl; j++)
-            ntt(p->st, pl->Tn, p->polys, n, p->lde + j * n, (size_t)Bl * n, W, false, &pl->coset[X.rank[l] + G * j],
-                nullptr, p->tmp);
+            ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, X.rank[l] + G * j, 0, 1, p->lde + j * n, (size_t)Bl * n, 0,
+                    p->tmp);
     }
     stage_mark(P0, "trace_lde");
     std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);
@@ -401,8 +401,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             for (int j = 0; j < Bl; j++)
-                ntt(p->st, X.pl[l]->Tn, p->cpolys, n, CLDE(p) + j * n, (size_t)Bl * n, CK, false,
-                    &X.pl[l]->coset[X.rank[l] + G * j], nullptr, p->tmp);
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys, n, CK, X.rank[l] + G * j, 0, 1, CLDE(p) + j * n,
+                        (size_t)Bl * n, 0, p->tmp);
         }
     }
     for (int l = 0; l < nlp; l++) {
@@ -445,7 +445,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
             // DEEP as an exact polynomial (kernels.hip): replicated coefficients, local cosets g + G j
             const fe *Dk = deep_poly(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch);
-            lde_cosets(p->st, pl->Tn, Dk, n, pl->coset_full, X.rank[l], G, Bl, p->deep, p->tmp);
+            lde_cosets(p->st, pl->Tn, pl->ct, Dk, n, X.rank[l], G, Bl, p->deep, p->tmp);
         }
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
@@ -466,7 +466,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
             const fe *Dk = deep_poly_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch);
             for (int plane = 0; plane < 2; plane++)  // planar per rank: plane stride Bl * n
-                lde_cosets(p->st, pl->Tn, Dk + plane * n, n, pl->coset_full, X.rank[l], G, Bl,
+                lde_cosets(p->st, pl->Tn, pl->ct, Dk + plane * n, n, X.rank[l], G, Bl,
                            p->x_deep + (size_t)plane * Bl * n, p->tmp);
         }
     }

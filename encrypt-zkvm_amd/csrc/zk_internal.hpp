@@ -78,6 +78,9 @@ struct NttTables {
 };
 // fill NttTables::fwd_pass / inv_pass (allocated by the caller, n elements each)
 void make_pass_twiddles(hipStream_t st, NttTables &T);
+// out[k1*n2 + j2] = s^k1 * fwd_pass[k1*n2 + j2] (s^t from split tables): CosetTables::pass of one coset
+void coset_pass_tables(hipStream_t st, const fe *s_lo, const fe *s_hi, const fe *fwd_pass, int log_n, int log_n2,
+                       fe *out);
 
 // A power series s^k, k < n, as split tables (s^k = lo[k & 2047] * hi[k >> 11])
 struct PowTable {
@@ -93,7 +96,19 @@ void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out);
 //   post_scale  : optional constant multiplied into every output (e.g. 1/n)
 // in and out must not alias.  tmp must hold batch * n elements when log_n > 12.
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride,
-         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, size_t pre_stride = 0);
+         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp);
+
+// Coset-LDE tables of one plan (LDE coset r < B, s_r = 3 w_N^r):
+//   n <= 4096 (single pass): full[r*n + k] = s_r^k (input pre-scale)
+//   four-step (n = n1*n2):   stage[r*4096 + h + j] = c_r^(n2/2h) w_2h^j, c_r = s_r^n1 (DIT stage twiddles of
+//                            the pass-1 line DFT over the coset c_r <w_n2>), pass[r*n + k1*n2 + j2] = (s_r w_n^j2)^k1
+struct CosetTables {
+    fe *full = nullptr, *stage = nullptr, *pass = nullptr;
+};
+// Forward coset LDE: for columns c < ncols (at in + c*in_stride) and coset slots j < ncos (coset r0 + j*rstride),
+// the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*ncos*n (four-step).
+void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
+             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp);
 
 // grinding: atomicMin into *best_dev of the nonces in [start, start+count) with >= bits trailing zeros
 void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,
@@ -173,9 +188,8 @@ struct DeepConsts {
     fe alpha_c[16];
     fe k1, k2, z, zg;
 };
-// LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j (coset_full: B contiguous
-// (3 w_N^r)^k tables): out[j*n ..], coset-major.  ntt_tmp: 8n.
-void lde_cosets(hipStream_t st, const NttTables &Tn, const fe *coeffs, size_t n, const fe *coset_full, size_t r0,
+// LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j: out[j*n ..], coset-major.  ntt_tmp: 8n.
+void lde_cosets(hipStream_t st, const NttTables &Tn, const CosetTables &CT, const fe *coeffs, size_t n, size_t r0,
                 size_t stride, int count, fe *out, fe *ntt_tmp);
 // The DEEP polynomial's coefficients (n; over E two planes of n) computed into scratch (returned)
 const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
@@ -183,16 +197,16 @@ const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccol
 const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
                         const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch);
 // DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
-// by suffix sums over the combined coefficients, one LDE over the B cosets (coset_full: B contiguous
-// (3 w_N^r)^k tables), natural-order output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
+// by suffix sums over the combined coefficients, one LDE over the B cosets (CosetTables), natural-order
+// output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
 // elements; ulde: B*n; ntt_tmp: 8n.
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                       int log_b, const void *deep_consts_dev, fe z, fe zg, const fe *coset_full, fe *scratch,
+                       int log_b, const void *deep_consts_dev, fe z, fe zg, const CosetTables &CT, fe *scratch,
                        fe *ulde, fe *ntt_tmp, fe *out);
 // the same over E (FieldExtension::Quadratic; DeepConstsE): scratch 8 (2048 + n/2048 + 2) + 6n + 4 ceil(n/256)
 // elements; ulde: 2*B*n; out planar (2N)
 void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,
-                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const fe *coset_full,
+                           int log_n, int log_b, const void *deep_consts_dev, fe2 z, fe2 zg, const CosetTables &CT,
                            fe *scratch, fe *ulde, fe *ntt_tmp, fe *out);
 // FRI fold: next[r] = p_r(alpha) over rows r < L/fold (consts: FoldConsts in device memory)
 struct FoldConsts {
