@@ -406,6 +406,10 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
 #endif
     a.has_post = post_scale != nullptr;
     a.post = post_scale ? *post_scale : fe_zero();
+    if (inverse && post_scale && T.log_n > 12 && T.inv_pass_n && fe_eq(*post_scale, T.inv_n)) {
+        a.pass_tw = T.inv_pass_n;  // interpolation: n^-1 folded into the pass-1 twiddles
+        a.has_post = 0;
+    }
     a.log_n = T.log_n;
     a.ncos = 1;
     a.cos_r0 = 0;
@@ -466,11 +470,13 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
     ntt_run(st, a, ncols * ncos, tmp);
 }
 
-__global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n2, fe *out) {
+__global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n2, fe *out, fe *out_scaled, fe scale) {
     const size_t n = (size_t)1 << log_n;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
         const size_t k1 = idx >> log_n2, j2 = idx & (((size_t)1 << log_n2) - 1);
-        out[idx] = pow_split(lo, hi, (j2 * k1) & (n - 1));
+        const fe w = pow_split(lo, hi, (j2 * k1) & (n - 1));
+        out[idx] = w;
+        if (out_scaled) out_scaled[idx] = fe_mul(w, scale);
     }
 }
 
@@ -492,8 +498,10 @@ void make_pass_twiddles(hipStream_t st, NttTables &T) {
     const size_t n = (size_t)1 << T.log_n;
     const int log_n2 = (T.log_n + 1) / 2;  // pass-1 line length, as in ntt()
     const unsigned blocks = std::min<size_t>(cdiv(n, 256), 65536);
-    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.fwd_lo, T.fwd_hi, T.log_n, log_n2, T.fwd_pass);
-    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.inv_lo, T.inv_hi, T.log_n, log_n2, T.inv_pass);
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.fwd_lo, T.fwd_hi, T.log_n, log_n2, T.fwd_pass,
+                       (fe *)nullptr, fe_zero());
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.inv_lo, T.inv_hi, T.log_n, log_n2, T.inv_pass,
+                       T.inv_pass_n, T.inv_n);
 }
 
 __global__ void k_pow_expand(const fe *lo, const fe *hi, size_t n, fe *out) {

@@ -120,6 +120,8 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     if (pl->log_n > 12) {  // four-step NTTs: inter-pass twiddle tables (2n elements)
         ZK_CHECK_HIP(p->arena.alloc(&pl->Tn.fwd_pass, n));
         ZK_CHECK_HIP(p->arena.alloc(&pl->Tn.inv_pass, n));
+        ZK_CHECK_HIP(p->arena.alloc(&pl->Tn.inv_pass_n, n));
+        pl->Tn.inv_n = h_inv(fe_make(n));
         make_pass_twiddles(p->st, pl->Tn);
     }
     ZK_CHECK_HIP(make_ntt_tables(p, pl->log_n + 3, &pl->Tce));

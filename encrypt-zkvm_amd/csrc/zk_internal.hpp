@@ -75,6 +75,10 @@ struct NttTables {
     // four-step inter-pass twiddles w^(j2*k1) laid out as pass 1 consumes them, [k1 * n2 + j2]
     // (n elements each; only for log_n > 12, else null)
     fe *fwd_pass = nullptr, *inv_pass = nullptr;
+    // optional: inv_pass * n^-1, used when an inverse NTT is post-scaled by n^-1 (interpolation): the
+    // scale rides on the pass-1 twiddle instead of costing a multiply per element in pass 2
+    fe *inv_pass_n = nullptr;
+    fe inv_n = {0, 0};
 };
 // fill NttTables::fwd_pass / inv_pass (allocated by the caller, n elements each)
 void make_pass_twiddles(hipStream_t st, NttTables &T);
