@@ -467,7 +467,15 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
         a.cos_stage = CT.stage;
         a.cos_pass = CT.pass;
     }
-    ntt_run(st, a, ncols * ncos, tmp);
+    // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so
+    // one launch drain per pass instead of one per coset
+    for (int j0 = 0; j0 < ncos; j0 += 8) {
+        NttArgs b = a;
+        b.ncos = std::min(8, ncos - j0);
+        b.cos_r0 = r0 + j0 * rstride;
+        b.out = out + (size_t)j0 * out_jstride;
+        ntt_run(st, b, ncols * b.ncos, tmp);
+    }
 }
 
 __global__ void k_pass_twiddles(const fe *lo, const fe *hi, int log_n, int log_n2, fe *out, fe *out_scaled, fe scale) {
@@ -1404,9 +1412,7 @@ __global__ void __launch_bounds__(256) k_coset_to_natural(const fe *src, int log
 // LDE of one n-coefficient polynomial over `count` cosets r0 + stride*j: out[j*n ..] (coset-major)
 void lde_cosets(hipStream_t st, const NttTables &Tn, const CosetTables &CT, const fe *coeffs, size_t n, size_t r0,
                 size_t stride, int count, fe *out, fe *ntt_tmp) {
-    for (int j0 = 0; j0 < count; j0 += 8)  // launches of up to 8 cosets (ntt_tmp holds 8n)
-        ntt_lde(st, Tn, CT, coeffs, 0, 1, (int)(r0 + stride * j0), (int)stride, std::min(8, count - j0),
-                out + (size_t)j0 * n, 0, n, ntt_tmp);
+    ntt_lde(st, Tn, CT, coeffs, 0, 1, (int)r0, (int)stride, count, out, 0, n, ntt_tmp);
 }
 
 const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,

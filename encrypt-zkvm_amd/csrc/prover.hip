@@ -215,7 +215,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
     ZK_CHECK_HIP(A.alloc(&p->polys, (size_t)W * n));
-    ZK_CHECK_HIP(A.alloc(&p->tmp, std::max((size_t)W * n, CE)));
+    // NTT scratch: the four-step intermediate of a whole 8-coset LDE of the trace (28 x 8 x n)
+    ZK_CHECK_HIP(A.alloc(&p->tmp, (size_t)W * 8 * n));
     ZK_CHECK_HIP(A.alloc(&p->lde, (size_t)W * N));
     ZK_CHECK_HIP(A.alloc(&p->comp, CE));
     ZK_CHECK_HIP(A.alloc(&p->ctmp, CE));
@@ -798,8 +799,7 @@ static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, 
     // interpolate 28 columns (winter-math interpolate_poly over <w_n>)
     ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
     // coset r of the LDE domain: NTT of the coefficients scaled by (3 w_N^r)^k
-    for (uint32_t r = 0; r < B; r++)
-        ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, (int)r, 0, 1, p->lde + r * n, B * n, 0, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, 0, 1, (int)B, p->lde, B * n, n, p->tmp);
     (void)N;
     return ZK_OK;
 }
@@ -916,8 +916,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
                           h_inv(h_pow(three, n)), C, p->cpolys + (size_t)j * n, p->flag);
     }
-    for (uint32_t r = 0; r < B; r++)
-        ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, (int)r, 0, 1, clde + r * n, B * n, 0, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, 0, 1, (int)B, clde, B * n, n, p->tmp);
     ZK_TRY(commit_rows(p, clde, CK, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;

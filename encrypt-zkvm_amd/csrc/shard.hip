@@ -301,9 +301,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         ZK_CHECK_HIP(hipSetDevice(p->device));
         if (trace) ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
         ntt(p->st, pl->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-        for (int j = 0; j < Bl; j++)
-            ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, X.rank[l] + G * j, 0, 1, p->lde + j * n, (size_t)Bl * n, 0,
-                    p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
     }
     stage_mark(P0, "trace_lde");
     std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);
@@ -400,9 +398,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            for (int j = 0; j < Bl; j++)
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys, n, CK, X.rank[l] + G * j, 0, 1, CLDE(p) + j * n,
-                        (size_t)Bl * n, 0, p->tmp);
+            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys, n, CK, X.rank[l], G, Bl, CLDE(p), (size_t)Bl * n, n, p->tmp);
         }
     }
     for (int l = 0; l < nlp; l++) {

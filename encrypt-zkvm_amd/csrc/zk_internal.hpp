@@ -110,7 +110,8 @@ struct CosetTables {
     fe *full = nullptr, *stage = nullptr, *pass = nullptr;
 };
 // Forward coset LDE: for columns c < ncols (at in + c*in_stride) and coset slots j < ncos (coset r0 + j*rstride),
-// the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*ncos*n (four-step).
+// the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*min(ncos, 8)*n
+// (four-step; launches of up to 8 cosets).
 void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
              int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp);
 
