@@ -238,6 +238,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
     ZK_CHECK_HIP(A.alloc(&p->gather_out, ZK_GATHER_CAP));
     ZK_CHECK_HIP(A.alloc(&p->gather_idx, ZK_GATHER_CAP));
+    ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_idx, ZK_GATHER_CAP * sizeof(uint64_t), hipHostMallocDefault));
+    ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_out, ZK_GATHER_CAP * sizeof(fe), hipHostMallocDefault));
     ZK_CHECK_HIP(A.alloc(&p->flag, 4));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
@@ -254,6 +256,8 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamSynchronize(p->st);
     for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
     (void)hipStreamDestroy(p->st);
+    if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
+    if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
     delete p;
 }
 
@@ -1033,7 +1037,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     // address upload, one gather kernel, one download.
     Openings O;
     O.plans.push_back(plan_batch(N, pos));
-    O.plans.push_back(plan_batch(N, pos));
+    O.plans.push_back(O.plans[0]);  // the composition tree opens the same positions
     for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(layer_len[l] / fold, fri_pos[l]));
     std::vector<uint64_t> addr;
     auto fe_at = [&](const fe *base, size_t idx) { addr.push_back((uint64_t)(uintptr_t)(base + idx)); };
@@ -1060,11 +1064,13 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             }
     }
     if (addr.size() > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
-    std::vector<fe> got(addr.size());
-    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, addr.data(), addr.size() * 8, hipMemcpyHostToDevice, p->st));
+    // staged through pinned host buffers (pageable copies go through a driver bounce buffer)
+    memcpy(p->h_gather_idx, addr.data(), addr.size() * 8);
+    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, p->h_gather_idx, addr.size() * 8, hipMemcpyHostToDevice, p->st));
     gather_chunks(p->st, p->gather_idx, addr.size(), p->gather_out);
-    ZK_CHECK_HIP(hipMemcpyAsync(got.data(), p->gather_out, got.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipMemcpyAsync(p->h_gather_out, p->gather_out, addr.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    const std::vector<fe> got(p->h_gather_out, p->h_gather_out + addr.size());
     {
         size_t off = 0;
         O.trace_rows.assign(got.begin(), got.begin() + nu * W);

@@ -98,6 +98,8 @@ struct zk_prover {
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
     fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;
+    uint64_t *h_gather_idx = nullptr;  // pinned host staging of the opening addresses / values
+    fe *h_gather_out = nullptr;
     unsigned *flag = nullptr;
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
     uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
