@@ -600,35 +600,6 @@ void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8
     merkle_tree(st, leaves, rows, nodes);
 }
 
-__global__ void __launch_bounds__(256) k_merge_level(const uint8_t *src, uint8_t *dst, size_t cnt) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cnt; i += (size_t)gridDim.x * blockDim.x) {
-        uint32_t l[8], r[8], h[8];
-        load_digest(src + 64 * i, l);
-        load_digest(src + 64 * i + 32, r);
-        b3::merge(l, r, h);
-        store_digest(dst + 32 * i, h);
-    }
-}
-
-// The top of a tree in one block: src holds 2*cnt digests (cnt <= 256); builds nodes[1 .. 2cnt).
-__global__ void __launch_bounds__(256) k_merge_top(const uint8_t *src, size_t cnt, uint8_t *nodes) {
-    __shared__ uint32_t lvl[512][8];
-    for (size_t i = threadIdx.x; i < 2 * cnt; i += blockDim.x) load_digest(src + 32 * i, lvl[i]);
-    __syncthreads();
-    for (size_t c = cnt; c >= 1; c /= 2) {
-        uint32_t h[8];
-        const bool act = threadIdx.x < c;
-        if (act) b3::merge(lvl[2 * threadIdx.x], lvl[2 * threadIdx.x + 1], h);
-        __syncthreads();
-        if (act) {
-#pragma unroll
-            for (int w = 0; w < 8; w++) lvl[threadIdx.x][w] = h[w];
-            store_digest(nodes + 32 * (c + threadIdx.x), h);
-        }
-        __syncthreads();
-    }
-}
-
 // Three Merkle levels per launch: thread t merges the 8 child digests src[8t .. 8t+8) into
 // nodes[cnt + 4t .. +4), their pairs into nodes[cnt/2 + 2t .. +2) and those into nodes[cnt/4 + t].
 // One compression per thread per level-launch left every wave with a single dependent compression
@@ -656,11 +627,48 @@ __global__ void __launch_bounds__(256) k_merge_level3(const uint8_t *src, uint8_
     }
 }
 
+// Up to log2(P) + 1 levels in one block of P = blockDim.x threads: thread t merges the children
+// src[2(bP + t)], src[2(bP + t) + 1] into first-level parent bP + t, then the block halves its level in
+// LDS with one compression per thread per level; every node goes to its heap position.  Used for the
+// upper part of a tree, where the three-level kernel's seven dependent compressions per thread made
+// each launch a latency chain (the whole tail of a 2^22-leaf tree: 88 -> ~40 us).
+__global__ void __launch_bounds__(512) k_merge_block(const uint8_t *src, uint8_t *nodes, size_t cnt) {
+    __shared__ uint32_t lvl[512][8];
+    const size_t P = blockDim.x, t = threadIdx.x, base = blockIdx.x * P;
+    {
+        uint32_t l[8], r[8], h[8];
+        load_digest(src + 64 * (base + t), l);
+        load_digest(src + 64 * (base + t) + 32, r);
+        b3::merge(l, r, h);
+        store_digest(nodes + 32 * (cnt + base + t), h);
+#pragma unroll
+        for (int w = 0; w < 8; w++) lvl[t][w] = h[w];
+    }
+    __syncthreads();
+    size_t c = cnt, width = P, off = base;
+    while (width > 1) {
+        c >>= 1;
+        width >>= 1;
+        off >>= 1;
+        uint32_t h[8];
+        const bool act = t < width;
+        if (act) b3::merge(lvl[2 * t], lvl[2 * t + 1], h);
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) lvl[t][w] = h[w];
+            store_digest(nodes + 32 * (c + off + t), h);
+        }
+        __syncthreads();
+    }
+}
+
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes) {
     // invariant: src holds 2*cnt digests whose parents go to nodes[cnt .. 2cnt)
     size_t cnt = nl / 2;
     const uint8_t *src = leaves;
-    while (cnt >= 2048) {
+    // wide levels: three per launch, seven compressions per thread (throughput)
+    while (cnt >= ((size_t)1 << 20)) {
         unsigned blocks = cdiv(cnt / 4, 256);
         if (blocks > 65536) blocks = 65536;
         ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
@@ -668,14 +676,15 @@ void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *node
         src = nodes + 32 * (cnt / 4);
         cnt /= 8;
     }
-    while (cnt > 256) {
-        unsigned blocks = cdiv(cnt, 256);
-        if (blocks > 65536) blocks = 65536;
-        ZK_PROF(st, "merkle_level", 96.0 * cnt, hipLaunchKernelGGL(k_merge_level, dim3(blocks), dim3(256), 0, st, src, nodes + 32 * cnt, cnt));
-        src = nodes + 32 * cnt;
-        cnt /= 2;
+    // upper part: up to 10 levels per launch, one compression per thread per level (latency)
+    while (cnt >= 1) {
+        const size_t P = std::min<size_t>(512, cnt), roots = cnt / P;
+        ZK_PROF(st, roots > 1 ? "merkle_level" : "merkle_top", 96.0 * 2 * cnt,
+                hipLaunchKernelGGL(k_merge_block, dim3((unsigned)roots), dim3((unsigned)P), 0, st, src, nodes, cnt));
+        if (roots == 1) break;
+        src = nodes + 32 * roots;
+        cnt = roots / 2;
     }
-    ZK_PROF(st, "merkle_top", 128.0 * cnt, hipLaunchKernelGGL(k_merge_top, dim3(1), dim3(256), 0, st, src, cnt, nodes));
 }
 
 __global__ void k_gather_digests(const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out) {
