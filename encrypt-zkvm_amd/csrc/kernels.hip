@@ -800,6 +800,9 @@ struct EvalShared {
     fe g_last2, g_last1, delta;
 };
 
+#ifndef ZK_EVAL_LAZY
+#define ZK_EVAL_LAZY 1  // lazy 288-bit sum over the selector section's terms (base field)
+#endif
 #ifndef ZK_EVAL_WAVES
 #define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
 #endif
@@ -889,19 +892,42 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         fe y[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) y[k] = fe_sub(NXT(7 + k), per[5 + k]);
+        // 12..15 share the factor fh and 16..19 the factor nfh: sum the coefficient-weighted values first,
+        // multiply by the flag once (ct_k (v_k f) summed = f (sum ct_k v_k): 6 multiplies fewer per row)
+        fe sR = fe_zero(), sR2 = fe_zero();
 #pragma unroll
         for (int r2 = 0; r2 < 4; r2++) {
             acc288 am = acc288_zero();
 #pragma unroll
             for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
             const fe acc = acc288_reduce(am);
-            ZK_ACC(12 + r2, fe_mul(fe_sub(cube(acc), m0[r2]), fh));
+            const fe v = fe_sub(cube(acc), m0[r2]);
+            sR = fe_add(sR, fe_mul(S.ct[12 + r2], v));
+            if (KE == 2) {
+                sR2 = fe_add(sR2, fe_mul(S.ct2[12 + r2], v));
+                asm volatile("" : "+v"(sR2.lo), "+v"(sR2.hi));
+            }
         }
+        t = fe_add(t, fe_mul(sR, fh));
+        if (KE == 2) t2 = fe_add(t2, fe_mul(sR2, fh));
         ZK_SEQ(cb, t.lo);
-        ZK_ACC(16, fe_mul(fe_sub(NXT(7), CUR(7)), nfh));
-        ZK_ACC(17, fe_mul(fe_sub(NXT(8), CUR(8)), nfh));
-        ZK_ACC(18, fe_mul(NXT(9), nfh));
-        ZK_ACC(19, fe_mul(NXT(10), nfh));
+        {
+            const fe d16 = fe_sub(NXT(7), CUR(7)), d17 = fe_sub(NXT(8), CUR(8)), n9 = NXT(9), n10 = NXT(10);
+            acc288 aC = acc288_zero();
+            acc288_madd(aC, S.ct[16], d16);
+            acc288_madd(aC, S.ct[17], d17);
+            acc288_madd(aC, S.ct[18], n9);
+            acc288_madd(aC, S.ct[19], n10);
+            t = fe_add(t, fe_mul(acc288_reduce(aC), nfh));
+            if (KE == 2) {
+                acc288 aD = acc288_zero();
+                acc288_madd(aD, S.ct2[16], d16);
+                acc288_madd(aD, S.ct2[17], d17);
+                acc288_madd(aD, S.ct2[18], n9);
+                acc288_madd(aD, S.ct2[19], n10);
+                t2 = fe_add(t2, fe_mul(acc288_reduce(aD), nfh));
+            }
+        }
     }
     ZK_SEQ(cb, t.lo);
     // 0..11: degree-5 selectors (flags.rs:45-79) with shared prefixes, each consumed right away.
@@ -910,23 +936,32 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     //   ct3*(X(1-b4))*d3 + ct6*(X b4)*d6 = X*(ct3 d3 + b4 (ct6 d6 - ct3 d3))
     //   ct8*(Z(1-b4))*d1 + ct9*(Z b4)*d1 = Z d1 * (ct8 + b4 (ct9 - ct8))
     // (exact field identities: the composition values are unchanged).
+    // KE = 1: the section's terms go into one lazy 288-bit sum (one reduction instead of one per term)
     {
+        constexpr bool LZ = KE == 1 && ZK_EVAL_LAZY;
+        acc288 aS = acc288_zero();
+#define ZK_ACCS(k, val)                                  \
+    do {                                                 \
+        if (LZ) acc288_madd(aS, S.ct[k], (val));    \
+        else ZK_ACC(k, val);                             \
+    } while (0)
+#define ZK_SEQS() ZK_SEQ(cb, LZ ? aS.w[0] : (uint32_t)t.lo)
         const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
         const fe nb0 = fe_sub(one, b0), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3), nb4 = fe_sub(one, b4);
         const fe s0 = CUR(12), s1 = CUR(13);
         // 0 clock, 2 shift
-        ZK_ACC(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
+        ZK_ACCS(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
         const fe b01 = fe_mul(b0, b1);
-        ZK_ACC(2, b01);
+        ZK_ACCS(2, b01);
         const fe b0n1 = fe_sub(b0, b01);   // b0 (1-b1)
         const fe n0_1 = fe_sub(b1, b01);   // (1-b0) b1
         const fe n01 = fe_sub(nb0, n0_1);  // (1-b0)(1-b1)
         // 11 noop
         {
             const fe is_noop = fe_mul(fe_mul(fe_mul(n01, nb2), nb3), nb4);
-            ZK_ACC(11, fe_mul(is_noop, fe_sub(s0n, s0)));
+            ZK_ACCS(11, fe_mul(is_noop, fe_sub(s0n, s0)));
         }
-        ZK_SEQ(cb, t.lo);
+        ZK_SEQS();
         const fe n0_1_b2 = fe_mul(n0_1, b2);
         const fe n0_1_n2 = fe_sub(n0_1, n0_1_b2);
         const fe Y = fe_mul(n0_1_n2, b3);  // (1-b0) b1 (1-b2) b3
@@ -936,8 +971,9 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             const fe X = fe_sub(n0_1_n2, Y);
             const fe e3 = fe_mul(S.ct[3], fe_sub(s0n, fe_add(s0, s1)));
             const fe e6 = fe_mul(S.ct[6], fe_sub(s0n, fe_mul(s0, s1)));
-            const fe v36 = fe_mul(X, fe_add(e3, fe_mul(b4, fe_sub(e6, e3))));
-            t = fe_add(t, v36);
+            const fe i36 = fe_add(e3, fe_mul(b4, fe_sub(e6, e3)));
+            if (LZ) acc288_madd(aS, X, i36);
+            else t = fe_add(t, fe_mul(X, i36));
             if (KE == 2) {
                 const fe f3 = fe_mul(S.ct2[3], fe_sub(s0n, fe_add(s0, s1)));
                 const fe f6 = fe_mul(S.ct2[6], fe_sub(s0n, fe_mul(s0, s1)));
@@ -945,7 +981,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
                 asm volatile("" : "+v"(t2.lo), "+v"(t2.hi));
             }
         }
-        ZK_SEQ(cb, t.lo);
+        ZK_SEQS();
         {
             // 4 sadd / 5 add2 / 7 smul over the lwe_size ciphertext limbs (fhe/src/server_key.rs:89-124)
             is_add2 = fe_mul(Y, b4);
@@ -963,11 +999,11 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             }
             const fe acc7 = fe_sub(sum_sn, fe_mul(sum_s1, s0));
             acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
-            ZK_ACC(4, fe_mul(is_sadd, acc4));
-            ZK_ACC(5, fe_mul(is_add2, acc5));
-            ZK_ACC(7, fe_mul(is_smul, acc7));
+            ZK_ACCS(4, fe_mul(is_sadd, acc4));
+            ZK_ACCS(5, fe_mul(is_add2, acc5));
+            ZK_ACCS(7, fe_mul(is_smul, acc7));
         }
-        ZK_SEQ(cb, t.lo);
+        ZK_SEQS();
         {
             // 8 push / 9 read / 10 read2
             const fe p0 = fe_mul(b0n1, nb2);     // b0 (1-b1)(1-b2)
@@ -975,12 +1011,14 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             const fe p0n3 = fe_sub(p0, p0b3);
             is_read2 = fe_mul(p0b3, nb4);
             const fe zd1 = fe_mul(p0n3, fe_sub(NXT(13), s0));
-            t = fe_add(t, fe_mul(zd1, fe_add(S.ct[8], fe_mul(b4, fe_sub(S.ct[9], S.ct[8])))));
+            const fe i89 = fe_add(S.ct[8], fe_mul(b4, fe_sub(S.ct[9], S.ct[8])));
+            if (LZ) acc288_madd(aS, zd1, i89);
+            else t = fe_add(t, fe_mul(zd1, i89));
             if (KE == 2) {
                 t2 = fe_add(t2, fe_mul(zd1, fe_add(S.ct2[8], fe_mul(b4, fe_sub(S.ct2[9], S.ct2[8])))));
                 asm volatile("" : "+v"(t2.lo), "+v"(t2.hi));
             }
-            ZK_ACC(10, fe_mul(is_read2, fe_sub(NXT(17), s0)));
+            ZK_ACCS(10, fe_mul(is_read2, fe_sub(NXT(17), s0)));
         }
         // 1 depth: (d' - d - shr + shl) - 4 read2 + 4 add2   (x4 as two doublings)
         {
@@ -988,8 +1026,11 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             fe d = fe_sub(is_add2, is_read2);
             d = fe_add(d, d);
             d = fe_add(d, d);
-            ZK_ACC(1, fe_add(v, d));
+            ZK_ACCS(1, fe_add(v, d));
         }
+        if (LZ) t = fe_add(t, acc288_reduce(aS));
+#undef ZK_ACCS
+#undef ZK_SEQS
     }
     ZK_SEQ(cb, t.lo);
     // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
