@@ -18,6 +18,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
@@ -28,6 +30,23 @@
 
 namespace zk {
 thread_local std::string g_err;
+// ZK_HOST_TIMING=1: per proof, the host-only critical-path segments (the GPU idles during these) to stderr
+struct HostTimer {
+    bool on = getenv("ZK_HOST_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    std::string log;
+    void start() { t = std::chrono::steady_clock::now(); }
+    void stop(const char *what) {
+        if (!on) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+        char b[96];
+        snprintf(b, sizeof b, " %s=%.1f", what, us);
+        log += b;
+    }
+    ~HostTimer() {
+        if (on && !log.empty()) fprintf(stderr, "[zk host us]%s\n", log.c_str());
+    }
+};
 }
 using namespace zk;
 
@@ -258,6 +277,7 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamDestroy(p->st);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
     if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
+    delete p->open;
     delete p;
 }
 
@@ -366,21 +386,23 @@ int zk_prover_kernel_ops(zk_prover *p, double *total_muls, double *total_addsubs
 }
 
 // ---------------------------------------------------------------- Merkle batch openings
-BatchPlan zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
-    BatchPlan bp;
+void zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx, BatchPlan &bp) {
     int depth = ilog2(nl);
+    bp.norm.clear();
     for (uint64_t i : idx) bp.norm.push_back(i & ~1ULL);
     std::sort(bp.norm.begin(), bp.norm.end());
     bp.norm.erase(std::unique(bp.norm.begin(), bp.norm.end()), bp.norm.end());
     bp.paths.resize(bp.norm.size());
-    std::vector<uint64_t> next, cur;
+    for (auto &path : bp.paths) path.clear();  // keep their capacity across proofs
+    std::vector<uint64_t> &next = bp.next, &cur = bp.cur;
+    next.clear();
     for (size_t i = 0; i < bp.norm.size(); i++) {
         for (uint64_t l = bp.norm[i]; l < bp.norm[i] + 2; l++)
             if (std::find(idx.begin(), idx.end(), l) == idx.end()) bp.paths[i].push_back({0, l});
         next.push_back((bp.norm[i] + nl) >> 1);
     }
     for (int lvl = 1; lvl < depth; lvl++) {
-        cur = next;
+        std::swap(cur, next);
         next.clear();
         for (size_t i = 0; i < cur.size(); i++) {
             uint64_t sib = cur[i] ^ 1;
@@ -391,6 +413,11 @@ BatchPlan zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
             next.push_back(sib >> 1);
         }
     }
+}
+
+BatchPlan zk::plan_batch(size_t nl, const std::vector<uint64_t> &idx) {
+    BatchPlan bp;
+    plan_batch(nl, idx, bp);
     return bp;
 }
 
@@ -723,10 +750,20 @@ std::vector<std::vector<uint64_t>> zk::fri_fold_positions(const std::vector<uint
 
 std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood,
                                          const Openings &O, const std::vector<fe> *rem_flat) {
+    std::vector<uint8_t> out;
+    serialize_proof(n, opt, C, R, ood, O, rem_flat, out);
+    return out;
+}
+
+void zk::serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood, const Openings &O,
+                         const std::vector<fe> *rem_flat, std::vector<uint8_t> &out) {
     const int nl = (int)R.num_fri_layers;
     const int K = (int)opt->field_extension, ES = 16 * K;
     const size_t nu = R.num_positions;
     Bytes pf;
+    pf.v.swap(out);  // write into the caller's storage (capacity kept across proofs: no page faults)
+    pf.v.clear();
+    static thread_local Bytes paths;
     pf.u8(W);
     pf.u8(0);
     pf.u8(0);
@@ -748,7 +785,7 @@ std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C,
     for (int l = 0; l < nl; l++) pf.put(R.fri_roots[l], 32);
     pf.put(R.remainder_commitment, 32);
     auto write_queries = [&](const void *vals, size_t vlen, int b) {
-        Bytes paths;
+        paths.v.clear();
         const BatchPlan &plan = O.plans[b];
         paths.u8((uint8_t)plan.paths.size());
         size_t k = 0;
@@ -780,7 +817,7 @@ std::vector<uint8_t> zk::serialize_proof(size_t n, const zk_options *opt, int C,
     pf.u8(0);
     pf.u64(R.pow_nonce);
     pf.u8(0);
-    return pf.v;
+    out.swap(pf.v);
 }
 
 int zk::deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, uint8_t *proof_out, size_t *proof_len) {
@@ -878,6 +915,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "trace_lde");
     ZK_TRY(commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root));
     stage_mark(p, "trace_commit");
+    HostTimer HT;
+    HT.start();
     coin.reseed(R.trace_root);
 
     // S3: constraint composition coefficients [P4] and evaluation over the CE domain.  With
@@ -896,6 +935,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
         eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, binv, (const AirConsts *)p->air_consts,
                          comp);
+        HT.stop("air_consts");
     } else {
         AirConsts Kp[2];
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
@@ -925,6 +965,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
     ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
+    HT.start();
     coin.reseed(R.constraint_root);
 
     // S5: OOD frame [P7], DEEP coefficients [P8] and evaluations.  h holds the frame flattened
@@ -934,14 +975,17 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const fe z = coin.draw(), zg = fe_mul(z, g);
         fe_to_bytes(z, R.z);
         ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
+        HT.stop("z");
         ZK_CHECK_HIP(hipMemcpyAsync(h.data(), p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        HT.start();
         ood_reseed(coin, h.data(), C, R);
         stage_mark(p, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
         deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->ct,
                           p->dscratch, p->ulde, p->tmp, deep);
+        HT.stop("deep_consts");
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
         fe_to_bytes(z.a, R.z);
@@ -1014,6 +1058,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         if (nl) ZK_CHECK_HIP(hipMemcpyAsync(dalpha.data(), p->fri_alphas, 2 * nl * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
         ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        HT.start();
         // host replay of the same transcript (it continues into the remainder, grinding and queries)
         for (int l = 0; l < nl; l++) {
             coin.reseed(R.fri_roots[l]);
@@ -1022,28 +1067,43 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             if (!fe_eq(alpha.a, dalpha[2 * l]) || (KX == 2 && !fe_eq(alpha.b, dalpha[2 * l + 1])))
                 ZK_FAIL(ZK_ERR_DEVICE, "device FRI transcript diverged from the host transcript");
         }
+        HT.stop("fri_replay");
+        HT.start();
         if (KX == 1) ZK_TRY(remainder_step(rv, B, coin, R, degree_flag));
         else ZK_TRY(remainder_step_ext(rv, B, coin, R, degree_flag, rem_flat));
     }
     stage_mark(p, "fri");
 
+    HT.stop("remainder");
+    HT.start();
     // S7: grinding and query positions [P10, P11]
     std::vector<uint64_t> pos;
     ZK_TRY(grind_and_positions(p, coin, opt, N, R, pos));
     const size_t nu = pos.size();
     const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
+    HT.stop("positions");
+    HT.start();
 
     // S8: openings.  Every value and digest the proof opens, as a list of 16-byte device chunks: one
     // address upload, one gather kernel, one download.
-    Openings O;
-    O.plans.push_back(plan_batch(N, pos));
-    O.plans.push_back(O.plans[0]);  // the composition tree opens the same positions
-    for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(layer_len[l] / fold, fri_pos[l]));
-    std::vector<uint64_t> addr;
-    auto fe_at = [&](const fe *base, size_t idx) { addr.push_back((uint64_t)(uintptr_t)(base + idx)); };
+    // The Openings and the address list live in the prover (pinned / capacity kept across proofs):
+    // fresh host allocations here cost page faults on every proof (~100 us at 2^20).
+    if (!p->open) p->open = new Openings();
+    Openings &O = *p->open;
+    O.reset(2 + nl);
+    plan_batch(N, pos, O.plans[0]);
+    O.plans[1] = O.plans[0];  // the composition tree opens the same positions
+    for (int l = 0; l < nl; l++) plan_batch(layer_len[l] / fold, fri_pos[l], O.plans[2 + l]);
+    uint64_t *addr = p->h_gather_idx;
+    size_t na = 0;
+    auto fe_at = [&](const fe *base, size_t idx) { addr[na++] = (uint64_t)(uintptr_t)(base + idx); };
     auto row_at = [&](const fe *base, int ncols, uint64_t i) {  // coset-major LDE row i
         for (int c = 0; c < ncols; c++) fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
     };
+    size_t need = nu * (W + CK);
+    for (int l = 0; l < nl; l++) need += fri_pos[l].size() * fold * KX;
+    for (int b = 0; b < 2 + nl; b++) need += 2 * O.plans[b].count();
+    if (need > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
     for (size_t q = 0; q < nu; q++) row_at(p->lde, W, pos[q]);
     for (size_t q = 0; q < nu; q++) row_at(clde, CK, pos[q]);
     for (int l = 0; l < nl; l++) {
@@ -1052,46 +1112,47 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             for (uint32_t k = 0; k < fold; k++)
                 for (int j = 0; j < KX; j++) fe_at(layer_vals[l], j * layer_len[l] + r + k * rows);
     }
-    const size_t off_dig = addr.size();
+    const size_t off_dig = na;
     for (int b = 0; b < 2 + nl; b++) {
         const uint8_t *lv = b == 0 ? p->leaves : b == 1 ? p->cleaves : layer_leaves[b - 2];
         const uint8_t *nd = b == 0 ? p->nodes : b == 1 ? p->cnodes : layer_nodes[b - 2];
         for (auto &path : O.plans[b].paths)
             for (auto &e : path) {
                 const uint8_t *d = (e.first ? nd : lv) + 32 * e.second;
-                addr.push_back((uint64_t)(uintptr_t)d);
-                addr.push_back((uint64_t)(uintptr_t)(d + 16));
+                addr[na++] = (uint64_t)(uintptr_t)d;
+                addr[na++] = (uint64_t)(uintptr_t)(d + 16);
             }
     }
-    if (addr.size() > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
-    // staged through pinned host buffers (pageable copies go through a driver bounce buffer)
-    memcpy(p->h_gather_idx, addr.data(), addr.size() * 8);
-    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, p->h_gather_idx, addr.size() * 8, hipMemcpyHostToDevice, p->st));
-    gather_chunks(p->st, p->gather_idx, addr.size(), p->gather_out);
-    ZK_CHECK_HIP(hipMemcpyAsync(p->h_gather_out, p->gather_out, addr.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
+    HT.stop("plans_addresses");
+    ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, p->h_gather_idx, na * 8, hipMemcpyHostToDevice, p->st));
+    gather_chunks(p->st, p->gather_idx, na, p->gather_out);
+    ZK_CHECK_HIP(hipMemcpyAsync(p->h_gather_out, p->gather_out, na * sizeof(fe), hipMemcpyDeviceToHost, p->st));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    const std::vector<fe> got(p->h_gather_out, p->h_gather_out + addr.size());
     {
+        const fe *got = p->h_gather_out;
         size_t off = 0;
-        O.trace_rows.assign(got.begin(), got.begin() + nu * W);
+        O.trace_rows.assign(got, got + nu * W);
         off += nu * W;
-        O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * CK);
+        O.comp_rows.assign(got + off, got + off + nu * CK);
         off += nu * CK;
         for (int l = 0; l < nl; l++) {
-            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold * KX);
+            O.fri_rows[l].assign(got + off, got + off + fri_pos[l].size() * fold * KX);
             off += fri_pos[l].size() * fold * KX;
         }
-        const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
+        const uint8_t *dg = (const uint8_t *)(got + off_dig);
         for (int b = 0; b < 2 + nl; b++) {
             const size_t bytes = 32 * O.plans[b].count();
-            O.digests.emplace_back(dg, dg + bytes);
+            O.digests[b].assign(dg, dg + bytes);
             dg += bytes;
         }
     }
     stage_mark(p, "queries");
 
     // S9: proof bytes [P13, P14]
-    const std::vector<uint8_t> bytes = serialize_proof(n, opt, C, R, h.data(), O, KX == 2 ? &rem_flat : nullptr);
+    HT.start();
+    std::vector<uint8_t> &bytes = p->proof_bytes;
+    serialize_proof(n, opt, C, R, h.data(), O, KX == 2 ? &rem_flat : nullptr, bytes);
+    HT.stop("serialize");
     stage_mark(p, "serialize");
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     stage_collect(p);

@@ -81,6 +81,7 @@ struct Plan {  // everything that depends only on (n, B)
 };
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
 const fe *boundary_inverses(zk_prover *p, Plan *pl);
+struct Openings;
 
 }  // namespace zk
 
@@ -100,6 +101,8 @@ struct zk_prover {
     uint64_t *gather_idx = nullptr;
     uint64_t *h_gather_idx = nullptr;  // pinned host staging of the opening addresses / values
     fe *h_gather_out = nullptr;
+    zk::Openings *open = nullptr;      // per-proof openings, storage kept across proofs
+    std::vector<uint8_t> proof_bytes;  // the serialized proof, storage kept across proofs
     unsigned *flag = nullptr;
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
     uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
@@ -155,6 +158,7 @@ struct Bytes {
 struct BatchPlan {
     std::vector<uint64_t> norm;                                // normalized (even, sorted, unique) leaf indexes
     std::vector<std::vector<std::pair<int, uint64_t>>> paths;  // per path: (0 = leaf, 1 = node, index)
+    std::vector<uint64_t> cur, next;                           // planning scratch (kept for reuse)
     size_t count() const {
         size_t k = 0;
         for (auto &p : paths) k += p.size();
@@ -162,6 +166,7 @@ struct BatchPlan {
     }
 };
 BatchPlan plan_batch(size_t nl, const std::vector<uint64_t> &idx);
+void plan_batch(size_t nl, const std::vector<uint64_t> &idx, BatchPlan &out);  // reuses out's storage
 
 // ---------------------------------------------------------------- protocol steps (host side)
 // argument checks shared by every prove entry point; returns ZK_OK or a status (g_err set)
@@ -208,12 +213,21 @@ struct Openings {
     std::vector<std::vector<fe>> fri_rows;       // per layer: |fri_pos[l]| x fold
     std::vector<BatchPlan> plans;                // 2 + nl
     std::vector<std::vector<uint8_t>> digests;   // 2 + nl, 32 B each, plan order
+    void reset(size_t nplans) {  // keeps every vector's capacity
+        trace_rows.clear();
+        comp_rows.clear();
+        fri_rows.resize(nplans - 2);
+        plans.resize(nplans);
+        digests.resize(nplans);
+    }
 };
 // S9: Proof::to_bytes [P13, P14].  E values are k = opt->field_extension base elements each:
 // ood_flat = [T(z)]_W ++ [T(zg)]_W ++ [H(z)]_C flattened, comp_rows nu x C*k, fri_rows |pos| x fold*k;
 // the remainder is R.remainder (k = 1) or rem_flat (rem_len x k).
 std::vector<uint8_t> serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood_flat,
                                      const Openings &O, const std::vector<fe> *rem_flat = nullptr);
+void serialize_proof(size_t n, const zk_options *opt, int C, const zk_record &R, const fe *ood_flat, const Openings &O,
+                     const std::vector<fe> *rem_flat, std::vector<uint8_t> &out);  // into out (storage reused)
 // copy the proof out (proof_len in/out) and fold the degree flag into the status
 int deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, uint8_t *proof_out, size_t *proof_len);
 
