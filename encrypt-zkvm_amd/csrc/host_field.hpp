@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <map>
+#include <utility>
 #include <vector>
 
 #include "blake3.hpp"
@@ -70,6 +72,50 @@ inline void h_interp_coset(std::vector<fe> &v, fe offset) {
         v[k] = fe_mul(v[k], s);
         s = fe_mul(s, io);
     }
+}
+
+// h_interp_coset for offset 3 with the per-size tables (inverse twiddles per stage, n^-1 3^-k)
+// cached per thread: the FRI remainder is interpolated on every proof while the GPU waits
+inline void h_interp_coset3_cached(std::vector<fe> &v) {
+    struct Tabs {
+        std::vector<fe> tw, scale;  // tw[len/2 + j] = w_len^-j for each stage len; scale[k] = n^-1 3^-k
+    };
+    static thread_local std::map<size_t, Tabs> cache;
+    const size_t n = v.size();
+    int lg = 0;
+    while (((size_t)1 << lg) < n) lg++;
+    auto it = cache.find(n);
+    if (it == cache.end()) {
+        Tabs t;
+        t.tw.assign(n, fe_zero());
+        const fe wi = h_inv(h_root_of_unity(lg));
+        for (size_t len = 2; len <= n; len <<= 1) {
+            const fe wl = h_pow(wi, n / len);
+            fe w = fe_one();
+            for (size_t j = 0; j < len / 2; j++, w = fe_mul(w, wl)) t.tw[len / 2 + j] = w;
+        }
+        t.scale.resize(n);
+        fe s = h_inv(fe_make(n));
+        const fe io = h_inv(fe_make(3));
+        for (size_t k = 0; k < n; k++, s = fe_mul(s, io)) t.scale[k] = s;
+        it = cache.emplace(n, std::move(t)).first;
+    }
+    const Tabs &t = it->second;
+    for (size_t i = 0; i < n; i++) {
+        size_t r = 0;
+        for (int b = 0; b < lg; b++) r |= ((i >> b) & 1) << (lg - 1 - b);
+        if (i < r) std::swap(v[i], v[r]);
+    }
+    for (size_t len = 2; len <= n; len <<= 1) {
+        const size_t half = len / 2;
+        for (size_t i = 0; i < n; i += len)
+            for (size_t j = 0; j < half; j++) {
+                const fe u = v[i + j], x = fe_mul(v[i + j + half], t.tw[half + j]);
+                v[i + j] = fe_add(u, x);
+                v[i + j + half] = fe_sub(u, x);
+            }
+    }
+    for (size_t k = 0; k < n; k++) v[k] = fe_mul(v[k], t.scale[k]);
 }
 
 inline fe h_poly_eval(const fe *c, size_t m, fe x) {

@@ -796,8 +796,8 @@ __device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
 // Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
 // SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
 struct EvalShared {
-    fe ct[20], cb[22], ct2[20], cb2[22], v1[10], xr[8], inv_zn[8], inv_mds[16];
-    fe g_last2, g_last1, delta;
+    fe ct[20], cb[22], ct2[20], cb2[22], xr[8], inv_zn[8], inv_mds[16];
+    fe g_last2, g_last1, delta, bnd1, bnd1b;
 };
 
 #ifndef ZK_EVAL_LAZY
@@ -824,7 +824,10 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         else if (KE == 2 && t >= 148 && t < 170) S.cb2[t - 148] = K2->coeff_b[t - 148];
         else if (t < 20) S.ct[t] = K->coeff_t[t];
         else if (t < 42) S.cb[t - 20] = K->coeff_b[t - 20];
-        else if (t < 52) S.v1[t - 42] = K->assert_val[12 + t - 42];
+        else if (t == 42) S.bnd1 = K->bnd1;
+        else if (t == 43) S.bnd1b = KE == 2 ? K2->bnd1 : fe_zero();
+        else if (t < 52) {
+        }  // idle
         else if (t < 60) S.xr[t - 52] = K->xr[t - 52];
         else if (t < 68) S.inv_zn[t - 60] = K->inv_zn[t - 60];
         else if (t < 84) S.inv_mds[t - 68] = c_inv_mds[t - 68];
@@ -1044,15 +1047,16 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     acc288_madd(a0, S.cb[1], CUR(7));
     acc288_madd(a0, S.cb[2], CUR(8));
     acc288_madd(a0, S.cb[3], CUR(11));
-    acc288_madd(a1, S.cb[12], fe_sub(CUR(7), S.v1[0]));
-    acc288_madd(a1, S.cb[13], fe_sub(CUR(8), S.v1[1]));
+    acc288_madd(a1, S.cb[12], CUR(7));
+    acc288_madd(a1, S.cb[13], CUR(8));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         fe c = CUR(12 + k);
         acc288_madd(a0, S.cb[4 + k], c);
-        acc288_madd(a1, S.cb[14 + k], fe_sub(c, S.v1[2 + k]));
+        acc288_madd(a1, S.cb[14 + k], c);
     }
-    const fe bs0 = acc288_reduce(a0), bs1 = acc288_reduce(a1);
+    // sum_k cb[12+k] (c_k - v_k) = sum_k cb[12+k] c_k - bnd1 (bnd1 precomputed on the host)
+    const fe bs0 = acc288_reduce(a0), bs1 = fe_sub(acc288_reduce(a1), S.bnd1);
     const fe ibd = inv_bd[t_id];
     fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
     res = fe_add(res, fe_mul(num, ibd));  // coset-major, like comp
@@ -1065,15 +1069,16 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         acc288_madd(c0, S.cb2[1], CUR(7));
         acc288_madd(c0, S.cb2[2], CUR(8));
         acc288_madd(c0, S.cb2[3], CUR(11));
-        acc288_madd(c1, S.cb2[12], fe_sub(CUR(7), S.v1[0]));
-        acc288_madd(c1, S.cb2[13], fe_sub(CUR(8), S.v1[1]));
+        acc288_madd(c1, S.cb2[12], CUR(7));
+        acc288_madd(c1, S.cb2[13], CUR(8));
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             fe c = CUR(12 + k);
             acc288_madd(c0, S.cb2[4 + k], c);
-            acc288_madd(c1, S.cb2[14 + k], fe_sub(c, S.v1[2 + k]));
+            acc288_madd(c1, S.cb2[14 + k], c);
         }
-        const fe num2 = fe_add(fe_mul(acc288_reduce(c0), xa), fe_mul(acc288_reduce(c1), fe_sub(x, one)));
+        const fe bs1b = fe_sub(acc288_reduce(c1), S.bnd1b);
+        const fe num2 = fe_add(fe_mul(acc288_reduce(c0), xa), fe_mul(bs1b, fe_sub(x, one)));
         comp[plane + t_id] = fe_add(res2, fe_mul(num2, ibd));
     }
 #undef ZK_ACC

@@ -465,6 +465,11 @@ Coin zk::seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub) {
 }
 
 // assertions (air/src/lib.rs:170-195) sorted by (stride, first_step, column) [P3]; CE-coset constants
+static void set_bnd1(AirConsts &K) {
+    K.bnd1 = fe_zero();
+    for (int k = 12; k < NUM_ASSERTS; k++) K.bnd1 = fe_add(K.bnd1, fe_mul(K.coeff_b[k], K.assert_val[k]));
+}
+
 static void air_static_consts(const zk_pub_inputs *pub, size_t n, AirConsts &K) {
     const int log_n = ilog2(n);
     const int first_cols[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
@@ -484,17 +489,33 @@ static void air_static_consts(const zk_pub_inputs *pub, size_t n, AirConsts &K) 
         K.assert_grp[k] = 1;
         K.assert_val[k] = fe_from_bytes(pub->stack_outputs[i]);
     }
-    const fe g = h_root_of_unity(log_n);
-    fe wce = h_root_of_unity(log_n + 3), x = fe_make(3);
-    for (int r = 0; r < 8; r++) {
-        K.xr[r] = x;
-        K.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));  // x^n constant on CE coset r
-        x = fe_mul(x, wce);
+    // the divisor constants depend only on n: computed once per n and thread (8 inversions and
+    // 10 exponentiations, host time the GPU would otherwise wait for on every proof)
+    struct DivConsts {
+        fe xr[8], inv_zn[8], g_last2, g_last1;
+    };
+    static thread_local std::map<size_t, DivConsts> cache;
+    auto it = cache.find(n);
+    if (it == cache.end()) {
+        DivConsts d;
+        const fe g = h_root_of_unity(log_n);
+        fe wce = h_root_of_unity(log_n + 3), x = fe_make(3);
+        for (int r = 0; r < 8; r++) {
+            d.xr[r] = x;
+            d.inv_zn[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));  // x^n constant on CE coset r
+            x = fe_mul(x, wce);
+        }
+        d.g_last2 = h_pow(g, n - 2);
+        d.g_last1 = h_pow(g, n - 1);
+        it = cache.emplace(n, d).first;
     }
-    K.g_last2 = h_pow(g, n - 2);
-    K.g_last1 = h_pow(g, n - 1);
+    memcpy(K.xr, it->second.xr, sizeof K.xr);
+    memcpy(K.inv_zn, it->second.inv_zn, sizeof K.inv_zn);
+    K.g_last2 = it->second.g_last2;
+    K.g_last1 = it->second.g_last1;
     K.delta = fe_make(pub->delta);
     K.lwe_size = (int)pub->lwe_size;
+    set_bnd1(K);
 }
 
 void zk::draw_air_consts(Coin &coin, const zk_pub_inputs *pub, size_t n, AirConsts &K, zk_record &R) {
@@ -524,6 +545,7 @@ void zk::draw_air_consts_ext(Coin &coin, const zk_pub_inputs *pub, size_t n, Air
     Kb = Ka;
     memcpy(Kb.coeff_t, tmp.coeff_t, sizeof Kb.coeff_t);
     memcpy(Kb.coeff_b, tmp.coeff_b, sizeof Kb.coeff_b);
+    set_bnd1(Kb);
 }
 
 void zk::ood_reseed(Coin &coin, const fe *h, int C, zk_record &R) {
@@ -578,7 +600,7 @@ FoldConsts zk::fold_consts(fe alpha, uint32_t fold) {
 
 int zk::remainder_step(std::vector<fe> &rv, uint32_t B, Coin &coin, zk_record &R, unsigned &degree_flag) {
     const size_t L = rv.size();
-    h_interp_coset(rv, fe_make(3));
+    h_interp_coset3_cached(rv);
     const size_t rl = L / B;
     for (size_t k = rl; k < L; k++)
         if (!fe_is_zero(rv[k])) degree_flag = 1;
@@ -660,8 +682,8 @@ int zk::remainder_step_ext(const std::vector<fe> &rv, uint32_t B, Coin &coin, zk
                            std::vector<fe> &rem_flat) {
     const size_t L = rv.size() / 2;
     std::vector<fe> va(rv.begin(), rv.begin() + L), vb(rv.begin() + L, rv.end());
-    h_interp_coset(va, fe_make(3));
-    h_interp_coset(vb, fe_make(3));
+    h_interp_coset3_cached(va);
+    h_interp_coset3_cached(vb);
     const size_t rl = L / B;
     if (rl > ZK_MAX_REMAINDER) ZK_FAIL(ZK_ERR_INVALID_ARG, "remainder too large");
     for (size_t k = rl; k < L; k++)

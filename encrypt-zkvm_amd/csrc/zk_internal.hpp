@@ -149,6 +149,7 @@ struct AirConsts {
     fe xr[8];       // 3 * w_CE^r
     fe g_last2, g_last1;
     fe delta;
+    fe bnd1;  // sum_k coeff_b[12+k] * assert_val[12+k]: the step n-2 group's values, subtracted once per row
     int lwe_size;
 };
 // inverse of (x - a) * (x - b) over the B cosets, written coset-major: out[r*n + q] for the point

@@ -98,6 +98,8 @@ CASES = [("push.5\npush.3\nadd", ProofOptions()), (LR_PROGRAM, ProofOptions()),
          (cipher_mix_program(60)[0], ProofOptions(num_queries=40, blowup_factor=16, fri_folding_factor=4,
                                                   fri_remainder_max_degree=31, grinding_factor=4)),
          (ops_for_trace_len(14, "cipher"), ProofOptions()),
+         # four-step coset-table LDE with 16 cosets: two 8-coset launches per pass
+         (ops_for_trace_len(13, "cipher"), ProofOptions(num_queries=28, blowup_factor=16)),
          (LR_PROGRAM, ProofOptions(num_queries=20, grinding_factor=18))]  # GPU proof-of-work search
 
 
