@@ -145,7 +145,9 @@ std::string trim(const std::string &x) {
     return a == std::string::npos ? "" : x.substr(a, b - a + 1);
 }
 
-int compile(const std::string &src, std::vector<Op> &code, fe hash[2]) {
+// Tokenize, parse and pad.  The program hash (Rescue over the padded code, mod.rs:88-95) is not computed
+// here: the processor's chiplet absorbs the same ops in the same order, so its final sponge state is it.
+int compile(const std::string &src, std::vector<Op> &code) {
     std::vector<std::string> toks;
     size_t start = 0;
     while (start <= src.size()) {
@@ -219,10 +221,6 @@ int compile(const std::string &src, std::vector<Op> &code, fe hash[2]) {
         code.push_back(op);
     }
     code.resize(pad16(code.size()), Op{NOOP, 0});
-    Rescue r;
-    for (const Op &o : code) r.update(o.code, o.value);
-    hash[0] = r.s[0];
-    hash[1] = r.s[1];
     return ZK_OK;
 }
 
@@ -349,8 +347,7 @@ extern "C" int zk_vm_trace(const char *source, const uint8_t *public_in, size_t 
     if (!source || !last_row || !n_out || lwe_size == 0 || lwe_size > 15 || (num_secret && !secret))
         return ZK_ERR_INVALID_ARG;
     std::vector<Op> code;
-    fe hash[2];
-    int rc = compile(source, code, hash);
+    int rc = compile(source, code);
     if (rc) return rc;
     if (!trace_out) {
         // size query: one clock per compiled op, so the length follows from the program alone
@@ -375,9 +372,9 @@ extern "C" int zk_vm_trace(const char *source, const uint8_t *public_in, size_t 
     P.write(reinterpret_cast<fe *>(trace_out), n, last.data());
     if (outputs)
         for (int i = 0; i < MAX_STACK; i++) fe_to_bytes(P.reg[i][P.clk], outputs + 16 * i);
-    if (program_hash) {
-        fe_to_bytes(hash[0], program_hash);
-        fe_to_bytes(hash[1], program_hash + 16);
+    if (program_hash) {  // Program::compile's hash = the chiplet's sponge after the whole program
+        fe_to_bytes(P.rescue.s[0], program_hash);
+        fe_to_bytes(P.rescue.s[1], program_hash + 16);
     }
     return ZK_OK;
 }
