@@ -25,6 +25,12 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_writ
 echo "pmc write ok"
 python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -o "$O/pmc_traffic_$TAG.json"
 cp "$O/pmc_traffic_$TAG.json" "$R/profiles/pmc_traffic.json"
+# VALU issue rate: 6 SQ + 2 GRBM counters, one pass of its own
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_LDS SQ_BUSY_CYCLES \
+  SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$O/pmc_sq_$TAG" -o sq -- \
+  python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_sq_$TAG.err"
+python3 "$R/tools/pmc_valu.py" "$O/pmc_sq_$TAG" -o "$O/pmc_valu_$TAG.md"
+echo "pmc sq ok"
 # keep only the summaries (the per-dispatch counter CSVs are large)
 find "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
 (cd "$R" && timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err")
