@@ -906,12 +906,35 @@ int zk::ensure_ext(zk_prover *p) {
     return ZK_OK;
 }
 
+// S4, shared by zk_prove_device and plug point 3 (build_constraint_commitment): interpolate the 8n
+// composition values (coset-major in comp, KX planes) over the CE coset, split the polynomial into C
+// column polynomials of n coefficients (p->cpolys; base column (c, j) of E column c at (c*KX + j)*n),
+// extend them over the B LDE cosets into clde and commit to its rows (a leaf is C E values).
+// p->flag is set when the interpolant has a coefficient at or beyond C*n (the degree check).
+static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe *ctmp, fe *clde, uint8_t root[32]) {
+    const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b, CE = 8 * n;
+    const int CK = C * KX;
+    ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
+    ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
+    for (int j = 0; j < KX; j++) {
+        CrossMap m;
+        for (int r = 0; r < 8; r++) m.c[r] = ctmp + (size_t)(8 * j + r) * n;
+        m.k0 = 0;
+        m.kcount = n;
+        m.pstride = (size_t)KX * n;
+        comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
+                          h_inv(h_pow(fe_make(3), n)), C, p->cpolys + (size_t)j * n, p->flag);
+    }
+    ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, 0, 1, (int)B, clde, B * n, n, p->tmp);
+    return commit_rows(p, clde, CK, pl->log_n, pl->log_b, p->cleaves, p->cnodes, root);
+}
+
 int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                     uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     if (!p || !d_trace_v || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
-    const size_t N = n * B, CE = 8 * n;
+    const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));
     Plan *pl = nullptr;
     ZK_TRY(get_plan(p, n, B, &pl));
@@ -919,7 +942,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     const int C = num_comp_cols(n);
     if (C > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition column count exceeds 8");
     const fe *d_trace = (const fe *)d_trace_v;
-    const fe g = h_root_of_unity(log_n), three = fe_make(3);
+    const fe g = h_root_of_unity(log_n);
     zk_record R;
     memset(&R, 0, sizeof R);
     R.trace_len = (uint32_t)n;
@@ -970,20 +993,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     stage_mark(p, "constraints");
 
     // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit.
-    // Base column (c, j) of the E column c lives at cpolys[(c*k + j)*n]: a leaf is C E values.
-    ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
-    ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
-    for (int j = 0; j < KX; j++) {
-        CrossMap m;
-        for (int r = 0; r < 8; r++) m.c[r] = ctmp + (size_t)(8 * j + r) * n;
-        m.k0 = 0;
-        m.kcount = n;
-        m.pstride = (size_t)KX * n;
-        comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
-                          h_inv(h_pow(three, n)), C, p->cpolys + (size_t)j * n, p->flag);
-    }
-    ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, 0, 1, (int)B, clde, B * n, n, p->tmp);
-    ZK_TRY(commit_rows(p, clde, CK, log_n, log_b, p->cleaves, p->cnodes, R.constraint_root));
+    ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
     ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
@@ -1242,18 +1252,19 @@ int zk_lde_read_frame(zk_trace_lde *h, size_t step, uint8_t *cur, uint8_t *next)
     return ZK_OK;
 }
 
-int zk_lde_query(zk_trace_lde *h, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
-                 size_t *proof_len) {
-    if (!h || !positions || !rows_out || !proof_len || k == 0 || k > ZK_MAX_QUERIES)
+// rows at `positions` of a committed coset-major LDE (ncols columns) + the batch Merkle proof bytes
+static int query_committed_rows(zk_prover *p, const fe *base, int ncols, size_t n, uint32_t B, const uint8_t *leaves,
+                                const uint8_t *nodes, const uint64_t *positions, size_t k, uint8_t *rows_out,
+                                uint8_t *proof_out, size_t *proof_len) {
+    if (!positions || !rows_out || !proof_len || k == 0 || k > ZK_MAX_QUERIES)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid query arguments");
-    zk_prover *p = h->p;
-    const size_t N = h->n * h->B;
+    const size_t N = n * B;
     std::vector<uint64_t> pos(positions, positions + k);
     for (uint64_t x : pos)
         if (x >= N) ZK_FAIL(ZK_ERR_INVALID_ARG, "query position out of range");
     ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, pos.data(), k * 8, hipMemcpyHostToDevice, p->st));
-    gather_rows(p->st, p->lde, W, ilog2(h->n), ilog2(h->B), p->gather_idx, k, p->gather_out);
-    ZK_CHECK_HIP(hipMemcpyAsync(rows_out, p->gather_out, k * W * 16, hipMemcpyDeviceToHost, p->st));
+    gather_rows(p->st, base, ncols, ilog2(n), ilog2(B), p->gather_idx, k, p->gather_out);
+    ZK_CHECK_HIP(hipMemcpyAsync(rows_out, p->gather_out, k * ncols * 16, hipMemcpyDeviceToHost, p->st));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     BatchPlan bp = plan_batch(N, pos);
     Bytes out;
@@ -1262,7 +1273,7 @@ int zk_lde_query(zk_trace_lde *h, const uint64_t *positions, size_t k, uint8_t *
         out.u8((uint8_t)path.size());
         for (auto &e : path) {
             uint8_t d[32];
-            ZK_CHECK_HIP(hipMemcpy(d, (e.first ? p->nodes : p->leaves) + 32 * e.second, 32, hipMemcpyDeviceToHost));
+            ZK_CHECK_HIP(hipMemcpy(d, (e.first ? nodes : leaves) + 32 * e.second, 32, hipMemcpyDeviceToHost));
             out.put(d, 32);
         }
     }
@@ -1271,6 +1282,14 @@ int zk_lde_query(zk_trace_lde *h, const uint64_t *positions, size_t k, uint8_t *
     if (!proof_out || cap < out.v.size()) ZK_FAIL(ZK_ERR_BUFFER_TOO_SMALL, "proof buffer too small");
     memcpy(proof_out, out.v.data(), out.v.size());
     return ZK_OK;
+}
+
+int zk_lde_query(zk_trace_lde *h, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
+                 size_t *proof_len) {
+    if (!h) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    zk_prover *p = h->p;
+    return query_committed_rows(p, p->lde, W, h->n, h->B, p->leaves, p->nodes, positions, k, rows_out, proof_out,
+                                proof_len);
 }
 
 void zk_lde_free(zk_trace_lde *h) { delete h; }
@@ -1299,6 +1318,52 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
     coset_major_rows_to_host(p, p->comp, 1, n, 8, out);
     return ZK_OK;
 }
+
+// ---------------------------------------------------------------- plug point 3: constraint commitment
+struct zk_comp_commit {
+    zk_prover *p;
+    size_t n;
+    uint32_t B;
+    int ncols;
+};
+
+int zk_commit_composition(zk_trace_lde *h, const uint8_t *composition, uint32_t num_cols, zk_comp_commit **out,
+                          uint8_t root[32], uint8_t *polys_out) {
+    if (!h || !composition || !out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (num_cols < 1 || num_cols > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "num_cols must be in [1, 8]");
+    zk_prover *p = h->p;
+    const size_t n = h->n, CE = 8 * n;
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    Plan *pl;
+    int rc = get_plan(p, n, h->B, &pl);
+    if (rc) return rc;
+    // natural CE order (step i = r + 8q) -> coset-major comp[r*n + q], the evaluator's layout
+    std::vector<fe> cm(CE);
+    const fe *in = reinterpret_cast<const fe *>(composition);
+    for (size_t i = 0; i < CE; i++) memcpy(&cm[(i & 7) * n + (i >> 3)], in + i, sizeof(fe));
+    ZK_CHECK_HIP(hipMemcpyAsync(p->comp, cm.data(), CE * sizeof(fe), hipMemcpyHostToDevice, p->st));
+    uint8_t r[32];
+    if ((rc = composition_stage(p, pl, 1, (int)num_cols, p->comp, p->ctmp, p->clde, r))) return rc;
+    unsigned degree_flag = 0;
+    ZK_CHECK_HIP(hipMemcpyAsync(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost, p->st));
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    if (degree_flag) ZK_FAIL(ZK_ERR_DEGREE, "composition polynomial degree exceeds num_cols * trace_len");
+    if (polys_out)
+        ZK_CHECK_HIP(hipMemcpy(polys_out, p->cpolys, (size_t)num_cols * n * sizeof(fe), hipMemcpyDeviceToHost));
+    if (root) memcpy(root, r, 32);
+    *out = new zk_comp_commit{p, n, h->B, (int)num_cols};
+    return ZK_OK;
+}
+
+int zk_comp_query(zk_comp_commit *h, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
+                  size_t *proof_len) {
+    if (!h) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    zk_prover *p = h->p;
+    return query_committed_rows(p, p->clde, h->ncols, h->n, h->B, p->cleaves, p->cnodes, positions, k, rows_out,
+                                proof_out, proof_len);
+}
+
+void zk_comp_free(zk_comp_commit *h) { delete h; }
 
 // ---------------------------------------------------------------- diagnostics
 // Host execution of the lazy dot product (acc288: unreduced 256-bit products, one reduction)

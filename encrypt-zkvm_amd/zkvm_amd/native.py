@@ -30,7 +30,7 @@ MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 3
 EXPORTED = (
     "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_destroy", "zk_prover_trace_buffer",
     "zk_prove", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
-    "zk_eval_constraints", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_vm_trace",
+    "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_vm_trace",
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_destroy", "zk_prove_sharded",
 )
 
@@ -98,6 +98,10 @@ def lib():
         L.zk_lde_free.argtypes = [vp]
         L.zk_lde_free.restype = None
         L.zk_eval_constraints.argtypes = [vp, C.POINTER(PubInputs), vp, vp, vp]
+        L.zk_commit_composition.argtypes = [vp, vp, u32, C.POINTER(vp), vp, vp]
+        L.zk_comp_query.argtypes = [vp, vp, sz, vp, vp, C.POINTER(sz)]
+        L.zk_comp_free.argtypes = [vp]
+        L.zk_comp_free.restype = None
         L.zk_prover_stage_times.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32, C.POINTER(i32)]
         L.zk_prover_profile.argtypes = [vp, i32]
         L.zk_prover_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(i32),

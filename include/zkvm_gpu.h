@@ -147,6 +147,23 @@ void zk_lde_free(zk_trace_lde *lde);
 int zk_eval_constraints(zk_trace_lde *lde, const zk_pub_inputs *pub, const uint8_t *coeff_t, const uint8_t *coeff_b,
                         uint8_t *out);
 
+/* ---- plug point 3: Prover::build_constraint_commitment (winterfell 0.9 provided method;
+ * SURVEY.md 8(b); its input is the CompositionPolyTrace new_evaluator's evaluate returns,
+ * prover/src/lib.rs:65-72) ----
+ * composition: the 8n values zk_eval_constraints writes (natural CE-domain order).  Interpolates them
+ * over the CE coset, splits the polynomial into num_cols column polynomials of n coefficients
+ * (CompositionPoly; polys_out, optional: num_cols x n, column-major), extends each over the trace
+ * LDE's blowup coset domain and commits to the rows (ConstraintCommitment; root).  Returns
+ * ZK_ERR_DEGREE (no handle) when the polynomial has a coefficient at or beyond num_cols * n.  The
+ * handle reads the prover's device memory: valid until the next proof or commitment on that prover. */
+typedef struct zk_comp_commit zk_comp_commit;
+int zk_commit_composition(zk_trace_lde *lde, const uint8_t *composition, uint32_t num_cols, zk_comp_commit **out,
+                          uint8_t root[32], uint8_t *polys_out);
+/* ConstraintCommitment::query: rows (num_cols elements each) at positions + batch Merkle proof bytes */
+int zk_comp_query(zk_comp_commit *comp, const uint64_t *positions, size_t k, uint8_t *rows_out, uint8_t *proof_out,
+                  size_t *proof_len);
+void zk_comp_free(zk_comp_commit *comp);
+
 /* ---- one proof sharded over several GPUs ----
  * The LDE domain is split by coset: rank g of `world` (1, 2, 4 or 8; blowup 8) owns cosets
  * r = g (mod world).  Exchanges (leaf digests, composition coefficient slices, FRI layer 1, openings)

@@ -215,6 +215,38 @@ def test_plug_points(gpu, oracle):
     L.zk_lde_free(h)
 
 
+def test_plug_point_constraint_commitment(gpu, oracle):
+    """zk_commit_composition / zk_comp_query (build_constraint_commitment) against the oracle's composition
+    column polynomials, composition LDE and constraint root."""
+    trace, pub = workload_trace(cipher_mix_program(60)[0], seed=7)
+    n = trace.shape[1]
+    L = native.lib()
+    h = C.c_void_p()
+    tb = np.ascontiguousarray(trace)
+    native.check(L.zk_lde_new(gpu.handle, tb.ctypes.data, 28, n, 8, C.byref(h), C.create_string_buffer(32)))
+    _, orec, od = oracle.prove(trace, oracle_pub(oracle, pub), want=("composition", "comp_polys", "comp_lde"))
+    ncols = orec.num_ccols
+    comp = np.ascontiguousarray(od["composition"])
+    cc, root = C.c_void_p(), C.create_string_buffer(32)
+    polys = C.create_string_buffer(16 * ncols * n)
+    native.check(L.zk_commit_composition(h, comp.ctypes.data, ncols, C.byref(cc), root, polys))
+    assert root.raw == bytes(orec.constraint_root)
+    assert polys.raw == od["comp_polys"].reshape(-1, 2)[: ncols * n].tobytes()
+    clde = od["comp_lde"].reshape(-1, 2)[: 8 * n * ncols].reshape(8 * n, ncols, 2)
+    pos = (C.c_uint64 * 4)(0, 3, 8 * n - 1, 77)
+    rows = C.create_string_buffer(4 * ncols * 16)
+    plen = C.c_size_t(1 << 16)
+    pbuf = C.create_string_buffer(1 << 16)
+    native.check(L.zk_comp_query(cc, pos, 4, rows, pbuf, C.byref(plen)))
+    assert rows.raw == b"".join(clde[p].tobytes() for p in (0, 3, 8 * n - 1, 77))
+    assert 0 < plen.value < (1 << 16)
+    L.zk_comp_free(cc)
+    # a composition of too high a degree is refused: more columns' worth of coefficients than num_cols
+    rc = L.zk_commit_composition(h, comp.ctypes.data, ncols - 1, C.byref(cc), root, None)
+    assert rc == native.ZK_ERR_DEGREE
+    L.zk_lde_free(h)
+
+
 def test_invalid_trace_is_reported(gpu):
     trace, pub = workload_trace(LR_PROGRAM, seed=4)
     bad = trace.copy()
