@@ -766,6 +766,31 @@ void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_
                                                 log_n, Tn.fwd_lo, Tn.fwd_hi, a, b, out, threads));
 }
 
+// Per-row divisor factors of the composition (once per plan: they depend only on the domain point x).
+// In place over the 1/((x - 1)(x - g2)) table that batch_inv_pairs wrote to plane 0:
+//   plane 0: (x - g2)(x - g1) / (x^n - 1)  transition divisor with the two exemptions, inverted
+//   plane 1: 1 / (x - 1)                    step-0 assertions
+//   plane 2: 1 / (x - g2)                   step-(n-2) assertions
+__global__ void __launch_bounds__(256) k_divisor_tables(const fe *xr, int log_n, size_t P, const fe *wlo, const fe *whi,
+                                                        fe g1, fe g2, Fe8 inv_zn, fe *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < P; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i >> log_n;
+        const fe x = fe_mul(xr[r], pow_split(wlo, whi, i & (((size_t)1 << log_n) - 1)));
+        const fe ibd = out[i], xa = fe_sub(x, g2), x1 = fe_sub(x, fe_one());
+        out[i] = fe_mul(fe_mul(xa, fe_sub(x, g1)), inv_zn.v[r]);
+        out[P + i] = fe_mul(xa, ibd);
+        out[2 * P + i] = fe_mul(x1, ibd);
+    }
+}
+
+void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_cos, int log_n, fe g1, fe g2,
+                    const Fe8 &inv_zn, fe *out) {
+    batch_inv_pairs(st, Tn, xr, log_cos, log_n, fe_one(), g2, out);
+    const size_t P = (size_t)1 << (log_cos + log_n);
+    ZK_PROF(st, "batch_inv", 64.0 * P, hipLaunchKernelGGL(k_divisor_tables, dim3(cdiv(P, 256)), dim3(256), 0, st, xr,
+                                                           log_n, P, Tn.fwd_lo, Tn.fwd_hi, g1, g2, inv_zn, out));
+}
+
 // ================================================================ constraint evaluation (K3)
 // ProcessorAir::evaluate_transition (air/src/lib.rs:104-168, constrains.rs:95-216, flags.rs:37-91)
 // fused with DefaultConstraintEvaluator's merge (sum of coeff * C_k), the transition divisor and the
@@ -796,8 +821,8 @@ __device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
 // Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
 // SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
 struct EvalShared {
-    fe ct[20], cb[22], ct2[20], cb2[22], xr[8], inv_zn[8], inv_mds[16];
-    fe g_last2, g_last1, delta, bnd1, bnd1b;
+    fe ct[20], cb[22], ct2[20], cb2[22], inv_mds[16];
+    fe delta, bnd1, bnd1b;
 };
 
 #ifndef ZK_EVAL_LAZY
@@ -813,27 +838,21 @@ struct EvalShared {
 // E values; the composition is linear in them, so each constraint value is folded into two
 // accumulators (K = a components, K2 = b components) and two planes comp[t], comp[plane + t] are written.
 template <int KE>
-__global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_EXT) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *wn_lo,
-                                                          const fe *wn_hi, const fe *periodic, const fe *inv_bd,
-                                                          const AirConsts *K, const AirConsts *K2, size_t plane,
-                                                          fe *comp) {
+__global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_EXT) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *periodic,
+                                                          const fe *divs, const AirConsts *K, const AirConsts *K2,
+                                                          size_t plane, fe *comp) {
     __shared__ EvalShared S;
     {
+        // one LDS slot per thread, every range bounded on both sides
         const int t = threadIdx.x;
-        if (KE == 2 && t >= 128 && t < 148) S.ct2[t - 128] = K2->coeff_t[t - 128];
-        else if (KE == 2 && t >= 148 && t < 170) S.cb2[t - 148] = K2->coeff_b[t - 148];
-        else if (t < 20) S.ct[t] = K->coeff_t[t];
+        if (t < 20) S.ct[t] = K->coeff_t[t];
         else if (t < 42) S.cb[t - 20] = K->coeff_b[t - 20];
         else if (t == 42) S.bnd1 = K->bnd1;
         else if (t == 43) S.bnd1b = KE == 2 ? K2->bnd1 : fe_zero();
-        else if (t < 52) {
-        }  // idle
-        else if (t < 60) S.xr[t - 52] = K->xr[t - 52];
-        else if (t < 68) S.inv_zn[t - 60] = K->inv_zn[t - 60];
-        else if (t < 84) S.inv_mds[t - 68] = c_inv_mds[t - 68];
-        else if (t == 84) S.g_last2 = K->g_last2;
-        else if (t == 85) S.g_last1 = K->g_last1;
-        else if (t == 86) S.delta = K->delta;
+        else if (t == 44) S.delta = K->delta;
+        else if (t >= 64 && t < 80) S.inv_mds[t - 64] = c_inv_mds[t - 64];
+        else if (KE == 2 && t >= 128 && t < 148) S.ct2[t - 128] = K2->coeff_t[t - 128];
+        else if (KE == 2 && t >= 148 && t < 170) S.cb2[t - 148] = K2->coeff_b[t - 148];
         __syncthreads();
     }
     const int L = K->lwe_size;
@@ -1036,10 +1055,10 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
 #undef ZK_SEQS
     }
     ZK_SEQ(cb, t.lo);
-    // divisors: transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1))); boundary groups (x - 1), (x - g^(n-2))
-    const fe x = fe_mul(S.xr[rc], pow_split(wn_lo, wn_hi, q));
-    const fe xa = fe_sub(x, S.g_last2);
-    fe res = fe_mul(fe_mul(fe_mul(t, xa), fe_sub(x, S.g_last1)), S.inv_zn[rc]);
+    // divisors (per-row factors from divisor_tables): transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1)));
+    // boundary groups (x - 1) and (x - g^(n-2)).  res = t dT + bs0 d0 + bs1 d1 as one lazy sum.
+    const size_t P = CE;
+    const fe dT = divs[t_id], d0 = divs[P + t_id], d1 = divs[2 * P + t_id];
     // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
     // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
     acc288 a0 = acc288_zero(), a1 = acc288_zero();
@@ -1057,13 +1076,14 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     }
     // sum_k cb[12+k] (c_k - v_k) = sum_k cb[12+k] c_k - bnd1 (bnd1 precomputed on the host)
     const fe bs0 = acc288_reduce(a0), bs1 = fe_sub(acc288_reduce(a1), S.bnd1);
-    const fe ibd = inv_bd[t_id];
-    fe num = fe_add(fe_mul(bs0, xa), fe_mul(bs1, fe_sub(x, one)));
-    res = fe_add(res, fe_mul(num, ibd));  // coset-major, like comp
-    comp[t_id] = res;
+    acc288 aR = acc288_zero();
+    acc288_madd(aR, t, dT);
+    acc288_madd(aR, bs0, d0);
+    acc288_madd(aR, bs1, d1);
+    const fe res = acc288_reduce(aR);
+    comp[t_id] = res;  // coset-major, like the divisor tables
     if (KE == 2) {
         ZK_SEQ(cb, res.lo);
-        fe res2 = fe_mul(fe_mul(fe_mul(t2, xa), fe_sub(x, S.g_last1)), S.inv_zn[rc]);
         acc288 c0 = acc288_zero(), c1 = acc288_zero();
         acc288_madd(c0, S.cb2[0], CUR(0));
         acc288_madd(c0, S.cb2[1], CUR(7));
@@ -1077,9 +1097,12 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             acc288_madd(c0, S.cb2[4 + k], c);
             acc288_madd(c1, S.cb2[14 + k], c);
         }
-        const fe bs1b = fe_sub(acc288_reduce(c1), S.bnd1b);
-        const fe num2 = fe_add(fe_mul(acc288_reduce(c0), xa), fe_mul(bs1b, fe_sub(x, one)));
-        comp[plane + t_id] = fe_add(res2, fe_mul(num2, ibd));
+        const fe bs0b = acc288_reduce(c0), bs1b = fe_sub(acc288_reduce(c1), S.bnd1b);
+        acc288 aR2 = acc288_zero();
+        acc288_madd(aR2, t2, dT);
+        acc288_madd(aR2, bs0b, d0);
+        acc288_madd(aR2, bs1b, d1);
+        comp[plane + t_id] = acc288_reduce(aR2);
     }
 #undef ZK_ACC
 #undef CUR
@@ -1100,33 +1123,31 @@ static void upload_rescue(hipStream_t st) {
     g_consts_uploaded = true;
 }
 
-void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
-                      const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
-    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, Tn, periodic, inv_bd, consts_dev,
-                            comp);
+void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+                      const AirConsts *consts_dev, fe *comp) {
+    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp);
 }
 
-void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
-                             const fe *periodic, const fe *inv_bd, const AirConsts *consts_dev, fe *comp) {
+void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+                             const fe *divs, const AirConsts *consts_dev, fe *comp) {
     upload_rescue(st);
     const size_t CE = (size_t)map.nce << log_n;
     ZK_PROF(st, "eval_constraints", (448.0 * (map.lshift == 0 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL((k_eval_constraints<1>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts_dev, consts_dev, (size_t)0, comp));
+                                                       map, periodic, divs, consts_dev, consts_dev, (size_t)0, comp));
 }
 
-void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
-                                 const fe *periodic, const fe *inv_bd, const AirConsts *consts2_dev, size_t plane,
-                                 fe *comp) {
+void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp) {
     upload_rescue(st);
     const size_t CE = (size_t)map.nce << log_n;
     ZK_PROF(st, "eval_constraints_ext", (448.0 * (map.lshift == 0 ? 1 : 2) + 48.0) * CE, hipLaunchKernelGGL((k_eval_constraints<2>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, Tn.fwd_lo, Tn.fwd_hi, periodic, inv_bd, consts2_dev, consts2_dev + 1, plane, comp));
+                                                       map, periodic, divs, consts2_dev, consts2_dev + 1, plane, comp));
 }
 
-void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
-                          const fe *inv_bd, const AirConsts *consts2_dev, fe *comp) {
-    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, Tn, periodic, inv_bd,
-                                consts2_dev, (size_t)8 << log_n, comp);
+void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+                          const AirConsts *consts2_dev, fe *comp) {
+    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
+                                (size_t)8 << log_n, comp);
 }
 
 // ================================================================ composition interpolation (K4)

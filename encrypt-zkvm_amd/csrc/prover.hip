@@ -199,12 +199,22 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     return ZK_OK;
 }
 
+Fe8 zk::ce_inv_zn(int log_n) {
+    const size_t n = (size_t)1 << log_n;
+    const fe wce = h_root_of_unity(log_n + 3);
+    Fe8 z;
+    fe x = fe_make(3);
+    for (int r = 0; r < 8; r++, x = fe_mul(x, wce)) z.v[r] = h_inv(fe_sub(h_pow(x, n), fe_one()));
+    return z;
+}
+
 const fe *zk::boundary_inverses(zk_prover *p, Plan *pl) {
     if (!pl->bnd_inv) {
-        const size_t CE = (size_t)8 << pl->log_n;
-        if (p->arena.alloc(&pl->bnd_inv, CE) != hipSuccess) return nullptr;
-        const fe g_last2 = h_pow(h_root_of_unity(pl->log_n), ((size_t)1 << pl->log_n) - 2);
-        batch_inv_pairs(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, fe_one(), g_last2, pl->bnd_inv);
+        const size_t CE = (size_t)8 << pl->log_n, n = (size_t)1 << pl->log_n;
+        if (p->arena.alloc(&pl->bnd_inv, 3 * CE) != hipSuccess) return nullptr;
+        const fe g = h_root_of_unity(pl->log_n);
+        divisor_tables(p->st, pl->Tn, pl->xr_ce, 3, pl->log_n, h_pow(g, n - 1), h_pow(g, n - 2), ce_inv_zn(pl->log_n),
+                       pl->bnd_inv);
     }
     return pl->bnd_inv;
 }
@@ -241,7 +251,6 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->ctmp, CE));
     ZK_CHECK_HIP(A.alloc(&p->cpolys, (size_t)ZK_MAX_CCOLS * n));
     ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * N));
-    ZK_CHECK_HIP(A.alloc(&p->inv, std::max(N, CE)));
     ZK_CHECK_HIP(A.alloc(&p->deep, N));
     ZK_CHECK_HIP(A.alloc(&p->ulde, N));
     ZK_CHECK_HIP(A.alloc(&p->dscratch, 4 * (2048 + n / 2048 + 2) + 3 * n + 2 * (n / 256 + 1)));
@@ -978,8 +987,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, binv, (const AirConsts *)p->air_consts,
-                         comp);
+        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp);
         HT.stop("air_consts");
     } else {
         AirConsts Kp[2];
@@ -987,8 +995,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->Tn, pl->periodic, binv, (const AirConsts *)p->x_air,
-                             comp);
+        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp);
     }
     stage_mark(p, "constraints");
 
@@ -1312,8 +1319,8 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
     ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
     const fe *binv = boundary_inverses(p, pl);
     if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->Tn, pl->periodic, binv,
-                     (const AirConsts *)p->air_consts, p->comp);
+    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->periodic, binv, (const AirConsts *)p->air_consts,
+                     p->comp);
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     coset_major_rows_to_host(p, p->comp, 1, n, 8, out);
     return ZK_OK;

@@ -80,7 +80,10 @@ struct Plan {  // everything that depends only on (n, B)
     fe *bnd_inv = nullptr;
 };
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
+// the evaluator's divisor tables for the 8 CE cosets (divisor_tables: 3 planes of 8n), built once per plan
 const fe *boundary_inverses(zk_prover *p, Plan *pl);
+// 1 / (x^n - 1) on the 8 CE cosets x = 3 w_8n^r <w_n>
+Fe8 ce_inv_zn(int log_n);
 struct Openings;
 
 }  // namespace zk
@@ -92,7 +95,7 @@ struct zk_prover {
     uint32_t max_b = 0;
     zk::DeviceArena arena;
     fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,
-       *cpolys = nullptr, *clde = nullptr, *inv = nullptr, *deep = nullptr, *fri = nullptr;
+       *cpolys = nullptr, *clde = nullptr, *deep = nullptr, *fri = nullptr;
     fe *ulde = nullptr;      // LDE of the DEEP polynomial (B*n, coset-major)
     fe *dscratch = nullptr;  // DEEP division scratch (power tables, suffix-sum inputs, coefficients)
     fe *x_ulde = nullptr, *x_dscratch = nullptr;  // the same for FieldExtension::Quadratic

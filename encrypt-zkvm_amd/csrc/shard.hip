@@ -335,15 +335,18 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         fe xr[8];
         for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] + G * j];
         ZK_CHECK_HIP(hipMemcpyAsync(p->sh_xr, xr, Bl * sizeof(fe), hipMemcpyHostToDevice, p->st));
-        batch_inv_pairs(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, fe_one(), K.g_last2, p->inv);
+        // divisor tables of the local CE cosets (3 planes of Bl*n) in the NTT scratch, free until S4
+        Fe8 zloc{};
+        for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] + G * j];
+        divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, p->tmp);
         const EvalMap em{Bl, X.rank[l], G, 0, Bl};
         if (KX == 1) {
             ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
-            eval_constraints_mapped(p->st, p->lde, log_n, em, pl->Tn, pl->periodic, p->inv,
+            eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
                                     (const AirConsts *)p->air_consts, p->comp);
         } else {
             ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
-            eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->Tn, pl->periodic, p->inv,
+            eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
                                         (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp);
         }
     }

@@ -156,13 +156,21 @@ struct AirConsts {
 // x = xr[r] * w_n^q (natural domain index i = r + B*q)
 void batch_inv_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe a, fe b,
                      fe *out);
+struct Fe8 {
+    fe v[8];
+};
+// The evaluator's per-row divisor factors over 2^log_cos cosets (offsets xr, coset-major, planes of
+// P = 2^(log_cos + log_n)): out[i] = (x - g2)(x - g1) inv_zn[coset], out[P + i] = 1/(x - 1),
+// out[2P + i] = 1/(x - g2); inv_zn[c] = 1/(xr[c]^n - 1).  3P elements.
+void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_cos, int log_n, fe g1, fe g2,
+                    const Fe8 &inv_zn, fe *out);
 // Which CE cosets one launch evaluates: local coset jl < nce is global CE coset ce0 + cestep*jl, and its
 // LDE rows are LDE coset slot jl << lshift of a buffer holding lde_cosets cosets per column.
 struct EvalMap {
     int nce, ce0, cestep, lshift, lde_cosets;
 };
-void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
-                             const fe *periodic, const fe *inv_bd, const AirConsts *consts_dev, fe *comp);
+void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+                             const fe *divs, const AirConsts *consts_dev, fe *comp);
 // Inputs of the cross-coset step for coefficients k0 .. k0+kcount: c[r][kl] = c_r[k0 + kl]; output
 // polys[k2 * pstride + kl].
 struct CrossMap {
@@ -172,8 +180,8 @@ struct CrossMap {
 void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, const PowTable &inv3, fe scale,
                        fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
-void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
-                      const fe *inv_bd, const AirConsts *consts_dev, fe *comp);
+void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+                      const AirConsts *consts_dev, fe *comp);
 // cross-coset step of the size-8n interpolation: per k1 < n, from the 8 per-coset inverse NTTs
 // (c_r[k1]), produce coefficients a[k1 + n*k2] = 3^-(k1+n k2) / (8n) * sum_r w8^(-r k2) w_8n^(-r k1) c_r[k1]
 // and write column k2 < ncols of the segmented composition polynomial: polys[k2*n + k1].
@@ -233,12 +241,11 @@ void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev
 void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
                   fe *tab, fe *partials, fe *out);
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
-void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const NttTables &Tn, const fe *periodic,
-                          const fe *inv_bd, const AirConsts *consts2_dev, fe *comp);
+void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+                          const AirConsts *consts2_dev, fe *comp);
 // ... over the CE cosets of `map` (see eval_constraints_mapped), b plane at comp + plane
-void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const NttTables &Tn,
-                                 const fe *periodic, const fe *inv_bd, const AirConsts *consts2_dev, size_t plane,
-                                 fe *comp);
+void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp);
 // out[i] = 1 / (N(x_i - z) N(x_i - zg)), N the norm E -> F (coset-major like batch_inv_pairs)
 void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,
                           fe *out);
