@@ -837,7 +837,9 @@ struct EvalShared {
 // KE coefficient planes: KE = 2 for FieldExtension::Quadratic, where the composition coefficients are
 // E values; the composition is linear in them, so each constraint value is folded into two
 // accumulators (K = a components, K2 = b components) and two planes comp[t], comp[plane + t] are written.
-template <int KE>
+// BND: evaluate the boundary (assertion) terms here.  The single-GPU prover passes false and adds them
+// in coefficient form instead (boundary_poly_add); the plug point and the sharded prover pass true.
+template <int KE, bool BND>
 __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_EXT) k_eval_constraints(const fe *lde, int log_n, EvalMap map, const fe *periodic,
                                                           const fe *divs, const AirConsts *K, const AirConsts *K2,
                                                           size_t plane, fe *comp) {
@@ -1058,51 +1060,57 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     // divisors (per-row factors from divisor_tables): transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1)));
     // boundary groups (x - 1) and (x - g^(n-2)).  res = t dT + bs0 d0 + bs1 d1 as one lazy sum.
     const size_t P = CE;
-    const fe dT = divs[t_id], d0 = divs[P + t_id], d1 = divs[2 * P + t_id];
-    // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
-    // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
-    acc288 a0 = acc288_zero(), a1 = acc288_zero();
-    acc288_madd(a0, S.cb[0], CUR(0));
-    acc288_madd(a0, S.cb[1], CUR(7));
-    acc288_madd(a0, S.cb[2], CUR(8));
-    acc288_madd(a0, S.cb[3], CUR(11));
-    acc288_madd(a1, S.cb[12], CUR(7));
-    acc288_madd(a1, S.cb[13], CUR(8));
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        fe c = CUR(12 + k);
-        acc288_madd(a0, S.cb[4 + k], c);
-        acc288_madd(a1, S.cb[14 + k], c);
-    }
-    // sum_k cb[12+k] (c_k - v_k) = sum_k cb[12+k] c_k - bnd1 (bnd1 precomputed on the host)
-    const fe bs0 = acc288_reduce(a0), bs1 = fe_sub(acc288_reduce(a1), S.bnd1);
-    acc288 aR = acc288_zero();
-    acc288_madd(aR, t, dT);
-    acc288_madd(aR, bs0, d0);
-    acc288_madd(aR, bs1, d1);
-    const fe res = acc288_reduce(aR);
-    comp[t_id] = res;  // coset-major, like the divisor tables
-    if (KE == 2) {
-        ZK_SEQ(cb, res.lo);
-        acc288 c0 = acc288_zero(), c1 = acc288_zero();
-        acc288_madd(c0, S.cb2[0], CUR(0));
-        acc288_madd(c0, S.cb2[1], CUR(7));
-        acc288_madd(c0, S.cb2[2], CUR(8));
-        acc288_madd(c0, S.cb2[3], CUR(11));
-        acc288_madd(c1, S.cb2[12], CUR(7));
-        acc288_madd(c1, S.cb2[13], CUR(8));
+    const fe dT = divs[t_id];
+    if constexpr (!BND) {
+        comp[t_id] = fe_mul(t, dT);  // coset-major, like the divisor tables
+        if (KE == 2) comp[plane + t_id] = fe_mul(t2, dT);
+    } else {
+        const fe d0 = divs[P + t_id], d1 = divs[2 * P + t_id];
+        // assertions (air/src/lib.rs:170-195), sorted: step 0 -> cols 0,7,8,11,12..19 (value 0);
+        // step n-2 -> cols 7,8 (program hash), 12..19 (outputs)
+        acc288 a0 = acc288_zero(), a1 = acc288_zero();
+        acc288_madd(a0, S.cb[0], CUR(0));
+        acc288_madd(a0, S.cb[1], CUR(7));
+        acc288_madd(a0, S.cb[2], CUR(8));
+        acc288_madd(a0, S.cb[3], CUR(11));
+        acc288_madd(a1, S.cb[12], CUR(7));
+        acc288_madd(a1, S.cb[13], CUR(8));
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             fe c = CUR(12 + k);
-            acc288_madd(c0, S.cb2[4 + k], c);
-            acc288_madd(c1, S.cb2[14 + k], c);
+            acc288_madd(a0, S.cb[4 + k], c);
+            acc288_madd(a1, S.cb[14 + k], c);
         }
-        const fe bs0b = acc288_reduce(c0), bs1b = fe_sub(acc288_reduce(c1), S.bnd1b);
-        acc288 aR2 = acc288_zero();
-        acc288_madd(aR2, t2, dT);
-        acc288_madd(aR2, bs0b, d0);
-        acc288_madd(aR2, bs1b, d1);
-        comp[plane + t_id] = acc288_reduce(aR2);
+        // sum_k cb[12+k] (c_k - v_k) = sum_k cb[12+k] c_k - bnd1 (bnd1 precomputed on the host)
+        const fe bs0 = acc288_reduce(a0), bs1 = fe_sub(acc288_reduce(a1), S.bnd1);
+        acc288 aR = acc288_zero();
+        acc288_madd(aR, t, dT);
+        acc288_madd(aR, bs0, d0);
+        acc288_madd(aR, bs1, d1);
+        const fe res = acc288_reduce(aR);
+        comp[t_id] = res;
+        if (KE == 2) {
+            ZK_SEQ(cb, res.lo);
+            acc288 c0 = acc288_zero(), c1 = acc288_zero();
+            acc288_madd(c0, S.cb2[0], CUR(0));
+            acc288_madd(c0, S.cb2[1], CUR(7));
+            acc288_madd(c0, S.cb2[2], CUR(8));
+            acc288_madd(c0, S.cb2[3], CUR(11));
+            acc288_madd(c1, S.cb2[12], CUR(7));
+            acc288_madd(c1, S.cb2[13], CUR(8));
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                fe c = CUR(12 + k);
+                acc288_madd(c0, S.cb2[4 + k], c);
+                acc288_madd(c1, S.cb2[14 + k], c);
+            }
+            const fe bs0b = acc288_reduce(c0), bs1b = fe_sub(acc288_reduce(c1), S.bnd1b);
+            acc288 aR2 = acc288_zero();
+            acc288_madd(aR2, t2, dT);
+            acc288_madd(aR2, bs0b, d0);
+            acc288_madd(aR2, bs1b, d1);
+            comp[plane + t_id] = acc288_reduce(aR2);
+        }
     }
 #undef ZK_ACC
 #undef CUR
@@ -1124,30 +1132,41 @@ static void upload_rescue(hipStream_t st) {
 }
 
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                      const AirConsts *consts_dev, fe *comp) {
-    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp);
+                      const AirConsts *consts_dev, fe *comp, bool bnd) {
+    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp,
+                            bnd);
 }
 
 void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
-                             const fe *divs, const AirConsts *consts_dev, fe *comp) {
+                             const fe *divs, const AirConsts *consts_dev, fe *comp, bool bnd) {
     upload_rescue(st);
     const size_t CE = (size_t)map.nce << log_n;
-    ZK_PROF(st, "eval_constraints", (448.0 * (map.lshift == 0 ? 1 : 2) + 32.0) * CE, hipLaunchKernelGGL((k_eval_constraints<1>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, periodic, divs, consts_dev, consts_dev, (size_t)0, comp));
+    const double bytes = (448.0 * (map.lshift == 0 ? 1 : 2) + (bnd ? 64.0 : 32.0)) * CE;
+    if (bnd)
+        ZK_PROF(st, "eval_constraints", bytes, hipLaunchKernelGGL((k_eval_constraints<1, true>), dim3(cdiv(CE, 256)), dim3(256), 0, st,
+                                                                  lde, log_n, map, periodic, divs, consts_dev, consts_dev, (size_t)0, comp));
+    else
+        ZK_PROF(st, "eval_constraints", bytes, hipLaunchKernelGGL((k_eval_constraints<1, false>), dim3(cdiv(CE, 256)), dim3(256), 0, st,
+                                                                  lde, log_n, map, periodic, divs, consts_dev, consts_dev, (size_t)0, comp));
 }
 
 void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
-                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp) {
+                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp, bool bnd) {
     upload_rescue(st);
     const size_t CE = (size_t)map.nce << log_n;
-    ZK_PROF(st, "eval_constraints_ext", (448.0 * (map.lshift == 0 ? 1 : 2) + 48.0) * CE, hipLaunchKernelGGL((k_eval_constraints<2>), dim3(cdiv(CE, 256)), dim3(256), 0, st, lde, log_n,
-                                                       map, periodic, divs, consts2_dev, consts2_dev + 1, plane, comp));
+    const double bytes = (448.0 * (map.lshift == 0 ? 1 : 2) + (bnd ? 80.0 : 48.0)) * CE;
+    if (bnd)
+        ZK_PROF(st, "eval_constraints_ext", bytes, hipLaunchKernelGGL((k_eval_constraints<2, true>), dim3(cdiv(CE, 256)), dim3(256), 0,
+                                                                      st, lde, log_n, map, periodic, divs, consts2_dev, consts2_dev + 1, plane, comp));
+    else
+        ZK_PROF(st, "eval_constraints_ext", bytes, hipLaunchKernelGGL((k_eval_constraints<2, false>), dim3(cdiv(CE, 256)), dim3(256), 0,
+                                                                      st, lde, log_n, map, periodic, divs, consts2_dev, consts2_dev + 1, plane, comp));
 }
 
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                          const AirConsts *consts2_dev, fe *comp) {
+                          const AirConsts *consts2_dev, fe *comp, bool bnd) {
     eval_constraints_ext_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
-                                (size_t)8 << log_n, comp);
+                                (size_t)8 << log_n, comp, bnd);
 }
 
 // ================================================================ composition interpolation (K4)
@@ -1431,9 +1450,12 @@ __global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
         }
 }
 
-// phase 3: thread owns 8 consecutive coefficients; D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k
+// phase 3: thread owns 8 consecutive coefficients; D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k.
+// ADD: D_k is added into Dk[k] (the boundary quotient into composition column 0).  rem_flag (optional):
+// set when sum_m g1_m or sum_m g2_m -- the remainders F1(z), F2(zg) of the divisions -- is nonzero.
+template <bool ADD>
 __global__ void __launch_bounds__(DIV_T) k_deep_div_q(const fe *g1, const fe *g2, const fe *carry, int nb1, size_t n,
-                                                     fe z, fe zg, const fe *pw, size_t H, fe *Dk) {
+                                                     fe z, fe zg, const fe *pw, size_t H, fe *Dk, unsigned *rem_flag) {
     __shared__ fe t1[DIV_T], t2[DIV_T];
     const size_t per = 2048 + H;
     const fe *ilo = pw + 2 * per, *ihi = ilo + 2048, *jlo = pw + 3 * per, *jhi = jlo + 2048;
@@ -1470,12 +1492,16 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_q(const fe *g1, const fe *g2
 #pragma unroll
     for (int e = DIV_E - 1; e >= 0; e--) {
         const size_t k = k0 + e;
-        if (k < n) Dk[k] = fe_add(fe_mul(pz, r1), fe_mul(pg, r2));
+        if (k < n) {
+            const fe q = fe_add(fe_mul(pz, r1), fe_mul(pg, r2));
+            Dk[k] = ADD ? fe_add(ld_fe(Dk + k), q) : q;
+        }
         r1 = fe_add(r1, a[e]);
         r2 = fe_add(r2, b[e]);
         pz = fe_mul(pz, z);
         pg = fe_mul(pg, zg);
     }
+    if (rem_flag && k0 == 0 && !(fe_is_zero(r1) && fe_is_zero(r2))) atomicOr(rem_flag, 1u);
 }
 
 // coset-major LDE -> natural order
@@ -1509,9 +1535,79 @@ const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccol
                                g1, g2, bs));
     hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
     ZK_PROF(st, "deep_divide", 48.0 * n,
-            hipLaunchKernelGGL(k_deep_div_q, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw, H,
-                               Dk));
+            hipLaunchKernelGGL(k_deep_div_q<false>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw,
+                               H, Dk, nullptr));
     return Dk;
+}
+
+// ---- boundary terms in coefficient form.  The assertion part of the composition,
+//   sum_k cb_k T_ck(x) / (x - 1)  +  sum_k cb'_k (T_c'k(x) - v_k) / (x - g^(n-2)),
+// is, for a trace that satisfies the assertions, a polynomial of degree n - 2: the same suffix-sum
+// division as DEEP (z = 1, zg = g^(n-2)) over f0 = sum cb_k T_ck and f1 = sum cb'_k T_c'k - bnd1, added into
+// composition column 0 after the interpolation.  The evaluator then skips the 22 products per CE row
+// (k_eval_constraints<KE, false>); the composition coefficients are the same field values.  Nonzero
+// remainders (an assertion that fails) set the degree flag.
+struct BndPoly {
+    fe cb[22];  // one coefficient plane (air/src/lib.rs:170-195 order: step 0 cols 0,7,8,11,12..19; step n-2 cols 7,8,12..19)
+    fe bnd1;    // sum_k cb[12+k] v_k
+};
+__global__ void __launch_bounds__(DIV_T) k_bnd_div_g(const fe *tpolys, size_t n, BndPoly bp, const fe *pw, size_t H,
+                                                    fe *g1, fe *g2, fe *bs) {
+    __shared__ fe red[DIV_T / 64];
+    const size_t per = 2048 + H;
+    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    fe v1 = fe_zero(), v2 = fe_zero();
+    if (k < n) {
+        auto T = [&](int c) { return ld_fe(tpolys + (size_t)c * n + k); };
+        acc288 a0 = acc288_zero(), a1 = acc288_zero();
+        acc288_madd(a0, bp.cb[0], T(0));
+        acc288_madd(a0, bp.cb[3], T(11));
+        const fe t7 = T(7), t8 = T(8);
+        acc288_madd(a0, bp.cb[1], t7);
+        acc288_madd(a0, bp.cb[2], t8);
+        acc288_madd(a1, bp.cb[12], t7);
+        acc288_madd(a1, bp.cb[13], t8);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const fe c = T(12 + j);
+            acc288_madd(a0, bp.cb[4 + j], c);
+            acc288_madd(a1, bp.cb[14 + j], c);
+        }
+        v1 = acc288_reduce(a0);
+        fe f1 = acc288_reduce(a1);
+        if (k == 0) f1 = fe_sub(f1, bp.bnd1);
+        v2 = fe_mul(f1, pow_split(pw + per, pw + per + 2048, k));  // f1_m (g^(n-2))^m
+        g1[k] = v1;
+        g2[k] = v2;
+    }
+    v1 = block_sum256(v1, red);
+    v2 = block_sum256(v2, red);
+    if (threadIdx.x == 0) {
+        bs[2 * blockIdx.x] = v1;
+        bs[2 * blockIdx.x + 1] = v2;
+    }
+}
+
+void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
+                       unsigned *flag) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH, nb1 = (n + DIV_T - 1) / DIV_T;
+    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *bs = g2 + 2 * n;  // layout of deep_poly's scratch
+    DeepPowBases pb;
+    pb.b[0] = fe_one();
+    pb.b[1] = c;
+    pb.b[2] = fe_one();
+    pb.b[3] = fe_inv(c);
+    hipLaunchKernelGGL(k_deep_pow_tables, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, pw);
+    BndPoly bp;
+    memcpy(bp.cb, K.coeff_b, sizeof bp.cb);
+    bp.bnd1 = K.bnd1;
+    ZK_PROF(st, "boundary_poly", (16.0 * 12 + 32.0) * n,
+            hipLaunchKernelGGL(k_bnd_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, n, bp, pw, H, g1, g2, bs));
+    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
+    ZK_PROF(st, "boundary_poly", 64.0 * n,
+            hipLaunchKernelGGL(k_deep_div_q<true>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, fe_one(),
+                               c, pw, H, col0, flag));
 }
 
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,

@@ -920,7 +920,10 @@ int zk::ensure_ext(zk_prover *p) {
 // column polynomials of n coefficients (p->cpolys; base column (c, j) of E column c at (c*KX + j)*n),
 // extend them over the B LDE cosets into clde and commit to its rows (a leaf is C E values).
 // p->flag is set when the interpolant has a coefficient at or beyond C*n (the degree check).
-static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe *ctmp, fe *clde, uint8_t root[32]) {
+// bnd (KX coefficient planes, or nullptr when comp already holds the assertion terms): add the assertion
+// terms' quotient polynomial to column 0 of each plane (boundary_poly_add) before the LDE.
+static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe *ctmp, fe *clde, uint8_t root[32],
+                             const AirConsts *bnd = nullptr) {
     const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b, CE = 8 * n;
     const int CK = C * KX;
     ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
@@ -934,6 +937,10 @@ static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe
         comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
                           h_inv(h_pow(fe_make(3), n)), C, p->cpolys + (size_t)j * n, p->flag);
     }
+    if (bnd)
+        for (int j = 0; j < KX; j++)
+            boundary_poly_add(p->st, p->polys, pl->log_n, bnd[j], bnd[0].g_last2, p->dscratch, p->cpolys + (size_t)j * n,
+                              p->flag);
     ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, 0, 1, (int)B, clde, B * n, n, p->tmp);
     return commit_rows(p, clde, CK, pl->log_n, pl->log_b, p->cleaves, p->cnodes, root);
 }
@@ -981,26 +988,28 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     fe *comp = KX == 2 ? p->x_comp : p->comp, *ctmp = KX == 2 ? p->x_ctmp : p->ctmp;
     fe *clde = KX == 2 ? p->x_clde : p->clde, *deep = KX == 2 ? p->x_deep : p->deep;
     fe *fri = KX == 2 ? p->x_fri : p->fri;
+    // The assertion terms are not evaluated per row here: S4 adds them in coefficient form (unless the
+    // caller dumps the composition values, which must then include them).
+    const bool bnd_rows = dump && dump->composition;
+    AirConsts Kp[2];
     if (KX == 1) {
-        AirConsts K;
-        draw_air_consts(coin, pub, n, K, R);
-        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+        draw_air_consts(coin, pub, n, Kp[0], R);
+        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &Kp[0], sizeof Kp[0], hipMemcpyHostToDevice, p->st));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp);
+        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp, bnd_rows);
         HT.stop("air_consts");
     } else {
-        AirConsts Kp[2];
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
         ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp);
+        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp, bnd_rows);
     }
     stage_mark(p, "constraints");
 
     // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit.
-    ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root));
+    ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root, bnd_rows ? nullptr : Kp));
     stage_mark(p, "composition");
     unsigned degree_flag = 0;
     ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));

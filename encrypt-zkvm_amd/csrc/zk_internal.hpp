@@ -169,8 +169,9 @@ void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_c
 struct EvalMap {
     int nce, ce0, cestep, lshift, lde_cosets;
 };
+// bnd: the boundary (assertion) terms are evaluated per row (else: boundary_poly_add after interpolation)
 void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
-                             const fe *divs, const AirConsts *consts_dev, fe *comp);
+                             const fe *divs, const AirConsts *consts_dev, fe *comp, bool bnd = true);
 // Inputs of the cross-coset step for coefficients k0 .. k0+kcount: c[r][kl] = c_r[k0 + kl]; output
 // polys[k2 * pstride + kl].
 struct CrossMap {
@@ -181,7 +182,11 @@ void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, 
                        fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                      const AirConsts *consts_dev, fe *comp);
+                      const AirConsts *consts_dev, fe *comp, bool bnd = true);
+// add the boundary terms' quotient polynomial (one coefficient plane K) into col0 (n coefficients);
+// c = g^(n-2); scratch: deep_poly's layout; sets *flag when an assertion fails
+void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
+                       unsigned *flag);
 // cross-coset step of the size-8n interpolation: per k1 < n, from the 8 per-coset inverse NTTs
 // (c_r[k1]), produce coefficients a[k1 + n*k2] = 3^-(k1+n k2) / (8n) * sum_r w8^(-r k2) w_8n^(-r k1) c_r[k1]
 // and write column k2 < ncols of the segmented composition polynomial: polys[k2*n + k1].
@@ -242,10 +247,10 @@ void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int
                   fe *tab, fe *partials, fe *out);
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                          const AirConsts *consts2_dev, fe *comp);
+                          const AirConsts *consts2_dev, fe *comp, bool bnd = true);
 // ... over the CE cosets of `map` (see eval_constraints_mapped), b plane at comp + plane
 void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
-                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp);
+                                 const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp, bool bnd = true);
 // out[i] = 1 / (N(x_i - z) N(x_i - zg)), N the norm E -> F (coset-major like batch_inv_pairs)
 void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,
                           fe *out);
