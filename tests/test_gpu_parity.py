@@ -255,6 +255,21 @@ def test_invalid_trace_is_reported(gpu):
     assert rc == native.ZK_ERR_DEGREE
 
 
+@pytest.mark.parametrize("ext", [1, 2])
+def test_failed_assertion_is_reported(gpu, ext):
+    """Public stack outputs that the trace does not end with: a step-(n-2) assertion fails.  The prover adds
+    the assertion terms in coefficient form; the division remainder must raise the degree error."""
+    trace, pub = workload_trace(LR_PROGRAM, seed=5)
+    wrong = native.PubInputs()
+    C.memmove(C.byref(wrong), C.byref(pub), C.sizeof(pub))
+    wrong.stack_outputs[0] ^= 1
+    _, _, _, rc = gpu.prove(trace, wrong, ProofOptions(field_extension=ext), allow_degree_error=True)
+    assert rc == native.ZK_ERR_DEGREE
+    # and the unmodified public inputs prove
+    _, _, _, rc = gpu.prove(trace, pub, ProofOptions(field_extension=ext))
+    assert rc == 0
+
+
 def test_bench_size_proof_verifies(gpu, oracle):
     """configs[2] size: 2^20-step ciphertext program; the GPU proof must verify (size-independent check)."""
     source = ops_for_trace_len(20, "cipher")
