@@ -1274,14 +1274,22 @@ __global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const
                                                   const fe *tab, int nw, fe *partials) {
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
-    if (gw >= nw) return;
     const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
     const int g = blockIdx.y;
     const bool comp = g >= tgroups;
     const int p0 = comp ? 0 : g * OOD_GROUP;
     const int p1 = comp ? C : min(W, p0 + OOD_GROUP);
     const size_t base = (size_t)gw * 64 * E + lane;
-    const fe y0 = fe_mul(tab[63], tab[1]), y1 = fe_mul(tab[127], tab[65]);  // x^64
+    // a lane's E coefficients sit 64 apart: sum_e v_e (x^64)^e as a lazy dot product against the powers
+    // (x^64)^e in LDS (one unreduced product per coefficient instead of a reduced Horner step)
+    __shared__ fe Y[2][E];
+    if (threadIdx.x < 2 * E) {
+        const int which = threadIdx.x / E, e = threadIdx.x % E;
+        const fe y = which ? fe_mul(tab[127], tab[65]) : fe_mul(tab[63], tab[1]);  // x^64
+        Y[which][e] = fe_exp(y, (uint64_t)e);
+    }
+    __syncthreads();
+    if (gw >= nw) return;
     const fe wz = fe_mul(tab[lane], tab[128 + gw]);
     const fe wzg = comp ? fe_zero() : fe_mul(tab[64 + lane], tab[128 + nw + gw]);
     for (int p = p0; p < p1; p++) {
@@ -1292,16 +1300,16 @@ __global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const
             const size_t k = base + 64 * (size_t)e;
             v[e] = k < n ? c[k] : fe_zero();
         }
-        fe hz = v[E - 1];
+        acc288 az = acc288_zero();
 #pragma unroll
-        for (int e = E - 2; e >= 0; e--) hz = fe_add(fe_mul(hz, y0), v[e]);
-        hz = wave_sum(fe_mul(hz, wz));
+        for (int e = 0; e < E; e++) acc288_madd(az, v[e], Y[0][e]);
+        const fe hz = wave_sum(fe_mul(acc288_reduce(az), wz));
         if (lane == 0) partials[(size_t)(comp ? 2 * W + p : p) * nw + gw] = hz;
         if (!comp) {
-            fe hg = v[E - 1];
+            acc288 ag = acc288_zero();
 #pragma unroll
-            for (int e = E - 2; e >= 0; e--) hg = fe_add(fe_mul(hg, y1), v[e]);
-            hg = wave_sum(fe_mul(hg, wzg));
+            for (int e = 0; e < E; e++) acc288_madd(ag, v[e], Y[1][e]);
+            const fe hg = wave_sum(fe_mul(acc288_reduce(ag), wzg));
             if (lane == 0) partials[(size_t)(W + p) * nw + gw] = hg;
         }
     }
@@ -1865,7 +1873,7 @@ void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const 
 }
 
 // ================================================================ FieldExtension::Quadratic (K5-K7 over E)
-// OOD over E points: the same wave layout as k_ood_eval with E-valued Horner steps.
+// OOD over E points: the same wave layout as k_ood_eval, E-valued powers.
 __global__ void k_ood_tables_ext(fe2 z, fe2 zg, uint64_t chunk, int nw, fe2 *tab) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 128 + 2 * nw) return;
@@ -1882,13 +1890,17 @@ __global__ void k_ood_tables_ext(fe2 z, fe2 zg, uint64_t chunk, int nw, fe2 *tab
     tab[t] = fe2_exp(x, e);
 }
 
-__device__ __forceinline__ fe2 horner_ext(const fe *v, int E, fe2 y) {
-    fe2 h = fe2_lift(v[E - 1]);
-    for (int e = E - 2; e >= 0; e--) {
-        h = fe2_mul(h, y);
-        h.a = fe_add(h.a, v[e]);
+// sum_e v_e y_e over E with base coefficients v: two lazy dot products (a and b components of y)
+template <int E>
+__device__ __forceinline__ fe2 dot_base_ext(const fe *v, const fe2 *y) {
+    acc288 aa = acc288_zero(), ab = acc288_zero();
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const fe2 w = y[e];
+        acc288_madd(aa, v[e], w.a);
+        acc288_madd(ab, v[e], w.b);
     }
-    return h;
+    return fe2{acc288_reduce(aa), acc288_reduce(ab)};
 }
 
 template <int E>
@@ -1896,7 +1908,6 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
                                                       const fe2 *tab, int nw, fe *partials) {
     const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
-    if (gw >= nw) return;
     const int np = 2 * W + C;
     const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
     const int g = blockIdx.y;
@@ -1904,7 +1915,15 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
     const int p0 = comp ? 0 : g * OOD_GROUP;
     const int p1 = comp ? C : min(W, p0 + OOD_GROUP);
     const size_t base = (size_t)gw * 64 * E + lane;
-    const fe2 y0 = fe2_mul(tab[63], tab[1]), y1 = fe2_mul(tab[127], tab[65]);  // x^64
+    // powers (x^64)^e in LDS: the lane's strided sum is a base x E dot product (see k_ood_eval)
+    __shared__ fe2 Y[2][E];
+    if (threadIdx.x < 2 * E) {
+        const int which = threadIdx.x / E, e = threadIdx.x % E;
+        const fe2 y = which ? fe2_mul(tab[127], tab[65]) : fe2_mul(tab[63], tab[1]);  // x^64
+        Y[which][e] = fe2_exp(y, (uint64_t)e);
+    }
+    __syncthreads();
+    if (gw >= nw) return;
     const fe2 wz = fe2_mul(tab[lane], tab[128 + gw]);
     const fe2 wzg = comp ? fe2_zero() : fe2_mul(tab[64 + lane], tab[128 + nw + gw]);
     for (int p = p0; p < p1; p++) {
@@ -1915,7 +1934,7 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
             const size_t k = base + 64 * (size_t)e;
             v[e] = k < n ? c[k] : fe_zero();
         }
-        const fe2 hz = fe2_mul(horner_ext(v, E, y0), wz);
+        const fe2 hz = fe2_mul(dot_base_ext<E>(v, Y[0]), wz);
         const fe sa = wave_sum(hz.a), sb = wave_sum(hz.b);
         const int slot = comp ? 2 * W + p : p;
         if (lane == 0) {
@@ -1923,7 +1942,7 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
             partials[(size_t)(np + slot) * nw + gw] = sb;
         }
         if (!comp) {
-            const fe2 hg = fe2_mul(horner_ext(v, E, y1), wzg);
+            const fe2 hg = fe2_mul(dot_base_ext<E>(v, Y[1]), wzg);
             const fe ga = wave_sum(hg.a), gb = wave_sum(hg.b);
             if (lane == 0) {
                 partials[(size_t)(W + p) * nw + gw] = ga;
