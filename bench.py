@@ -149,10 +149,12 @@ def main():
     world, rank, local, pg = setup_dist(args.gpus)
     from zkvm_amd import native
     from zkvm_amd.prover import GpuProver, ProofOptions, make_pub_inputs, vm_trace
-    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len, padded_length
 
     native.lib()  # fail loudly without the HIP library
     src = ops_for_trace_len(args.log_n, "cipher")
+    program_ops = sum(1 for ln in src.splitlines() if ln.split("#")[0].strip())  # #program ops
+    padded_ops = padded_length(src)
     w = make_workload(src, seed=1000 + rank)
     t0 = time.perf_counter()
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
@@ -228,6 +230,7 @@ def main():
         "config": {"workload": f"configs[{4 if args.config5 else 2}]: 2^{args.log_n}-step READ2/ADD2/SMUL cipher-mix program, "
                                f"full prove" + (" at 128-bit conjectured security" if args.config5 else ""),
                    "trace_len": n, "trace_width": 28, "lde_len": n * opts.blowup_factor,
+                   "program_ops": program_ops, "padded_ops": padded_ops,
                    "options": opts_str, "parallelism": f"independent proof per GPU x{world}"},
         "security_bits_checked": min_sec,
         "roofline": roofline, "cpu_baseline": cpu,
@@ -245,10 +248,11 @@ def run_sharded(args):
     from zkvm_amd import native
     from zkvm_amd.prover import ProofOptions, make_pub_inputs, vm_trace
     from zkvm_amd.sharded import ShardedProver
-    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len, padded_length
 
     native.lib()
     src = ops_for_trace_len(args.log_n, "cipher")
+    program_ops = sum(1 for ln in src.splitlines() if ln.split("#")[0].strip())
     w = make_workload(src, seed=1000)  # the same trace on every rank: one proof
     t0 = time.perf_counter()
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
@@ -292,6 +296,7 @@ def run_sharded(args):
             "config": {"workload": f"configs[{4 if args.config5 else 3}]: one 2^{args.log_n}-step cipher-mix proof, "
                                    f"LDE domain sharded by coset",
                        "trace_len": n, "trace_width": 28, "lde_len": 8 * n,
+                       "program_ops": program_ops, "padded_ops": padded_length(src),
                        "options": ("ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5
                                    else "ProofOptions(32, 8, 0, None, 8, 127)"),
                        "parallelism": f"coset-sharded x{world} (RCCL all-to-all / all-gather)"},
