@@ -1780,7 +1780,7 @@ __device__ __forceinline__ bool fe_canon_dev(uint32_t w0, uint32_t w1, uint32_t 
     const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
     return !(hi == ZK_P_HI && lo >= ZK_P_LO);
 }
-__global__ void k_fri_coin(uint32_t *seed, const uint8_t *root, int k, fe *alpha_out) {
+__global__ void k_fri_coin(uint32_t *seed, const uint8_t *root, int k, fe *alpha_out, fe *alpha_log) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     uint32_t s[8], r[8], h[8];
     for (int i = 0; i < 8; i++) s[i] = seed[i];
@@ -1793,15 +1793,18 @@ __global__ void k_fri_coin(uint32_t *seed, const uint8_t *root, int k, fe *alpha
         b3::iv(d);
         b3::compress(d, m, 0, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
         if (fe_canon_dev(d[0], d[1], d[2], d[3]) && (k == 1 || fe_canon_dev(d[4], d[5], d[6], d[7]))) {
-            alpha_out[0] = fe{(uint64_t)d[0] | ((uint64_t)d[1] << 32), (uint64_t)d[2] | ((uint64_t)d[3] << 32)};
-            if (k == 2) alpha_out[1] = fe{(uint64_t)d[4] | ((uint64_t)d[5] << 32), (uint64_t)d[6] | ((uint64_t)d[7] << 32)};
+            const fe a0 = fe{(uint64_t)d[0] | ((uint64_t)d[1] << 32), (uint64_t)d[2] | ((uint64_t)d[3] << 32)};
+            const fe a1 = fe{(uint64_t)d[4] | ((uint64_t)d[5] << 32), (uint64_t)d[6] | ((uint64_t)d[7] << 32)};
+            alpha_out[0] = alpha_log[0] = a0;
+            if (k == 2) alpha_out[1] = alpha_log[1] = a1;
             return;
         }
     }
 }
 
-void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev, int k, fe *alpha_dev) {
-    hipLaunchKernelGGL(k_fri_coin, dim3(1), dim3(64), 0, st, seed_dev, root_dev, k, alpha_dev);
+void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev, int k, fe *alpha_dev,
+                     fe *alpha_log) {
+    hipLaunchKernelGGL(k_fri_coin, dim3(1), dim3(64), 0, st, seed_dev, root_dev, k, alpha_dev, alpha_log);
 }
 
 // ================================================================ FRI fold (K7)

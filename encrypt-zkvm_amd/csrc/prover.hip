@@ -52,6 +52,41 @@ using namespace zk;
 
 const char *zk_last_error(void) { return g_err.c_str(); }
 
+// ---- small transfers through the pinned staging area (zk_prover::h_io)
+static uint8_t *io_take(zk_prover *p, size_t len) {
+    const size_t a = (len + 63) & ~(size_t)63;
+    if (p->io_used + a > p->io_cap) return nullptr;
+    uint8_t *r = p->h_io + p->io_used;
+    p->io_used += a;
+    return r;
+}
+// enqueue host -> device from a pinned copy of src (src may be reused as soon as this returns)
+static int h2d_small(zk_prover *p, void *dst_dev, const void *src, size_t len) {
+    uint8_t *s = io_take(p, len);
+    if (!s) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "pinned staging area exhausted");
+    memcpy(s, src, len);
+    ZK_CHECK_HIP(hipMemcpyAsync(dst_dev, s, len, hipMemcpyHostToDevice, p->st));
+    return ZK_OK;
+}
+// enqueue device -> host into the staging area; dst is written by d2h_flush
+static int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
+    uint8_t *s = io_take(p, len);
+    if (!s) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "pinned staging area exhausted");
+    ZK_CHECK_HIP(hipMemcpyAsync(s, src_dev, len, hipMemcpyDeviceToHost, p->st));
+    p->io_pending.push_back({dst, s, len});
+    return ZK_OK;
+}
+// one stream sync for every pending read; every copy enqueued before it has then completed, so the
+// staging area starts over
+static int d2h_flush(zk_prover *p) {
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    for (const auto &r : p->io_pending) memcpy(r.dst, r.src, r.len);
+    p->io_pending.clear();
+    p->io_used = 0;
+    return ZK_OK;
+}
+
+
 struct zk_trace_lde {
     zk_prover *p;
     size_t n;
@@ -266,6 +301,9 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
     ZK_CHECK_HIP(A.alloc(&p->gather_out, ZK_GATHER_CAP));
     ZK_CHECK_HIP(A.alloc(&p->gather_idx, ZK_GATHER_CAP));
+    p->io_cap = (size_t)1 << 20;
+    ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_io, p->io_cap, hipHostMallocDefault));
+    p->io_pending.reserve(64);
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_idx, ZK_GATHER_CAP * sizeof(uint64_t), hipHostMallocDefault));
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_out, ZK_GATHER_CAP * sizeof(fe), hipHostMallocDefault));
     ZK_CHECK_HIP(A.alloc(&p->flag, 4));
@@ -284,6 +322,7 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamSynchronize(p->st);
     for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
     (void)hipStreamDestroy(p->st);
+    if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
     if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
     delete p->open;
@@ -727,15 +766,15 @@ int zk::grind_and_positions(zk_prover *p, Coin &coin, const zk_options *opt, siz
             ZK_CHECK_HIP(p->arena.alloc(&p->pow_seed, 8));
             ZK_CHECK_HIP(p->arena.alloc(&p->pow_best, 1));
         }
-        ZK_CHECK_HIP(hipMemcpyAsync(p->pow_seed, coin.seed, 32, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->pow_seed, coin.seed, 32));
         const unsigned long long none = ~0ULL;
         unsigned long long best = none;
-        ZK_CHECK_HIP(hipMemcpyAsync(p->pow_best, &none, 8, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->pow_best, &none, 8));
         const uint32_t batch = 1u << 22;
         for (uint64_t start = 1; best == none; start += batch) {
             grind_launch(p->st, p->pow_seed, start, batch, (int)opt->grinding, p->pow_best);
-            ZK_CHECK_HIP(hipMemcpyAsync(&best, p->pow_best, 8, hipMemcpyDeviceToHost, p->st));
-            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+            ZK_TRY(d2h_small(p, &best, p->pow_best, 8));
+            ZK_TRY(d2h_flush(p));
         }
         nonce = best;
         if (!nonce_ok(coin.seed, nonce, opt->grinding)) ZK_FAIL(ZK_ERR_DEVICE, "GPU grinding returned an invalid nonce");
@@ -876,12 +915,11 @@ static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, 
     return ZK_OK;
 }
 
+// hash the rows and build the tree; the root is read back with the caller's next d2h_flush
 static int commit_rows(zk_prover *p, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves, uint8_t *nodes,
                        uint8_t root[32]) {
     commit_rows_coset_major(p->st, base, ncols, log_n, log_b, leaves, nodes);
-    ZK_CHECK_HIP(hipMemcpyAsync(root, nodes + 32, 32, hipMemcpyDeviceToHost, p->st));
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    return ZK_OK;
+    return d2h_small(p, root, nodes + 32, 32);
 }
 
 static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, size_t n, uint32_t B, uint8_t *dst) {
@@ -975,6 +1013,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     ZK_TRY(trace_lde_stage(p, pl, d_trace, n, B));
     stage_mark(p, "trace_lde");
     ZK_TRY(commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root));
+    ZK_TRY(d2h_flush(p));
     stage_mark(p, "trace_commit");
     HostTimer HT;
     HT.start();
@@ -994,14 +1033,14 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     AirConsts Kp[2];
     if (KX == 1) {
         draw_air_consts(coin, pub, n, Kp[0], R);
-        ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &Kp[0], sizeof Kp[0], hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->air_consts, &Kp[0], sizeof Kp[0]));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
         eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp, bnd_rows);
         HT.stop("air_consts");
     } else {
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
-        ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
         eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp, bnd_rows);
@@ -1010,9 +1049,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
 
     // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit.
     ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root, bnd_rows ? nullptr : Kp));
-    stage_mark(p, "composition");
     unsigned degree_flag = 0;
-    ZK_CHECK_HIP(hipMemcpy(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost));
+    ZK_TRY(d2h_small(p, &degree_flag, p->flag, 4));
+    ZK_TRY(d2h_flush(p));
+    stage_mark(p, "composition");
     HT.start();
     coin.reseed(R.constraint_root);
 
@@ -1024,13 +1064,13 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         fe_to_bytes(z, R.z);
         ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood);
         HT.stop("z");
-        ZK_CHECK_HIP(hipMemcpyAsync(h.data(), p->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        ZK_TRY(d2h_small(p, h.data(), p->ood, (2 * W + C) * sizeof(fe)));
+        ZK_TRY(d2h_flush(p));
         HT.start();
         ood_reseed(coin, h.data(), C, R);
         stage_mark(p, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
-        ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->deep_consts, &D, sizeof D));
         deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->ct,
                           p->dscratch, p->ulde, p->tmp, deep);
         HT.stop("deep_consts");
@@ -1040,13 +1080,13 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const int np = 2 * W + CK;  // E values of the trace polys at z, zg and of the C*k base composition polys at z
         ood_eval_ext(p->st, p->polys, W, p->cpolys, CK, log_n, z, zg, p->x_tab, p->x_partials, p->ood);
         std::vector<fe> hv(2 * np);
-        ZK_CHECK_HIP(hipMemcpyAsync(hv.data(), p->ood, hv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        ZK_TRY(d2h_small(p, hv.data(), p->ood, hv.size() * sizeof(fe)));
+        ZK_TRY(d2h_flush(p));
         std::vector<fe2> e;
         ood_reseed_ext(coin, hv, C, R, e, h);
         stage_mark(p, "ood");
         const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
-        ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
         deep_coeff_ext_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->x_deep_consts, z, zg,
                               pl->ct, p->x_dscratch, p->x_ulde, p->tmp, deep);
     }
@@ -1075,14 +1115,14 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         fe *alpha_dev = nullptr;
         if (KX == 1) {
             const FoldConsts F = fold_consts(fe_zero(), fold);
-            ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->fold_consts, &F, sizeof F));
             alpha_dev = &((FoldConsts *)p->fold_consts)->alpha;
         } else {
             const FoldConstsE F = fold_consts_ext(fe2_zero(), fold);
-            ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->x_fold_consts, &F, sizeof F));
             alpha_dev = &((FoldConstsE *)p->x_fold_consts)->alpha.a;
         }
-        ZK_CHECK_HIP(hipMemcpyAsync(p->fri_seed, coin.seed, 32, hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->fri_seed, coin.seed, 32));
         for (int l = 0; l < nl; l++) {
             const size_t L = layer_len[l], rows = L / fold;
             layer_leaves[l] = dig;
@@ -1090,8 +1130,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             dig += 64 * rows;
             if (KX == 1) commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
             else commit_fri_layer_ext(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-            fri_coin_launch(p->st, (uint32_t *)p->fri_seed, layer_nodes[l] + 32, KX, alpha_dev);
-            ZK_CHECK_HIP(hipMemcpyAsync(p->fri_alphas + 2 * l, alpha_dev, KX * sizeof(fe), hipMemcpyDeviceToDevice, p->st));
+            fri_coin_launch(p->st, (uint32_t *)p->fri_seed, layer_nodes[l] + 32, KX, alpha_dev, p->fri_alphas + 2 * l);
             if (KX == 1) fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
             else fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
             layer_vals[l + 1] = next;
@@ -1101,11 +1140,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         // one round trip for the whole commit phase: roots, device alphas, the last layer
         const size_t L = layer_len[nl];
         std::vector<fe> rv(KX * L), dalpha(2 * nl);
-        for (int l = 0; l < nl; l++)
-            ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, p->st));
-        if (nl) ZK_CHECK_HIP(hipMemcpyAsync(dalpha.data(), p->fri_alphas, 2 * nl * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        for (int l = 0; l < nl; l++) ZK_TRY(d2h_small(p, R.fri_roots[l], layer_nodes[l] + 32, 32));
+        if (nl) ZK_TRY(d2h_small(p, dalpha.data(), p->fri_alphas, 2 * nl * sizeof(fe)));
+        ZK_TRY(d2h_small(p, rv.data(), layer_vals[nl], rv.size() * sizeof(fe)));
+        ZK_TRY(d2h_flush(p));
         HT.start();
         // host replay of the same transcript (it continues into the remainder, grinding and queries)
         for (int l = 0; l < nl; l++) {
@@ -1247,6 +1285,7 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     if ((rc = trace_lde_stage(p, pl, p->d_trace, n, blowup))) return rc;
     uint8_t r[32];
     if ((rc = commit_rows(p, p->lde, W, pl->log_n, pl->log_b, p->leaves, p->nodes, r))) return rc;
+    if ((rc = d2h_flush(p))) return rc;
     if (root) memcpy(root, r, 32);
     *out = new zk_trace_lde{p, n, blowup, W};
     return ZK_OK;
@@ -1361,8 +1400,7 @@ int zk_commit_composition(zk_trace_lde *h, const uint8_t *composition, uint32_t 
     uint8_t r[32];
     if ((rc = composition_stage(p, pl, 1, (int)num_cols, p->comp, p->ctmp, p->clde, r))) return rc;
     unsigned degree_flag = 0;
-    ZK_CHECK_HIP(hipMemcpyAsync(&degree_flag, p->flag, 4, hipMemcpyDeviceToHost, p->st));
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    if ((rc = d2h_small(p, &degree_flag, p->flag, 4)) || (rc = d2h_flush(p))) return rc;  // root and flag
     if (degree_flag) ZK_FAIL(ZK_ERR_DEGREE, "composition polynomial degree exceeds num_cols * trace_len");
     if (polys_out)
         ZK_CHECK_HIP(hipMemcpy(polys_out, p->cpolys, (size_t)num_cols * n * sizeof(fe), hipMemcpyDeviceToHost));

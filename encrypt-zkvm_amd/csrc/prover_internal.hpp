@@ -102,6 +102,19 @@ struct zk_prover {
     uint8_t *leaves = nullptr, *nodes = nullptr, *cleaves = nullptr, *cnodes = nullptr, *fri_dig = nullptr;
     fe *partials = nullptr, *ood_tab = nullptr, *ood = nullptr, *gather_out = nullptr;
     uint64_t *gather_idx = nullptr;
+    // Pinned host staging for the small transfers on a proof's critical path (constants up; roots, the
+    // degree flag, OOD values, FRI results down).  hipMemcpyAsync from or to pageable memory is staged
+    // synchronously by the runtime (~20 us each between kernels); from pinned memory it is a DMA in
+    // stream order.  Bump-allocated per proof (io_reset at the start of each), so no region is reused
+    // while a copy from it may still be in flight.
+    struct PendingRead {
+        void *dst;
+        const uint8_t *src;
+        size_t len;
+    };
+    uint8_t *h_io = nullptr;
+    size_t io_cap = 0, io_used = 0;
+    std::vector<PendingRead> io_pending;
     uint64_t *h_gather_idx = nullptr;  // pinned host staging of the opening addresses / values
     fe *h_gather_out = nullptr;
     zk::Openings *open = nullptr;      // per-proof openings, storage kept across proofs

@@ -236,8 +236,10 @@ void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const 
                      const NttTables &TN, size_t wstride, fe *next);
 void coset_major_to_natural(hipStream_t st, const fe *src, int log_n, int log_b, fe *dst);
 // FRI commit-phase coin on the device: seed = merge(seed, root_dev), alpha (k = 1 or 2 components) drawn
-// into alpha_dev (kernels.hip)
-void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev, int k, fe *alpha_dev);
+// into alpha_dev (where the fold reads it) and alpha_log (the per-layer record the host replay is checked
+// against)
+void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev, int k, fe *alpha_dev,
+                     fe *alpha_log);
 
 // ---------------------------------------------------------------- FieldExtension::Quadratic (ext2.hpp)
 // Every E-valued buffer is planar: component a at [0, M), component b at [M, 2M).
