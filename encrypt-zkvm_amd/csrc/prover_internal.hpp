@@ -105,8 +105,8 @@ struct zk_prover {
     // Pinned host staging for the small transfers on a proof's critical path (constants up; roots, the
     // degree flag, OOD values, FRI results down).  hipMemcpyAsync from or to pageable memory is staged
     // synchronously by the runtime (~20 us each between kernels); from pinned memory it is a DMA in
-    // stream order.  Bump-allocated per proof (io_reset at the start of each), so no region is reused
-    // while a copy from it may still be in flight.
+    // stream order.  Bump-allocated and rewound only by d2h_flush, after a stream sync, so no region is
+    // reused while a copy from it may still be in flight.
     struct PendingRead {
         void *dst;
         const uint8_t *src;
