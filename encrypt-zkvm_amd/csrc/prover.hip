@@ -301,7 +301,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
     ZK_CHECK_HIP(A.alloc(&p->gather_out, ZK_GATHER_CAP));
     ZK_CHECK_HIP(A.alloc(&p->gather_idx, ZK_GATHER_CAP));
-    p->io_cap = (size_t)1 << 20;
+    // the largest read is the last FRI layer: up to ZK_MAX_REMAINDER * blowup values, two planes over E
+    p->io_cap = ((size_t)64 << 10) + (size_t)2 * ZK_MAX_REMAINDER * p->max_b * sizeof(fe);
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_io, p->io_cap, hipHostMallocDefault));
     p->io_pending.reserve(64);
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_idx, ZK_GATHER_CAP * sizeof(uint64_t), hipHostMallocDefault));
@@ -475,7 +476,8 @@ int zk::check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_option
     if (!o || !pub) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     if ((o->field_extension != 1 && o->field_extension != 2) || o->blowup < 8 || (o->blowup & (o->blowup - 1)) ||
         (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) ||
-        ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) || o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES)
+        ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) || o->fri_rem_max_deg + 1 > ZK_MAX_REMAINDER ||
+        o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
     if (n < 16 || (n & (n - 1)) || n > max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace length must be a power of two in [16, max_trace_len]");
     if (o->blowup > max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "blowup exceeds the prover's max_blowup");
