@@ -663,12 +663,15 @@ __global__ void __launch_bounds__(512) k_merge_block(const uint8_t *src, uint8_t
     }
 }
 
+#ifndef ZK_MERKLE_L3_MIN
+#define ZK_MERKLE_L3_MIN 17  // log2 of the smallest level the three-level kernel takes (A/B: 17 > 20 > 16 > 14)
+#endif
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes) {
     // invariant: src holds 2*cnt digests whose parents go to nodes[cnt .. 2cnt)
     size_t cnt = nl / 2;
     const uint8_t *src = leaves;
     // wide levels: three per launch, seven compressions per thread (throughput)
-    while (cnt >= ((size_t)1 << 20)) {
+    while (cnt >= ((size_t)1 << ZK_MERKLE_L3_MIN)) {
         unsigned blocks = cdiv(cnt / 4, 256);
         if (blocks > 65536) blocks = 65536;
         ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
