@@ -52,39 +52,6 @@ using namespace zk;
 
 const char *zk_last_error(void) { return g_err.c_str(); }
 
-// ---- small transfers through the pinned staging area (zk_prover::h_io)
-static uint8_t *io_take(zk_prover *p, size_t len) {
-    const size_t a = (len + 63) & ~(size_t)63;
-    if (p->io_used + a > p->io_cap) return nullptr;
-    uint8_t *r = p->h_io + p->io_used;
-    p->io_used += a;
-    return r;
-}
-// enqueue host -> device from a pinned copy of src (src may be reused as soon as this returns)
-static int h2d_small(zk_prover *p, void *dst_dev, const void *src, size_t len) {
-    uint8_t *s = io_take(p, len);
-    if (!s) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "pinned staging area exhausted");
-    memcpy(s, src, len);
-    ZK_CHECK_HIP(hipMemcpyAsync(dst_dev, s, len, hipMemcpyHostToDevice, p->st));
-    return ZK_OK;
-}
-// enqueue device -> host into the staging area; dst is written by d2h_flush
-static int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
-    uint8_t *s = io_take(p, len);
-    if (!s) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "pinned staging area exhausted");
-    ZK_CHECK_HIP(hipMemcpyAsync(s, src_dev, len, hipMemcpyDeviceToHost, p->st));
-    p->io_pending.push_back({dst, s, len});
-    return ZK_OK;
-}
-// one stream sync for every pending read; every copy enqueued before it has then completed, so the
-// staging area starts over
-static int d2h_flush(zk_prover *p) {
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    for (const auto &r : p->io_pending) memcpy(r.dst, r.src, r.len);
-    p->io_pending.clear();
-    p->io_used = 0;
-    return ZK_OK;
-}
 
 
 struct zk_trace_lde {

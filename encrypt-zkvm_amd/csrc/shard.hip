@@ -253,8 +253,8 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     }
     ZK_TRY(X.comm->all_gather(X.P, rs, rr, 32));
     std::vector<uint8_t> roots(32 * X.G);
-    ZK_CHECK_HIP(hipMemcpyAsync(roots.data(), X.P[0]->sh_roots, roots.size(), hipMemcpyDeviceToHost, X.P[0]->st));
-    ZK_CHECK_HIP(hipStreamSynchronize(X.P[0]->st));
+    ZK_TRY(d2h_small(X.P[0], roots.data(), X.P[0]->sh_roots, roots.size()));
+    ZK_TRY(d2h_flush(X.P[0]));
     T.top.assign(2 * X.G, {});
     for (int d = 0; d < X.G; d++) memcpy(T.top[X.G + d].data(), &roots[32 * d], 32);
     for (int k = X.G - 1; k >= 1; k--) {
@@ -283,6 +283,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     const int log_m = ilog2(m);
     const fe g = h_root_of_unity(log_n), three = fe_make(3);
     zk_prover *P0 = X.P[0];
+    for (zk_prover *p : X.P) ZK_TRY(io_rewind(p));  // the pinned staging areas start over
     zk_record R;
     memset(&R, 0, sizeof R);
     R.trace_len = (uint32_t)n;
@@ -334,18 +335,18 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         ZK_CHECK_HIP(hipSetDevice(p->device));
         fe xr[8];
         for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] + G * j];
-        ZK_CHECK_HIP(hipMemcpyAsync(p->sh_xr, xr, Bl * sizeof(fe), hipMemcpyHostToDevice, p->st));
+        ZK_TRY(h2d_small(p, p->sh_xr, xr, Bl * sizeof(fe)));
         // divisor tables of the local CE cosets (3 planes of Bl*n) in the NTT scratch, free until S4
         Fe8 zloc{};
         for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] + G * j];
         divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, p->tmp);
         const EvalMap em{Bl, X.rank[l], G, 0, Bl};
         if (KX == 1) {
-            ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
             eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
                                     (const AirConsts *)p->air_consts, p->comp);
         } else {
-            ZK_CHECK_HIP(hipMemcpyAsync(p->x_air, Kp, sizeof Kp, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
             eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
                                         (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp);
         }
@@ -419,7 +420,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     unsigned degree_flag = 0;
     {
         std::vector<unsigned> f(G);
-        ZK_CHECK_HIP(hipMemcpy(f.data(), P0->sh_flags, G * sizeof(unsigned), hipMemcpyDeviceToHost));
+        ZK_TRY(d2h_small(P0, f.data(), P0->sh_flags, G * sizeof(unsigned)));
+        ZK_TRY(d2h_flush(P0));
         for (unsigned v : f) degree_flag |= v;
     }
     coin.reseed(R.constraint_root);
@@ -432,8 +434,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         fe_to_bytes(z, R.z);
         h.resize(2 * W + C);
         ood_eval(P0->st, P0->polys, W, P0->cpolys, C, log_n, z, zg, P0->ood_tab, P0->partials, P0->ood);
-        ZK_CHECK_HIP(hipMemcpyAsync(h.data(), P0->ood, (2 * W + C) * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        ZK_TRY(d2h_small(P0, h.data(), P0->ood, (2 * W + C) * sizeof(fe)));
+        ZK_TRY(d2h_flush(P0));
         ood_reseed(coin, h.data(), C, R);
         stage_mark(P0, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
@@ -441,7 +443,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ZK_CHECK_HIP(hipMemcpyAsync(p->deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->deep_consts, &D, sizeof D));
             // DEEP as an exact polynomial (kernels.hip): replicated coefficients, local cosets g + G j
             const fe *Dk = deep_poly(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch);
             lde_cosets(p->st, pl->Tn, pl->ct, Dk, n, X.rank[l], G, Bl, p->deep, p->tmp);
@@ -452,8 +454,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         const int np = 2 * W + CK;
         ood_eval_ext(P0->st, P0->polys, W, P0->cpolys, CK, log_n, z, zg, P0->x_tab, P0->x_partials, P0->ood);
         std::vector<fe> hv(2 * np);
-        ZK_CHECK_HIP(hipMemcpyAsync(hv.data(), P0->ood, hv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        ZK_TRY(d2h_small(P0, hv.data(), P0->ood, hv.size() * sizeof(fe)));
+        ZK_TRY(d2h_flush(P0));
         std::vector<fe2> e;
         ood_reseed_ext(coin, hv, C, R, e, h);
         stage_mark(P0, "ood");
@@ -462,7 +464,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ZK_CHECK_HIP(hipMemcpyAsync(p->x_deep_consts, &D, sizeof D, hipMemcpyHostToDevice, p->st));
+            ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
             const fe *Dk = deep_poly_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch);
             for (int plane = 0; plane < 2; plane++)  // planar per rank: plane stride Bl * n
                 lde_cosets(p->st, pl->Tn, pl->ct, Dk + plane * n, n, X.rank[l], G, Bl,
@@ -503,8 +505,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                                (const uint8_t *)(COMP(P0) + (size_t)pln * Bl * n), G, Bl, log_n, 16,
                                (size_t)KX * Bl * n, (uint8_t *)(FRI(P0) + pln * N));
         std::vector<fe> rv(KX * N);
-        ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), FRI(P0), rv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+        ZK_TRY(d2h_small(P0, rv.data(), FRI(P0), rv.size() * sizeof(fe)));
+        ZK_TRY(d2h_flush(P0));
         ZK_TRY(remainder(rv));
     } else {
         for (int l = 0; l < nlp; l++) {
@@ -540,12 +542,12 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
                 if (KX == 1) {
-                    ZK_CHECK_HIP(hipMemcpyAsync(p->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, p->st));
+                    ZK_TRY(h2d_small(p, p->fold_consts, &F, sizeof F));
                     hipLaunchKernelGGL(k_sh_fri_fold0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n,
                                        Bl, X.rank[l], G, (int)fold, log_m, (const FoldConsts *)p->fold_consts,
                                        X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, p->ctmp);
                 } else {
-                    ZK_CHECK_HIP(hipMemcpyAsync(p->x_fold_consts, &FE, sizeof FE, hipMemcpyHostToDevice, p->st));
+                    ZK_TRY(h2d_small(p, p->x_fold_consts, &FE, sizeof FE));
                     hipLaunchKernelGGL(k_sh_fri_fold0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st,
                                        p->x_deep, log_n, Bl, X.rank[l], G, (int)fold, log_m,
                                        (const FoldConstsE *)p->x_fold_consts, X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi,
@@ -573,20 +575,20 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 dig += 64 * rows;
                 if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
                 else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-                ZK_CHECK_HIP(hipMemcpyAsync(R.fri_roots[l], layer_nodes[l] + 32, 32, hipMemcpyDeviceToHost, P0->st));
-                ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+                ZK_TRY(d2h_small(P0, R.fri_roots[l], layer_nodes[l] + 32, 32));
+                ZK_TRY(d2h_flush(P0));
                 coin.reseed(R.fri_roots[l]);
                 if (KX == 1) {
                     const fe alpha = coin.draw();
                     fe_to_bytes(alpha, R.fri_alphas[l]);
                     const FoldConsts F = fold_consts(alpha, fold);
-                    ZK_CHECK_HIP(hipMemcpyAsync(P0->fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
+                    ZK_TRY(h2d_small(P0, P0->fold_consts, &F, sizeof F));
                     fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
                 } else {
                     const fe2 alpha = coin.draw_ext(2);
                     fe_to_bytes(alpha.a, R.fri_alphas[l]);
                     const FoldConstsE F = fold_consts_ext(alpha, fold);
-                    ZK_CHECK_HIP(hipMemcpyAsync(P0->x_fold_consts, &F, sizeof F, hipMemcpyHostToDevice, P0->st));
+                    ZK_TRY(h2d_small(P0, P0->x_fold_consts, &F, sizeof F));
                     fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L,
                                         next);
                 }
@@ -595,8 +597,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 next += KX * rows;
             }
             std::vector<fe> rv(KX * layer_len[nl]);
-            ZK_CHECK_HIP(hipMemcpyAsync(rv.data(), layer_vals[nl], rv.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));
-            ZK_CHECK_HIP(hipStreamSynchronize(P0->st));
+            ZK_TRY(d2h_small(P0, rv.data(), layer_vals[nl], rv.size() * sizeof(fe)));
+            ZK_TRY(d2h_flush(P0));
             ZK_TRY(remainder(rv));
         }
     }
