@@ -10,6 +10,8 @@
 //   * digests: 32-byte BLAKE3 words, leaves in natural order, nodes[1] = root.
 // All arithmetic is exact f128 (f128.hpp); no floating point anywhere.
 #include <hip/hip_runtime.h>
+#include <bitset>
+#include <mutex>
 
 #include "blake3.hpp"
 #include "rescue_consts.hpp"
@@ -1120,19 +1122,29 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
 #undef NXT
 }
 
-static bool g_consts_uploaded = false;
-static void upload_rescue(hipStream_t st) {
-    if (g_consts_uploaded) return;
+// __constant__ memory is per device: track the upload per device (a process may run provers on
+// several GPUs, and the loopback sharded prover's ranks may sit on different devices).
+static std::mutex g_consts_mu;
+static std::bitset<256> g_consts_done;
+hipError_t upload_rescue_consts(hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 256) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_consts_mu);
+    if (g_consts_done.test((size_t)dev)) return hipSuccess;
     fe m[16], im[16];
     for (int i = 0; i < 16; i++) {
         m[i] = fe_make(ZK_MDS[i][0], ZK_MDS[i][1]);
         im[i] = fe_make(ZK_INV_MDS[i][0], ZK_INV_MDS[i][1]);
     }
-    hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mds), m, sizeof m, 0, hipMemcpyHostToDevice, st);
-    hipMemcpyToSymbolAsync(HIP_SYMBOL(c_inv_mds), im, sizeof im, 0, hipMemcpyHostToDevice, st);
-    hipStreamSynchronize(st);
-    g_consts_uploaded = true;
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mds), m, sizeof m, 0, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_inv_mds), im, sizeof im, 0, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) g_consts_done.set((size_t)dev);
+    return e;
 }
+static void upload_rescue(hipStream_t st) { (void)upload_rescue_consts(st); }
 
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                       const AirConsts *consts_dev, fe *comp, bool bnd) {

@@ -82,19 +82,22 @@ static hipError_t make_pow_table(zk_prover *p, fe s, size_t n, PowTable *out) {
 
 static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
     T->log_n = log_n;
-    static std::vector<fe> d4096f, d4096i;
-    if (d4096f.empty()) {
-        d4096f.resize(2048);
-        d4096i.resize(2048);
-        fe w = h_root_of_unity(12), wi = h_inv(w);
-        d4096f[0] = d4096i[0] = fe_one();
-        for (int t = 1; t < 2048; t++) {
-            d4096f[t] = fe_mul(d4096f[t - 1], w);
-            d4096i[t] = fe_mul(d4096i[t - 1], wi);
+    // w_4096 powers, forward and inverse: built once per process (a function-local static is
+    // initialised exactly once even when provers on several threads reach it together)
+    struct Dft4096 {
+        std::vector<fe> f, i;
+        Dft4096() : f(2048), i(2048) {
+            const fe w = h_root_of_unity(12), wi = h_inv(w);
+            f[0] = i[0] = fe_one();
+            for (int t = 1; t < 2048; t++) {
+                f[t] = fe_mul(f[t - 1], w);
+                i[t] = fe_mul(i[t - 1], wi);
+            }
         }
-    }
-    hipError_t e = upload(p, &T->dft_fwd, d4096f);
-    if (e == hipSuccess) e = upload(p, &T->dft_inv, d4096i);
+    };
+    static const Dft4096 d4096;
+    hipError_t e = upload(p, &T->dft_fwd, d4096.f);
+    if (e == hipSuccess) e = upload(p, &T->dft_inv, d4096.i);
     size_t n = (size_t)1 << log_n;
     fe w = h_root_of_unity(log_n);
     PowTable f, i;
@@ -242,6 +245,7 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     p->max_n = max_n;
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+    ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
@@ -446,22 +450,14 @@ int zk::check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_option
         ((o->fri_rem_max_deg + 1) & o->fri_rem_max_deg) || o->fri_rem_max_deg + 1 > ZK_MAX_REMAINDER ||
         o->num_queries == 0 || o->num_queries > ZK_MAX_QUERIES)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "unsupported proof options");
+    // winter-air ProofOptions::new asserts grinding_factor <= 32 (and the proof stores it as one byte)
+    if (o->grinding > 32) ZK_FAIL(ZK_ERR_INVALID_ARG, "grinding factor must be at most 32");
     if (n < 16 || (n & (n - 1)) || n > max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace length must be a power of two in [16, max_trace_len]");
     if (o->blowup > max_b) ZK_FAIL(ZK_ERR_INVALID_ARG, "blowup exceeds the prover's max_blowup");
     if (pub->lwe_size == 0 || pub->lwe_size > 5)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (enforce_add2 reads 2*lwe_size stack items, constrains.rs:129)");
     if (o->num_queries >= n * o->blowup) ZK_FAIL(ZK_ERR_INVALID_ARG, "num_queries must be smaller than the LDE domain");
     return ZK_OK;
-}
-
-// num_constraint_composition_columns for the ProcessorAir degrees (air/src/lib.rs:69-90) [P5]
-int zk::num_comp_cols(size_t n) {
-    static const int base[NUM_TCONS] = {1, 5, 2, 6, 6, 6, 7, 7, 6, 6, 6, 6, 4, 7, 4, 4, 2, 2, 2, 2};
-    static const int cyc[NUM_TCONS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1};
-    size_t hi = 0;
-    for (int k = 0; k < NUM_TCONS; k++) hi = std::max(hi, (size_t)base[k] * (n - 1) + (cyc[k] ? (n / 16) * 15 : 0));
-    size_t c = (hi - (n - 2) + n - 1) / n;
-    return (int)std::max<size_t>(c, 1);
 }
 
 Coin zk::seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub) {
@@ -959,6 +955,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));
+    IoScope io_scope(p);
     Plan *pl = nullptr;
     ZK_TRY(get_plan(p, n, B, &pl));
     const int log_n = pl->log_n, log_b = pl->log_b;
@@ -1247,6 +1244,7 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     if (n < 16 || (n & (n - 1)) || n > p->max_n || blowup < 8 || (blowup & (blowup - 1)) || blowup > p->max_b)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid trace length or blowup");
     ZK_CHECK_HIP(hipSetDevice(p->device));
+    IoScope io_scope(p);
     Plan *pl;
     int rc = get_plan(p, n, blowup, &pl);
     if (rc) return rc;
@@ -1358,6 +1356,7 @@ int zk_commit_composition(zk_trace_lde *h, const uint8_t *composition, uint32_t 
     zk_prover *p = h->p;
     const size_t n = h->n, CE = 8 * n;
     ZK_CHECK_HIP(hipSetDevice(p->device));
+    IoScope io_scope(p);
     Plan *pl;
     int rc = get_plan(p, n, h->B, &pl);
     if (rc) return rc;

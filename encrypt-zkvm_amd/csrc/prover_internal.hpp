@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/zkvm_gpu.h"
+#include "air_shape.hpp"
 #include "host_field.hpp"
 #include "zk_internal.hpp"
 
@@ -178,15 +179,32 @@ inline int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
 // one stream sync for every pending read; every copy enqueued before it has then completed, so the
 // staging area starts over
 inline int d2h_flush(zk_prover *p) {
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    for (const auto &r : p->io_pending) memcpy(r.dst, r.src, r.len);
+    const hipError_t e = hipStreamSynchronize(p->st);
+    if (e == hipSuccess)
+        for (const auto &r : p->io_pending) memcpy(r.dst, r.src, r.len);
+    // on a failed sync the destinations are not written (they may be gone once the caller returns)
     p->io_pending.clear();
     p->io_used = 0;
+    ZK_CHECK_HIP(e);
     return ZK_OK;
 }
 // sync the prover's stream and start its staging area over (a sharded proof's non-lead provers only
 // stage uploads, so they are rewound at the start of each proof)
 inline int io_rewind(zk_prover *p) { return d2h_flush(p); }
+// Scope guard for an entry point that stages transfers: whatever way the scope is left, reads still
+// pending (an error return between d2h_small and d2h_flush) are dropped, never delivered later into
+// the caller's stack or per-proof buffers, and the staging area starts over once the stream is idle.
+struct IoScope {
+    zk_prover *p;
+    explicit IoScope(zk_prover *q) : p(q) { drop(); }
+    ~IoScope() { drop(); }
+    void drop() {
+        if (p->io_pending.empty() && p->io_used == 0) return;
+        (void)hipStreamSynchronize(p->st);
+        p->io_pending.clear();
+        p->io_used = 0;
+    }
+};
 
 
 int get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out);
@@ -226,7 +244,6 @@ void plan_batch(size_t nl, const std::vector<uint64_t> &idx, BatchPlan &out);  /
 // argument checks shared by every prove entry point; returns ZK_OK or a status (g_err set)
 int check_prove_args(size_t n, size_t max_n, uint32_t max_b, const zk_options *opt, const zk_pub_inputs *pub);
 // num_constraint_composition_columns for the ProcessorAir degrees [P5]
-int num_comp_cols(size_t n);
 // S0: public coin seeded with Context::to_elements || PublicInputs::to_elements [P1]
 Coin seed_coin(size_t n, const zk_options *opt, const zk_pub_inputs *pub);
 // S3: composition coefficients (20 transition, 22 boundary) and the evaluator's constants [P3, P4]

@@ -794,5 +794,11 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
             ZK_CHECK_HIP(hipMemset(p->sh_zero, 0, sizeof(fe)));
         }
     }
+    // drop any staged reads an earlier failed proof left behind, and again on every way out of this one
+    std::vector<std::unique_ptr<IoScope>> io_scopes;
+    for (auto *p : X.P) {
+        ZK_CHECK_HIP(hipSetDevice(p->device));
+        io_scopes.push_back(std::make_unique<IoScope>(p));
+    }
     return prove_sharded(X, trace, opt, pub, proof_out, proof_len, rec);
 }

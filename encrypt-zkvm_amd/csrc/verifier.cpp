@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/zkvm_gpu.h"
+#include "air_shape.hpp"
 #include "host_field.hpp"
 #include "rescue_consts.hpp"
 
@@ -317,6 +318,8 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
     if (r.bad || tsl != 1 + 2 * W * ES || ts[0] != 2 || oel == 0 || oel % ES || oel / ES > ZK_MAX_CCOLS)
         fail("malformed out-of-domain frame");
     const int C = oel / ES;
+    // the composition column count follows from the AIR (winter-air derives it from the context)
+    if (C != zk::num_comp_cols(n)) fail("malformed out-of-domain frame");
     std::vector<fe2> ood(2 * W + C);
     for (int c = 0; c < W; c++) {
         ood[c] = elem_ext(ts + 1 + 2 * ES * c, K);
@@ -500,6 +503,12 @@ int zk_verify(const uint8_t *proof, size_t proof_len, const zk_pub_inputs *pub, 
     if (msg && msg_cap) msg[0] = 0;
     if (!proof || !pub) {
         if (msg && msg_cap) snprintf(msg, msg_cap, "null argument");
+        return ZK_ERR_INVALID_ARG;
+    }
+    // air_eval indexes the OOD frame by lwe_size: the same bound (and message) as the prover
+    if (pub->lwe_size == 0 || pub->lwe_size > 5) {
+        if (msg && msg_cap)
+            snprintf(msg, msg_cap, "lwe_size must be in [1, 5] (enforce_add2 reads 2*lwe_size stack items, constrains.rs:129)");
         return ZK_ERR_INVALID_ARG;
     }
     try {

@@ -169,6 +169,9 @@ void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_c
 struct EvalMap {
     int nce, ce0, cestep, lshift, lde_cosets;
 };
+// Rescue MDS / inverse-MDS __constant__ tables on the current device (once per device; thread-safe).
+// zk_prover_create calls it; the evaluator launches check it again (the plug point may run first).
+hipError_t upload_rescue_consts(hipStream_t st);
 // bnd: the boundary (assertion) terms are evaluated per row (else: boundary_poly_add after interpolation)
 void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                              const fe *divs, const AirConsts *consts_dev, fe *comp, bool bnd = true);

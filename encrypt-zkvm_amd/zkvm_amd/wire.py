@@ -13,7 +13,7 @@ Parity at this layer is unpinned like the rest of the winterfell layout (SURVEY.
 from __future__ import annotations
 
 import struct
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 P = 2**128 - 45 * 2**40 + 1
 
@@ -72,6 +72,8 @@ class ProofView:
     commitments: bytes
     num_fri_layers: int
     pow_nonce: int
+    # length-prefixed sections: name -> (offset of the length prefix in ``raw``, prefix bytes, body length)
+    sections: dict = field(default_factory=dict)
 
 
 class _R:
@@ -110,10 +112,18 @@ def parse_proof(buf: bytes, off: int = 0) -> tuple[ProofView, int]:
     for _ in range(r.u8()):  # trace segments: values + batch proof
         r.take(r.u32())
         r.take(r.u32())
-    r.take(r.u32())  # constraint values
-    r.take(r.u32())  # constraint batch proof
-    r.take(r.u16())  # OOD trace states
-    r.take(r.u16())  # OOD constraint evaluations
+    sections = {}
+
+    def sect(name, width):
+        at = r.o - off
+        ln = r.u16() if width == 2 else r.u32()
+        r.take(ln)
+        sections[name] = (at, width, ln)
+
+    sect("constraint_values", 4)
+    sect("constraint_proof", 4)
+    sect("ood_trace_states", 2)
+    sect("ood_evaluations", 2)
     nl = r.u8()
     for _ in range(nl):
         r.take(r.u32())
@@ -123,7 +133,8 @@ def parse_proof(buf: bytes, off: int = 0) -> tuple[ProofView, int]:
     nonce = r.u64()
     if r.u8():  # gkr proof: Some(..) is not produced by this AIR
         raise ValueError("unexpected GKR proof")
-    view = ProofView(bytes(buf[off:r.o]), width, 1 << log_n, nq, blowup, grind, ext, fold, remdeg, nu, coms, nl, nonce)
+    view = ProofView(bytes(buf[off:r.o]), width, 1 << log_n, nq, blowup, grind, ext, fold, remdeg, nu, coms, nl, nonce,
+                     sections)
     if aux_w or aux_r:
         raise ValueError("unexpected auxiliary trace segment")
     return view, r.o

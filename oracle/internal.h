@@ -114,4 +114,8 @@ uint8_t *merkle_build(const uint8_t *leaves, size_t num_leaves);
 void air_eval_u(const u128 *cur, const u128 *nxt, const u128 *per, uint32_t lwe, u128 delta, u128 *out);
 void air_periodic_u(unsigned step16, u128 *out9);
 
+
+/* winter-air AirContext::num_constraint_composition_columns for ProcessorAir (prover.c) */
+size_t or_num_comp_cols(size_t n);
+
 #endif

@@ -165,7 +165,7 @@ static const int DEG_BASE[NUM_TCONS] = {1, 5, 2, 6, 6, 6, 7, 7, 6, 6, 6, 6, 4, 7
 static const int DEG_CYC[NUM_TCONS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1};
 
 /* winter-air AirContext::num_constraint_composition_columns [P5] */
-static size_t num_comp_cols(size_t n) {
+size_t or_num_comp_cols(size_t n) {
     size_t hi = 0;
     for (int k = 0; k < NUM_TCONS; k++) {
         size_t d = (size_t)DEG_BASE[k] * (n - 1) + (DEG_CYC[k] ? (n / 16) * 15 : 0);
@@ -204,7 +204,7 @@ int or_prove(const void *trace_v, size_t n, const or_options *opt, const or_pub_
     const u128 *trace = (const u128 *)trace_v;
     const size_t B = opt->blowup, N = B * n, CE = CE_BLOWUP * n, fold = opt->fri_folding;
     if (opt->num_queries >= N) return OR_ERR_INVALID_ARG;
-    const size_t C = num_comp_cols(n);
+    const size_t C = or_num_comp_cols(n);
     const int K = (int)opt->field_extension; /* 1: FieldExtension::None, 2: Quadratic */
     const u128 offset = F_GENERATOR; /* StarkDomain offset = GENERATOR [P1] */
     const u128 g_n = f_root_of_unity(ilog2_sz(n));

@@ -300,3 +300,42 @@ def test_reference_vm_prove_and_verify(gpu):
     assert sk.decrypt(output[:5]) == (a + clear_x) * 3
     pub = make_pub_inputs(h, output, sk.lwe_size(), sk.parameters.delta)
     assert verify(proof, pub, 95) == (0, "")
+
+
+@pytest.mark.parametrize("grinding", [33, 64, 255])
+def test_grinding_factor_bound(gpu, grinding):
+    """winter-air ProofOptions caps grinding_factor at 32: larger values are refused up front (a search for
+    more than 64 trailing zero bits would never end; the proof stores the factor in one byte)."""
+    trace, pub = workload_trace(LR_PROGRAM, seed=4)
+    with pytest.raises(native.ZkError) as e:
+        gpu.prove(trace, pub, ProofOptions(grinding_factor=grinding))
+    assert e.value.code == native.ZK_ERR_INVALID_ARG and "grinding" in str(e.value)
+
+
+def test_error_then_proof_is_unchanged(gpu, oracle):
+    """A proof that fails part-way (degree error after staged reads) leaves nothing pending in the
+    prover's pinned staging area: the next proof is byte-identical to the oracle's."""
+    trace, pub = workload_trace(LR_PROGRAM, seed=6)
+    bad = trace.copy()
+    bad[12, 10, 0] ^= 1
+    _, _, _, rc = gpu.prove(bad, pub, ProofOptions(), allow_degree_error=True)
+    assert rc == native.ZK_ERR_DEGREE
+    proof, _, _, rc = gpu.prove(trace, pub, ProofOptions())
+    assert rc == 0
+    oproof, _, _ = oracle.prove(trace, oracle_pub(oracle, pub))
+    assert proof == oproof
+
+
+def test_provers_on_every_device_agree(oracle):
+    """__constant__ tables (Rescue MDS / inverse MDS) are per device: a prover on each visible GPU of one
+    process, created after another device already proved, gives the same proof bytes."""
+    n_dev = native.device_count()
+    trace, pub = workload_trace(LR_PROGRAM, seed=8)
+    oproof, _, _ = oracle.prove(trace, oracle_pub(oracle, pub))
+    for dev in range(min(n_dev, 8)):
+        g = GpuProver(dev, max_trace_len=trace.shape[1])
+        try:
+            proof, _, _, rc = g.prove(trace, pub, ProofOptions())
+        finally:
+            g.close()
+        assert rc == 0 and proof == oproof, f"device {dev}"

@@ -51,3 +51,38 @@ def test_output_data_roundtrip(c):
         wire.OutputData.from_bytes(blob[:-1])
     with pytest.raises(ValueError):
         wire.OutputData.from_bytes(blob + b"\x00")
+
+
+def _case(name):
+    c = next(c for c in CASES if c["name"] == name)
+    pub = make_pub_inputs(ints(c["program_hash"]), ints(c["stack_outputs"]), c["lwe_size"], c["delta"])
+    return c, (GOLD / f"{name}.proof").read_bytes(), pub
+
+
+@pytest.mark.parametrize("lwe_size", [0, 6, 255])
+def test_verify_rejects_lwe_size_out_of_range(lwe_size):
+    """zk_verify bounds lwe_size like the prover (air_eval indexes the OOD frame with it)."""
+    from zkvm_amd import native
+    c, proof, pub = _case("lr")
+    pub.lwe_size = lwe_size
+    rc, msg = verify(proof, pub, 0)
+    assert rc == native.ZK_ERR_INVALID_ARG and "lwe_size" in msg
+
+
+@pytest.mark.parametrize("name", ["lr", "lr_quad"])
+@pytest.mark.parametrize("delta_cols", [-1, +1])
+def test_verify_requires_air_composition_width(name, delta_cols):
+    """The OOD constraint frame must hold exactly num_comp_cols(n) values (winter-air derives the count
+    from the AIR); a frame one column shorter or longer is malformed, not re-interpreted."""
+    from zkvm_amd import native
+    c, proof, pub = _case(name)
+    view, _ = wire.parse_proof(proof)
+    at, width, ln = view.sections["ood_evaluations"]
+    es = 16 * view.field_extension
+    assert width == 2 and ln % es == 0 and ln // es == 7
+    body = proof[at + 2:at + 2 + ln]
+    body = body[:-es] if delta_cols < 0 else body + body[:es]
+    bad = proof[:at] + len(body).to_bytes(2, "little") + body + proof[at + 2 + ln:]
+    rc, msg = verify(bad, pub, 0)
+    assert rc == native.ZK_ERR_VERIFY and msg == "malformed out-of-domain frame"
+    assert verify(proof, pub, 0) == (0, "")
