@@ -4,6 +4,9 @@
 
 #include <algorithm>
 
+#include "../../include/zkvm_gpu.h"
+#include "ext2.hpp"
+
 namespace zk {
 // num_constraint_composition_columns for the ProcessorAir transition degrees (air/src/lib.rs:69-90;
 // winter-air TransitionConstraintDegree::get_evaluation_degree, cycle length 16) [DESIGN P6]:
@@ -16,4 +19,7 @@ inline int num_comp_cols(size_t n) {
     size_t c = (hi - (n - 2) + n - 1) / n;
     return (int)std::max<size_t>(c, 1);
 }
+// verifier.cpp: the out-of-domain constraint identity at z (ood = [T(z)]_W ++ [T(zg)]_W ++ [H_j(z)]_C;
+// ct: 20 transition, cb: 22 boundary composition coefficients), over E (base values lift with b = 0)
+bool ood_identity(const fe2 *ood, int C, const fe2 *ct, const fe2 *cb, fe2 z, size_t n, const zk_pub_inputs *pub);
 }  // namespace zk

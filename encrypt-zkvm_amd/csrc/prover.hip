@@ -948,6 +948,22 @@ static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe
     return commit_rows(p, clde, CK, pl->log_n, pl->log_b, p->cleaves, p->cnodes, root);
 }
 
+// Degree check of the composition: the verifier's out-of-domain identity (zk::ood_identity) on the
+// frame the proof will carry.  For a trace that satisfies ProcessorAir the composition columns are
+// exactly C(x)/Z(x) + boundary quotients, so the identity holds; for any other trace the committed
+// columns interpolate a function that is not a polynomial of degree < C*n and the identity fails at the
+// transcript-derived z except with probability ~ (degree / p) ~ 2^-100 (Schwartz-Zippel).
+// K: the composition coefficients (planes a, b for FieldExtension::Quadratic).
+static int check_ood_identity(const std::vector<fe2> &e, int C, const AirConsts *K, int KX, fe2 z, size_t n,
+                              const zk_pub_inputs *pub) {
+    fe2 ct[NUM_TCONS], cb[NUM_ASSERTS];
+    for (int k = 0; k < NUM_TCONS; k++) ct[k] = fe2{K[0].coeff_t[k], KX == 2 ? K[1].coeff_t[k] : fe_zero()};
+    for (int k = 0; k < NUM_ASSERTS; k++) cb[k] = fe2{K[0].coeff_b[k], KX == 2 ? K[1].coeff_b[k] : fe_zero()};
+    if (!ood_identity(e.data(), C, ct, cb, z, n, pub))
+        ZK_FAIL(ZK_ERR_DEGREE, "the trace does not satisfy ProcessorAir (out-of-domain constraint identity failed)");
+    return ZK_OK;
+}
+
 int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                     uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     if (!p || !d_trace_v || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
@@ -1040,6 +1056,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->ct,
                           p->dscratch, p->ulde, p->tmp, deep);
         HT.stop("deep_consts");
+        // while the GPU runs DEEP: the verifier's out-of-domain identity on the frame just read
+        std::vector<fe2> e(2 * W + C);
+        for (int i = 0; i < 2 * W + C; i++) e[i] = fe2_lift(h[i]);
+        ZK_TRY(check_ood_identity(e, C, Kp, 1, fe2_lift(z), n, pub));
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
         fe_to_bytes(z.a, R.z);
@@ -1055,6 +1075,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
         deep_coeff_ext_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->x_deep_consts, z, zg,
                               pl->ct, p->x_dscratch, p->x_ulde, p->tmp, deep);
+        ZK_TRY(check_ood_identity(e, C, Kp, 2, z, n, pub));
     }
     stage_mark(p, "deep");
 

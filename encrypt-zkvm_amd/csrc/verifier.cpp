@@ -334,32 +334,7 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
         coin.reseed(d);
     }
     // out-of-domain identity
-    {
-        const fe g = h_root_of_unity(logn);
-        const fe2 one = fe2_one();
-        fe2 per[9], ev[NT];
-        periodic_at(fe2_exp(z, n / 16), per);
-        air_eval(ood.data(), ood.data() + W, per, pub->lwe_size, fe_make(pub->delta), ev);
-        fe2 t = fe2_zero();
-        for (int k = 0; k < NT; k++) t = fe2_add(t, fe2_mul(ct[k], ev[k]));
-        const fe2 gl2 = fe2_lift(h_pow(g, n - 2)), gl1 = fe2_lift(h_pow(g, n - 1)), zn = fe2_exp(z, n);
-        fe2 h = fe2_mul(fe2_mul(t, fe2_mul(fe2_sub(z, gl2), fe2_sub(z, gl1))), fe2_inv(fe2_sub(zn, one)));
-        const int fc[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
-        fe2 bs0 = fe2_zero(), bs1 = fe2_zero();
-        for (int i = 0; i < 12; i++) bs0 = fe2_add(bs0, fe2_mul(cb[i], ood[fc[i]]));
-        for (int i = 0; i < 2; i++)
-            bs1 = fe2_add(bs1, fe2_mul(cb[12 + i], fe2_sub(ood[7 + i], fe2_lift(fe_from_bytes(pub->program_hash[i])))));
-        for (int i = 0; i < 8; i++)
-            bs1 = fe2_add(bs1, fe2_mul(cb[14 + i], fe2_sub(ood[12 + i], fe2_lift(fe_from_bytes(pub->stack_outputs[i])))));
-        h = fe2_add(h, fe2_mul(bs0, fe2_inv(fe2_sub(z, one))));
-        h = fe2_add(h, fe2_mul(bs1, fe2_inv(fe2_sub(z, gl2))));
-        fe2 hc = fe2_zero(), zz = one;
-        for (int j = 0; j < C; j++) {
-            hc = fe2_add(hc, fe2_mul(zz, ood[2 * W + j]));
-            zz = fe2_mul(zz, zn);
-        }
-        if (!fe2_eq(h, hc)) fail("out-of-domain constraint evaluation mismatch");
-    }
+    if (!zk::ood_identity(ood.data(), C, ct, cb, z, n, pub)) fail("out-of-domain constraint evaluation mismatch");
     fe2 at[W], ac[ZK_MAX_CCOLS];
     for (auto &v : at) v = coin.draw_ext(K);
     for (int j = 0; j < C; j++) ac[j] = coin.draw_ext(K);
@@ -497,6 +472,38 @@ void verify(const uint8_t *proof, size_t plen, const zk_pub_inputs *pub, uint32_
 }
 
 }  // namespace
+
+
+// The verifier's out-of-domain identity (winterfell verifier: evaluate_constraints at z against the
+// composition columns): sum_k ct_k C_k(z) * divisor(z) + boundary terms == sum_j z^(jn) H_j(z).
+// ood = [T(z)]_W ++ [T(zg)]_W ++ [H_j(z)]_C.  The prover runs it as its degree check.
+bool zk::ood_identity(const fe2 *ood, int C, const fe2 *ct, const fe2 *cb, fe2 z, size_t n, const zk_pub_inputs *pub) {
+    const int logn = ilog2z(n);
+    const fe g = h_root_of_unity(logn);
+    const fe2 one = fe2_one();
+    fe2 per[9], ev[NT];
+    periodic_at(fe2_exp(z, n / 16), per);
+    air_eval(ood, ood + W, per, pub->lwe_size, fe_make(pub->delta), ev);
+    fe2 t = fe2_zero();
+    for (int k = 0; k < NT; k++) t = fe2_add(t, fe2_mul(ct[k], ev[k]));
+    const fe2 gl2 = fe2_lift(h_pow(g, n - 2)), gl1 = fe2_lift(h_pow(g, n - 1)), zn = fe2_exp(z, n);
+    fe2 h = fe2_mul(fe2_mul(t, fe2_mul(fe2_sub(z, gl2), fe2_sub(z, gl1))), fe2_inv(fe2_sub(zn, one)));
+    const int fc[12] = {0, 7, 8, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+    fe2 bs0 = fe2_zero(), bs1 = fe2_zero();
+    for (int i = 0; i < 12; i++) bs0 = fe2_add(bs0, fe2_mul(cb[i], ood[fc[i]]));
+    for (int i = 0; i < 2; i++)
+        bs1 = fe2_add(bs1, fe2_mul(cb[12 + i], fe2_sub(ood[7 + i], fe2_lift(fe_from_bytes(pub->program_hash[i])))));
+    for (int i = 0; i < 8; i++)
+        bs1 = fe2_add(bs1, fe2_mul(cb[14 + i], fe2_sub(ood[12 + i], fe2_lift(fe_from_bytes(pub->stack_outputs[i])))));
+    h = fe2_add(h, fe2_mul(bs0, fe2_inv(fe2_sub(z, one))));
+    h = fe2_add(h, fe2_mul(bs1, fe2_inv(fe2_sub(z, gl2))));
+    fe2 hc = fe2_zero(), zz = one;
+    for (int j = 0; j < C; j++) {
+        hc = fe2_add(hc, fe2_mul(zz, ood[2 * W + j]));
+        zz = fe2_mul(zz, zn);
+    }
+    return fe2_eq(h, hc);
+}
 
 int zk_verify(const uint8_t *proof, size_t proof_len, const zk_pub_inputs *pub, uint32_t min_security, char *msg,
               size_t msg_cap) {

@@ -68,16 +68,17 @@ class ShardedProver:
             trace = np.ascontiguousarray(trace, dtype=np.uint64)
             n = trace.shape[1]
         opt = options.to_c()
-        cap = 4 << 20
-        buf = C.create_string_buffer(cap)
-        plen = C.c_size_t(cap)
+        if getattr(self, "_proof_buf", None) is None:  # reused across proofs (see GpuProver.prove_device)
+            self._proof_buf = C.create_string_buffer(4 << 20)
+        buf = self._proof_buf
+        plen = C.c_size_t(len(buf))
         rec = Record() if record else None
         arr = (C.c_void_p * len(self.provers))(*[p.value for p in self.provers])
         rc = lib().zk_prove_sharded(self.comm, arr, len(self.provers),
                                     trace.ctypes.data if trace is not None else None, n, C.byref(opt),
                                     C.byref(pub), buf, C.byref(plen), C.byref(rec) if rec is not None else None)
         check(rc, "zk_prove_sharded")
-        return buf.raw[:plen.value], rec
+        return C.string_at(buf, plen.value), rec
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 32)()
