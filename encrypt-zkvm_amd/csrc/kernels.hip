@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <bitset>
 #include <mutex>
+#include <stdlib.h>
+#include <string.h>
 
 #include "blake3.hpp"
 #include "rescue_consts.hpp"
@@ -387,6 +389,16 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
 
 void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp);
 
+int ntt_log_n2(int L) {
+    static const bool balanced = [] {
+        const char *e = getenv("ZK_NTT_SPLIT");
+        return e && !strcmp(e, "balanced");
+    }();
+    const int bal = (L + 1) / 2;
+    if (balanced || L < 20) return bal;
+    return std::min(12, L - 10);  // pass-2 lines of 1024 while pass-1 lines fit a 4096-element tile
+}
+
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
          bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
     NttArgs a;
@@ -429,8 +441,8 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
         ZK_DISPATCH_LOGM(L, launch_single, st, a, batch);
         return;
     }
-    // n = n1 * n2 with n2 = 2^ceil(L/2) (pass-1 lines), n1 = 2^floor(L/2) (pass-2 lines)
-    const int log_n2 = (L + 1) / 2, log_n1 = L / 2;
+    // n = n1 * n2: pass-1 lines of n2 = 2^log_n2, pass-2 lines of n1 = 2^log_n1 (ntt_log_n2)
+    const int log_n2 = ntt_log_n2(L), log_n1 = L - log_n2;
     NttArgs a1 = a;
     a1.out = tmp;
     a1.out_stride = (size_t)1 << L;
@@ -506,7 +518,7 @@ void coset_pass_tables(hipStream_t st, const fe *s_lo, const fe *s_hi, const fe 
 
 void make_pass_twiddles(hipStream_t st, NttTables &T) {
     const size_t n = (size_t)1 << T.log_n;
-    const int log_n2 = (T.log_n + 1) / 2;  // pass-1 line length, as in ntt()
+    const int log_n2 = ntt_log_n2(T.log_n);  // pass-1 line length, as in ntt_run()
     const unsigned blocks = std::min<size_t>(cdiv(n, 256), 65536);
     hipLaunchKernelGGL(k_pass_twiddles, dim3(blocks), dim3(256), 0, st, T.fwd_lo, T.fwd_hi, T.log_n, log_n2, T.fwd_pass,
                        (fe *)nullptr, fe_zero());

@@ -160,7 +160,7 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
         ZK_CHECK_HIP(p->arena.alloc(&pl->ct.pass, (size_t)B * n));
         ZK_CHECK_HIP(p->arena.alloc(&pl->ct.stage, (size_t)B * 4096));
     }
-    const int log_n2 = (pl->log_n + 1) / 2;  // pass-1 line length of the four-step split (as in ntt())
+    const int log_n2 = ntt_log_n2(pl->log_n);  // pass-1 line length of the four-step split (as in ntt_run())
     const size_t n2 = (size_t)1 << log_n2, n1 = n >> log_n2;
     std::vector<fe> stage(pl->log_n > 12 ? (size_t)B * 4096 : 0);
     for (uint32_t r = 0; r < B; r++) {

@@ -80,6 +80,14 @@ struct NttTables {
     fe *inv_pass_n = nullptr;
     fe inv_n = {0, 0};
 };
+// Four-step split of a size-2^L NTT (L > 12): log2 of the pass-1 line length n2 (pass-2 lines are
+// n1 = 2^(L - log_n2)).  Pass 1 reads strided and writes contiguous runs; pass 2 reads and writes
+// LPB-element row segments at stride n2, so pass 2 gets the shorter lines when the split is uneven:
+// at L = 22 the balanced 11/11 split leaves pass 2 with 32-B segments (2 lines of 2048 per
+// 4096-element tile) and an extra radix-2 LDS stage; 12/10 gives it the 64-B segments of 2^20.
+// Every table builder and the NTT dispatcher use this one function, so they always agree.
+// ZK_NTT_SPLIT=balanced restores the ceil(L/2) split (A/B runs); read once per process.
+int ntt_log_n2(int L);
 // fill NttTables::fwd_pass / inv_pass (allocated by the caller, n elements each)
 void make_pass_twiddles(hipStream_t st, NttTables &T);
 // out[k1*n2 + j2] = s^k1 * fwd_pass[k1*n2 + j2] (s^t from split tables): CosetTables::pass of one coset

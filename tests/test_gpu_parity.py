@@ -73,6 +73,32 @@ def test_ntt(gpu, oracle, log_n):
         assert got[b * n:(b + 1) * n] == oracle.interp_coset(vals[b * n:(b + 1) * n], 1), f"inverse batch {b}"
 
 
+def _random_elems_bytes(count, seed):
+    """count canonical field elements as 16-byte LE words (hi < 2^64 - 1 keeps every value below p)."""
+    rng = np.random.default_rng(seed)
+    a = np.empty((count, 2), dtype=np.uint64)
+    a[:, 0] = rng.integers(0, 2**64, size=count, dtype=np.uint64)
+    a[:, 1] = rng.integers(0, 2**64 - 1, size=count, dtype=np.uint64)
+    return a.tobytes()
+
+
+@pytest.mark.parametrize("log_n", [20, 21, 22])
+def test_ntt_four_step_splits(oracle, log_n):
+    """Sizes whose four-step split is uneven or LOGM-odd (ntt_log_n2: 2^21 -> 11/10, 2^22 -> 12/10),
+    one column, against the oracle's radix-2 transforms (bytes compared directly)."""
+    n = 1 << log_n
+    vals = _random_elems_bytes(n, log_n)
+    out = C.create_string_buffer(16 * n)
+    native.check(native.lib().zk_diag_ntt(0, vals, n, 1, 0, elems_bytes([3]), out))
+    ref = C.create_string_buffer(16 * n)
+    assert oracle.lib().or_eval_coset(vals, n, n, elems_bytes([3]), ref) == 0
+    assert out.raw == ref.raw, "forward coset NTT differs"
+    native.check(native.lib().zk_diag_ntt(0, vals, n, 1, 1, None, out))
+    buf = C.create_string_buffer(vals, 16 * n)
+    assert oracle.lib().or_interp_coset(buf, n, elems_bytes([1])) == 0
+    assert out.raw == buf.raw, "inverse NTT differs"
+
+
 def workload_trace(source, seed=3):
     w = make_workload(source, seed=seed)
     trace, outputs, h = vm_trace(source, w.public, w.secret, w.server_key, w.last_row)
@@ -282,6 +308,23 @@ def test_bench_size_proof_verifies(gpu, oracle):
     # proof is deterministic for a fixed trace
     proof2, _, _, _ = gpu.prove(trace, pub, ProofOptions())
     assert proof2 == proof
+
+
+def test_2_22_proof_verifies(oracle):
+    """configs[3] size on one GPU: a 2^22-step cipher-mix proof (the four-step NTTs take the 12/10 split
+    here) verifies with zk_verify and the oracle's verifier."""
+    from zkvm_amd.prover import verify
+    source = ops_for_trace_len(22, "cipher")
+    trace, pub = workload_trace(source, seed=22)
+    assert trace.shape[1] == 1 << 22
+    g = GpuProver(0, max_trace_len=1 << 22)
+    try:
+        proof, _, _, rc = g.prove(trace, pub, ProofOptions())
+    finally:
+        g.close()
+    assert rc == 0
+    assert verify(proof, pub, 95) == (0, "")
+    assert oracle.verify(proof, oracle_pub(oracle, pub), 95) == (0, "")
 
 
 def test_reference_vm_prove_and_verify(gpu):
