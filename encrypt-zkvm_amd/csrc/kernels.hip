@@ -2117,6 +2117,22 @@ __global__ void k_gather_chunks(const uint64_t *addr, size_t k, fe *out) {
     if (t < k) out[t] = *reinterpret_cast<const fe *>((uintptr_t)addr[t]);
 }
 
+__global__ void __launch_bounds__(256) k_copy_to_host(CopyList L) {
+    const int e = blockIdx.y;
+    if (e >= L.n) return;
+    const uint32_t *src = L.src[e];
+    uint32_t *dst = L.dst[e];
+    for (size_t w = blockIdx.x * (size_t)blockDim.x + threadIdx.x; w < L.words[e]; w += (size_t)gridDim.x * blockDim.x)
+        dst[w] = src[w];
+    __threadfence_system();
+}
+
+void copy_to_host(hipStream_t st, const CopyList &L, size_t max_words) {
+    if (L.n <= 0) return;
+    const unsigned bx = std::max(1u, std::min(cdiv(max_words, 256), 64u));
+    hipLaunchKernelGGL(k_copy_to_host, dim3(bx, (unsigned)L.n), dim3(256), 0, st, L);
+}
+
 void gather_chunks(hipStream_t st, const uint64_t *addr, size_t k, fe *out) {
     if (k) ZK_PROF(st, "gather_chunks", 24.0 * k, hipLaunchKernelGGL(k_gather_chunks, dim3(cdiv(k, 256)), dim3(256), 0, st, addr, k, out));
 }

@@ -240,6 +240,13 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) ZK_FAIL(ZK_ERR_DEVICE, "no HIP device available");
     if (device < 0 || device >= cnt) ZK_FAIL(ZK_ERR_INVALID_ARG, "device index out of range");
     ZK_CHECK_HIP(hipSetDevice(device));
+    // The host waits on the prover stream a few times per proof (transcript round trips): spin instead
+    // of yielding (A/B: -0.05 ms per 2^20 proof).  Only takes effect if this is the first use of the
+    // device in the process; ZK_SPIN_WAIT=0 keeps the runtime's default.
+    {
+        const char *e = getenv("ZK_SPIN_WAIT");
+        if (!e || atoi(e)) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+    }
     auto p = std::make_unique<zk_prover>();
     p->device = device;
     p->max_n = max_n;

@@ -141,6 +141,16 @@ void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *node
 // out[t] = the 16 bytes at device address addr[t] (query openings: LDE values and Merkle digests)
 constexpr size_t ZK_GATHER_CAP = 1 << 17;
 void gather_chunks(hipStream_t st, const uint64_t *addr, size_t k, fe *out);
+// Up to ZK_COPY_LIST_MAX device -> pinned-host copies (32-bit words) in one launch: blockIdx.y picks
+// the entry.  dst must be host memory from hipHostMalloc (device-accessible, coherent).
+constexpr int ZK_COPY_LIST_MAX = 32;
+struct CopyList {
+    int n;
+    const uint32_t *src[ZK_COPY_LIST_MAX];
+    uint32_t *dst[ZK_COPY_LIST_MAX];
+    uint32_t words[ZK_COPY_LIST_MAX];
+};
+void copy_to_host(hipStream_t st, const CopyList &L, size_t max_words);
 void gather_digests(hipStream_t st, const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out);
 // out[q*ncols + c] = element (c, pos[q]) of a coset-major column set
 void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,

@@ -36,12 +36,13 @@ def fits(c, world):
     return n // fold >= 8 * world and n // world >= 8
 
 
+FITTING = [(c, w) for c in CASES for w in (1, 2, 4, 8) if fits(c, w)]
+TOO_SHORT = [(c, w) for c in CASES for w in (1, 2, 4, 8) if not fits(c, w)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+@pytest.mark.parametrize("c,world", FITTING, ids=[f"{c['name']}-w{w}" for c, w in FITTING])
 def test_sharded_matches_golden(c, world):
-    if not fits(c, world):
-        pytest.skip("trace too short for this many ranks")
     trace, proof, pub, opts = case_inputs(c)
     sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
     try:
@@ -52,6 +53,21 @@ def test_sharded_matches_golden(c, world):
     assert bytes(rec.constraint_root).hex() == c["constraint_root"]
     assert [bytes(rec.fri_roots[i]).hex() for i in range(rec.num_fri_layers)] == c["fri_roots"]
     assert got == proof
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,world", TOO_SHORT, ids=[f"{c['name']}-w{w}" for c, w in TOO_SHORT])
+def test_sharded_refuses_too_short_trace(c, world):
+    """A trace whose FRI layer 1 or coset slices are smaller than the rank count is refused up front
+    (ZK_ERR_INVALID_ARG), never proved with a wrong split."""
+    trace, _, pub, opts = case_inputs(c)
+    sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
+    try:
+        with pytest.raises(native.ZkError) as e:
+            sp.prove(trace, pub, opts)
+    finally:
+        sp.close()
+    assert e.value.code == native.ZK_ERR_INVALID_ARG and "too short" in str(e.value)
 
 
 @pytest.mark.gpu
