@@ -245,7 +245,10 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     // device in the process; ZK_SPIN_WAIT=0 keeps the runtime's default.
     {
         const char *e = getenv("ZK_SPIN_WAIT");
-        if (!e || atoi(e)) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        if (!e || atoi(e)) {
+            (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+            (void)hipGetLastError();  // refused once the context exists: leave no sticky error behind
+        }
     }
     auto p = std::make_unique<zk_prover>();
     p->device = device;
