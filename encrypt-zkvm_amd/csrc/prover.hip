@@ -302,7 +302,7 @@ void zk_prover_destroy(zk_prover *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     (void)hipStreamSynchronize(p->st);
-    for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
+    for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
@@ -319,26 +319,31 @@ int zk_prover_trace_buffer(zk_prover *p, void **d_trace) {
 
 // ---------------------------------------------------------------- stage timing
 void zk::stage_begin(zk_prover *p) {
-    for (auto &e : p->stage_ev) (void)hipEventDestroy(e.second);
-    p->stage_ev.clear();
+    p->stage_names.clear();
+    p->stage_done = false;
 }
 void zk::stage_mark(zk_prover *p, const char *name) {
-    hipEvent_t e;
-    (void)hipEventCreate(&e);
-    (void)hipEventRecord(e, p->st);
-    p->stage_ev.push_back({name, e});
-}
-void zk::stage_collect(zk_prover *p) {
-    p->stage_ms.clear();
-    for (size_t i = 1; i < p->stage_ev.size(); i++) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, p->stage_ev[i - 1].second, p->stage_ev[i].second);
-        p->stage_ms.push_back({p->stage_ev[i].first, ms});
+    const size_t i = p->stage_names.size();
+    if (i == p->stage_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;  // timing only: a missing mark is not an error
+        p->stage_pool.push_back(e);
     }
+    (void)hipEventRecord(p->stage_pool[i], p->st);
+    p->stage_names.push_back(name);
 }
+// the proof is complete (its stream synchronized): its stage events may be read until the next proof
+void zk::stage_collect(zk_prover *p) { p->stage_done = true; }
 
 int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, int *count) {
     if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    p->stage_ms.clear();
+    if (p->stage_done)
+        for (size_t i = 1; i < p->stage_names.size(); i++) {
+            float t = 0;
+            (void)hipEventElapsedTime(&t, p->stage_pool[i - 1], p->stage_pool[i]);
+            p->stage_ms.push_back({p->stage_names[i], t});
+        }
     int k = (int)p->stage_ms.size();
     for (int i = 0; i < k && i < cap; i++) {
         if (names) names[i] = p->stage_ms[i].first;

@@ -93,18 +93,20 @@ class GpuProver:
         buf = self._proof_buf
         plen = C.c_size_t(len(buf))
         rec = Record() if record else None
-        dmp = Dump()
         held = {}
-        N = n * options.blowup_factor
-        sizes = {"trace_polys": 28 * n, "trace_lde": N * 28, "trace_leaves": N * 2, "composition": 8 * n,
-                 "comp_polys": 16 * n, "comp_lde": N * 16, "deep": N,
-                 "fri_layer1": max(1, N // options.fri_folding_factor)}
-        for name in dump:
-            held[name] = np.zeros((sizes[name], 2), dtype=np.uint64)
-            setattr(dmp, name, held[name].ctypes.data)
-        rc = lib().zk_prove_device(self.handle, C.c_void_p(d_trace), n, C.byref(opt), C.byref(pub), buf,
-                                   C.byref(plen), C.byref(rec) if rec is not None else None,
-                                   C.byref(dmp) if dump else None)
+        dmp = None
+        if dump:
+            dmp = Dump()
+            N = n * options.blowup_factor
+            sizes = {"trace_polys": 28 * n, "trace_lde": N * 28, "trace_leaves": N * 2, "composition": 8 * n,
+                     "comp_polys": 16 * n, "comp_lde": N * 16, "deep": N,
+                     "fri_layer1": max(1, N // options.fri_folding_factor)}
+            for name in dump:
+                held[name] = np.zeros((sizes[name], 2), dtype=np.uint64)
+                setattr(dmp, name, held[name].ctypes.data)
+        rc = lib().zk_prove_device(self.handle, d_trace, n, C.byref(opt), C.byref(pub), buf, C.byref(plen),
+                                   C.byref(rec) if rec is not None else None,
+                                   C.byref(dmp) if dmp is not None else None)
         if not (rc == 0 or (allow_degree_error and rc == native.ZK_ERR_DEGREE)):
             check(rc, "zk_prove_device")
         return C.string_at(buf, plen.value), rec, held, rc
