@@ -4,11 +4,15 @@ Counters (one pass; see tools/gpu_profile.sh): SQ_INSTS_VALU, SQ_ACTIVE_INST_VAL
 SQ_BUSY_CYCLES, SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE, GRBM_COUNT.
 
   clock      = GRBM_GUI_ACTIVE / n_xcd / kernel duration     (GRBM counts are summed over the 8 XCDs)
-  valu_issue = SQ_INSTS_VALU * 4 / (1024 SIMDs * GRBM_GUI_ACTIVE / n_xcd)
-               (a wave64 VALU instruction occupies its SIMD for 4 cycles; 256 CUs x 4 SIMDs)
+  slot_util  = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / n_xcd)
+               (CDNA4 SIMDs are 32 lanes wide: a plain wave64 VALU instruction issues in 2 cycles;
+               measured in tools/ubench/instr*_ubench, profiles/r02_ubench_issue.txt)
 
-valu_issue near 1.0 means the SIMDs issued a VALU instruction on (nearly) every cycle the kernel ran:
-the kernel is bound by its instruction count, not by memory or latency.
+slot_util is the fraction of 2-cycle issue slots that carried a VALU instruction.  It cannot reach 1.0
+for the f128 kernels: instructions that read or write an SGPR (carry-in/-out, lane-mask selects, the
+v_mad_u64_u32 carry-out) issue at most about once per 3.4 cycles per SIMD, and 3-source ops (v_add3,
+v_alignbit, v_mad_u64_u32) take two slots, so carry-chain arithmetic saturates near 0.5-0.6 and BLAKE3
+near 0.65.  (Round 1 divided by 4-cycle slots and read the same counters as "1.0, instruction bound".)
 Usage: python3 tools/pmc_valu.py <counter_collection.csv | rocprofv3 output dir> [-o out.md]
 """
 import argparse
@@ -56,19 +60,19 @@ def main():
         for k in ("SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_INSTS_LDS", "SQ_ACTIVE_INST_VALU",
                   "SQ_BUSY_CYCLES"):
             a[k] += d.get(k, 0.0)
-    lines = ["| kernel | launches | time (ms) | clock (GHz) | VALU instr (G) | valu_issue |",
+    lines = ["| kernel | launches | time (ms) | clock (GHz) | VALU instr (G) | slot_util |",
              "|---|---|---|---|---|---|"]
     tot = collections.Counter()
     for g, a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
         cyc = a["GRBM_GUI_ACTIVE"] / N_XCD
-        issue = a["SQ_INSTS_VALU"] * 4 / (SIMDS * cyc) if cyc else 0.0
+        issue = a["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc) if cyc else 0.0
         clock = cyc / a["ns"] if a["ns"] else 0.0
         lines.append(f"| {g} | {a['n']} | {a['ns'] / 1e6:.3f} | {clock:.2f} | {a['SQ_INSTS_VALU'] / 1e9:.2f} | "
                      f"{issue:.2f} |")
         tot.update(a)
     cyc = tot["GRBM_GUI_ACTIVE"] / N_XCD
     lines.append(f"| **all above** | {tot['n']} | {tot['ns'] / 1e6:.3f} | {cyc / tot['ns']:.2f} | "
-                 f"{tot['SQ_INSTS_VALU'] / 1e9:.2f} | {tot['SQ_INSTS_VALU'] * 4 / (SIMDS * cyc):.2f} |")
+                 f"{tot['SQ_INSTS_VALU'] / 1e9:.2f} | {tot['SQ_INSTS_VALU'] * 2 / (SIMDS * cyc):.2f} |")
     out = "\n".join(lines) + "\n"
     if args.o:
         open(args.o, "w").write(out)
