@@ -224,6 +224,109 @@ __device__ __forceinline__ void mul_wide(fe A, fe Bv, uint32_t r[8]) {
 }
 #undef ZK_SHIFT
 
+// ---- multiplication by a wave-uniform constant through its "W set" (DESIGN.md "What bounds the f128
+// kernels").  For a constant w, W_i = w 2^(32i) mod p (i < 4), so a w = sum_i a_i W_i (mod p): a 162-bit sum
+// of four 32 x 128-bit products, product-scanned in four columns, then ONE fold of its top 35 bits
+// instead of the two folds of a 256-bit product.  29 % fewer issue slots than fe_mul (80 vs 113, tools/
+// ubench/fmul_lab.hip).  The W words are read from SGPRs (scalar loads of a table the wave indexes
+// uniformly), so the constant costs no VGPRs and no vector loads.
+struct fe_ws {
+    uint32_t w[16];  // w[4j + i] = 32-bit word j of W_i
+};
+__host__ inline fe_ws make_fe_ws(fe w);  // defined below the host fe_mul
+
+// one column of the W-set product: like col3 / col4, the multiplier words in SGPRs
+__device__ __forceinline__ void col3s(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2) {
+    uint64_t k0, k1, k2, kd;
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %8, %9, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %10, %11, %0\n\t"
+        "v_addc_co_u32 %1, %5, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %4"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(kd)
+        : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2));
+}
+__device__ __forceinline__ void col4s(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+    uint64_t k0, k1, k2, k3, kd;
+    asm("v_mad_u64_u32 %0, %2, %7, %8, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %11, %12, %0\n\t"
+        "v_mad_u64_u32 %0, %5, %13, %14, %0\n\t"
+        "v_addc_co_u32 %1, %6, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %4\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %5"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(kd)
+        : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2), "v"(x3), "s"(y3));
+}
+
+// (r0..r3) + (s4 + s5 2^32) 2^128 mod p for s5 < 2^3.  With T = s4 + s5 2^32 and S = L + T C:
+// U = L - (T + 1) + ((T + 1) K) << 32 = S + C; the result is U - 2^128 when bit 128 of U is set (S >= p),
+// else U - C (= S).  Carry chains with explicit SGPR pairs: 2 wait states between a VALU writing an SGPR
+// and a VALU reading it (the s_nops); VALU -> SALU and SALU -> VALU need none here.
+__device__ __forceinline__ fe ws_fold(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t s4, uint32_t s5) {
+    const uint32_t K = 0x2d00u;
+    const uint64_t m = (uint64_t)s4 * K + K;
+    const uint32_t m0 = lo32(m), m1 = hi32(m) + s5 * K;
+    uint32_t e0, e1, e2, e3, e4, u1, u2, u3, u4, nm, cw, o0, o1, o2, o3;
+    uint64_t sB, sC, sD;
+    const uint64_t ones = ~0ull;
+    asm("v_subb_co_u32 %0, %15, %19, %23, %18\n\t"  // e0 = r0 - s4 - 1
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %1, %15, %20, %24, %15\n\t"  // e1 = r1 - s5 - B
+        "v_add_co_u32 %5, %16, %1, %25\n\t"         // u1 = e1 + m0
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %2, %15, %21, 0, %15\n\t"    // e2
+        "v_addc_co_u32 %6, %16, %2, %26, %16\n\t"   // u2 = e2 + m1 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %3, %15, %22, 0, %15\n\t"    // e3
+        "v_addc_co_u32 %7, %16, %3, 0, %16\n\t"     // u3
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %4, %15, 0, 0, %15\n\t"      // e4 = -B
+        "v_addc_co_u32 %8, %16, %4, 0, %16\n\t"     // u4 = bit 128 of U
+        "v_add_u32 %9, -1, %8\n\t"                  // nm: all ones when U < 2^128
+        "v_and_b32 %10, 0x2cff, %9\n\t"
+        "v_sub_co_u32 %11, %17, %0, %9\n\t"         // U - (nm ? C : 0)
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %12, %17, %5, %10, %17\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %13, %17, %6, 0, %17\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %14, %17, %7, 0, %17"
+        : "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&v"(e4), "=&v"(u1), "=&v"(u2), "=&v"(u3), "=&v"(u4), "=&v"(nm),
+          "=&v"(cw), "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3), "=&s"(sB), "=&s"(sC), "=&s"(sD)
+        : "s"(ones), "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(s4), "v"(s5), "v"(m0), "v"(m1));
+    return fe{join32(o0, o1), join32(o2, o3)};
+}
+
+// a * w for a wave-uniform constant w given by its W set (every word must be wave-uniform: load it with
+// load_fe_ws at a uniform index)
+__device__ __forceinline__ fe fe_mul_uniform(fe A, const fe_ws &W) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint32_t r0, r1, r2, r3, h = 0;
+    uint64_t a, kd;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a), "=s"(kd) : "v"(x0), "s"(W.w[0]));
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col3s(a, h, x1, W.w[1], x2, W.w[2], x3, W.w[3]);                 ZK_WSHIFT(r0);
+    col4s(a, h, x0, W.w[4], x1, W.w[5], x2, W.w[6], x3, W.w[7]);     ZK_WSHIFT(r1);
+    col4s(a, h, x0, W.w[8], x1, W.w[9], x2, W.w[10], x3, W.w[11]);   ZK_WSHIFT(r2);
+    col4s(a, h, x0, W.w[12], x1, W.w[13], x2, W.w[14], x3, W.w[15]); ZK_WSHIFT(r3);
+#undef ZK_WSHIFT
+    return ws_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
+}
+
+// the W set tab[idx] for a wave-uniform idx, through scalar loads
+__device__ __forceinline__ fe_ws load_fe_ws(const fe_ws *__restrict__ tab, int idx) {
+    fe_ws r;
+    idx = __builtin_amdgcn_readfirstlane(idx);
+#pragma unroll
+    for (int k = 0; k < 16; k++) r.w[k] = __builtin_amdgcn_readfirstlane(tab[idx].w[k]);
+    return r;
+}
+
 __device__ __forceinline__ fe fe_mul_asm(fe A, fe Bv) {
     uint32_t r[8];
     mul_wide(A, Bv, r);
@@ -290,6 +393,19 @@ __host__ static inline fe fe_mul(fe a, fe b) {
 }
 
 ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }
+
+__host__ inline fe_ws make_fe_ws(fe w) {
+    fe_ws W;
+    const fe two32 = fe{1ull << 32, 0};
+    for (int i = 0; i < 4; i++) {
+        W.w[0 + i] = lo32(w.lo);
+        W.w[4 + i] = hi32(w.lo);
+        W.w[8 + i] = lo32(w.hi);
+        W.w[12 + i] = hi32(w.hi);
+        w = fe_mul(w, two32);
+    }
+    return W;
+}
 
 // ---- multiply-accumulate by small (< 2^32) constants, reduced once: for the Rescue MDS matrix,
 // whose entries are small signed integers (crypto/src/rescue.rs:197-214).

@@ -64,14 +64,22 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 //   lanes vary in the load and pass-2 store phases.  sw is linear over XOR, so an element at pos + d
 //   (d's bits zero in pos) is idx ^ sw(d).
 //   padded (small M): line*(M + 1) + pos.
+//   The 1024-point / 4-line tile of the 2^20 NTTs (UNI below) uses sw(x) = x ^ bits 4-7 ^ bits 8-9 instead:
+//   its rounds with h <= 16 give every wave one butterfly index j (lanes spread over lines and groups,
+//   stride 4h), which the bits-4-5 fold leaves 4- and 16-way conflicted; this one is conflict-free for
+//   those, the other rounds, both load orders and the stores (host model: tools/lds_bank_model.py).
 template <int LOGM, int TILE>
 struct Lds {
     static constexpr int M = 1 << LOGM, LPB = TILE >> LOGM;
     static constexpr bool SWZ = ZK_NTT_SWZ && LOGM >= 6;
+    static constexpr bool UNI = LOGM == 10 && TILE == 4096 && NTT_THREADS == 1024;
     static constexpr int LLPB = LPB >= 16 ? 4 : LPB >= 8 ? 3 : LPB >= 4 ? 2 : LPB >= 2 ? 1 : 0;
     static constexpr int R = 4 - LLPB;
     static constexpr int LMASK = (1 << LLPB) - 1;
-    __device__ __forceinline__ static int sw(int x) { return SWZ ? x ^ (((x >> 4) & 3) * 5) : x; }
+    __device__ __forceinline__ static int sw(int x) {
+        if constexpr (UNI) return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3);
+        return SWZ ? x ^ (((x >> 4) & 3) * 5) : x;
+    }
     __device__ __forceinline__ static int idx(int line, int pos) {
         if constexpr (SWZ) return line * M + (sw(pos) ^ ((line & LMASK) << R));
         else return line * (M + (LOGM >= 4 ? 1 : 0)) + pos;
@@ -92,12 +100,35 @@ struct Lds {
 // One radix-4 round (stages lg, lg+1), compile-time lg so every shift and mask is an immediate.
 // CT (coset-table mode): tw is a per-line-set stage table, tw[h + j] = the stage twiddle for half-size h
 // and butterfly index j (a DFT evaluated on a coset c<w_M>: c^(M/2h) w_2h^j), instead of w_4096 powers.
+// UNI tiles, rounds with h <= 16: wave w takes butterfly index j = w / (16/h) for 1024/h (line, group)
+// pairs, so its three twiddles are wave-uniform and multiply through their W sets (fe_mul_uniform, scalar
+// loads from `ws`, the W-set table indexed exactly like `tw4096`).  Same butterflies, same values.
 template <int LOGM, int TILE, int LG, bool CT>
-__device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
+__device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *ws) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
     constexpr int h = 1 << (LG - 1);
     using L = Lds<LOGM, TILE>;
+    if constexpr (L::UNI && h <= 16) {
+        constexpr int LH = LG - 1;
+        const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), l = threadIdx.x & 63;
+        const int j = w >> (4 - LH);
+        const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;
+        const int line = pidx >> (8 - LH), grp = pidx & ((256 >> LH) - 1);
+        const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+        const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
+        const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+        const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
+        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
+        const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
+        s[p] = fe_add(a0, u2);
+        s[p2h] = fe_sub(a0, u2);
+        s[ph] = fe_add(a1, u3);
+        s[p3h] = fe_sub(a1, u3);
+        __syncthreads();
+        return;
+    }
 #pragma unroll
     for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
         const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
@@ -120,10 +151,10 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096) {
 
 // rounds LG, LG+2, ... while LG + 1 <= LOGM, then the trailing radix-2 stage of an odd LOGM
 template <int LOGM, int TILE, int LG, bool CT>
-__device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
+__device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *ws) {
     if constexpr (LG + 1 <= LOGM) {
-        r4_round<LOGM, TILE, LG, CT>(s, tw4096);
-        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096);
+        r4_round<LOGM, TILE, LG, CT>(s, tw4096, ws);
+        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096, ws);
     } else if constexpr (LG == LOGM) {
         constexpr int M = 1 << LOGM;
         constexpr int half = 1 << (LG - 1);
@@ -153,31 +184,37 @@ __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096) {
 // global one (global_load, counted by vmcnt only; as a called function both were flat accesses
 // and every LDS wait also waited for the twiddle loads).
 // CT: coset-table mode (every round generic, the first one included: 4 multiplies per 4 points).
+// ws: the W sets of tw4096 (same indexing), used by the rounds with wave-uniform twiddles (UNI tiles).
 template <int LOGM, int TILE, bool CT = false>
-__device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096) {
+__device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
     if constexpr (CT) {
-        r4_rounds<LOGM, TILE, 1, true>(s, tw4096);
+        r4_rounds<LOGM, TILE, 1, true>(s, tw4096, ws);
     } else if constexpr (LOGM >= 2) {
-        const fe w4 = tw4096[1024];
         using L = Lds<LOGM, TILE>;
+        fe w4;
+        fe_ws W4;
+        if constexpr (L::UNI) W4 = load_fe_ws(ws, 1024);
+        else w4 = tw4096[1024];
 #pragma unroll
         for (int q = threadIdx.x; q < Q; q += NTT_THREADS) {
             const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
             const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
             const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
             const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
-            const fe a3 = fe_mul(fe_sub(x2, x3), w4);
+            fe a3;
+            if constexpr (L::UNI) a3 = fe_mul_uniform(fe_sub(x2, x3), W4);
+            else a3 = fe_mul(fe_sub(x2, x3), w4);
             s[p] = fe_add(a0, a2);
             s[p2] = fe_sub(a0, a2);
             s[p1] = fe_add(a1, a3);
             s[p3] = fe_sub(a1, a3);
         }
         __syncthreads();
-        r4_rounds<LOGM, TILE, 3, false>(s, tw4096);
+        r4_rounds<LOGM, TILE, 3, false>(s, tw4096, ws);
     } else {
-        r4_rounds<LOGM, TILE, 1, false>(s, tw4096);
+        r4_rounds<LOGM, TILE, 1, false>(s, tw4096, ws);
     }
 }
 
@@ -193,6 +230,7 @@ struct NttArgs {
     fe *out;
     size_t in_stride, out_stride;
     const fe *tw4096;             // DFT-stage table (forward or inverse)
+    const fe_ws *tw_ws;           // ... its W sets (the wave-uniform rounds of UNI tiles)
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
     const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
     const fe *pre_full;           // ... or the same from a full table (preferred when present)
@@ -206,6 +244,7 @@ struct NttArgs {
     int ncos, cos_r0, cos_rstride;
     size_t out_jstride;
     const fe *cos_stage;  // coset LDE (four-step): per-coset stage tables, 4096 apart (CosetTables::stage)
+    const fe_ws *cos_stage_ws;  // ... their W sets
     const fe *cos_pass;   // ... and per-coset pass-1 twiddles (s_r w_n^j2)^k1, n apart (CosetTables::pass)
     __device__ __forceinline__ int coset_of(size_t b) const { return cos_r0 + (int)(b % ncos) * cos_rstride; }
     __device__ __forceinline__ fe *out_of(size_t b) const { return out + (b / ncos) * out_stride + (b % ncos) * out_jstride; }
@@ -230,7 +269,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    lds_dft<LOGM, TILE>(s, a.tw4096);
+    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j = e & (M - 1);
         int b = b0 + line;
@@ -275,8 +314,8 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    if constexpr (CT) lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096);
-    else lds_dft<LOGM, TILE>(s, a.tw4096);
+    if constexpr (CT) lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096, a.cos_stage_ws + (size_t)r * 4096);
+    else lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
     fe *out = a.out + b * a.out_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j2 = e & (M - 1);
@@ -312,7 +351,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    lds_dft<LOGM, TILE>(s, a.tw4096);
+    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
     fe *out = a.out_of(b);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, j1 = e / LPB;
@@ -407,6 +446,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.in_stride = in_stride;
     a.out_stride = out_stride;
     a.tw4096 = inverse ? T.dft_inv : T.dft_fwd;
+    a.tw_ws = inverse ? T.dft_inv_ws : T.dft_fwd_ws;
     a.big_lo = inverse ? T.inv_lo : T.fwd_lo;
     a.big_hi = inverse ? T.inv_hi : T.fwd_hi;
     a.pre_lo = pre ? pre->lo : nullptr;
@@ -430,6 +470,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.cos_rstride = 0;
     a.out_jstride = 0;
     a.cos_stage = a.cos_pass = nullptr;
+    a.cos_stage_ws = nullptr;
     ntt_run(st, a, batch, tmp);
 }
 
@@ -453,6 +494,7 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     a2.in_stride = (size_t)1 << L;
     a2.pre_lo = a2.pre_hi = a2.pre_full = nullptr;
     a2.cos_stage = a2.cos_pass = nullptr;
+    a2.cos_stage_ws = nullptr;
     ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
 }
 
@@ -466,6 +508,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
     a.out_stride = out_cstride;
     a.out_jstride = out_jstride;
     a.tw4096 = T.dft_fwd;
+    a.tw_ws = T.dft_fwd_ws;
     a.big_lo = T.fwd_lo;
     a.big_hi = T.fwd_hi;
     a.pass_tw = T.fwd_pass;
@@ -479,6 +522,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
         a.pre_stride = n;
     } else {
         a.cos_stage = CT.stage;
+        a.cos_stage_ws = CT.stage_ws;
         a.cos_pass = CT.pass;
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so

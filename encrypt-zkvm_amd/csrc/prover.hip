@@ -62,10 +62,16 @@ struct zk_trace_lde {
 };
 
 // ---------------------------------------------------------------- table construction
-static hipError_t upload(zk_prover *p, fe **dst, const std::vector<fe> &v) {
+template <typename T>
+static hipError_t upload(zk_prover *p, T **dst, const std::vector<T> &v) {
     hipError_t e = p->arena.alloc(dst, v.size());
     if (e != hipSuccess) return e;
-    return hipMemcpy(*dst, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice);
+    return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+static std::vector<fe_ws> ws_of(const std::vector<fe> &v) {
+    std::vector<fe_ws> w(v.size());
+    for (size_t i = 0; i < v.size(); i++) w[i] = make_fe_ws(v[i]);
+    return w;
 }
 
 static hipError_t make_pow_table(zk_prover *p, fe s, size_t n, PowTable *out) {
@@ -86,6 +92,7 @@ static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
     // initialised exactly once even when provers on several threads reach it together)
     struct Dft4096 {
         std::vector<fe> f, i;
+        std::vector<fe_ws> fw, iw;
         Dft4096() : f(2048), i(2048) {
             const fe w = h_root_of_unity(12), wi = h_inv(w);
             f[0] = i[0] = fe_one();
@@ -93,11 +100,15 @@ static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
                 f[t] = fe_mul(f[t - 1], w);
                 i[t] = fe_mul(i[t - 1], wi);
             }
+            fw = ws_of(f);
+            iw = ws_of(i);
         }
     };
     static const Dft4096 d4096;
     hipError_t e = upload(p, &T->dft_fwd, d4096.f);
     if (e == hipSuccess) e = upload(p, &T->dft_inv, d4096.i);
+    if (e == hipSuccess) e = upload(p, &T->dft_fwd_ws, d4096.fw);
+    if (e == hipSuccess) e = upload(p, &T->dft_inv_ws, d4096.iw);
     size_t n = (size_t)1 << log_n;
     fe w = h_root_of_unity(log_n);
     PowTable f, i;
@@ -186,8 +197,10 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
         pl->coset.push_back(t);
         s = fe_mul(s, wN);
     }
-    if (pl->log_n > 12)
+    if (pl->log_n > 12) {
         ZK_CHECK_HIP(hipMemcpy(pl->ct.stage, stage.data(), stage.size() * sizeof(fe), hipMemcpyHostToDevice));
+        ZK_CHECK_HIP(upload(p, &pl->ct.stage_ws, ws_of(stage)));
+    }
     s = fe_make(3);
     for (int r = 0; r < 8; r++) {
         xrce[r] = s;

@@ -71,6 +71,7 @@ KernelProfiler &profiler();
 struct NttTables {
     int log_n = 0;
     fe *dft_fwd = nullptr, *dft_inv = nullptr;
+    fe_ws *dft_fwd_ws = nullptr, *dft_inv_ws = nullptr;  // their W sets (f128.hpp fe_mul_uniform)
     fe *fwd_lo = nullptr, *fwd_hi = nullptr, *inv_lo = nullptr, *inv_hi = nullptr;
     // four-step inter-pass twiddles w^(j2*k1) laid out as pass 1 consumes them, [k1 * n2 + j2]
     // (n elements each; only for log_n > 12, else null)
@@ -116,6 +117,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
 //                            the pass-1 line DFT over the coset c_r <w_n2>), pass[r*n + k1*n2 + j2] = (s_r w_n^j2)^k1
 struct CosetTables {
     fe *full = nullptr, *stage = nullptr, *pass = nullptr;
+    fe_ws *stage_ws = nullptr;  // W sets of `stage` (four-step plans)
 };
 // Forward coset LDE: for columns c < ncols (at in + c*in_stride) and coset slots j < ncos (coset r0 + j*rstride),
 // the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*min(ncos, 8)*n

@@ -1,8 +1,10 @@
 // candidate device multiplies for tools/ubench/fmul_lab.hip (variant 0 = the library's fe_mul)
 #pragma once
-#define FMUL_NVARIANTS 3
+#define FMUL_NVARIANTS 5
 static const char *fmul_variant_name(int v) {
-    static const char *n[] = {"library fe_mul", "v1: U = T + C final step", "v2: independent fold products, mask final step"};
+    static const char *n[] = {"library fe_mul", "v1: U = T + C final step", "v2: independent fold products, mask final step",
+                              "v3: precomputed W_i = b 2^(32i) mod p (16 words), one 35-bit fold",
+                              "v4: as v3, two products sharing one W set"};
     return n[v];
 }
 
@@ -90,9 +92,85 @@ __device__ __forceinline__ fe reduce_v2(uint32_t r0, uint32_t r1, uint32_t r2, u
     return fe{join32(o0, o1), join32(o2, o3)};
 }
 
+
+// ---- multiply by a precomputed constant: x * w = sum_i x_i (w 2^(32i) mod p) (mod p).  Wc[4j + i] is
+// word j of W_i = w 2^(32i) mod p.  The four columns of the 162-bit sum are product-scanned (4 MADs each),
+// the top 35 bits T = s4 + s5 2^32 fold once: U = L - (T + 1) + ((T + 1) K) << 32 = S + C, and the result
+// is U - 2^128 when bit 128 of U is set, else U - C.
+struct WSet {
+    uint32_t w[16];
+};
+__host__ inline WSet make_wset(fe b) {
+    WSet W;
+    fe t = b;
+    const fe two32 = fe{1ull << 32, 0};
+    for (int i = 0; i < 4; i++) {
+        W.w[0 * 4 + i] = lo32(t.lo);
+        W.w[1 * 4 + i] = hi32(t.lo);
+        W.w[2 * 4 + i] = lo32(t.hi);
+        W.w[3 * 4 + i] = hi32(t.hi);
+        t = fe_mul(t, two32);
+    }
+    return W;
+}
+#define ZK_SHIFT2(a, h, out) do { out = (uint32_t)(a); a = ((a) >> 32) | ((uint64_t)(h) << 32); h = 0; } while (0)
+__device__ __forceinline__ void pre_cols(fe A, const uint32_t *W, uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3,
+                                         uint32_t &s4, uint32_t &s5) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint64_t a = (uint64_t)x0 * W[0];
+    uint32_t h = 0;
+    col3(a, h, x1, W[1], x2, W[2], x3, W[3]);               ZK_SHIFT2(a, h, r0);
+    col4(a, h, x0, W[4], x1, W[5], x2, W[6], x3, W[7]);     ZK_SHIFT2(a, h, r1);
+    col4(a, h, x0, W[8], x1, W[9], x2, W[10], x3, W[11]);   ZK_SHIFT2(a, h, r2);
+    col4(a, h, x0, W[12], x1, W[13], x2, W[14], x3, W[15]); ZK_SHIFT2(a, h, r3);
+    s4 = (uint32_t)a;
+    s5 = (uint32_t)(a >> 32);
+}
+// fold of (r0..r3) + (s4 + s5 2^32) 2^128, s5 < 8; hazard rule: 2 wait states between a VALU SGPR write
+// and a VALU read of it
+__device__ __forceinline__ fe pre_fold(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t s4, uint32_t s5) {
+    const uint32_t K = 0x2d00u;
+    const uint64_t m = (uint64_t)s4 * K + K;
+    const uint32_t m0 = lo32(m), m1 = hi32(m) + s5 * K;
+    uint32_t e0, e1, e2, e3, e4, u1, u2, u3, u4, nm, cw, o0, o1, o2, o3;
+    uint64_t sB, sC, sD;
+    const uint64_t ones = ~0ull;
+    asm("v_subb_co_u32 %0, %15, %19, %23, %18\n\t"   // e0 = r0 - s4 - 1
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %1, %15, %20, %24, %15\n\t"   // e1 = r1 - s5 - B
+        "v_add_co_u32 %5, %16, %1, %25\n\t"          // u1 = e1 + m0
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %2, %15, %21, 0, %15\n\t"     // e2
+        "v_addc_co_u32 %6, %16, %2, %26, %16\n\t"    // u2 = e2 + m1 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %3, %15, %22, 0, %15\n\t"     // e3
+        "v_addc_co_u32 %7, %16, %3, 0, %16\n\t"      // u3
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %4, %15, 0, 0, %15\n\t"       // e4 = -B
+        "v_addc_co_u32 %8, %16, %4, 0, %16\n\t"      // u4 = bit 128 of U
+        "v_add_u32 %9, -1, %8\n\t"                   // nm: all ones when U < 2^128
+        "v_and_b32 %10, 0x2cff, %9\n\t"
+        "v_sub_co_u32 %11, %17, %0, %9\n\t"          // U - (nm ? C : 0)
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %12, %17, %5, %10, %17\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %13, %17, %6, 0, %17\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %14, %17, %7, 0, %17"
+        : "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&v"(e4), "=&v"(u1), "=&v"(u2), "=&v"(u3), "=&v"(u4), "=&v"(nm),
+          "=&v"(cw), "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3), "=&s"(sB), "=&s"(sC), "=&s"(sD)
+        : "s"(ones), "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(s4), "v"(s5), "v"(m0), "v"(m1));
+    return fe{join32(o0, o1), join32(o2, o3)};
+}
+__device__ __forceinline__ fe fe_mul_pre(fe a, const uint32_t *W) {
+    uint32_t r0, r1, r2, r3, s4, s5;
+    pre_cols(a, W, r0, r1, r2, r3, s4, s5);
+    return pre_fold(r0, r1, r2, r3, s4, s5);
+}
 template <int V>
-__device__ __forceinline__ fe fmul_variant(fe a, fe b) {
+__device__ __forceinline__ fe fmul_variant(fe a, fe b, const uint32_t *W = nullptr) {
     if constexpr (V == 0) return fe_mul(a, b);
+    if constexpr (V == 3 || V == 4) return fe_mul_pre(a, W);
     uint32_t r[8];
     mul_wide(a, b, r);
     if constexpr (V == 1) return reduce_v1(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);

@@ -6,6 +6,7 @@
 #include "../../encrypt-zkvm_amd/csrc/host_field.hpp"
 #include <stdio.h>
 #include <vector>
+#include "fmul_variants.hpp"
 
 using namespace zk;
 
@@ -190,6 +191,336 @@ __global__ void __launch_bounds__(1024, 8) lab_pass2(NttArgs a, fe wfake) {
         out[n2 * (size_t)j1 + j2_0 + line] = s[Lds<LOGM, TILE>::idx(line, j1)];
     }
 }
+
+// ---------------------------------------------------------------- tile-size sweep of the barrier-per-round pass 2
+// TILE elements per block (TILE / 1024 lines of 1024), TILE / 4 threads (one radix-4 butterfly each per round)
+template <int TILE, int LG>
+__device__ __forceinline__ void sw_round(fe *s, const fe *tw4096) {
+    constexpr int LOGM = 10, M = 1 << LOGM, h = 1 << (LG - 1);
+    using L = Lds<LOGM, TILE>;
+    const int q = threadIdx.x;
+    const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+    const int j = local & (h - 1), grp = local >> (LG - 1);
+    const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+    const fe w1 = tw4096[j << (12 - LG)];
+    const fe w2 = tw4096[j << (11 - LG)];
+    const fe w3 = tw4096[(j + h) << (11 - LG)];
+    const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+    const fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
+    const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+    const fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
+    s[p] = fe_add(a0, u2);
+    s[p2h] = fe_sub(a0, u2);
+    s[ph] = fe_add(a1, u3);
+    s[p3h] = fe_sub(a1, u3);
+    __syncthreads();
+}
+template <int TILE>
+__global__ void __launch_bounds__(TILE / 4, 8) sw_pass2(NttArgs a) {
+    extern __shared__ fe s[];
+    constexpr int LOGM = 10, M = 1 << LOGM, LPB = TILE / M, T = TILE / 4;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n2 = n >> LOGM;
+    const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
+    const fe *in = a.in + (size_t)blockIdx.y * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += T) {
+        int line = e % LPB, k1 = Lds<LOGM, TILE>::load_k(e / LPB);
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = in[(size_t)k1 * n2 + j2_0 + line];
+    }
+    __syncthreads();
+    {
+        const fe w4 = a.tw4096[1024];
+        using L = Lds<LOGM, TILE>;
+        const int q = threadIdx.x;
+        const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+        const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
+        const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
+        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+        const fe a3 = fe_mul(fe_sub(x2, x3), w4);
+        s[p] = fe_add(a0, a2);
+        s[p2] = fe_sub(a0, a2);
+        s[p1] = fe_add(a1, a3);
+        s[p3] = fe_sub(a1, a3);
+        __syncthreads();
+    }
+    sw_round<TILE, 3>(s, a.tw4096);
+    sw_round<TILE, 5>(s, a.tw4096);
+    sw_round<TILE, 7>(s, a.tw4096);
+    sw_round<TILE, 9>(s, a.tw4096);
+    fe *out = a.out + (size_t)blockIdx.y * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += T) {
+        int line = e % LPB, j1 = e / LPB;
+        out[n2 * (size_t)j1 + j2_0 + line] = s[Lds<LOGM, TILE>::idx(line, j1)];
+    }
+}
+
+// ---------------------------------------------------------------- pass 2 with precomputed-constant twiddles
+// Stage twiddles as W sets (tools/ubench/fmul_variants.hpp fe_mul_pre): 64 B per twiddle, 29 % fewer issue
+// slots per multiply.  WAVES: launch-bounds waves per SIMD (8: the 64-VGPR budget of the library kernel).
+template <int LG, int WAVES, bool FIXEDW = false>
+__device__ __forceinline__ void pre_round(fe *s, const WSet *tw, const uint32_t *WF = nullptr) {
+    constexpr int LOGM = 10, TILE = 4096, M = 1 << LOGM, h = 1 << (LG - 1);
+    using L = Lds<LOGM, TILE>;
+    const int q = threadIdx.x;
+    const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+    const int j = local & (h - 1), grp = local >> (LG - 1);
+    const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+    const uint32_t *W1 = FIXEDW ? WF : tw[j << (12 - LG)].w;
+    const uint32_t *W2 = FIXEDW ? WF : tw[j << (11 - LG)].w;
+    const uint32_t *W3 = FIXEDW ? WF : tw[(j + h) << (11 - LG)].w;
+    const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+    const fe t1 = fe_mul_pre(x1, W1), t3 = fe_mul_pre(x3, W1);
+    const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+    const fe u2 = fe_mul_pre(a2, W2), u3 = fe_mul_pre(a3, W3);
+    s[p] = fe_add(a0, u2);
+    s[p2h] = fe_sub(a0, u2);
+    s[ph] = fe_add(a1, u3);
+    s[p3h] = fe_sub(a1, u3);
+    __syncthreads();
+}
+template <int WAVES, bool FIXEDW = false>
+__global__ void __launch_bounds__(1024, WAVES) pre_pass2(NttArgs a, const WSet *tw) {
+    uint32_t WF[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) WF[k] = __builtin_amdgcn_readfirstlane(tw[77].w[k]);
+    extern __shared__ fe s[];
+    constexpr int LOGM = 10, TILE = 4096, M = 1 << LOGM, LPB = TILE / M;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n2 = n >> LOGM;
+    const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
+    const fe *in = a.in + (size_t)blockIdx.y * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, k1 = Lds<LOGM, TILE>::load_k(e / LPB);
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = in[(size_t)k1 * n2 + j2_0 + line];
+    }
+    __syncthreads();
+    {
+        using L = Lds<LOGM, TILE>;
+        const int q = threadIdx.x;
+        const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+        const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
+        const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
+        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+        const fe a3 = fe_mul_pre(fe_sub(x2, x3), tw[1024].w);
+        s[p] = fe_add(a0, a2);
+        s[p2] = fe_sub(a0, a2);
+        s[p1] = fe_add(a1, a3);
+        s[p3] = fe_sub(a1, a3);
+        __syncthreads();
+    }
+    pre_round<3, WAVES, FIXEDW>(s, tw, WF);
+    pre_round<5, WAVES, FIXEDW>(s, tw, WF);
+    pre_round<7, WAVES, FIXEDW>(s, tw, WF);
+    pre_round<9, WAVES, FIXEDW>(s, tw, WF);
+    fe *out = a.out + (size_t)blockIdx.y * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, j1 = e / LPB;
+        out[n2 * (size_t)j1 + j2_0 + line] = s[Lds<LOGM, TILE>::idx(line, j1)];
+    }
+}
+
+// ---------------------------------------------------------------- uniform-twiddle rounds
+// Rounds with half-size h <= 16 remap threads to butterflies so that every wave shares one twiddle index j:
+// the twiddle's W set is wave-uniform (scalar loads into SGPRs) and the multiply is the precomputed-
+// constant form.  Rounds h = 64, 256 keep the library mapping and plain multiplies.
+__device__ __forceinline__ void col3s(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2) {
+    uint64_t k0, k1, k2, kd;
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %8, %9, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %10, %11, %0\n\t"
+        "v_addc_co_u32 %1, %5, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %4"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(kd)
+        : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2));
+}
+__device__ __forceinline__ void col4s(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+    uint64_t k0, k1, k2, k3, kd;
+    asm("v_mad_u64_u32 %0, %2, %7, %8, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %11, %12, %0\n\t"
+        "v_mad_u64_u32 %0, %5, %13, %14, %0\n\t"
+        "v_addc_co_u32 %1, %6, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %4\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %5"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(kd)
+        : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2), "v"(x3), "s"(y3));
+}
+struct WS {
+    uint32_t w[16];
+};
+// W set of a wave-uniform twiddle, loaded with scalar loads
+__device__ __forceinline__ WS load_ws(const WSet *__restrict__ tw, int idx) {
+    WS r;
+#pragma unroll
+    for (int k = 0; k < 16; k++) r.w[k] = __builtin_amdgcn_readfirstlane(tw[idx].w[k]);
+    return r;
+}
+__device__ __forceinline__ fe fe_mul_ws(fe A, const WS &W) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint32_t r0, r1, r2, r3;
+    uint64_t a;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a), "=s"(*(uint64_t[1]){}) : "v"(x0), "s"(W.w[0]));
+    uint32_t h = 0;
+    col3s(a, h, x1, W.w[1], x2, W.w[2], x3, W.w[3]);               ZK_SHIFT2(a, h, r0);
+    col4s(a, h, x0, W.w[4], x1, W.w[5], x2, W.w[6], x3, W.w[7]);   ZK_SHIFT2(a, h, r1);
+    col4s(a, h, x0, W.w[8], x1, W.w[9], x2, W.w[10], x3, W.w[11]); ZK_SHIFT2(a, h, r2);
+    col4s(a, h, x0, W.w[12], x1, W.w[13], x2, W.w[14], x3, W.w[15]); ZK_SHIFT2(a, h, r3);
+    return pre_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
+}
+template <int LG>
+__device__ __forceinline__ void uni_round(fe *s, const WSet *__restrict__ tw) {
+    constexpr int LOGM = 10, TILE = 4096, M = 1 << LOGM, h = 1 << (LG - 1), LH = LG - 1;
+    using L = Lds<LOGM, TILE>;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+    const int j = w >> (4 - LH);
+    const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;
+    const int line = pidx >> (8 - LH), grp = pidx & ((256 >> LH) - 1);
+    const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+    const WS W1 = load_ws(tw, j << (12 - LG));
+    const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+    const fe t1 = fe_mul_ws(x1, W1), t3 = fe_mul_ws(x3, W1);
+    const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+    const WS W2 = load_ws(tw, j << (11 - LG));
+    const fe u2 = fe_mul_ws(a2, W2);
+    const WS W3 = load_ws(tw, (j + h) << (11 - LG));
+    const fe u3 = fe_mul_ws(a3, W3);
+    s[p] = fe_add(a0, u2);
+    s[p2h] = fe_sub(a0, u2);
+    s[ph] = fe_add(a1, u3);
+    s[p3h] = fe_sub(a1, u3);
+    __syncthreads();
+}
+__global__ void __launch_bounds__(1024, 8) uni_pass2(NttArgs a, const WSet *__restrict__ tw) {
+    extern __shared__ fe s[];
+    constexpr int LOGM = 10, TILE = 4096, M = 1 << LOGM, LPB = TILE / M;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n2 = n >> LOGM;
+    const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
+    const fe *in = a.in + (size_t)blockIdx.y * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, k1 = Lds<LOGM, TILE>::load_k(e / LPB);
+        s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = in[(size_t)k1 * n2 + j2_0 + line];
+    }
+    __syncthreads();
+    {
+        using L = Lds<LOGM, TILE>;
+        const int q = threadIdx.x;
+        const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+        const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
+        const WS W4 = load_ws(tw, 1024);
+        const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
+        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+        const fe a3 = fe_mul_ws(fe_sub(x2, x3), W4);
+        s[p] = fe_add(a0, a2);
+        s[p2] = fe_sub(a0, a2);
+        s[p1] = fe_add(a1, a3);
+        s[p3] = fe_sub(a1, a3);
+        __syncthreads();
+    }
+    uni_round<3>(s, tw);
+    uni_round<5>(s, tw);
+    lab_round<7, false, false>(s, a.tw4096, fe_zero());
+    lab_round<9, false, false>(s, a.tw4096, fe_zero());
+    fe *out = a.out + (size_t)blockIdx.y * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, j1 = e / LPB;
+        out[n2 * (size_t)j1 + j2_0 + line] = s[Lds<LOGM, TILE>::idx(line, j1)];
+    }
+}
+
+// ---------------------------------------------------------------- uniform-twiddle rounds on a re-swizzled tile
+// sw(x) = x ^ bits 4-7 ^ bits 8-9 (folded into bits 0-3): conflict-free for the remapped rounds h = 4, 16
+// as well as the library mapping of h = 1, 64, 256 and the load / store phases (host model).
+struct NL {
+    __device__ __forceinline__ static int sw(int x) { return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3); }
+    __device__ __forceinline__ static int idx(int line, int pos) { return line * 1024 + (sw(pos) ^ ((line & 3) << 2)); }
+    __device__ __forceinline__ static int at(int p, int d) { return p ^ sw(d); }
+};
+template <int LG, bool UNI>
+__device__ __forceinline__ void nl_round(fe *s, const WSet *__restrict__ tw, const fe *tw4096) {
+    constexpr int h = 1 << (LG - 1), LH = LG - 1;
+    int line, grp, j;
+    if constexpr (UNI) {
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+        j = w >> (4 - LH);
+        const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;
+        line = pidx >> (8 - LH);
+        grp = pidx & ((256 >> LH) - 1);
+    } else {
+        const int q = threadIdx.x;
+        line = q >> 8;
+        const int local = q & 255;
+        j = local & (h - 1);
+        grp = local >> LH;
+    }
+    const int p = NL::idx(line, grp * 4 * h + j), ph = NL::at(p, h), p2h = NL::at(p, 2 * h), p3h = NL::at(p, 3 * h);
+    const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+    fe t1, t3, u2, u3, a0, a1, a2, a3;
+    if constexpr (UNI) {
+        const WS W1 = load_ws(tw, j << (12 - LG));
+        t1 = fe_mul_ws(x1, W1);
+        t3 = fe_mul_ws(x3, W1);
+        a0 = fe_add(x0, t1); a1 = fe_sub(x0, t1); a2 = fe_add(x2, t3); a3 = fe_sub(x2, t3);
+        const WS W2 = load_ws(tw, j << (11 - LG));
+        u2 = fe_mul_ws(a2, W2);
+        const WS W3 = load_ws(tw, (j + h) << (11 - LG));
+        u3 = fe_mul_ws(a3, W3);
+    } else {
+        const fe w1 = tw4096[j << (12 - LG)], w2 = tw4096[j << (11 - LG)], w3 = tw4096[(j + h) << (11 - LG)];
+        t1 = fe_mul(x1, w1);
+        t3 = fe_mul(x3, w1);
+        a0 = fe_add(x0, t1); a1 = fe_sub(x0, t1); a2 = fe_add(x2, t3); a3 = fe_sub(x2, t3);
+        u2 = fe_mul(a2, w2);
+        u3 = fe_mul(a3, w3);
+    }
+    s[p] = fe_add(a0, u2);
+    s[p2h] = fe_sub(a0, u2);
+    s[ph] = fe_add(a1, u3);
+    s[p3h] = fe_sub(a1, u3);
+    __syncthreads();
+}
+template <bool UNI>
+__global__ void __launch_bounds__(1024, 8) nl_pass2(NttArgs a, const WSet *__restrict__ tw) {
+    extern __shared__ fe s[];
+    constexpr int LOGM = 10, TILE = 4096, LPB = 4;
+    const size_t n = (size_t)1 << a.log_n;
+    const size_t n2 = n >> LOGM;
+    const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
+    const fe *in = a.in + (size_t)blockIdx.y * a.in_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, v = e / LPB, k1 = ((v & 3) << 8) | (v >> 2);
+        s[NL::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = in[(size_t)k1 * n2 + j2_0 + line];
+    }
+    __syncthreads();
+    {
+        const int q = threadIdx.x;
+        const int line = q >> 8, local = q & 255;
+        const int p = NL::idx(line, local * 4), p1 = NL::at(p, 1), p2 = NL::at(p, 2), p3 = NL::at(p, 3);
+        const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
+        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+        fe a3;
+        if constexpr (UNI) a3 = fe_mul_ws(fe_sub(x2, x3), load_ws(tw, 1024));
+        else a3 = fe_mul(fe_sub(x2, x3), a.tw4096[1024]);
+        s[p] = fe_add(a0, a2);
+        s[p2] = fe_sub(a0, a2);
+        s[p1] = fe_add(a1, a3);
+        s[p3] = fe_sub(a1, a3);
+        __syncthreads();
+    }
+    nl_round<3, UNI>(s, tw, a.tw4096);
+    nl_round<5, UNI>(s, tw, a.tw4096);
+    nl_round<7, false>(s, tw, a.tw4096);
+    nl_round<9, false>(s, tw, a.tw4096);
+    fe *out = a.out + (size_t)blockIdx.y * a.out_stride;
+    for (int e = threadIdx.x; e < TILE; e += 1024) {
+        int line = e % LPB, j1 = e / LPB;
+        out[n2 * (size_t)j1 + j2_0 + line] = s[NL::idx(line, j1)];
+    }
+}
 // ---------------------------------------------------------------- harness
 static fe h_pow(fe b, uint64_t e) {
     fe r = fe_one();
@@ -274,6 +605,55 @@ int main(int argc, char **argv) {
             if (v == 3) hipLaunchKernelGGL((lab_pass2<true, true>), dim3(n / 4096, batch), dim3(1024), sh, 0, b, wf);
         };
         printf("lab pass2 nosync=%d notw=%d: %.3f ms\n", (int)ns, (int)nt, timeit(f));
+    }
+
+    {
+        NttArgs b = a;
+        b.out = dout1;
+        std::vector<fe> ref(tot), got(tot);
+        hipLaunchKernelGGL((ntt_pass2<10, 4096>), dim3(n / 4096, batch), dim3(1024), sh, 0, a);
+        (void)hipMemcpy(ref.data(), dout0, tot * sizeof(fe), hipMemcpyDeviceToHost);
+        auto sweep = [&](auto kern, int tile, size_t shb) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shb);
+            auto f = [&] { hipLaunchKernelGGL(kern, dim3(n / tile, batch), dim3(tile / 4), shb, 0, b); };
+            const float t = timeit(f);
+            (void)hipMemcpy(got.data(), dout1, tot * sizeof(fe), hipMemcpyDeviceToHost);
+            size_t bad = 0;
+            for (size_t i = 0; i < tot; i++) bad += !fe_eq(ref[i], got[i]);
+            printf("tile %4d (%d threads, %d lines): %.3f ms, mismatches %zu\n", tile, tile / 4, tile / 1024, t, bad);
+        };
+        sweep(sw_pass2<4096>, 4096, Lds<10, 4096>::bytes());
+        sweep(sw_pass2<2048>, 2048, Lds<10, 2048>::bytes());
+        sweep(sw_pass2<1024>, 1024, Lds<10, 1024>::bytes());
+        sweep(sw_pass2<8192>, 8192, Lds<10, 8192>::bytes());
+    }
+
+    {
+        std::vector<WSet> hw(4096);
+        for (int i = 0; i < 4096; i++) hw[i] = make_wset(tw[i]);
+        WSet *dws;
+        (void)hipMalloc(&dws, 4096 * sizeof(WSet));
+        (void)hipMemcpy(dws, hw.data(), 4096 * sizeof(WSet), hipMemcpyHostToDevice);
+        NttArgs b = a;
+        b.out = dout1;
+        std::vector<fe> ref(tot), got(tot);
+        hipLaunchKernelGGL((ntt_pass2<10, 4096>), dim3(n / 4096, batch), dim3(1024), sh, 0, a);
+        (void)hipMemcpy(ref.data(), dout0, tot * sizeof(fe), hipMemcpyDeviceToHost);
+        auto run_pre = [&](auto kern, const char *name) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+            auto f = [&] { hipLaunchKernelGGL(kern, dim3(n / 4096, batch), dim3(1024), sh, 0, b, (const WSet *)dws); };
+            const float t = timeit(f);
+            (void)hipMemcpy(got.data(), dout1, tot * sizeof(fe), hipMemcpyDeviceToHost);
+            size_t bad = 0;
+            for (size_t i = 0; i < tot; i++) bad += !fe_eq(ref[i], got[i]);
+            printf("%s: %.3f ms, mismatches %zu\n", name, t, bad);
+        };
+        run_pre(pre_pass2<8>, "pre-twiddle pass2, 8 waves/SIMD");
+        run_pre(pre_pass2<4>, "pre-twiddle pass2, 4 waves/SIMD");
+        run_pre(pre_pass2<8, true>, "pre-twiddle pass2, 8 waves/SIMD, one W set in SGPRs (timing only)");
+        run_pre(uni_pass2, "uniform-twiddle rounds h<=16 (scalar W sets), plain h=64,256");
+        run_pre(nl_pass2<false>, "new swizzle, library mapping and multiplies");
+        run_pre(nl_pass2<true>, "new swizzle, uniform-twiddle rounds h<=16");
     }
     const float t0 = timeit(base), t1 = timeit(wv);
     std::vector<fe> o0(tot), o1(tot);
