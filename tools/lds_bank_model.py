@@ -57,9 +57,9 @@ def phases(idx, remap):
     return out
 old = lambda x: x ^ (((x >> 4) & 3) * 5)
 new = lambda x: x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3)
-print("round-1 swizzle, library mapping :"', phases(make(old), False))
-print("round-1 swizzle, uniform h<=16   :"', phases(make(old), True))
-print("current swizzle, uniform h<=16   :"', phases(make(new), True))
+print('round-1 swizzle, library mapping :', phases(make(old), False))
+print('round-1 swizzle, uniform h<=16   :', phases(make(old), True))
+print('current swizzle, uniform h<=16   :', phases(make(new), True))
 def extra(idx):
     out = {}
     m = 1
