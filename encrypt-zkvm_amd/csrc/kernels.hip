@@ -246,8 +246,11 @@ struct NttArgs {
     const fe *cos_stage;  // coset LDE (four-step): per-coset stage tables, 4096 apart (CosetTables::stage)
     const fe_ws *cos_stage_ws;  // ... their W sets
     const fe *cos_pass;   // ... and per-coset pass-1 twiddles (s_r w_n^j2)^k1, n apart (CosetTables::pass)
-    __device__ __forceinline__ int coset_of(size_t b) const { return cos_r0 + (int)(b % ncos) * cos_rstride; }
-    __device__ __forceinline__ fe *out_of(size_t b) const { return out + (b / ncos) * out_stride + (b % ncos) * out_jstride; }
+    // (32-bit: batch entries and grid sizes are < 2^32; 64-bit division is a long VALU sequence)
+    __device__ __forceinline__ int coset_of(uint32_t b) const { return cos_r0 + (int)(b % (uint32_t)ncos) * cos_rstride; }
+    __device__ __forceinline__ fe *out_of(uint32_t b) const {
+        return out + (size_t)(b / (uint32_t)ncos) * out_stride + (size_t)(b % (uint32_t)ncos) * out_jstride;
+    }
 };
 
 // Single pass: whole polynomial (n = M <= TILE) per line, LPB = TILE / n polys per block.
@@ -299,9 +302,10 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     const size_t n = (size_t)1 << a.log_n;
     const size_t n1 = n >> LOGM;
     const size_t lin = xcd_block(blockIdx.x, gridDim.x);
-    const size_t k1_0 = (lin / batch) * LPB;
-    const size_t b = lin % batch;
-    const fe *in = a.in + (b / a.ncos) * a.in_stride;
+    const uint32_t lin32 = (uint32_t)lin;
+    const size_t k1_0 = (size_t)(lin32 / (uint32_t)batch) * LPB;
+    const uint32_t b = lin32 % (uint32_t)batch;
+    const fe *in = a.in + (size_t)(b / (uint32_t)a.ncos) * a.in_stride;
     const int r = a.coset_of(b);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
