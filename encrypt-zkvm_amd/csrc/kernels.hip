@@ -64,20 +64,21 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 //   lanes vary in the load and pass-2 store phases.  sw is linear over XOR, so an element at pos + d
 //   (d's bits zero in pos) is idx ^ sw(d).
 //   padded (small M): line*(M + 1) + pos.
-//   The 1024-point / 4-line tile of the 2^20 NTTs (UNI below) uses sw(x) = x ^ bits 4-7 ^ bits 8-9 instead:
-//   its rounds with h <= 16 give every wave one butterfly index j (lanes spread over lines and groups,
-//   stride 4h), which the bits-4-5 fold leaves 4- and 16-way conflicted; this one is conflict-free for
-//   those, the other rounds, both load orders and the stores (host model: tools/lds_bank_model.py).
+//   The 1024-point / 4-line and 4096-point / 1-line tiles (UNI below: the 2^20 and 2^22 four-step passes)
+//   fold bits 4-7, 8-9 and 10-11 into bits 0-3 instead: their rounds with h <= 16 give every wave one
+//   butterfly index j (lanes spread over lines and groups, stride 4h), which the bits-4-5 fold leaves 4- and
+//   16-way conflicted; this one is conflict-free for those, the other rounds, the load orders and the
+//   stores (host model: tools/lds_bank_model.py).
 template <int LOGM, int TILE>
 struct Lds {
     static constexpr int M = 1 << LOGM, LPB = TILE >> LOGM;
     static constexpr bool SWZ = ZK_NTT_SWZ && LOGM >= 6;
-    static constexpr bool UNI = LOGM == 10 && TILE == 4096 && NTT_THREADS == 1024;
+    static constexpr bool UNI = (LOGM == 10 || LOGM == 12) && TILE == 4096 && NTT_THREADS == 1024;
     static constexpr int LLPB = LPB >= 16 ? 4 : LPB >= 8 ? 3 : LPB >= 4 ? 2 : LPB >= 2 ? 1 : 0;
     static constexpr int R = 4 - LLPB;
     static constexpr int LMASK = (1 << LLPB) - 1;
     __device__ __forceinline__ static int sw(int x) {
-        if constexpr (UNI) return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3);
+        if constexpr (UNI) return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3) ^ (((x >> 10) & 3) << 2);
         return SWZ ? x ^ (((x >> 4) & 3) * 5) : x;
     }
     __device__ __forceinline__ static int idx(int line, int pos) {
@@ -113,8 +114,8 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         constexpr int LH = LG - 1;
         const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), l = threadIdx.x & 63;
         const int j = w >> (4 - LH);
-        const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;
-        const int line = pidx >> (8 - LH), grp = pidx & ((256 >> LH) - 1);
+        const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;  // < 1024 / h: (line, group) pairs
+        const int line = pidx >> (LOGM - 2 - LH), grp = pidx & ((M >> (2 + LH)) - 1);
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
         const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];

@@ -79,3 +79,48 @@ def extra(idx):
     out['pass1/single store'] = m
     return out
 print('current swizzle, other phases   :', extra(make(new)), ' round-1 swizzle:', extra(make(old)))
+
+# the 4096-point / 1-line tile (2^22 pass 1, single-pass n = 4096)
+def check12(sw, LOGM=12):
+    M = 1 << LOGM; idx = lambda pos: sw(pos)
+    out = {}
+    R = 4
+    m = 1
+    for it in range(4):
+        for wv in range(16):
+            acc = []
+            for l in range(64):
+                v = it * 1024 + wv * 64 + l
+                k = ((v & 15) << (LOGM - R)) | (v >> R)
+                acc.append(idx(bitrev(k, LOGM)))
+            m = max(m, worst(acc))
+    out['load'] = m
+    m = 1
+    for it in range(4):
+        for wv in range(16):
+            m = max(m, worst([idx(it * 1024 + wv * 64 + l) for l in range(64)]))
+    out['store'] = m
+    m = 1
+    for it in range(4):
+        for wv in range(16):
+            m = max(m, worst([idx(bitrev(it * 1024 + wv * 64 + l, LOGM)) for l in range(64)]))
+    out['single_load'] = m
+    for LG in range(1, LOGM, 2):
+        h = 1 << (LG - 1); LH = LG - 1
+        for uni in ((False, True) if h <= 16 else (False,)):
+            m = 1
+            for wv in range(16):
+                for k in range(4):
+                    acc = []
+                    for l in range(64):
+                        if uni:
+                            j = wv >> (4 - LH); pidx = ((wv & ((16 >> LH) - 1)) << 6) | l; grp = pidx
+                        else:
+                            q = wv * 64 + l; j = q & (h - 1); grp = q >> LH
+                        acc.append(idx(grp * 4 * h + j + k * h))
+                    m = max(m, worst(acc))
+            out[f'h={h}{" uni" if uni else ""}'] = m
+    return out
+new12 = lambda x: x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3) ^ (((x >> 10) & 3) << 2)
+print('LOGM 12 round-1 swizzle      :', check12(old))
+print('LOGM 12 current swizzle      :', check12(new12))
