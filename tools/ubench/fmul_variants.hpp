@@ -1,10 +1,11 @@
 // candidate device multiplies for tools/ubench/fmul_lab.hip (variant 0 = the library's fe_mul)
 #pragma once
-#define FMUL_NVARIANTS 5
+#define FMUL_NVARIANTS 6
 static const char *fmul_variant_name(int v) {
     static const char *n[] = {"library fe_mul", "v1: U = T + C final step", "v2: independent fold products, mask final step",
                               "v3: precomputed W_i = b 2^(32i) mod p (16 words), one 35-bit fold",
-                              "v4: as v3, two products sharing one W set"};
+                              "v4: as v3, two products sharing one W set",
+                              "v5: two constants w, w 2^64 mod p (per-lane form, 32 B)"};
     return n[v];
 }
 
@@ -167,10 +168,53 @@ __device__ __forceinline__ fe fe_mul_pre(fe a, const uint32_t *W) {
     pre_cols(a, W, r0, r1, r2, r3, s4, s5);
     return pre_fold(r0, r1, r2, r3, s4, s5);
 }
+
+// ---- per-lane constant in two parts: a w = (a mod 2^64) w + (a >> 64) (w 2^64 mod p), a 193-bit sum of two
+// 64 x 128-bit products (five columns), one K-fold of its top 65 bits, then ws_fold's final step.
+__device__ __forceinline__ fe fe_mul_w2(fe A, fe W0, fe W2) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    const uint32_t a0 = lo32(W0.lo), a1 = hi32(W0.lo), a2 = lo32(W0.hi), a3 = hi32(W0.hi);
+    const uint32_t b0 = lo32(W2.lo), b1 = hi32(W2.lo), b2 = lo32(W2.hi), b3 = hi32(W2.hi);
+    uint32_t r0, r1, r2, r3, r4;
+    uint64_t a = (uint64_t)x0 * a0;
+    uint32_t h = 0;
+    col1(a, h, x2, b0);                                   ZK_SHIFT2(a, h, r0);
+    col4(a, h, x0, a1, x1, a0, x2, b1, x3, b0);           ZK_SHIFT2(a, h, r1);
+    col4(a, h, x0, a2, x1, a1, x2, b2, x3, b1);           ZK_SHIFT2(a, h, r2);
+    col4(a, h, x0, a3, x1, a2, x2, b3, x3, b2);           ZK_SHIFT2(a, h, r3);
+    col2(a, h, x1, a3, x3, b3);                           ZK_SHIFT2(a, h, r4);
+    const uint32_t s5 = (uint32_t)a, s6 = (uint32_t)(a >> 32);
+    // S' = L - H + (H K) << 32, H = r4 + s5 2^32 + s6 2^64 (s6 <= 1)
+    const uint32_t K = 0x2d00u;
+    uint64_t q = (uint64_t)r4 * K;
+    const uint32_t q0 = lo32(q);
+    q = (uint64_t)s5 * K + (q >> 32);
+    const uint32_t q1 = lo32(q), q2 = hi32(q) + s6 * K;
+    uint32_t d0, d1, d2, d3, dm, e1, e2, e3, e4;
+    uint64_t sB, sC;
+    asm("v_sub_co_u32 %0, %9, %11, %15\n\t"        // d0 = r0 - r4
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %1, %9, %12, %16, %9\n\t"   // d1 = r1 - s5 - b
+        "v_add_co_u32 %5, %10, %1, %19\n\t"        // e1 = d1 + q0
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %2, %9, %13, %17, %9\n\t"   // d2 = r2 - s6 - b
+        "v_addc_co_u32 %6, %10, %2, %20, %10\n\t"  // e2 = d2 + q1 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %3, %9, %14, 0, %9\n\t"     // d3
+        "v_addc_co_u32 %7, %10, %3, %21, %10\n\t"  // e3 = d3 + q2 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %4, %9, 0, 0, %9\n\t"       // dm = -b
+        "v_addc_co_u32 %8, %10, %4, 0, %10"        // e4 = bit 128 of S'
+        : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(dm), "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&v"(e4), "=&s"(sB),
+          "=&s"(sC)
+        : "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(s5), "v"(s6), "v"(0u), "v"(q0), "v"(q1), "v"(q2));
+    return pre_fold(d0, e1, e2, e3, e4, 0u);
+}
 template <int V>
 __device__ __forceinline__ fe fmul_variant(fe a, fe b, const uint32_t *W = nullptr) {
     if constexpr (V == 0) return fe_mul(a, b);
     if constexpr (V == 3 || V == 4) return fe_mul_pre(a, W);
+    if constexpr (V == 5) return fe_mul_w2(a, fe{join32(W[0], W[4]), join32(W[8], W[12])}, fe{join32(W[2], W[6]), join32(W[10], W[14])});
     uint32_t r[8];
     mul_wide(a, b, r);
     if constexpr (V == 1) return reduce_v1(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
