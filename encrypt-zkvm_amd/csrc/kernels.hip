@@ -373,6 +373,16 @@ static double dft_muls_per_elem(int logm) {
     if (logm < 2) return 0.5;
     return 0.25 + (double)((logm - 2) / 2) + ((logm & 1) ? 0.5 : 0.0);
 }
+// The profiler's multiply count is in fe_mul-equivalents: a multiply by a wave-uniform twiddle through its
+// W set costs 80 issue slots against fe_mul's 113 (tools/ubench/fmul_lab.hip), so it counts 0.71.  UNI
+// tiles do their rounds h = 1, 4, 16 that way: 2.25 multiplies per element in the plain form (the first
+// round has one multiply per four points), 3 in the coset-table form.
+static constexpr double ZK_UNIFORM_MUL_COST = 80.0 / 113.0;
+template <int LOGM, int TILE>
+static double uniform_mul_discount(bool ct) {
+    if (!Lds<LOGM, TILE>::UNI) return 0.0;
+    return (ct ? 3.0 : 2.25) * (1.0 - ZK_UNIFORM_MUL_COST);
+}
 
 template <int LOGM, int TILE>
 static void launch_single(hipStream_t st, const NttArgs &a, int batch) {
@@ -380,7 +390,8 @@ static void launch_single(hipStream_t st, const NttArgs &a, int batch) {
     size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_single<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * (1 << LOGM);
-    ZK_PROF_OPS(st, "ntt_single", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.pre_full || a.pre_lo ? 1 : 0) + (a.has_post ? 1 : 0)),
+    ZK_PROF_OPS(st, "ntt_single", 32.0 * el,
+                el * (dft_muls_per_elem(LOGM) - uniform_mul_discount<LOGM, TILE>(false) + (a.pre_full || a.pre_lo ? 1 : 0) + (a.has_post ? 1 : 0)),
                 el * LOGM, hipLaunchKernelGGL((ntt_single<LOGM, TILE>), dim3(cdiv(batch, LPB)), dim3(NTT_THREADS), sh, st, a, batch));
 }
 
@@ -393,13 +404,15 @@ static void launch_pass1(hipStream_t st, const NttArgs &a, int batch) {
     const dim3 grid(cdiv(n1, LPB) * batch);
     if (a.cos_stage) {
         hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-        ZK_PROF_OPS(st, "ntt_pass1", 32.0 * el, el * ((double)LOGM / 2.0 + 1.0), el * LOGM,
+        ZK_PROF_OPS(st, "ntt_pass1", 32.0 * el, el * ((double)LOGM / 2.0 + 1.0 - uniform_mul_discount<LOGM, TILE>(true)), el * LOGM,
                     hipLaunchKernelGGL((ntt_pass1<LOGM, TILE, true>), grid, dim3(NTT_THREADS), sh, st, a, batch));
         return;
     }
     hipFuncSetAttribute((const void *)ntt_pass1<LOGM, TILE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     ZK_PROF_OPS(st, "ntt_pass1", (a.pre_full ? 48.0 : 32.0) * el,
-                el * (dft_muls_per_elem(LOGM) + 1.0 + (a.pre_full || a.pre_lo ? 1 : 0) + (a.pass_tw ? 0 : 1)), el * LOGM,
+                el * (dft_muls_per_elem(LOGM) - uniform_mul_discount<LOGM, TILE>(false) + 1.0 + (a.pre_full || a.pre_lo ? 1 : 0) +
+                      (a.pass_tw ? 0 : 1)),
+                el * LOGM,
                 hipLaunchKernelGGL((ntt_pass1<LOGM, TILE, false>), grid, dim3(NTT_THREADS), sh, st, a, batch));
 }
 
@@ -410,7 +423,8 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
-    ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) + (a.has_post ? 1 : 0)), el * LOGM,
+    ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) - uniform_mul_discount<LOGM, TILE>(false) + (a.has_post ? 1 : 0)),
+                el * LOGM,
                 hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
 }
 
