@@ -318,6 +318,54 @@ __device__ __forceinline__ fe fe_mul_uniform(fe A, const fe_ws &W) {
     return ws_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
 }
 
+// ---- per-lane constant in two parts (32 B): a w = (a mod 2^64) w + (a >> 64) (w 2^64 mod p), a 193-bit sum
+// of two 64 x 128-bit products (five columns), one K-fold of its top 65 bits (H C = H K 2^32 - H), then
+// ws_fold's final step.  99 issue slots against fe_mul's 113 (tools/ubench/fmul_lab.hip v5): for per-lane
+// twiddles, where a 64-B W set per lane costs more in loads than it saves.
+struct fe_w2 {
+    fe w, w64;  // w and w 2^64 mod p
+};
+__device__ __forceinline__ fe fe_mul_w2(fe A, const fe_w2 &W) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    const uint32_t a0 = lo32(W.w.lo), a1 = hi32(W.w.lo), a2 = lo32(W.w.hi), a3 = hi32(W.w.hi);
+    const uint32_t b0 = lo32(W.w64.lo), b1 = hi32(W.w64.lo), b2 = lo32(W.w64.hi), b3 = hi32(W.w64.hi);
+    uint32_t r0, r1, r2, r3, r4, h = 0;
+    uint64_t a = (uint64_t)x0 * a0;
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col1(a, h, x2, b0);                          ZK_WSHIFT(r0);
+    col4(a, h, x0, a1, x1, a0, x2, b1, x3, b0);  ZK_WSHIFT(r1);
+    col4(a, h, x0, a2, x1, a1, x2, b2, x3, b1);  ZK_WSHIFT(r2);
+    col4(a, h, x0, a3, x1, a2, x2, b3, x3, b2);  ZK_WSHIFT(r3);
+    col2(a, h, x1, a3, x3, b3);                  ZK_WSHIFT(r4);
+#undef ZK_WSHIFT
+    const uint32_t s5 = (uint32_t)a, s6 = (uint32_t)(a >> 32);  // s6 <= 1
+    // S' = L - H + (H K) << 32 with H = r4 + s5 2^32 + s6 2^64; S' < 2^128 + 2^111, bit 128 in e4
+    const uint32_t K = 0x2d00u;
+    uint64_t q = (uint64_t)r4 * K;
+    const uint32_t q0 = lo32(q);
+    q = (uint64_t)s5 * K + (q >> 32);
+    const uint32_t q1 = lo32(q), q2 = hi32(q) + s6 * K;
+    uint32_t d0, d1, d2, d3, dm, e1, e2, e3, e4;
+    uint64_t sB, sC;
+    asm("v_sub_co_u32 %0, %9, %11, %15\n\t"        // d0 = r0 - r4
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %1, %9, %12, %16, %9\n\t"   // d1 = r1 - s5 - b
+        "v_add_co_u32 %5, %10, %1, %18\n\t"        // e1 = d1 + q0
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %2, %9, %13, %17, %9\n\t"   // d2 = r2 - s6 - b
+        "v_addc_co_u32 %6, %10, %2, %19, %10\n\t"  // e2 = d2 + q1 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %3, %9, %14, 0, %9\n\t"     // d3
+        "v_addc_co_u32 %7, %10, %3, %20, %10\n\t"  // e3 = d3 + q2 + c
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %4, %9, 0, 0, %9\n\t"       // dm = -b
+        "v_addc_co_u32 %8, %10, %4, 0, %10"        // e4
+        : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(dm), "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&v"(e4), "=&s"(sB),
+          "=&s"(sC)
+        : "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(s5), "v"(s6), "v"(q0), "v"(q1), "v"(q2));
+    return ws_fold(d0, e1, e2, e3, e4, 0u);
+}
+
 // the W set tab[idx] for a wave-uniform idx, through scalar loads
 __device__ __forceinline__ fe_ws load_fe_ws(const fe_ws *__restrict__ tab, int idx) {
     fe_ws r;
@@ -394,6 +442,10 @@ __host__ static inline fe fe_mul(fe a, fe b) {
 
 ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }
 
+__host__ inline fe_w2 make_fe_w2(fe w) {
+    const fe two64 = fe{0, 1};
+    return fe_w2{w, fe_mul(w, two64)};
+}
 __host__ inline fe_ws make_fe_ws(fe w) {
     fe_ws W;
     const fe two32 = fe{1ull << 32, 0};

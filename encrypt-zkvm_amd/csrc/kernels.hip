@@ -105,7 +105,7 @@ struct Lds {
 // pairs, so its three twiddles are wave-uniform and multiply through their W sets (fe_mul_uniform, scalar
 // loads from `ws`, the W-set table indexed exactly like `tw4096`).  Same butterflies, same values.
 template <int LOGM, int TILE, int LG, bool CT>
-__device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *ws) {
+__device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
     constexpr int h = 1 << (LG - 1);
@@ -123,6 +123,25 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
         const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
+        s[p] = fe_add(a0, u2);
+        s[p2h] = fe_sub(a0, u2);
+        s[ph] = fe_add(a1, u3);
+        s[p3h] = fe_sub(a1, u3);
+        __syncthreads();
+        return;
+    }
+    if constexpr (L::UNI) {
+        // per-lane twiddles (h >= 64): the two-part form (fe_w2, 32 B per twiddle)
+        const int q = threadIdx.x;
+        const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
+        const int j = local & (h - 1), grp = local >> (LG - 1);
+        const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+        const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
+        const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+        const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
+        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
+        const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
         s[p] = fe_add(a0, u2);
         s[p2h] = fe_sub(a0, u2);
         s[ph] = fe_add(a1, u3);
@@ -152,10 +171,10 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
 
 // rounds LG, LG+2, ... while LG + 1 <= LOGM, then the trailing radix-2 stage of an odd LOGM
 template <int LOGM, int TILE, int LG, bool CT>
-__device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *ws) {
+__device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
     if constexpr (LG + 1 <= LOGM) {
-        r4_round<LOGM, TILE, LG, CT>(s, tw4096, ws);
-        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096, ws);
+        r4_round<LOGM, TILE, LG, CT>(s, tw4096, ws, w2t);
+        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096, ws, w2t);
     } else if constexpr (LG == LOGM) {
         constexpr int M = 1 << LOGM;
         constexpr int half = 1 << (LG - 1);
@@ -187,11 +206,11 @@ __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *
 // CT: coset-table mode (every round generic, the first one included: 4 multiplies per 4 points).
 // ws: the W sets of tw4096 (same indexing), used by the rounds with wave-uniform twiddles (UNI tiles).
 template <int LOGM, int TILE, bool CT = false>
-__device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws) {
+__device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
     if constexpr (CT) {
-        r4_rounds<LOGM, TILE, 1, true>(s, tw4096, ws);
+        r4_rounds<LOGM, TILE, 1, true>(s, tw4096, ws, w2t);
     } else if constexpr (LOGM >= 2) {
         using L = Lds<LOGM, TILE>;
         fe w4;
@@ -213,9 +232,9 @@ __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws
             s[p3] = fe_sub(a1, a3);
         }
         __syncthreads();
-        r4_rounds<LOGM, TILE, 3, false>(s, tw4096, ws);
+        r4_rounds<LOGM, TILE, 3, false>(s, tw4096, ws, w2t);
     } else {
-        r4_rounds<LOGM, TILE, 1, false>(s, tw4096, ws);
+        r4_rounds<LOGM, TILE, 1, false>(s, tw4096, ws, w2t);
     }
 }
 
@@ -232,6 +251,7 @@ struct NttArgs {
     size_t in_stride, out_stride;
     const fe *tw4096;             // DFT-stage table (forward or inverse)
     const fe_ws *tw_ws;           // ... its W sets (the wave-uniform rounds of UNI tiles)
+    const fe_w2 *tw_w2;           // ... in two-part form (the per-lane rounds of UNI tiles)
     const fe *big_lo, *big_hi;    // w_n^t split tables (forward or inverse) for the inter-pass twiddle
     const fe *pre_lo, *pre_hi;    // optional pre-scale s^k (split table)
     const fe *pre_full;           // ... or the same from a full table (preferred when present)
@@ -246,6 +266,7 @@ struct NttArgs {
     size_t out_jstride;
     const fe *cos_stage;  // coset LDE (four-step): per-coset stage tables, 4096 apart (CosetTables::stage)
     const fe_ws *cos_stage_ws;  // ... their W sets
+    const fe_w2 *cos_stage_w2;  // ... and two-part forms
     const fe *cos_pass;   // ... and per-coset pass-1 twiddles (s_r w_n^j2)^k1, n apart (CosetTables::pass)
     // (32-bit: batch entries and grid sizes are < 2^32; 64-bit division is a long VALU sequence)
     __device__ __forceinline__ int coset_of(uint32_t b) const { return cos_r0 + (int)(b % (uint32_t)ncos) * cos_rstride; }
@@ -273,7 +294,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
+    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws, a.tw_w2);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j = e & (M - 1);
         int b = b0 + line;
@@ -319,8 +340,9 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    if constexpr (CT) lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096, a.cos_stage_ws + (size_t)r * 4096);
-    else lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
+    if constexpr (CT)
+        lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096, a.cos_stage_ws + (size_t)r * 4096, a.cos_stage_w2 + (size_t)r * 4096);
+    else lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws, a.tw_w2);
     fe *out = a.out + b * a.out_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j2 = e & (M - 1);
@@ -356,7 +378,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k1) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
-    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws);
+    lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws, a.tw_w2);
     fe *out = a.out_of(b);
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, j1 = e / LPB;
@@ -466,6 +488,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.out_stride = out_stride;
     a.tw4096 = inverse ? T.dft_inv : T.dft_fwd;
     a.tw_ws = inverse ? T.dft_inv_ws : T.dft_fwd_ws;
+    a.tw_w2 = inverse ? T.dft_inv_w2 : T.dft_fwd_w2;
     a.big_lo = inverse ? T.inv_lo : T.fwd_lo;
     a.big_hi = inverse ? T.inv_hi : T.fwd_hi;
     a.pre_lo = pre ? pre->lo : nullptr;
@@ -490,6 +513,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.out_jstride = 0;
     a.cos_stage = a.cos_pass = nullptr;
     a.cos_stage_ws = nullptr;
+    a.cos_stage_w2 = nullptr;
     ntt_run(st, a, batch, tmp);
 }
 
@@ -514,6 +538,7 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     a2.pre_lo = a2.pre_hi = a2.pre_full = nullptr;
     a2.cos_stage = a2.cos_pass = nullptr;
     a2.cos_stage_ws = nullptr;
+    a2.cos_stage_w2 = nullptr;
     ZK_DISPATCH_LOGM(log_n1, launch_pass2, st, a2, batch);
 }
 
@@ -528,6 +553,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
     a.out_jstride = out_jstride;
     a.tw4096 = T.dft_fwd;
     a.tw_ws = T.dft_fwd_ws;
+    a.tw_w2 = T.dft_fwd_w2;
     a.big_lo = T.fwd_lo;
     a.big_hi = T.fwd_hi;
     a.pass_tw = T.fwd_pass;
@@ -542,6 +568,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
     } else {
         a.cos_stage = CT.stage;
         a.cos_stage_ws = CT.stage_ws;
+        a.cos_stage_w2 = CT.stage_w2;
         a.cos_pass = CT.pass;
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so

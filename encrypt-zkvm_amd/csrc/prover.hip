@@ -73,6 +73,11 @@ static std::vector<fe_ws> ws_of(const std::vector<fe> &v) {
     for (size_t i = 0; i < v.size(); i++) w[i] = make_fe_ws(v[i]);
     return w;
 }
+static std::vector<fe_w2> w2_of(const std::vector<fe> &v) {
+    std::vector<fe_w2> w(v.size());
+    for (size_t i = 0; i < v.size(); i++) w[i] = make_fe_w2(v[i]);
+    return w;
+}
 
 static hipError_t make_pow_table(zk_prover *p, fe s, size_t n, PowTable *out) {
     std::vector<fe> lo(2048), hi(n / 2048 + 1);
@@ -93,6 +98,7 @@ static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
     struct Dft4096 {
         std::vector<fe> f, i;
         std::vector<fe_ws> fw, iw;
+        std::vector<fe_w2> f2, i2;
         Dft4096() : f(2048), i(2048) {
             const fe w = h_root_of_unity(12), wi = h_inv(w);
             f[0] = i[0] = fe_one();
@@ -102,6 +108,8 @@ static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
             }
             fw = ws_of(f);
             iw = ws_of(i);
+            f2 = w2_of(f);
+            i2 = w2_of(i);
         }
     };
     static const Dft4096 d4096;
@@ -109,6 +117,8 @@ static hipError_t make_ntt_tables(zk_prover *p, int log_n, NttTables *T) {
     if (e == hipSuccess) e = upload(p, &T->dft_inv, d4096.i);
     if (e == hipSuccess) e = upload(p, &T->dft_fwd_ws, d4096.fw);
     if (e == hipSuccess) e = upload(p, &T->dft_inv_ws, d4096.iw);
+    if (e == hipSuccess) e = upload(p, &T->dft_fwd_w2, d4096.f2);
+    if (e == hipSuccess) e = upload(p, &T->dft_inv_w2, d4096.i2);
     size_t n = (size_t)1 << log_n;
     fe w = h_root_of_unity(log_n);
     PowTable f, i;
@@ -200,6 +210,7 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     if (pl->log_n > 12) {
         ZK_CHECK_HIP(hipMemcpy(pl->ct.stage, stage.data(), stage.size() * sizeof(fe), hipMemcpyHostToDevice));
         ZK_CHECK_HIP(upload(p, &pl->ct.stage_ws, ws_of(stage)));
+        ZK_CHECK_HIP(upload(p, &pl->ct.stage_w2, w2_of(stage)));
     }
     s = fe_make(3);
     for (int r = 0; r < 8; r++) {

@@ -72,6 +72,7 @@ struct NttTables {
     int log_n = 0;
     fe *dft_fwd = nullptr, *dft_inv = nullptr;
     fe_ws *dft_fwd_ws = nullptr, *dft_inv_ws = nullptr;  // their W sets (f128.hpp fe_mul_uniform)
+    fe_w2 *dft_fwd_w2 = nullptr, *dft_inv_w2 = nullptr;  // and two-part forms (f128.hpp fe_mul_w2)
     fe *fwd_lo = nullptr, *fwd_hi = nullptr, *inv_lo = nullptr, *inv_hi = nullptr;
     // four-step inter-pass twiddles w^(j2*k1) laid out as pass 1 consumes them, [k1 * n2 + j2]
     // (n elements each; only for log_n > 12, else null)
@@ -118,6 +119,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
 struct CosetTables {
     fe *full = nullptr, *stage = nullptr, *pass = nullptr;
     fe_ws *stage_ws = nullptr;  // W sets of `stage` (four-step plans)
+    fe_w2 *stage_w2 = nullptr;  // two-part forms of `stage`
 };
 // Forward coset LDE: for columns c < ncols (at in + c*in_stride) and coset slots j < ncos (coset r0 + j*rstride),
 // the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*min(ncos, 8)*n
