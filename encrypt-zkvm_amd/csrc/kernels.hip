@@ -395,15 +395,15 @@ static double dft_muls_per_elem(int logm) {
     if (logm < 2) return 0.5;
     return 0.25 + (double)((logm - 2) / 2) + ((logm & 1) ? 0.5 : 0.0);
 }
-// The profiler's multiply count is in fe_mul-equivalents: a multiply by a wave-uniform twiddle through its
-// W set costs 80 issue slots against fe_mul's 113 (tools/ubench/fmul_lab.hip), so it counts 0.71.  UNI
-// tiles do their rounds h = 1, 4, 16 that way: 2.25 multiplies per element in the plain form (the first
-// round has one multiply per four points), 3 in the coset-table form.
-static constexpr double ZK_UNIFORM_MUL_COST = 80.0 / 113.0;
+// The profiler's multiply count is in fe_mul-equivalents, each kind priced at its issue cost relative to
+// fe_mul's 113 slots (tools/ubench/fmul_lab.hip): a wave-uniform twiddle through its W set 80 (UNI rounds
+// h = 1, 4, 16: 2.25 multiplies per element in the plain form, whose first round has one per four points,
+// 3 in the coset-table form), a per-lane two-part twiddle 99 (the remaining LOGM/2 - 3 rounds).
+static constexpr double ZK_UNIFORM_MUL_COST = 80.0 / 113.0, ZK_W2_MUL_COST = 99.0 / 113.0;
 template <int LOGM, int TILE>
 static double uniform_mul_discount(bool ct) {
     if (!Lds<LOGM, TILE>::UNI) return 0.0;
-    return (ct ? 3.0 : 2.25) * (1.0 - ZK_UNIFORM_MUL_COST);
+    return (ct ? 3.0 : 2.25) * (1.0 - ZK_UNIFORM_MUL_COST) + (LOGM / 2 - 3) * (1.0 - ZK_W2_MUL_COST);
 }
 
 template <int LOGM, int TILE>
