@@ -664,28 +664,37 @@ __device__ __forceinline__ void load_digest(const uint8_t *src, uint32_t h[8]) {
     h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
 }
 
-// leaf hash of natural LDE row i over a coset-major column set (K3/K5 of SURVEY 7)
-// Leaf digests of coset-major LDE rows, one thread per row.  (Fusing the bottom Merkle levels into
-// this kernel was measured: the merges are compute-bound either way and the fused form lost.)
-__global__ void __launch_bounds__(256) k_hash_rows(const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves) {
-    const size_t N = (size_t)1 << (log_n + log_b);
+// Leaf digests of coset-major LDE rows, one thread per row (K3/K5 of SURVEY 7): the rows i = 8q + r of the
+// 2^log_rc cosets r0 <= r < r0 + 2^log_rc (all of them: r0 = 0, log_rc = log_b), leaves in natural order.
+// (Fusing the bottom Merkle levels into this kernel was measured: the merges are compute-bound either way
+// and the fused form lost.)
+__global__ void __launch_bounds__(256) k_hash_rows(const fe *base, int ncols, int log_n, int log_b, int r0, int log_rc,
+                                                   uint8_t *leaves) {
+    const size_t M = (size_t)1 << (log_n + log_rc);
     const size_t n = (size_t)1 << log_n;
     const size_t B = (size_t)1 << log_b;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < N; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i & (B - 1), q = i >> log_b;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < M; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = r0 + (t & (((size_t)1 << log_rc) - 1)), q = t >> log_rc;
         const fe *p = base + r * n + q;
         const size_t cstride = B * n;
         uint32_t h[8];
         b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cstride]; }, h);
-        store_digest(leaves + 32 * i, h);
+        store_digest(leaves + 32 * ((q << log_b) + r), h);
     }
+}
+
+void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int r0, int log_rc,
+                      uint8_t *leaves) {
+    const size_t M = (size_t)1 << (log_n + log_rc);
+    ZK_PROF(st, "hash_rows", (16.0 * ncols + 32) * M,
+            hipLaunchKernelGGL(k_hash_rows, dim3(cdiv(M, 256)), dim3(256), 0, st, base, ncols, log_n, log_b, r0, log_rc, leaves));
 }
 
 // Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).
 void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
                              uint8_t *nodes) {
     const size_t N = (size_t)1 << (log_n + log_b);
-    ZK_PROF(st, "hash_rows", (16.0 * ncols + 32) * N, hipLaunchKernelGGL(k_hash_rows, dim3(cdiv(N, 256)), dim3(256), 0, st, base, ncols, log_n, log_b, leaves));
+    hash_rows_cosets(st, base, ncols, log_n, log_b, 0, log_b, leaves);
     merkle_tree(st, leaves, N, nodes);
 }
 

@@ -279,6 +279,9 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     p->max_n = max_n;
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+    ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+    for (auto &e : p->ev_fork) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
     DeviceArena &A = p->arena;
@@ -326,7 +329,12 @@ void zk_prover_destroy(zk_prover *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     (void)hipStreamSynchronize(p->st);
+    if (p->st2) (void)hipStreamSynchronize(p->st2);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
+    for (auto &e : p->ev_fork)
+        if (e) (void)hipEventDestroy(e);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->st2) (void)hipStreamDestroy(p->st2);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
@@ -908,22 +916,47 @@ int zk::deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, u
 }
 
 // ---------------------------------------------------------------- the single-GPU prove path
-static int trace_lde_stage(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, uint32_t B) {
-    const size_t N = n * B;
-    fe inv_n = h_inv(fe_make(n));
-    // interpolate 28 columns (winter-math interpolate_poly over <w_n>)
-    ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-    // coset r of the LDE domain: NTT of the coefficients scaled by (3 w_N^r)^k
-    ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, 0, 1, (int)B, p->lde, B * n, n, p->tmp);
-    (void)N;
-    return ZK_OK;
+// Coset LDE of the ncols column polynomials at `polys` into the coset-major `lde` and the commitment to
+// its rows (leaves, nodes; the root is read back with the caller's next d2h_flush).  With parts > 1 the
+// cosets go in `parts` groups: the rows of a finished group are hashed on the second stream while the
+// NTT of the next group runs (ZK_PIPE; default 1 = LDE then hashing on one stream: A/B 13.89 ms for 1, 14.05 for 2, 14.38 for 4 parts -- co-resident NTT and BLAKE3 waves do not issue faster than either alone).
+static int pipe_parts(uint32_t B) {
+    static const int parts = [] {
+        const char *e = getenv("ZK_PIPE");
+        const int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 8 && !(v & (v - 1)) ? v : 1;
+    }();
+    return std::min<int>(parts, (int)B);
+}
+static int lde_commit(zk_prover *p, Plan *pl, const fe *polys, int ncols, fe *lde, uint8_t *leaves, uint8_t *nodes,
+                      uint8_t root[32]) {
+    const int log_n = pl->log_n, log_b = pl->log_b;
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b;
+    const int parts = pipe_parts((uint32_t)B), per = (int)B / parts, log_per = ilog2((size_t)per);
+    for (int h = 0; h < parts; h++) {
+        ntt_lde(p->st, pl->Tn, pl->ct, polys, n, ncols, h * per, 1, per, lde + (size_t)h * per * n, B * n, n, p->tmp);
+        if (h + 1 < parts) {
+            ZK_CHECK_HIP(hipEventRecord(p->ev_fork[h], p->st));
+            ZK_CHECK_HIP(hipStreamWaitEvent(p->st2, p->ev_fork[h], 0));
+            hash_rows_cosets(p->st2, lde, ncols, log_n, log_b, h * per, log_per, leaves);
+        } else {
+            hash_rows_cosets(p->st, lde, ncols, log_n, log_b, h * per, log_per, leaves);
+        }
+    }
+    if (parts > 1) {
+        ZK_CHECK_HIP(hipEventRecord(p->ev_join, p->st2));
+        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_join, 0));
+    }
+    merkle_tree(p->st, leaves, n * B, nodes);
+    return d2h_small(p, root, nodes + 32, 32);
 }
 
-// hash the rows and build the tree; the root is read back with the caller's next d2h_flush
-static int commit_rows(zk_prover *p, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves, uint8_t *nodes,
-                       uint8_t root[32]) {
-    commit_rows_coset_major(p->st, base, ncols, log_n, log_b, leaves, nodes);
-    return d2h_small(p, root, nodes + 32, 32);
+// S2: interpolate the 28 trace columns (winter-math interpolate_poly over <w_n>), extend them over the B
+// cosets of the LDE domain (coset r: the coefficients scaled by (3 w_N^r)^k) and commit to the rows
+static int trace_lde_commit(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, uint8_t root[32]) {
+    fe inv_n = h_inv(fe_make(n));
+    ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+    return lde_commit(p, pl, p->polys, W, p->lde, p->leaves, p->nodes, root);
 }
 
 static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, size_t n, uint32_t B, uint8_t *dst) {
@@ -983,8 +1016,8 @@ static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe
         for (int j = 0; j < KX; j++)
             boundary_poly_add(p->st, p->polys, pl->log_n, bnd[j], bnd[0].g_last2, p->dscratch, p->cpolys + (size_t)j * n,
                               p->flag);
-    ntt_lde(p->st, pl->Tn, pl->ct, p->cpolys, n, CK, 0, 1, (int)B, clde, B * n, n, p->tmp);
-    return commit_rows(p, clde, CK, pl->log_n, pl->log_b, p->cleaves, p->cnodes, root);
+    (void)B;
+    return lde_commit(p, pl, p->cpolys, CK, clde, p->cleaves, p->cnodes, root);
 }
 
 // Degree check of the composition: the verifier's out-of-domain identity (zk::ood_identity) on the
@@ -1031,9 +1064,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     Coin coin = seed_coin(n, opt, pub);
 
     // S2: trace LDE + commitment
-    ZK_TRY(trace_lde_stage(p, pl, d_trace, n, B));
-    stage_mark(p, "trace_lde");
-    ZK_TRY(commit_rows(p, p->lde, W, log_n, log_b, p->leaves, p->nodes, R.trace_root));
+    ZK_TRY(trace_lde_commit(p, pl, d_trace, n, R.trace_root));
     ZK_TRY(d2h_flush(p));
     stage_mark(p, "trace_commit");
     HostTimer HT;
@@ -1309,9 +1340,8 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     int rc = get_plan(p, n, blowup, &pl);
     if (rc) return rc;
     ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
-    if ((rc = trace_lde_stage(p, pl, p->d_trace, n, blowup))) return rc;
     uint8_t r[32];
-    if ((rc = commit_rows(p, p->lde, W, pl->log_n, pl->log_b, p->leaves, p->nodes, r))) return rc;
+    if ((rc = trace_lde_commit(p, pl, p->d_trace, n, r))) return rc;
     if ((rc = d2h_flush(p))) return rc;
     if (root) memcpy(root, r, 32);
     *out = new zk_trace_lde{p, n, blowup, W};

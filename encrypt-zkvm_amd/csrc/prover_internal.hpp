@@ -92,6 +92,10 @@ struct Openings;
 struct zk_prover {
     int device = 0;
     hipStream_t st = nullptr;
+    // second stream: row hashing of finished LDE cosets runs beside the NTT of the next ones (the NTT is
+    // bound by carry-writing VALU issue, BLAKE3 by 3-source ops: co-resident waves fill each other's gaps)
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_fork[8] = {}, ev_join = nullptr;
     size_t max_n = 0;
     uint32_t max_b = 0;
     zk::DeviceArena arena;

@@ -135,6 +135,9 @@ void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint
 // leaf[i] = BLAKE3(row i) for natural LDE index i < N = B*n of a coset-major column set:
 // element (column c, index i) lives at base[(c*B + i%B)*n + i/B].
 // leaves (N x 32 B) and the heap-ordered Merkle tree nodes[1..N) of coset-major rows / FRI layer rows
+// leaf digests of the rows of LDE cosets r0 .. r0 + 2^log_rc - 1 (coset-major columns), natural leaf order
+void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int r0, int log_rc,
+                      uint8_t *leaves);
 void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
                              uint8_t *nodes);
 // FRI layer leaves: row r of a natural-order layer of size L (rows = L/fold): [e[r + k*L/fold]]
