@@ -740,6 +740,66 @@ __global__ void __launch_bounds__(256) k_merge_level3(const uint8_t *src, uint8_
     }
 }
 
+// The same three levels with the child loads software-pipelined: a grid of a few waves per SIMD walks the
+// groups, each thread loading its next group's 8 children (into registers) before merging the current one.
+// With one group per thread every wave of a launch loads at the same moment and then merges at the same
+// moment, so the child fetch (the launch reads all 2^k leaf digests) is never hidden behind compute.
+// ZK_MERKLE_PF: grid cap of the pipelined kernel (0: the one-group-per-thread kernel above).  A/B on one box:
+// merkle 0.64 -> 0.55 ms per 2^20 proof for caps 1024 / 2048 / 4096 (two rounds of four waves per SIMD kept)
+#ifndef ZK_MERKLE_PF
+#define ZK_MERKLE_PF 2048
+#endif
+// half `half` of group t: children 8t + 4 half .. + 4 (c: 8 uint4) -> two parents and their parent g
+__device__ __forceinline__ void merge_half3(const uint4 c[8], uint8_t *nodes, size_t cnt, size_t t, int half,
+                                            uint32_t g[8]) {
+    uint32_t l[8], r[8], h0[8], h1[8];
+    auto dig = [&](int k, uint32_t d[8]) {
+        const uint4 a = c[2 * k], b = c[2 * k + 1];
+        d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+        d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    };
+    const size_t c0 = 4 * t + 2 * half;
+    dig(0, l);
+    dig(1, r);
+    b3::merge(l, r, h0);
+    store_digest(nodes + 32 * (cnt + c0), h0);
+    dig(2, l);
+    dig(3, r);
+    b3::merge(l, r, h1);
+    store_digest(nodes + 32 * (cnt + c0 + 1), h1);
+    b3::merge(h0, h1, g);
+    store_digest(nodes + 32 * (cnt / 2 + 2 * t + half), g);
+}
+__global__ void __launch_bounds__(256, 4) k_merge_level3_pf(const uint8_t *src, uint8_t *nodes, size_t cnt) {
+    const size_t q = cnt / 4, stride = (size_t)gridDim.x * blockDim.x;
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 cur[8], nxt[8];
+    if (t < q) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) cur[k] = s4[16 * t + k];
+    }
+    while (t < q) {
+        const size_t tn = t + stride;
+        uint32_t g0[8], g1[8], h[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) nxt[k] = s4[16 * t + 8 + k];  // second half of this group
+        merge_half3(cur, nodes, cnt, t, 0, g0);
+#pragma unroll
+        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+        if (tn < q) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) nxt[k] = s4[16 * tn + k];  // first half of the next group
+        }
+        merge_half3(cur, nodes, cnt, t, 1, g1);
+        b3::merge(g0, g1, h);
+        store_digest(nodes + 32 * (cnt / 4 + t), h);
+#pragma unroll
+        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+        t = tn;
+    }
+}
+
 // Up to log2(P) + 1 levels in one block of P = blockDim.x threads: thread t merges the children
 // src[2(bP + t)], src[2(bP + t) + 1] into first-level parent bP + t, then the block halves its level in
 // LDS with one compression per thread per level; every node goes to its heap position.  Used for the
@@ -787,8 +847,15 @@ void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *node
     while (cnt >= ((size_t)1 << ZK_MERKLE_L3_MIN)) {
         unsigned blocks = cdiv(cnt / 4, 256);
         if (blocks > 65536) blocks = 65536;
-        ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
-                hipLaunchKernelGGL(k_merge_level3, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
+        if (ZK_MERKLE_PF) {
+            // at most ZK_MERKLE_PF blocks (1024: one round of four waves per SIMD on 256 CUs)
+            blocks = std::min<unsigned>(blocks, ZK_MERKLE_PF);
+            ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
+                    hipLaunchKernelGGL(k_merge_level3_pf, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
+        } else {
+            ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
+                    hipLaunchKernelGGL(k_merge_level3, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
+        }
         src = nodes + 32 * (cnt / 4);
         cnt /= 8;
     }
