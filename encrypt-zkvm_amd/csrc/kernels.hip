@@ -1325,8 +1325,10 @@ hipError_t upload_rescue_consts(hipStream_t st) {
 static void upload_rescue(hipStream_t st) { (void)upload_rescue_consts(st); }
 
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                      const AirConsts *consts_dev, fe *comp, bool bnd) {
-    eval_constraints_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp,
+                      const AirConsts *consts_dev, fe *comp, bool bnd, int nce) {
+    // (with bnd the kernel reads the boundary divisor planes at stride nce * n: all 8 cosets then)
+    if (bnd) nce = 8;
+    eval_constraints_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp,
                             bnd);
 }
 
@@ -1357,8 +1359,9 @@ void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalM
 }
 
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                          const AirConsts *consts2_dev, fe *comp, bool bnd) {
-    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{8, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
+                          const AirConsts *consts2_dev, fe *comp, bool bnd, int nce) {
+    if (bnd) nce = 8;
+    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
                                 (size_t)8 << log_n, comp, bnd);
 }
 
@@ -1374,6 +1377,14 @@ __global__ void __launch_bounds__(256) k_comp_cross(CrossMap m, const fe *wi_lo,
         fe wr = fe_one();
 #pragma unroll
         for (int r = 0; r < 8; r++) {
+            if (r == 7 && m.derive7) {
+                // the unevaluated coset: b_7 = 0 for a composition of degree < 7n (CrossMap::derive7)
+                acc288 a7 = acc288_zero();
+#pragma unroll
+                for (int j = 0; j < 7; j++) acc288_madd(a7, m.k7[j], d[j]);
+                d[7] = acc288_reduce(a7);
+                break;
+            }
             fe v = m.c[r][kl];
             d[r] = r ? fe_mul(v, wr) : v;
             wr = fe_mul(wr, w);

@@ -997,26 +997,37 @@ int zk::ensure_ext(zk_prover *p) {
 // p->flag is set when the interpolant has a coefficient at or beyond C*n (the degree check).
 // bnd (KX coefficient planes, or nullptr when comp already holds the assertion terms): add the assertion
 // terms' quotient polynomial to column 0 of each plane (boundary_poly_add) before the LDE.
+// nce = 7 (C <= 7): only CE cosets 0..6 were evaluated; the cross-coset step derives coset 7 from the degree
+// bound (CrossMap::derive7).  Same polynomial for a trace that satisfies the AIR; for one that does not, the
+// out-of-domain identity check (check_ood_identity) reports it instead of the top-block flag.
 static int composition_stage(zk_prover *p, Plan *pl, int KX, int C, fe *comp, fe *ctmp, fe *clde, uint8_t root[32],
-                             const AirConsts *bnd = nullptr) {
-    const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b, CE = 8 * n;
+                             const AirConsts *bnd = nullptr, int nce = 8) {
+    const size_t n = (size_t)1 << pl->log_n, CE = 8 * n;
     const int CK = C * KX;
-    ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
+    if (nce != 8 && (nce != 7 || C > 7)) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition: unsupported CE coset count");
+    if (nce == 8) ntt(p->st, pl->Tn, comp, n, ctmp, n, 8 * KX, true, nullptr, nullptr, p->tmp);
+    else
+        for (int j = 0; j < KX; j++) ntt(p->st, pl->Tn, comp + j * CE, n, ctmp + j * CE, n, nce, true, nullptr, nullptr, p->tmp);
     ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
+    const fe w8 = h_root_of_unity(3);
     for (int j = 0; j < KX; j++) {
         CrossMap m;
         for (int r = 0; r < 8; r++) m.c[r] = ctmp + (size_t)(8 * j + r) * n;
         m.k0 = 0;
         m.kcount = n;
         m.pstride = (size_t)KX * n;
-        comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(h_root_of_unity(3)),
-                          h_inv(h_pow(fe_make(3), n)), C, p->cpolys + (size_t)j * n, p->flag);
+        if (nce == 7) {
+            m.derive7 = 1;
+            fe w = w8;
+            for (int r = 0; r < 7; r++, w = fe_mul(w, w8)) m.k7[r] = fe_sub(fe_zero(), w);  // -w_8^(r+1)
+        }
+        comp_cross_mapped(p->st, m, pl->Tce, pl->inv3, h_inv(fe_make(CE)), h_inv(w8), h_inv(h_pow(fe_make(3), n)), C,
+                          p->cpolys + (size_t)j * n, p->flag);
     }
     if (bnd)
         for (int j = 0; j < KX; j++)
             boundary_poly_add(p->st, p->polys, pl->log_n, bnd[j], bnd[0].g_last2, p->dscratch, p->cpolys + (size_t)j * n,
                               p->flag);
-    (void)B;
     return lde_commit(p, pl, p->cpolys, CK, clde, p->cleaves, p->cnodes, root);
 }
 
@@ -1082,25 +1093,33 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     // The assertion terms are not evaluated per row here: S4 adds them in coefficient form (unless the
     // caller dumps the composition values, which must then include them).
     const bool bnd_rows = dump && dump->composition;
+    // CE cosets evaluated: 7 when the composition has at most 7 columns (the stage derives the 8th)
+    static const bool ce7 = [] {
+        const char *e = getenv("ZK_CE7");
+        return !e || atoi(e) != 0;
+    }();
+    const int nce = (ce7 && !bnd_rows && C <= 7) ? 7 : 8;
     AirConsts Kp[2];
     if (KX == 1) {
         draw_air_consts(coin, pub, n, Kp[0], R);
         ZK_TRY(h2d_small(p, p->air_consts, &Kp[0], sizeof Kp[0]));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp, bnd_rows);
+        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp, bnd_rows,
+                         nce);
         HT.stop("air_consts");
     } else {
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
         ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp, bnd_rows);
+        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp, bnd_rows,
+                             nce);
     }
     stage_mark(p, "constraints");
 
     // S4: composition polynomial (interpolate over the CE coset, segment into C columns) + commit.
-    ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root, bnd_rows ? nullptr : Kp));
+    ZK_TRY(composition_stage(p, pl, KX, C, comp, ctmp, clde, R.constraint_root, bnd_rows ? nullptr : Kp, nce));
     unsigned degree_flag = 0;
     ZK_TRY(d2h_small(p, &degree_flag, p->flag, 4));
     ZK_TRY(d2h_flush(p));

@@ -205,12 +205,17 @@ void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap m
 struct CrossMap {
     const fe *c[8];
     size_t k0, kcount, pstride;
+    // derive7: coset 7 was not evaluated (c[7] unused).  A composition polynomial of degree < 7n has a zero
+    // top block, b_7 = sum_r w8^(7r) ... = 0, which fixes d_7 = sum_{r<7} k7[r] d_r with k7[r] = -w_8^(r+1).
+    int derive7 = 0;
+    fe k7[7] = {};
 };
 void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, const PowTable &inv3, fe scale,
                        fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
+// nce: evaluate CE cosets 0 .. nce-1 (8: all; 7: the composition stage derives the last one, bnd = false)
 void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                      const AirConsts *consts_dev, fe *comp, bool bnd = true);
+                      const AirConsts *consts_dev, fe *comp, bool bnd = true, int nce = 8);
 // add the boundary terms' quotient polynomial (one coefficient plane K) into col0 (n coefficients);
 // c = g^(n-2); scratch: deep_poly's layout; sets *flag when an assertion fails
 void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
@@ -277,7 +282,7 @@ void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int
                   fe *tab, fe *partials, fe *out);
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
 void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
-                          const AirConsts *consts2_dev, fe *comp, bool bnd = true);
+                          const AirConsts *consts2_dev, fe *comp, bool bnd = true, int nce = 8);
 // ... over the CE cosets of `map` (see eval_constraints_mapped), b plane at comp + plane
 void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                                  const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp, bool bnd = true);
