@@ -68,7 +68,8 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 //   fold bits 4-7, 8-9 and 10-11 into bits 0-3 instead: their rounds with h <= 16 give every wave one
 //   butterfly index j (lanes spread over lines and groups, stride 4h), which the bits-4-5 fold leaves 4- and
 //   16-way conflicted; this one is conflict-free for those, the other rounds, the load orders and the
-//   stores (host model: tools/lds_bank_model.py).
+//   stores (host model: tools/lds_bank_model.py).  Bits 2-3 are folded into bits 0-1 too, for the fused first round
+//   (ZK_NTT_FUSE: lanes spread over 4 lines x 4 butterflies write one position each, 4-way conflicted without it).
 template <int LOGM, int TILE>
 struct Lds {
     static constexpr int M = 1 << LOGM, LPB = TILE >> LOGM;
@@ -78,7 +79,7 @@ struct Lds {
     static constexpr int R = 4 - LLPB;
     static constexpr int LMASK = (1 << LLPB) - 1;
     __device__ __forceinline__ static int sw(int x) {
-        if constexpr (UNI) return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3) ^ (((x >> 10) & 3) << 2);
+        if constexpr (UNI) return x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3) ^ (((x >> 10) & 3) << 2) ^ ((x >> 2) & 3);
         return SWZ ? x ^ (((x >> 4) & 3) * 5) : x;
     }
     __device__ __forceinline__ static int idx(int line, int pos) {
@@ -169,13 +170,13 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
     __syncthreads();
 }
 
-// rounds LG, LG+2, ... while LG + 1 <= LOGM, then the trailing radix-2 stage of an odd LOGM
-template <int LOGM, int TILE, int LG, bool CT>
+// rounds LG, LG+2, ... while LG + 1 <= STOP, then (STOP = LOGM) the trailing radix-2 stage of an odd LOGM
+template <int LOGM, int TILE, int LG, bool CT, int STOP = LOGM>
 __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
-    if constexpr (LG + 1 <= LOGM) {
+    if constexpr (LG + 1 <= STOP) {
         r4_round<LOGM, TILE, LG, CT>(s, tw4096, ws, w2t);
-        r4_rounds<LOGM, TILE, LG + 2, CT>(s, tw4096, ws, w2t);
-    } else if constexpr (LG == LOGM) {
+        r4_rounds<LOGM, TILE, LG + 2, CT, STOP>(s, tw4096, ws, w2t);
+    } else if constexpr (LG == LOGM && STOP == LOGM) {
         constexpr int M = 1 << LOGM;
         constexpr int half = 1 << (LG - 1);
         using L = Lds<LOGM, TILE>;
@@ -236,6 +237,71 @@ __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws
     } else {
         r4_rounds<LOGM, TILE, 1, false>(s, tw4096, ws, w2t);
     }
+}
+
+// ---- first and last radix-4 rounds fused with the tile's global load and store (ZK_NTT_FUSE, UNI tiles of
+// 1024 threads, one butterfly per thread and round).  The first round's four inputs come straight from memory
+// and the last round's four outputs go straight to memory, so a tile makes 4 LDS round trips and 4 block
+// barriers for its 5 radix-4 rounds instead of 6 and 6, and a wave starts computing as soon as its own loads
+// arrive.  Lanes take the line fastest (q % LPB), as the library's load and store phases do, so every wave
+// access still covers 64-B row segments (LPB = 4) or 1-KiB runs (LPB = 1).
+#ifndef ZK_NTT_FUSE
+#define ZK_NTT_FUSE 1
+#endif
+template <int LOGM, int TILE>
+struct Fuse {
+    static constexpr bool OK = ZK_NTT_FUSE && Lds<LOGM, TILE>::UNI && (LOGM % 2 == 0) && TILE / 4 == NTT_THREADS;
+};
+// First round: thread q takes line q % LPB and the butterfly at bit-reversed positions 4g .. 4g+3 (g = q / LPB),
+// i.e. DFT inputs k0 + {0, M/2, M/4, 3M/4} with k0 = brev(4g), fetched by load(line, k).  Plain: one multiply by
+// w_4 (W set ws[1024]); CT (coset stage table): twiddles ws[1], ws[2], ws[3] as in r4_round<LG = 1, CT>.
+template <int LOGM, int TILE, bool CT, typename Load>
+__device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *ws) {
+    using L = Lds<LOGM, TILE>;
+    constexpr int M = 1 << LOGM, LPB = TILE / M;
+    const int q = threadIdx.x, line = q % LPB, g = q / LPB;
+    const int k0 = (int)(__brev((unsigned)(4 * g)) >> (32 - LOGM));
+    const fe x0 = load(line, k0), x1 = load(line, k0 + M / 2), x2 = load(line, k0 + M / 4), x3 = load(line, k0 + 3 * M / 4);
+    const int p = L::idx(line, 4 * g), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
+    if constexpr (!CT) {
+        const fe_ws W4 = load_fe_ws(ws, 1024);
+        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
+        const fe a3 = fe_mul_uniform(fe_sub(x2, x3), W4);
+        s[p] = fe_add(a0, a2);
+        s[p2] = fe_sub(a0, a2);
+        s[p1] = fe_add(a1, a3);
+        s[p3] = fe_sub(a1, a3);
+    } else {
+        const fe_ws W1 = load_fe_ws(ws, 1);
+        const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
+        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, 2));
+        const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, 3));
+        s[p] = fe_add(a0, u2);
+        s[p2] = fe_sub(a0, u2);
+        s[p1] = fe_add(a1, u3);
+        s[p3] = fe_sub(a1, u3);
+    }
+    __syncthreads();
+}
+// Last round (h = M/4): thread q takes line q % LPB and butterfly index j = q / LPB; its outputs at positions
+// j + {0, h, 2h, 3h} go to store(line, pos, value).  Per-lane two-part twiddles as in r4_round's UNI branch.
+template <int LOGM, int TILE, bool CT, typename Store>
+__device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Store store) {
+    using L = Lds<LOGM, TILE>;
+    constexpr int M = 1 << LOGM, LPB = TILE / M, LG = LOGM - 1, h = M / 4;
+    const int q = threadIdx.x, line = q % LPB, j = q / LPB;
+    const int p = L::idx(line, j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+    const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
+    const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+    const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
+    const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+    const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
+    const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+    store(line, j, fe_add(a0, u2));
+    store(line, j + h, fe_add(a1, u3));
+    store(line, j + 2 * h, fe_sub(a0, u2));
+    store(line, j + 3 * h, fe_sub(a1, u3));
 }
 
 // XCD-aware block order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs
@@ -329,6 +395,24 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     const uint32_t b = lin32 % (uint32_t)batch;
     const fe *in = a.in + (size_t)(b / (uint32_t)a.ncos) * a.in_stride;
     const int r = a.coset_of(b);
+    fe *out = a.out + b * a.out_stride;
+    if constexpr (Fuse<LOGM, TILE>::OK) {
+      // (the plain form only without an input pre-scale and with a pass-twiddle table, as ntt() sets it up)
+      if (CT || (!a.pre_full && !a.pre_lo && a.pass_tw)) {
+        const fe *stage = CT ? a.cos_stage + (size_t)r * 4096 : a.tw4096;
+        const fe_ws *stage_ws = CT ? a.cos_stage_ws + (size_t)r * 4096 : a.tw_ws;
+        const fe_w2 *stage_w2 = CT ? a.cos_stage_w2 + (size_t)r * 4096 : a.tw_w2;
+        first_round_from<LOGM, TILE, CT>(s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); },
+                                         stage_ws);
+        r4_rounds<LOGM, TILE, 3, CT, LOGM - 2>(s, stage, stage_ws, stage_w2);
+        const fe *ptw = CT ? a.cos_pass + (size_t)r * n : a.pass_tw;
+        last_round_to<LOGM, TILE, CT>(s, stage_w2, [&](int line, int j2, fe v) {
+            const size_t o = (k1_0 + line) * M + j2;
+            out[o] = fe_mul(v, ptw[o]);  // inter-pass twiddle w^(j2 k1) (CT: (s_r w_n^j2)^k1), contiguous over the block
+        });
+        return;
+      }
+    }
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
         size_t k = k1_0 + line + n1 * (size_t)k2;
@@ -343,7 +427,6 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
     if constexpr (CT)
         lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096, a.cos_stage_ws + (size_t)r * 4096, a.cos_stage_w2 + (size_t)r * 4096);
     else lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws, a.tw_w2);
-    fe *out = a.out + b * a.out_stride;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e >> LOGM, j2 = e & (M - 1);
         size_t k1 = k1_0 + line;
@@ -372,6 +455,16 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
     const size_t b = blockIdx.y;
     const fe *in = a.in + b * a.in_stride;
+    if constexpr (Fuse<LOGM, TILE>::OK) {
+        fe *out = a.out_of(b);
+        first_round_from<LOGM, TILE, false>(s, [&](int line, int k1) { return in[(size_t)k1 * n2 + j2_0 + line]; }, a.tw_ws);
+        r4_rounds<LOGM, TILE, 3, false, LOGM - 2>(s, a.tw4096, a.tw_ws, a.tw_w2);
+        last_round_to<LOGM, TILE, false>(s, a.tw_w2, [&](int line, int j1, fe v) {
+            if (a.has_post) v = fe_mul(v, a.post);
+            out[n2 * (size_t)j1 + j2_0 + line] = v;
+        });
+        return;
+    }
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k1 = Lds<LOGM, TILE>::load_k(e / LPB);
         fe v = in[(size_t)k1 * n2 + j2_0 + line];
