@@ -121,13 +121,16 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
         const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
-        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        fe a0, a1, a2, a3;
+        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
-        s[p] = fe_add(a0, u2);
-        s[p2h] = fe_sub(a0, u2);
-        s[ph] = fe_add(a1, u3);
-        s[p3h] = fe_sub(a1, u3);
+        fe o0, o1, o2, o3;
+        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2h] = o2;
+        s[ph] = o1;
+        s[p3h] = o3;
         __syncthreads();
         return;
     }
@@ -140,13 +143,16 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
         const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
-        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        fe a0, a1, a2, a3;
+        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
         const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
-        s[p] = fe_add(a0, u2);
-        s[p2h] = fe_sub(a0, u2);
-        s[ph] = fe_add(a1, u3);
-        s[p3h] = fe_sub(a1, u3);
+        fe o0, o1, o2, o3;
+        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2h] = o2;
+        s[ph] = o1;
+        s[p3h] = o3;
         __syncthreads();
         return;
     }
@@ -160,12 +166,15 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const fe w3 = CT ? tw4096[3 * h + j] : tw4096[(j + h) << (11 - LG)];
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
         const fe t1 = fe_mul(x1, w1), t3 = fe_mul(x3, w1);
-        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        fe a0, a1, a2, a3;
+        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul(a2, w2), u3 = fe_mul(a3, w3);
-        s[p] = fe_add(a0, u2);
-        s[p2h] = fe_sub(a0, u2);
-        s[ph] = fe_add(a1, u3);
-        s[p3h] = fe_sub(a1, u3);
+        fe o0, o1, o2, o3;
+        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2h] = o2;
+        s[ph] = o1;
+        s[p3h] = o3;
     }
     __syncthreads();
 }
@@ -223,14 +232,16 @@ __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws
             const int line = q >> (LOGM - 2), local = q & (M / 4 - 1);
             const int p = L::idx(line, local * 4), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
             const fe x0 = s[p], x1 = s[p1], x2 = s[p2], x3 = s[p3];
-            const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
-            fe a3;
-            if constexpr (L::UNI) a3 = fe_mul_uniform(fe_sub(x2, x3), W4);
-            else a3 = fe_mul(fe_sub(x2, x3), w4);
-            s[p] = fe_add(a0, a2);
-            s[p2] = fe_sub(a0, a2);
-            s[p1] = fe_add(a1, a3);
-            s[p3] = fe_sub(a1, a3);
+            fe a0, a1, a2, d23, a3;
+            fe_addsub2(x0, x1, x2, x3, a0, a1, a2, d23);
+            if constexpr (L::UNI) a3 = fe_mul_uniform(d23, W4);
+            else a3 = fe_mul(d23, w4);
+            fe o0, o1, o2, o3;
+            fe_addsub2(a0, a2, a1, a3, o0, o2, o1, o3);
+            s[p] = o0;
+            s[p2] = o2;
+            s[p1] = o1;
+            s[p3] = o3;
         }
         __syncthreads();
         r4_rounds<LOGM, TILE, 3, false>(s, tw4096, ws, w2t);
@@ -265,22 +276,28 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
     const int p = L::idx(line, 4 * g), p1 = L::at(p, 1), p2 = L::at(p, 2), p3 = L::at(p, 3);
     if constexpr (!CT) {
         const fe_ws W4 = load_fe_ws(ws, 1024);
-        const fe a0 = fe_add(x0, x1), a1 = fe_sub(x0, x1), a2 = fe_add(x2, x3);
-        const fe a3 = fe_mul_uniform(fe_sub(x2, x3), W4);
-        s[p] = fe_add(a0, a2);
-        s[p2] = fe_sub(a0, a2);
-        s[p1] = fe_add(a1, a3);
-        s[p3] = fe_sub(a1, a3);
+        fe a0, a1, a2, d23;
+        fe_addsub2(x0, x1, x2, x3, a0, a1, a2, d23);
+        const fe a3 = fe_mul_uniform(d23, W4);
+        fe o0, o1, o2, o3;
+        fe_addsub2(a0, a2, a1, a3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2] = o2;
+        s[p1] = o1;
+        s[p3] = o3;
     } else {
         const fe_ws W1 = load_fe_ws(ws, 1);
         const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
-        const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+        fe a0, a1, a2, a3;
+        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, 2));
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, 3));
-        s[p] = fe_add(a0, u2);
-        s[p2] = fe_sub(a0, u2);
-        s[p1] = fe_add(a1, u3);
-        s[p3] = fe_sub(a1, u3);
+        fe o0, o1, o2, o3;
+        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2] = o2;
+        s[p1] = o1;
+        s[p3] = o3;
     }
     __syncthreads();
 }
@@ -295,13 +312,16 @@ __device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Sto
     const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
     const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
     const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
-    const fe a0 = fe_add(x0, t1), a1 = fe_sub(x0, t1), a2 = fe_add(x2, t3), a3 = fe_sub(x2, t3);
+    fe a0, a1, a2, a3;
+        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
     const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
     const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
-    store(line, j, fe_add(a0, u2));
-    store(line, j + h, fe_add(a1, u3));
-    store(line, j + 2 * h, fe_sub(a0, u2));
-    store(line, j + 3 * h, fe_sub(a1, u3));
+    fe o0, o1, o2, o3;
+    fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+    store(line, j, o0);
+    store(line, j + h, o1);
+    store(line, j + 2 * h, o2);
+    store(line, j + 3 * h, o3);
 }
 
 // XCD-aware block order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs
@@ -791,18 +811,30 @@ void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_
     merkle_tree(st, leaves, N, nodes);
 }
 
-__global__ void __launch_bounds__(256) k_hash_fri_rows(const fe *layer, size_t L, int fold, uint8_t *leaves) {
+// FRI layer element i (natural index) of a layer stored natural (FriLayout::lb = 0) or coset-major over
+// 2^lb cosets of 2^lcn points (layer 0 is the DEEP LDE as the coset NTT writes it: no reordering pass)
+__device__ __forceinline__ size_t fri_at(FriLayout f, size_t i) {
+    return ((i & (((size_t)1 << f.lb) - 1)) << f.lcn) + (i >> f.lb);
+}
+FriLayout fri_layout(size_t L, int lb) {
+    int lg = 0;
+    while (((size_t)1 << lg) < L) lg++;
+    return FriLayout{lb, lg - lb};
+}
+
+__global__ void __launch_bounds__(256) k_hash_fri_rows(const fe *layer, size_t L, int fold, FriLayout f, uint8_t *leaves) {
     const size_t rows = L / fold;
     for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
         uint32_t h[8];
-        b3::hash_elements(fold, [&](int k) { return layer[r + (size_t)k * rows]; }, h);
+        b3::hash_elements(fold, [&](int k) { return layer[fri_at(f, r + (size_t)k * rows)]; }, h);
         store_digest(leaves + 32 * r, h);
     }
 }
 
-void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes) {
+void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes, int lb) {
     const size_t rows = L / fold;
-    ZK_PROF(st, "hash_fri_rows", 16.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, leaves));
+    const FriLayout f = fri_layout(L, lb);
+    ZK_PROF(st, "hash_fri_rows", 16.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, f, leaves));
     merkle_tree(st, leaves, rows, nodes);
 }
 
@@ -1921,6 +1953,7 @@ void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, co
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
     const fe *Dk = deep_poly(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
     lde_cosets(st, Tn, CT, Dk, n, 0, 1, (int)B, ulde, ntt_tmp);
+    if (!out) return;  // FRI layer 0 is read coset-major from ulde
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     ZK_PROF(st, "deep", 32.0 * N, hipLaunchKernelGGL(k_coset_to_natural, dim3(pb2), dim3(256), 0, st, ulde, log_n, log_b, out));
@@ -2060,6 +2093,7 @@ void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b, N = n << log_b;
     const fe *Dk = deep_poly_ext(st, tpolys, cpolys, ccols, log_n, deep_consts_dev, z, zg, scratch);
     for (int plane = 0; plane < 2; plane++) lde_cosets(st, Tn, CT, Dk + plane * n, n, 0, 1, (int)B, ulde + plane * N, ntt_tmp);
+    if (!out) return;
     unsigned pb2 = cdiv(N, 256);
     if (pb2 > 65536) pb2 = 65536;
     for (int plane = 0; plane < 2; plane++)
@@ -2141,12 +2175,12 @@ __device__ __forceinline__ void idft_small(fe v[F], const fe *zinv) {
 // sum_m V_m (alpha / x_r)^m / F, with x_r = offset * w_L^r.
 template <int F>
 __global__ void __launch_bounds__(256) k_fri_fold(const fe *layer, size_t L, const FoldConsts *Fc, const fe *wi_lo,
-                                                  const fe *wi_hi, size_t wstride, fe *next) {
+                                                  const fe *wi_hi, size_t wstride, FriLayout f, fe *next) {
     const size_t rows = L / F;
     for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
         fe v[F];
 #pragma unroll
-        for (int k = 0; k < F; k++) v[k] = layer[r + (size_t)k * rows];
+        for (int k = 0; k < F; k++) v[k] = layer[fri_at(f, r + (size_t)k * rows)];
         // beta = alpha / x_r, 1/x_r = offset^-1 * w_L^-r = offset^-1 * w_N^(-r*wstride)
         const fe beta = fe_mul(Fc->alpha, fe_mul(Fc->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
         idft_small<F>(v, Fc->zinv);
@@ -2158,11 +2192,12 @@ __global__ void __launch_bounds__(256) k_fri_fold(const fe *layer, size_t L, con
 }
 
 void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
-                     const NttTables &TN, size_t wstride, fe *next) {
+                     const NttTables &TN, size_t wstride, fe *next, int lb) {
     unsigned blocks = cdiv(L / fold, 256);
     if (blocks > 65536) blocks = 65536;
     const FoldConsts *F = (const FoldConsts *)fold_consts_dev;
-#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold", 16.0 * L + 16.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, next))
+    const FriLayout fl = fri_layout(L, lb);
+#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold", 16.0 * L + 16.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, fl, next))
     switch (fold) {
         case 2: ZK_FOLD(2); break;
         case 4: ZK_FOLD(4); break;
@@ -2320,18 +2355,19 @@ void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int
 }
 
 // FRI row r over E: [e(r + k rows)]_k, each value hashed as (a, b)
-__global__ void __launch_bounds__(256) k_hash_fri_rows_ext(const fe *layer, size_t L, int fold, uint8_t *leaves) {
+__global__ void __launch_bounds__(256) k_hash_fri_rows_ext(const fe *layer, size_t L, int fold, FriLayout f, uint8_t *leaves) {
     const size_t rows = L / fold;
     for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
         uint32_t h[8];
-        b3::hash_elements(2 * fold, [&](int t) { return layer[(size_t)(t & 1) * L + r + (size_t)(t >> 1) * rows]; }, h);
+        b3::hash_elements(2 * fold, [&](int t) { return layer[(size_t)(t & 1) * L + fri_at(f, r + (size_t)(t >> 1) * rows)]; }, h);
         store_digest(leaves + 32 * r, h);
     }
 }
 
-void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes) {
+void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes, int lb) {
     const size_t rows = L / fold;
-    ZK_PROF(st, "hash_fri_rows_ext", 32.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows_ext, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, leaves));
+    const FriLayout f = fri_layout(L, lb);
+    ZK_PROF(st, "hash_fri_rows_ext", 32.0 * L + 32.0 * rows, hipLaunchKernelGGL(k_hash_fri_rows_ext, dim3(cdiv(rows, 256)), dim3(256), 0, st, layer, L, fold, f, leaves));
     merkle_tree(st, leaves, rows, nodes);
 }
 
@@ -2339,14 +2375,15 @@ void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, u
 // resulting E coefficients are evaluated at beta = alpha / x_r by an E Horner.
 template <int F>
 __global__ void __launch_bounds__(256) k_fri_fold_ext(const fe *layer, size_t L, const FoldConstsE *Fc, const fe *wi_lo,
-                                                      const fe *wi_hi, size_t wstride, fe *next) {
+                                                      const fe *wi_hi, size_t wstride, FriLayout f, fe *next) {
     const size_t rows = L / F;
     for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x) {
         fe va[F], vb[F];
 #pragma unroll
         for (int k = 0; k < F; k++) {
-            va[k] = layer[r + (size_t)k * rows];
-            vb[k] = layer[L + r + (size_t)k * rows];
+            const size_t at = fri_at(f, r + (size_t)k * rows);
+            va[k] = layer[at];
+            vb[k] = layer[L + at];
         }
         const fe2 beta = fe2_mulb(Fc->alpha, fe_mul(Fc->inv_offset, pow_split(wi_lo, wi_hi, r * wstride)));
         idft_small<F>(va, Fc->zinv);
@@ -2361,11 +2398,12 @@ __global__ void __launch_bounds__(256) k_fri_fold_ext(const fe *layer, size_t L,
 }
 
 void fri_fold_ext_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
-                         const NttTables &TN, size_t wstride, fe *next) {
+                         const NttTables &TN, size_t wstride, fe *next, int lb) {
     unsigned blocks = cdiv(L / fold, 256);
     if (blocks > 65536) blocks = 65536;
     const FoldConstsE *F = (const FoldConstsE *)fold_consts_dev;
-#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold_ext", 32.0 * L + 32.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold_ext<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, next))
+    const FriLayout fl = fri_layout(L, lb);
+#define ZK_FOLD(FF) ZK_PROF(st, "fri_fold_ext", 32.0 * L + 32.0 * (L / fold), hipLaunchKernelGGL((k_fri_fold_ext<FF>), dim3(blocks), dim3(256), 0, st, layer, L, F, TN.inv_lo, TN.inv_hi, wstride, fl, next))
     switch (fold) {
         case 2: ZK_FOLD(2); break;
         case 4: ZK_FOLD(4); break;

@@ -1127,6 +1127,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     HT.start();
     coin.reseed(R.constraint_root);
 
+    // FRI layer 0 is the DEEP LDE, coset-major as the coset NTT wrote it (FriLayout lb0 = log_b), unless it is
+    // already the remainder (no fold layers), which the host reads in natural order
+    const int nl = fri_num_layers(N, opt);
+    const int lb0 = nl > 0 ? log_b : 0;
     // S5: OOD frame [P7], DEEP coefficients [P8] and evaluations.  h holds the frame flattened
     // (k base elements per E value): [T(z)]_W ++ [T(zg)]_W ++ [H(z)]_C.
     std::vector<fe> h((2 * W + C) * KX);
@@ -1143,7 +1147,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
         ZK_TRY(h2d_small(p, p->deep_consts, &D, sizeof D));
         deep_coeff_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->deep_consts, z, zg, pl->ct,
-                          p->dscratch, p->ulde, p->tmp, deep);
+                          p->dscratch, p->ulde, p->tmp, lb0 ? nullptr : deep);
         HT.stop("deep_consts");
         // while the GPU runs DEEP: the verifier's out-of-domain identity on the frame just read
         std::vector<fe2> e(2 * W + C);
@@ -1163,13 +1167,12 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
         ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
         deep_coeff_ext_launch(p->st, pl->Tn, p->polys, p->cpolys, C, log_n, log_b, p->x_deep_consts, z, zg,
-                              pl->ct, p->x_dscratch, p->x_ulde, p->tmp, deep);
+                              pl->ct, p->x_dscratch, p->x_ulde, p->tmp, lb0 ? nullptr : deep);
         ZK_TRY(check_ood_identity(e, C, Kp, 2, z, n, pub));
     }
     stage_mark(p, "deep");
 
     // S6: FRI [P9, P10]; E layers are planar (k planes of L values)
-    const int nl = fri_num_layers(N, opt);
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
     {
@@ -1181,7 +1184,8 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
     std::vector<fe> rem_flat;
-    layer_vals[0] = deep;
+    const fe *deep0 = lb0 ? (KX == 2 ? p->x_ulde : p->ulde) : deep;
+    layer_vals[0] = deep0;
     layer_len[0] = N;
     {
         // The layer coins run on the device (fri_coin_launch): no host round trip per layer.  The
@@ -1204,11 +1208,12 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
             layer_leaves[l] = dig;
             layer_nodes[l] = dig + 32 * rows;
             dig += 64 * rows;
-            if (KX == 1) commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-            else commit_fri_layer_ext(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+            const int lb = l ? 0 : lb0;
+            if (KX == 1) commit_fri_layer(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
+            else commit_fri_layer_ext(p->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
             fri_coin_launch(p->st, (uint32_t *)p->fri_seed, layer_nodes[l] + 32, KX, alpha_dev, p->fri_alphas + 2 * l);
-            if (KX == 1) fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next);
-            else fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next);
+            if (KX == 1) fri_fold_launch(p->st, layer_vals[l], L, (int)fold, p->fold_consts, pl->TN, N / L, next, lb);
+            else fri_fold_ext_launch(p->st, layer_vals[l], L, (int)fold, p->x_fold_consts, pl->TN, N / L, next, lb);
             layer_vals[l + 1] = next;
             layer_len[l + 1] = rows;
             next += KX * rows;
@@ -1272,7 +1277,10 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         const size_t rows = layer_len[l] / fold;
         for (uint64_t r : fri_pos[l])
             for (uint32_t k = 0; k < fold; k++)
-                for (int j = 0; j < KX; j++) fe_at(layer_vals[l], j * layer_len[l] + r + k * rows);
+                for (int j = 0; j < KX; j++) {
+                    const uint64_t i = r + k * rows;  // natural index in layer l
+                    fe_at(layer_vals[l], j * layer_len[l] + ((l || !lb0) ? i : ((i & (B - 1)) << log_n) + (i >> log_b)));
+                }
     }
     const size_t off_dig = na;
     for (int b = 0; b < 2 + nl; b++) {
@@ -1328,7 +1336,11 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         if (dump->composition) coset_major_rows_to_host(p, comp, 1, n, 8, dump->composition);
         if (dump->comp_polys) ZK_CHECK_HIP(hipMemcpy(dump->comp_polys, p->cpolys, (size_t)CK * n * 16, hipMemcpyDeviceToHost));
         if (dump->comp_lde) coset_major_rows_to_host(p, clde, CK, n, B, dump->comp_lde);
-        if (dump->deep) ZK_CHECK_HIP(hipMemcpy(dump->deep, deep, N * 16, hipMemcpyDeviceToHost));
+        if (dump->deep) {
+            if (lb0) coset_major_to_natural(p->st, deep0, log_n, log_b, deep);
+            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+            ZK_CHECK_HIP(hipMemcpy(dump->deep, deep, N * 16, hipMemcpyDeviceToHost));
+        }
         if (dump->fri_layer1 && nl > 0)
             ZK_CHECK_HIP(hipMemcpy(dump->fri_layer1, layer_vals[1], layer_len[1] * 16, hipMemcpyDeviceToHost));
     }

@@ -140,8 +140,14 @@ void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int 
                       uint8_t *leaves);
 void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
                              uint8_t *nodes);
-// FRI layer leaves: row r of a natural-order layer of size L (rows = L/fold): [e[r + k*L/fold]]
-void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes);
+// Storage of a FRI layer of L values: natural order (lb = 0), or coset-major over 2^lb cosets of 2^lcn
+// points (natural index i at (i mod 2^lb) 2^lcn + i / 2^lb): layer 0 as the DEEP coset LDE leaves it
+struct FriLayout {
+    int lb, lcn;
+};
+FriLayout fri_layout(size_t L, int lb);
+// FRI layer leaves: row r of a layer of size L (rows = L/fold): [e[r + k*L/fold]]
+void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes, int lb = 0);
 // nodes[1..nl) of a binary Merkle tree over nl leaves (nodes[nl/2..nl) = merges of leaf pairs)
 void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *nodes);
 // out[k] = src[idx[k]] for 32-byte digests
@@ -249,8 +255,8 @@ const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccol
 const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
                         const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch);
 // DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
-// by suffix sums over the combined coefficients, one LDE over the B cosets (CosetTables), natural-order
-// output.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
+// by suffix sums over the combined coefficients, one LDE over the B cosets (CosetTables) into ulde
+// (coset-major), and (out != nullptr) a natural-order copy in out.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
 // elements; ulde: B*n; ntt_tmp: 8n.
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
                        int log_b, const void *deep_consts_dev, fe z, fe zg, const CosetTables &CT, fe *scratch,
@@ -266,7 +272,7 @@ struct FoldConsts {
     fe alpha, inv_offset, inv_fold;
 };
 void fri_fold_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
-                     const NttTables &TN, size_t wstride, fe *next);
+                     const NttTables &TN, size_t wstride, fe *next, int lb = 0);
 void coset_major_to_natural(hipStream_t st, const fe *src, int log_n, int log_b, fe *dst);
 // FRI commit-phase coin on the device: seed = merge(seed, root_dev), alpha (k = 1 or 2 components) drawn
 // into alpha_dev (where the fold reads it) and alpha_log (the per-layer record the host replay is checked
@@ -301,9 +307,9 @@ struct FoldConstsE {
     fe inv_offset, inv_fold;
 };
 // layer planar (2L), next planar (2 L/fold); leaves hash rows of fold E values (a, b per value)
-void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes);
+void commit_fri_layer_ext(hipStream_t st, const fe *layer, size_t L, int fold, uint8_t *leaves, uint8_t *nodes, int lb = 0);
 void fri_fold_ext_launch(hipStream_t st, const fe *layer, size_t L, int fold, const void *fold_consts_dev,
-                         const NttTables &TN, size_t wstride, fe *next);
+                         const NttTables &TN, size_t wstride, fe *next, int lb = 0);
 // out[k] = src[idx[k]] for field elements
 void gather_fe(hipStream_t st, const fe *src, const uint64_t *idx, size_t k, fe *out);
 
