@@ -1126,10 +1126,59 @@ __device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
     return fe_sub(acc160_reduce(pos), acc160_reduce(neg));
 }
 
+// Rescue inverse MDS through its adjugate (crypto/src/rescue.rs:197-233): INV_MDS = adj(MDS) / det with
+// det = 3^24 and |adj| < 2^39 (every row signed + - + -; tests/test_oracle_core.py checks adj, det and the
+// reference INV_MDS).  adj_row(r, y) = 3^24 (INV_MDS y)_r: four 128 x 39-bit products (8 MADs each) into a
+// 192-bit accumulator and one reduction, instead of four full 128 x 128-bit products.
+#ifndef ZK_EVAL_ADJ
+#define ZK_EVAL_ADJ 1
+#endif
+// s[0..6) += x * c, c < 2^40 (s stays below 2^192)
+__device__ __forceinline__ void acc192_madd(uint32_t s[6], fe x, uint64_t c) {
+    const uint32_t xs[4] = {lo32(x.lo), hi32(x.lo), lo32(x.hi), hi32(x.hi)};
+    const uint32_t c0 = lo32(c), c1 = hi32(c);
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        t = (uint64_t)xs[k] * c0 + s[k] + (t >> 32);
+        s[k] = lo32(t);
+    }
+    t = (uint64_t)s[4] + (t >> 32);
+    s[4] = lo32(t);
+    s[5] += hi32(t);
+    t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        t = (uint64_t)xs[k] * c1 + s[k + 1] + (t >> 32);
+        s[k + 1] = lo32(t);
+    }
+    s[5] += hi32(t);
+}
+__device__ __forceinline__ fe adj_row(int r, const fe y[4]) {
+    constexpr uint64_t A[16] = {491992666011ull, 234927627480ull, 26031357990ull, 666860040ull,
+                                486140969160ull, 228216177189ull, 25147788120ull, 643043610ull,
+                                468778791690ull, 208346129640ull, 22570830711ull, 573956280ull,
+                                418414128120ull, 151093990710ull, 15496819560ull, 387420489ull};
+    // pos starts at p 2^41 (> any sum of the negative terms), so pos - neg >= 0; both stay below 2^170
+    uint32_t pos[6] = {0x0u, 0x200u, 0xffa60000u, 0xffffffffu, 0xffffffffu, 0x1ffu}, neg[6] = {0, 0, 0, 0, 0, 0};
+    acc192_madd(pos, y[0], A[4 * r + 0]);
+    acc192_madd(neg, y[1], A[4 * r + 1]);
+    acc192_madd(pos, y[2], A[4 * r + 2]);
+    acc192_madd(neg, y[3], A[4 * r + 3]);
+    uint32_t d[6], b;
+    d[0] = __builtin_subc(pos[0], neg[0], 0u, &b);
+#pragma unroll
+    for (int k = 1; k < 6; k++) d[k] = __builtin_subc(pos[k], neg[k], b, &b);
+    return reduce_fold(d[0], d[1], d[2], d[3], d[4], d[5], 0u, 0u);
+}
+// 3^-72 mod p: the adjugate path's cubes carry 3^72, folded into the coefficients (ct3 = ct 3^-72)
+static constexpr fe ZK_INV3_72 = fe{0x8092deb1ab776293ull, 0xf0185d00eca40a3bull};
+
 // Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
 // SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
 struct EvalShared {
     fe ct[20], cb[22], ct2[20], cb2[22], inv_mds[16];
+    fe ct3[4], nct[4], ct3b[4], nctb[4];  // constraints 12..15: ct 3^-72 and -ct (planes a, b)
     fe delta, bnd1, bnd1b;
 };
 
@@ -1161,6 +1210,13 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         else if (t == 43) S.bnd1b = KE == 2 ? K2->bnd1 : fe_zero();
         else if (t == 44) S.delta = K->delta;
         else if (t >= 64 && t < 80) S.inv_mds[t - 64] = c_inv_mds[t - 64];
+        else if (t >= 80 && t < 84) {
+            S.ct3[t - 80] = fe_mul(K->coeff_t[12 + t - 80], ZK_INV3_72);
+            S.nct[t - 80] = fe_neg(K->coeff_t[12 + t - 80]);
+        } else if (KE == 2 && t >= 84 && t < 88) {
+            S.ct3b[t - 84] = fe_mul(K2->coeff_t[12 + t - 84], ZK_INV3_72);
+            S.nctb[t - 84] = fe_neg(K2->coeff_t[12 + t - 84]);
+        }
         else if (KE == 2 && t >= 128 && t < 148) S.ct2[t - 128] = K2->coeff_t[t - 128];
         else if (KE == 2 && t >= 148 && t < 170) S.cb2[t - 148] = K2->coeff_b[t - 148];
         __syncthreads();
@@ -1227,17 +1283,34 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         // 12..15 share the factor fh and 16..19 the factor nfh: sum the coefficient-weighted values first,
         // multiply by the flag once (ct_k (v_k f) summed = f (sum ct_k v_k): 6 multiplies fewer per row)
         fe sR = fe_zero(), sR2 = fe_zero();
+        if (ZK_EVAL_ADJ) {
+            // ct_r ((INV_MDS y)_r^3 - m0_r) = ct3_r (adj_r y)^3 + (-ct_r) m0_r, summed lazily
+            acc288 aR = acc288_zero(), aR2 = acc288_zero();
 #pragma unroll
-        for (int r2 = 0; r2 < 4; r2++) {
-            acc288 am = acc288_zero();
+            for (int r2 = 0; r2 < 4; r2++) {
+                const fe v3 = cube(adj_row(r2, y));
+                acc288_madd(aR, S.ct3[r2], v3);
+                acc288_madd(aR, S.nct[r2], m0[r2]);
+                if (KE == 2) {
+                    acc288_madd(aR2, S.ct3b[r2], v3);
+                    acc288_madd(aR2, S.nctb[r2], m0[r2]);
+                }
+            }
+            sR = acc288_reduce(aR);
+            if (KE == 2) sR2 = acc288_reduce(aR2);
+        } else {
 #pragma unroll
-            for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
-            const fe acc = acc288_reduce(am);
-            const fe v = fe_sub(cube(acc), m0[r2]);
-            sR = fe_add(sR, fe_mul(S.ct[12 + r2], v));
-            if (KE == 2) {
-                sR2 = fe_add(sR2, fe_mul(S.ct2[12 + r2], v));
-                asm volatile("" : "+v"(sR2.lo), "+v"(sR2.hi));
+            for (int r2 = 0; r2 < 4; r2++) {
+                acc288 am = acc288_zero();
+#pragma unroll
+                for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
+                const fe acc = acc288_reduce(am);
+                const fe v = fe_sub(cube(acc), m0[r2]);
+                sR = fe_add(sR, fe_mul(S.ct[12 + r2], v));
+                if (KE == 2) {
+                    sR2 = fe_add(sR2, fe_mul(S.ct2[12 + r2], v));
+                    asm volatile("" : "+v"(sR2.lo), "+v"(sR2.hi));
+                }
             }
         }
         t = fe_add(t, fe_mul(sR, fh));
