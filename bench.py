@@ -166,8 +166,8 @@ def pmc_traffic(kernel: str, config5: bool = False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--cpu-log-n", type=int, default=18)  # ~20 s of single-core oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -213,7 +213,9 @@ def main():
     fns = [prover_step(k) for k in range(P)]
     for f in fns:  # every prover's first proof builds its per-size tables
         f()
-    run_proofs(fns, max(0, args.warmup - P))
+    # warm-up: W proofs, at least three per prover (the first proofs after the tables pay page faults
+    # and clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms, tools/proof_times.py)
+    run_proofs(fns, max(args.warmup, 3 * P) - P)
     barrier(pg, local)
     t0 = time.perf_counter()
     run_proofs(fns, args.steps)
