@@ -63,6 +63,38 @@ ZK_HD fe fe_sub(fe a, fe b) {
 
 ZK_HD fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
 
+// ---- lazy (partially reduced) forms for the NTT butterflies: values < 2^128, congruent mod p, not
+// necessarily canonical.  Contract: the FIRST operand may be any value < 2^128, the SECOND must be
+// canonical (< p) -- in a radix-4 butterfly the second operands are multiply outputs, which are canonical.
+//   fe_add_lazy: s = a + b < 2^128 + p; on carry s - 2^128 + C = s - p < 2^128 (one fold, no compare with p).
+//   fe_sub (above) already satisfies it: no borrow gives a - b < 2^128; a borrow means a < b < p, and
+//   a - b + p lies in (0, p).
+// A lazy value goes to memory only through fe_canon or a multiply (whose output is canonical).
+ZK_HD fe fe_add_lazy(fe a, fe b) {
+    uint32_t c, d;
+    const uint32_t s0 = __builtin_addc(lo32(a.lo), lo32(b.lo), 0u, &c);
+    const uint32_t s1 = __builtin_addc(hi32(a.lo), hi32(b.lo), c, &c);
+    const uint32_t s2 = __builtin_addc(lo32(a.hi), lo32(b.hi), c, &c);
+    const uint32_t s3 = __builtin_addc(hi32(a.hi), hi32(b.hi), c, &c);
+    const uint32_t m = 0u - (c & 1u);  // C = 0x2cff_ffffffff on carry
+    const uint32_t t0 = __builtin_addc(s0, m, 0u, &d);
+    const uint32_t t1 = __builtin_addc(s1, m & 0x2cffu, d, &d);
+    const uint32_t t2 = __builtin_addc(s2, 0u, d, &d);
+    const uint32_t t3 = s3 + d;
+    return fe{join32(t0, t1), join32(t2, t3)};
+}
+// the canonical representative of a value < 2^128: v >= p  <=>  carry(v + C), and then v - p = v + C mod 2^128
+ZK_HD fe fe_canon(fe v) {
+    uint32_t d;
+    const uint32_t t0 = __builtin_addc(lo32(v.lo), 0xffffffffu, 0u, &d);
+    const uint32_t t1 = __builtin_addc(hi32(v.lo), 0x2cffu, d, &d);
+    const uint32_t t2 = __builtin_addc(lo32(v.hi), 0u, d, &d);
+    const uint32_t t3 = __builtin_addc(hi32(v.hi), 0u, d, &d);
+    const uint32_t m = 0u - (d & 1u);
+    return fe{join32((t0 & m) | (lo32(v.lo) & ~m), (t1 & m) | (hi32(v.lo) & ~m)),
+              join32((t2 & m) | (lo32(v.hi) & ~m), (t3 & m) | (hi32(v.hi) & ~m))};
+}
+
 // r[0..8) = x[0..4) * y[0..4) (operand scanning; each step fits one v_mad_u64_u32 + carry add)
 ZK_HD void mul_4x4(const uint32_t x[4], const uint32_t y[4], uint32_t r[8]) {
     uint64_t t;
@@ -454,6 +486,18 @@ __device__ __forceinline__ void fe_addsub2(fe a, fe b, fe c, fe d, fe &apb, fe &
     cpd = fe_add(c, d);
     cmd = fe_sub(c, d);
 #endif
+}
+// the same with lazy sums (fe_add_lazy's contract: a, c any value < 2^128; b, d canonical)
+template <bool LZ>
+__device__ __forceinline__ void addsub2(fe a, fe b, fe c, fe d, fe &apb, fe &amb, fe &cpd, fe &cmd) {
+    if constexpr (LZ) {
+        apb = fe_add_lazy(a, b);
+        amb = fe_sub(a, b);
+        cpd = fe_add_lazy(c, d);
+        cmd = fe_sub(c, d);
+    } else {
+        fe_addsub2(a, b, c, d, apb, amb, cpd, cmd);
+    }
 }
 
 // the W set tab[idx] for a wave-uniform idx, through scalar loads

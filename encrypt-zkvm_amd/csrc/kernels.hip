@@ -52,6 +52,15 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 #endif
 constexpr int NTT_THREADS = ZK_NTT_THREADS;
 
+#ifndef ZK_NTT_LAZY
+#define ZK_NTT_LAZY 1  // fused UNI pass-1 rounds keep butterfly sums partially reduced (fe_add_lazy); the pass
+#endif                 // twiddle multiply makes the stored values canonical (A/B: pass 1 -0.09 ms per proof)
+#ifndef ZK_NTT_LAZY2
+#define ZK_NTT_LAZY2 0  // the same in pass 2, with fe_canon at the store: +0.1 ms per proof (A/B), off
+#endif
+#ifndef ZK_NTT_J0
+#define ZK_NTT_J0 1  // plain-DFT wave-uniform rounds: the waves with j = 0 skip their three unit-twiddle multiplies
+#endif
 #ifndef ZK_NTT_SWZ
 #define ZK_NTT_SWZ 1  // XOR-swizzled LDS tiles (0: one pad element per line)
 #endif
@@ -105,7 +114,7 @@ struct Lds {
 // UNI tiles, rounds with h <= 16: wave w takes butterfly index j = w / (16/h) for 1024/h (line, group)
 // pairs, so its three twiddles are wave-uniform and multiply through their W sets (fe_mul_uniform, scalar
 // loads from `ws`, the W-set table indexed exactly like `tw4096`).  Same butterflies, same values.
-template <int LOGM, int TILE, int LG, bool CT>
+template <int LOGM, int TILE, int LG, bool CT, bool LZ = false>
 __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
     constexpr int M = 1 << LOGM;
     constexpr int Q = TILE / 4;
@@ -118,15 +127,22 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const int pidx = ((w & ((16 >> LH) - 1)) << 6) | l;  // < 1024 / h: (line, group) pairs
         const int line = pidx >> (LOGM - 2 - LH), grp = pidx & ((M >> (2 + LH)) - 1);
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
-        const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-        const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
+        // plain DFT, j = 0 (wave-uniform): w_2h^0 = w_4h^0 = 1, only w_4h^h = w_4 remains
+        const bool triv = !CT && ZK_NTT_J0 && j == 0;
+        fe t1 = x1, t3 = x3;
+        if (!triv) {
+            const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
+            t1 = fe_mul_uniform(x1, W1);
+            t3 = fe_mul_uniform(x3, W1);
+        }
         fe a0, a1, a2, a3;
-        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
-        const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
+        fe u2 = a2;
+        if (!triv) u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
         fe o0, o1, o2, o3;
-        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
         s[p2h] = o2;
         s[ph] = o1;
@@ -144,11 +160,11 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
         const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
         fe a0, a1, a2, a3;
-        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
         const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
         fe o0, o1, o2, o3;
-        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
         s[p2h] = o2;
         s[ph] = o1;
@@ -180,12 +196,13 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
 }
 
 // rounds LG, LG+2, ... while LG + 1 <= STOP, then (STOP = LOGM) the trailing radix-2 stage of an odd LOGM
-template <int LOGM, int TILE, int LG, bool CT, int STOP = LOGM>
+template <int LOGM, int TILE, int LG, bool CT, int STOP = LOGM, bool LZ = false>
 __device__ __forceinline__ void r4_rounds(fe *s, const fe *tw4096, const fe_ws *ws, const fe_w2 *w2t) {
     if constexpr (LG + 1 <= STOP) {
-        r4_round<LOGM, TILE, LG, CT>(s, tw4096, ws, w2t);
-        r4_rounds<LOGM, TILE, LG + 2, CT, STOP>(s, tw4096, ws, w2t);
+        r4_round<LOGM, TILE, LG, CT, LZ>(s, tw4096, ws, w2t);
+        r4_rounds<LOGM, TILE, LG + 2, CT, STOP, LZ>(s, tw4096, ws, w2t);
     } else if constexpr (LG == LOGM && STOP == LOGM) {
+        static_assert(!LZ, "lazy sums only in the fused UNI rounds");
         constexpr int M = 1 << LOGM;
         constexpr int half = 1 << (LG - 1);
         using L = Lds<LOGM, TILE>;
@@ -266,7 +283,7 @@ struct Fuse {
 // First round: thread q takes line q % LPB and the butterfly at bit-reversed positions 4g .. 4g+3 (g = q / LPB),
 // i.e. DFT inputs k0 + {0, M/2, M/4, 3M/4} with k0 = brev(4g), fetched by load(line, k).  Plain: one multiply by
 // w_4 (W set ws[1024]); CT (coset stage table): twiddles ws[1], ws[2], ws[3] as in r4_round<LG = 1, CT>.
-template <int LOGM, int TILE, bool CT, typename Load>
+template <int LOGM, int TILE, bool CT, bool LZ, typename Load>
 __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *ws) {
     using L = Lds<LOGM, TILE>;
     constexpr int M = 1 << LOGM, LPB = TILE / M;
@@ -277,10 +294,11 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
     if constexpr (!CT) {
         const fe_ws W4 = load_fe_ws(ws, 1024);
         fe a0, a1, a2, d23;
-        fe_addsub2(x0, x1, x2, x3, a0, a1, a2, d23);
+        fe_addsub2(x0, x1, x2, x3, a0, a1, a2, d23);  // a2 is a second operand below: keep it canonical
+        if constexpr (LZ) a0 = fe_add_lazy(x0, x1);
         const fe a3 = fe_mul_uniform(d23, W4);
         fe o0, o1, o2, o3;
-        fe_addsub2(a0, a2, a1, a3, o0, o2, o1, o3);
+        addsub2<LZ>(a0, a2, a1, a3, o0, o2, o1, o3);
         s[p] = o0;
         s[p2] = o2;
         s[p1] = o1;
@@ -289,11 +307,11 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
         const fe_ws W1 = load_fe_ws(ws, 1);
         const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
         fe a0, a1, a2, a3;
-        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
         const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, 2));
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, 3));
         fe o0, o1, o2, o3;
-        fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+        addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
         s[p2] = o2;
         s[p1] = o1;
@@ -303,7 +321,7 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
 }
 // Last round (h = M/4): thread q takes line q % LPB and butterfly index j = q / LPB; its outputs at positions
 // j + {0, h, 2h, 3h} go to store(line, pos, value).  Per-lane two-part twiddles as in r4_round's UNI branch.
-template <int LOGM, int TILE, bool CT, typename Store>
+template <int LOGM, int TILE, bool CT, bool LZ, typename Store>
 __device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Store store) {
     using L = Lds<LOGM, TILE>;
     constexpr int M = 1 << LOGM, LPB = TILE / M, LG = LOGM - 1, h = M / 4;
@@ -313,11 +331,11 @@ __device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Sto
     const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
     const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
     fe a0, a1, a2, a3;
-        fe_addsub2(x0, t1, x2, t3, a0, a1, a2, a3);
+    addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
     const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
     const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
     fe o0, o1, o2, o3;
-    fe_addsub2(a0, u2, a1, u3, o0, o2, o1, o3);
+    addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);  // LZ: the store canonicalises (a multiply or fe_canon)
     store(line, j, o0);
     store(line, j + h, o1);
     store(line, j + 2 * h, o2);
@@ -422,11 +440,11 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         const fe *stage = CT ? a.cos_stage + (size_t)r * 4096 : a.tw4096;
         const fe_ws *stage_ws = CT ? a.cos_stage_ws + (size_t)r * 4096 : a.tw_ws;
         const fe_w2 *stage_w2 = CT ? a.cos_stage_w2 + (size_t)r * 4096 : a.tw_w2;
-        first_round_from<LOGM, TILE, CT>(s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); },
-                                         stage_ws);
-        r4_rounds<LOGM, TILE, 3, CT, LOGM - 2>(s, stage, stage_ws, stage_w2);
+        first_round_from<LOGM, TILE, CT, ZK_NTT_LAZY>(
+            s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); }, stage_ws);
+        r4_rounds<LOGM, TILE, 3, CT, LOGM - 2, ZK_NTT_LAZY>(s, stage, stage_ws, stage_w2);
         const fe *ptw = CT ? a.cos_pass + (size_t)r * n : a.pass_tw;
-        last_round_to<LOGM, TILE, CT>(s, stage_w2, [&](int line, int j2, fe v) {
+        last_round_to<LOGM, TILE, CT, ZK_NTT_LAZY>(s, stage_w2, [&](int line, int j2, fe v) {
             const size_t o = (k1_0 + line) * M + j2;
             out[o] = fe_mul(v, ptw[o]);  // inter-pass twiddle w^(j2 k1) (CT: (s_r w_n^j2)^k1), contiguous over the block
         });
@@ -477,10 +495,12 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const fe *in = a.in + b * a.in_stride;
     if constexpr (Fuse<LOGM, TILE>::OK) {
         fe *out = a.out_of(b);
-        first_round_from<LOGM, TILE, false>(s, [&](int line, int k1) { return in[(size_t)k1 * n2 + j2_0 + line]; }, a.tw_ws);
-        r4_rounds<LOGM, TILE, 3, false, LOGM - 2>(s, a.tw4096, a.tw_ws, a.tw_w2);
-        last_round_to<LOGM, TILE, false>(s, a.tw_w2, [&](int line, int j1, fe v) {
+        first_round_from<LOGM, TILE, false, ZK_NTT_LAZY2>(
+            s, [&](int line, int k1) { return in[(size_t)k1 * n2 + j2_0 + line]; }, a.tw_ws);
+        r4_rounds<LOGM, TILE, 3, false, LOGM - 2, ZK_NTT_LAZY2>(s, a.tw4096, a.tw_ws, a.tw_w2);
+        last_round_to<LOGM, TILE, false, ZK_NTT_LAZY2>(s, a.tw_w2, [&](int line, int j1, fe v) {
             if (a.has_post) v = fe_mul(v, a.post);
+            else if (ZK_NTT_LAZY2) v = fe_canon(v);
             out[n2 * (size_t)j1 + j2_0 + line] = v;
         });
         return;
@@ -2553,6 +2573,9 @@ __global__ void k_field_op(int op, const fe *a, const fe *b, fe *out, size_t cou
     case 1: r = fe_sub(x, y); break;
     case 2: r = fe_mul(x, y); break;
     case 3: r = fe_inv(x); break;
+    case 5: r = fe_add_lazy(x, y); break;  // the NTT's lazy forms: x any value < 2^128, y canonical
+    case 6: r = fe_canon(x); break;
+    case 7: r = fe_mul_w2(x, fe_w2{y, fe_mul(y, fe{0, 1})}); break;  // two-part constant (w, w 2^64)
     default: r = fe_exp(x, y.lo, y.hi); break;
     }
     out[t] = r;

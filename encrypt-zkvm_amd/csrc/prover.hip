@@ -1523,7 +1523,8 @@ extern "C" void zk_diag_mul_limbs_host(const uint8_t *a, const uint8_t *b, uint8
 }
 extern "C" void zk_diag_blake3_host(const uint8_t *in, size_t len, uint8_t out[32]) { b3::hash_bytes(in, len, out); }
 
-// GPU elementwise field op: 0 add, 1 sub, 2 mul, 3 inv(a), 4 a^b (b as a 128-bit exponent)
+// GPU elementwise field op: 0 add, 1 sub, 2 mul, 3 inv(a), 4 a^b (b as a 128-bit exponent), 5 lazy add,
+// 6 canonical form of a, 7 multiply by b in two-part form
 extern "C" int zk_diag_field_op(int device, int op, const uint8_t *a, const uint8_t *b, uint8_t *out, size_t count) {
     if (!a || !b || !out || count == 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     ZK_CHECK_HIP(hipSetDevice(device));

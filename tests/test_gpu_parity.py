@@ -44,6 +44,29 @@ def test_field_ops(gpu):
     assert bytes_elems(out.raw) == [pow(x, y, P) for x, y in zip(a, e)]
 
 
+def test_lazy_field_forms(gpu):
+    """The NTT's partially reduced forms (f128.hpp fe_add_lazy / fe_sub / fe_canon and the multiplies): the
+    first operand may be any value below 2^128, the second is canonical; results stay below 2^128 and are
+    congruent mod p.  Non-canonical values are rare on random data (~2^-82 per sum), so the edges are crafted."""
+    rnd = random.Random(11)
+    hi = [2**128 - 1, 2**128 - 2, P, P + 1, 2**128 - 45 * 2**40, P - 1, 2**127, 0]
+    a = [x for x in hi for _ in hi] + [rnd.randrange(P, 2**128) for _ in range(2000)] + [rnd.randrange(2**128) for _ in range(2000)]
+    bl = [P - 1, P - 2, 0, 1, 2**127, P - 2**64, 45 * 2**40, 2**64 - 1]
+    b = [y for _ in hi for y in bl] + [rnd.choice([P - 1, rnd.randrange(P)]) for _ in range(4000)]
+
+    def run(op, xs, ys):
+        out = C.create_string_buffer(16 * len(xs))
+        native.check(native.lib().zk_diag_field_op(0, op, elems_bytes(xs), elems_bytes(ys), out, len(xs)))
+        return bytes_elems(out.raw)
+
+    for op, f in [(5, lambda x, y: x + y), (1, lambda x, y: x - y), (2, lambda x, y: x * y), (7, lambda x, y: x * y)]:
+        for g, x, y in zip(run(op, a, b), a, b):
+            assert 0 <= g < 2**128 and g % P == f(x, y) % P, (op, x, y, g)
+            if op in (2, 7):
+                assert g < P, (op, x, y, g)  # multiplies return canonical values
+    assert run(6, a, b) == [x % P for x in a]
+
+
 @pytest.mark.parametrize("k", [1, 4, 7, 8, 28])
 def test_blake3_rows(gpu, oracle, k):
     rnd = random.Random(k)
