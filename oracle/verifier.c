@@ -276,7 +276,7 @@ int or_verify(const uint8_t *proof, size_t proof_len, const or_pub_inputs *pub, 
     uint16_t oel = rd_u16(&r);
     const uint8_t *oe = rd(&r, oel);
     if (r.bad || tsl != 1 + 2 * W * 16 * K || ts[0] != 2 || oel % (16 * K) || oel / (16 * K) > OR_MAX_CCOLS ||
-        oel == 0 || oel / (16 * K) != or_num_comp_cols((size_t)1 << logn))
+        oel == 0 || (size_t)(oel / (16 * K)) != (size_t)or_num_comp_cols((size_t)1 << logn))
         FAIL("malformed OOD frame");
     const size_t C = oel / (16 * K);
     e2 oz[W], ozg[W], oc[OR_MAX_CCOLS];
