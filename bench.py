@@ -129,7 +129,7 @@ def run_proofs(fns, count: int):
         raise errs[0]
 
 
-def cpu_baseline(log_n: int, config5: bool = False):
+def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0):
     """The oracle's single-threaded CPU prove (the build's restatement of the reference path; the
     reference Rust prover cannot be built here) on a bounded sample of the same generator."""
     from oracle import oracle as orc
@@ -145,9 +145,46 @@ def cpu_baseline(log_n: int, config5: bool = False):
     orc.prove(trace, pub, opts)
     dt = time.perf_counter() - t0
     n = trace.shape[1]
-    return {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle or_prove (C, 1 thread) on one 2^{log_n}-step trace of the same cipher-mix "
-                      f"generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s"}
+    out = {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port",
+           "sample": f"oracle or_prove (C, 1 thread) on one 2^{log_n}-step trace of the same cipher-mix "
+                     f"generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s"}
+    if all_cores > 1:
+        # the reference prover is single-threaded (no rayon), so its whole-host throughput is one proof per
+        # core: all_cores threads each prove the same trace at once (ctypes releases the GIL; the oracle
+        # keeps no global state)
+        errs = []
+
+        def one():
+            try:
+                orc.prove(trace, pub, opts)
+            except BaseException as e:  # re-raised below
+                errs.append(e)
+
+        ths = [threading.Thread(target=one) for _ in range(all_cores)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dta = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        out["all_cores"] = {"value": all_cores * n / dta, "unit": "trace-steps/s", "cores": all_cores,
+                            "sample": f"{all_cores} concurrent single-thread oracle proofs of the same 2^{log_n} "
+                                      f"trace: {dta:.1f} s"}
+    return out
+
+
+def host_cores(req: int) -> int:
+    """Threads for the all-cores CPU sample: the requested count, else this process's CPU share (affinity,
+    OMP_NUM_THREADS: the GPU box sets it to the box's share of a larger machine), capped at 16."""
+    if req >= 0:
+        return req
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, 16))
 
 
 def pmc_traffic(kernel: str, config5: bool = False):
@@ -171,6 +208,8 @@ def main():
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--cpu-log-n", type=int, default=18)  # ~20 s of single-core oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cores", type=int, default=-1,
+                    help="threads of the all-cores CPU sample (-1: the host share, at most 16; 0: skip it)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--inflight", type=int, default=2, help="independent provers (proofs in flight) per GPU")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
@@ -276,7 +315,7 @@ def main():
                             "floor_ms_per_launch": round(floor_ms / launches, 4), "frac": round(floor_ms / tot_ms, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_log_n, args.config5)
+        cpu = cpu_baseline(args.cpu_log_n, args.config5, host_cores(args.cpu_cores))
     value = world * n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
