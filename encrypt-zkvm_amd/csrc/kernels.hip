@@ -915,7 +915,11 @@ __device__ __forceinline__ void merge_half3(const uint4 c[8], uint8_t *nodes, si
     b3::merge(h0, h1, g);
     store_digest(nodes + 32 * (cnt / 2 + 2 * t + half), g);
 }
-__global__ void __launch_bounds__(256, 4) k_merge_level3_pf(const uint8_t *src, uint8_t *nodes, size_t cnt) {
+#ifndef ZK_MERKLE_WAVES
+#define ZK_MERKLE_WAVES 4  // waves per SIMD the pipelined three-level kernel targets (A/B: merkle 0.56-0.58 ms per
+                           // proof at 4, 0.60-0.62 at 5, 0.67 at 6: the pipelined loads need the registers)
+#endif
+__global__ void __launch_bounds__(256, ZK_MERKLE_WAVES) k_merge_level3_pf(const uint8_t *src, uint8_t *nodes, size_t cnt) {
     const size_t q = cnt / 4, stride = (size_t)gridDim.x * blockDim.x;
     size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
