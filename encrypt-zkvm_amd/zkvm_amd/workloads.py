@@ -153,9 +153,12 @@ class Workload:
     last_row: list[int]
 
 
-def make_workload(source: str, seed: int = 1, n_pub: int | None = None, n_sec: int | None = None) -> Workload:
+def make_workload(source: str, seed: int = 1, n_pub: int | None = None, n_sec: int | None = None,
+                  params: LweParameters | None = None) -> Workload:
+    """Inputs for `source`: public u8 values for READ, ciphertexts for READ2 under a seeded ServerKey
+    (params: its LWE parameters, default LweParameters(): lwe_size 5), and a random non-zero last row."""
     rng = np.random.default_rng(seed + 1000)
-    sk = ServerKey(seed=seed)
+    sk = ServerKey(params, seed=seed) if params is not None else ServerKey(seed=seed)
     ops = [ln.split("#")[0].strip() for ln in source.splitlines()]
     ops = [o for o in ops if o]
     n_pub = n_pub if n_pub is not None else sum(o == "read" for o in ops)

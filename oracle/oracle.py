@@ -253,6 +253,15 @@ def make_pub(program_hash, outputs, lwe_size=5, delta=16) -> PubInputs:
 
 def prove(trace: np.ndarray, pub: PubInputs, options: Options | None = None, want=()):
     """trace: (28, n, 2) uint64.  want: names of Dump fields to return as uint64 arrays."""
+    rc, proof, rec, held = prove_rc(trace, pub, options, want)
+    if rc != 0:
+        raise OracleError(rc, f"or_prove failed with status {rc}")
+    return proof, rec, held
+
+
+def prove_rc(trace: np.ndarray, pub: PubInputs, options: Options | None = None, want=()):
+    """prove() that returns the status instead of raising: (rc, proof, record, dumps).  A trace that
+    violates the AIR still runs every stage (the stage dumps are filled) and ends with OR_ERR_DEGREE."""
     options = options or default_options()
     trace = np.ascontiguousarray(trace, dtype=np.uint64)
     n = trace.shape[1]
@@ -270,9 +279,7 @@ def prove(trace: np.ndarray, pub: PubInputs, options: Options | None = None, wan
     plen = C.c_size_t(cap)
     rc = lib().or_prove(trace.ctypes.data, n, C.byref(options), C.byref(pub), buf, C.byref(plen), C.byref(rec),
                         C.byref(dump))
-    if rc != 0:
-        raise OracleError(rc, f"or_prove failed with status {rc}")
-    return buf.raw[:plen.value], rec, held
+    return rc, (buf.raw[:plen.value] if rc == 0 else b""), rec, held
 
 
 def verify(proof: bytes, pub: PubInputs, min_security: int = 95):

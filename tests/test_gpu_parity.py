@@ -368,6 +368,36 @@ def test_reference_vm_prove_and_verify(gpu):
     assert verify(proof, pub, 95) == (0, "")
 
 
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_other_lwe_sizes(gpu, oracle, k):
+    """Ciphertexts of k + 1 elements (lwe_size 2..4 instead of the example's 5).  The reference AIR hard-codes
+    the 5-element ciphertext in its depth and read2 constraints (tests/test_oracle_vm_air.py), so such traces
+    are refused -- here and by the oracle, both with a degree error -- but the evaluator's lwe_size loop must
+    still agree with the oracle: the zk_eval_constraints plug point reproduces the oracle's composition
+    values (every CE step) at lwe_size = k + 1."""
+    from zkvm_amd.workloads import LweParameters
+    src = cipher_mix_program(12)[0]
+    w = make_workload(src, seed=30 + k, params=LweParameters(8, 128, k, 2.412_390_240_121_573e-5))
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    assert pub.lwe_size == k + 1
+    _, _, _, rc = gpu.prove(trace, pub, ProofOptions(), allow_degree_error=True)
+    assert rc == native.ZK_ERR_DEGREE
+    orc, _, orec, od = oracle.prove_rc(trace, oracle_pub(oracle, pub), want=("composition",))
+    assert orc == native.ZK_ERR_DEGREE
+    n = trace.shape[1]
+    L = native.lib()
+    hnd = C.c_void_p()
+    tb = np.ascontiguousarray(trace)
+    native.check(L.zk_lde_new(gpu.handle, tb.ctypes.data, 28, n, 8, C.byref(hnd), C.create_string_buffer(32)))
+    try:
+        out = C.create_string_buffer(16 * 8 * n)
+        native.check(L.zk_eval_constraints(hnd, C.byref(pub), bytes(orec.coeff_t), bytes(orec.coeff_b), out))
+        assert out.raw == od["composition"].tobytes()
+    finally:
+        L.zk_lde_free(hnd)
+
+
 @pytest.mark.parametrize("grinding", [33, 64, 255])
 def test_grinding_factor_bound(gpu, grinding):
     """winter-air ProofOptions caps grinding_factor at 32: larger values are refused up front (a search for

@@ -255,6 +255,28 @@ def test_vm_trace_satisfies_air(oracle, source):
     assert eval_trace_rows(oracle, t2, rows=range(max(0, r - 1), r + 1)) != []
 
 
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_other_lwe_sizes_break_the_hardcoded_constraints(oracle, k):
+    """LWE dimensions other than the example's k = 4 (fhe/src/parameters.rs:13-21).  The LWE constraints
+    (sadd / add2 / smul, constrains.rs:112-164) loop over server_key.lwe_size(), but the stack-depth and
+    read2 constraints hard-code a 5-element ciphertext (constrains.rs:103-106: depth moves by 4 on
+    read2 / add2; :174-176: read2 checks stack item 5).  So the reference AIR accepts the VM's traces only
+    at lwe_size 5: at k + 1 < 5 exactly those two constraints fail, the lwe_size-dependent ones hold.  The
+    product VM and the oracle VM produce the same trace."""
+    from zkvm_amd.prover import vm_trace
+    from zkvm_amd.workloads import LweParameters
+    src = cipher_mix_program(3)[0]
+    w = make_workload(src, seed=20 + k, params=LweParameters(8, 128, k, 2.412_390_240_121_573e-5))
+    L = w.server_key.lwe_size()
+    assert L == k + 1 and all(len(c) == L for c in w.secret)
+    codes, values, h = oracle.program_compile(src)
+    trace, out = oracle.processor_trace(codes, values, w.public, w.secret, lwe_size=L, last_row=w.last_row)
+    ptrace, pout, ph = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    assert (ptrace == trace).all()
+    bad = eval_trace_rows(oracle, trace, lwe=L)
+    assert bad and {c for _, cs in bad for c in cs} <= {1, 10}
+
+
 def test_lr_example_decrypts(oracle):
     # examples/linear_regression/src/main.rs:20-86 with its own plaintexts
     sk = ServerKey(seed=42)
