@@ -149,7 +149,10 @@ CASES = [("push.5\npush.3\nadd", ProofOptions()), (LR_PROGRAM, ProofOptions()),
          (ops_for_trace_len(14, "cipher"), ProofOptions()),
          # four-step coset-table LDE with 16 cosets: two 8-coset launches per pass
          (ops_for_trace_len(13, "cipher"), ProofOptions(num_queries=28, blowup_factor=16)),
-         (LR_PROGRAM, ProofOptions(num_queries=20, grinding_factor=18))]  # GPU proof-of-work search
+         (LR_PROGRAM, ProofOptions(num_queries=20, grinding_factor=18)),  # GPU proof-of-work search
+         # option maxima: 255 queries (many shared Merkle paths in the batch openings), remainder degree 255
+         (cipher_mix_program(60)[0], ProofOptions(num_queries=255, fri_remainder_max_degree=255)),
+         (cipher_mix_program(60)[0], ProofOptions(num_queries=255, fri_folding_factor=2, fri_remainder_max_degree=7))]
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
