@@ -4,8 +4,12 @@ Workload (BASELINE.json configs[2]): a 2^20-step Encrypt-zkVM program mixing REA
 ciphertext ops (zkvm_amd.workloads.cipher_mix_program), proved with the reference options
 ProofOptions(32, 8, 0, None, 8, 127) (vm/src/lib.rs:20).  One step = one full Prover::prove of that
 trace: trace LDE + commitment, constraint evaluation, composition commitment, OOD/DEEP, FRI,
-queries and proof bytes.  The trace is generated once on the host (VM, untimed) and uploaded to
-HBM before the timed region; each timed step proves it from device memory to proof bytes.
+queries and proof bytes.  The trace is generated once on the host (VM, untimed) straight into page-locked host memory; each timed step
+is one zk_prove call from that host-resident trace to proof bytes (the reference's call shape: vm/src/lib.rs
+builds a TraceTable in host memory and hands it to Prover::prove).  The library uploads it in column groups
+on a copy stream, overlapped with the interpolation and, with two provers in flight, with the other proof's
+kernels.  Beside `value` the line reports device_resident_ms (the trace already in HBM), pageable_host_ms
+(the trace in ordinary pageable memory) and latency_ms (one prove() call alone on the GPU).
 
 Proofs in flight (--inflight P, default 2): each GPU holds P independent provers (own HBM buffers and
 stream, zk_prover objects) driven by P host threads, so one prover's host-side transcript round trips and
@@ -32,6 +36,8 @@ import sys
 import threading
 import time
 from pathlib import Path
+
+import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 for p in (ROOT, ROOT / "encrypt-zkvm_amd"):
@@ -200,6 +206,15 @@ def pmc_traffic(kernel: str, config5: bool = False):
         return None
 
 
+def run_proofs_timed(fns, count: int, pg, local: int) -> float:
+    """count proofs over the provers' step functions, bracketed by barrier + device sync; max over ranks (s)."""
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    run_proofs(fns, count)
+    barrier(pg, local)
+    return max_over_ranks(pg, time.perf_counter() - t0, local)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -213,6 +228,8 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--inflight", type=int, default=2, help="independent provers (proofs in flight) per GPU")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
+    ap.add_argument("--sharded-log-n", type=int, default=22,
+                    help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
@@ -221,17 +238,20 @@ def main():
 
     world, rank, local, pg = setup_dist(args.gpus)
     from zkvm_amd import native
-    from zkvm_amd.prover import GpuProver, ProofOptions, make_pub_inputs, vm_trace
-    from zkvm_amd.workloads import make_workload, ops_for_trace_len, padded_length
+    from zkvm_amd.prover import GpuProver, HostTrace, ProofOptions, make_pub_inputs, vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len, padded_length, trace_length
 
     native.lib()  # fail loudly without the HIP library
     src = ops_for_trace_len(args.log_n, "cipher")
     program_ops = sum(1 for ln in src.splitlines() if ln.split("#")[0].strip())  # #program ops
     padded_ops = padded_length(src)
     w = make_workload(src, seed=1000 + rank)
+    n = trace_length(src)
+    # the VM writes its TraceTable straight into page-locked host memory (zk_host_alloc): the host-resident
+    # trace the timed region starts from (vm/src/lib.rs:18 builds it, :26 hands it to prove)
+    host = HostTrace(n)
     t0 = time.perf_counter()
-    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
-    n = trace.shape[1]
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row, out=host)
     log(f"[rank {rank}] VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
     opts = ProofOptions(43, 8, 0, 2, 8, 127) if args.config5 else ProofOptions()
@@ -239,38 +259,60 @@ def main():
     opts_str = "ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5 else "ProofOptions(32, 8, 0, None, 8, 127)"
     P = max(1, args.inflight)
     provers = [GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor) for _ in range(P)]
-    d_traces = [g.upload_trace(trace)[0] for g in provers]
-    gpu, d_trace = provers[0], d_traces[0]
-
+    gpu = provers[0]
     last = [None] * P
 
-    def prover_step(k):
+    def host_step(k, tr):
+        def f():
+            last[k] = provers[k].prove_host(tr, pub, opts)[0]
+        return f
+
+    # ---- value: zk_prove from the host-resident (page-locked) trace to proof bytes, P proofs in flight
+    fns = [host_step(k, trace) for k in range(P)]
+    for f in fns:  # every prover's first proof builds its per-size tables
+        f()
+    # warm-up: at least three proofs per prover (the first proofs after the tables pay page faults and
+    # clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms, tools/proof_times.py)
+    warm = max(args.warmup, 3 * P)
+    run_proofs(fns, warm - P)
+    elapsed = run_proofs_timed(fns, args.steps, pg, local)
+    proof = last[0]
+    assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
+
+    # ---- comparison legs (same provers, same count, outside the headline): the trace already in HBM
+    # (zk_prove_device), and the host trace in pageable memory (runtime-staged copies)
+    cmp_steps = max(2 * P, min(args.steps, 10))
+    d_traces = [g.upload_trace(trace)[0] for g in provers]
+
+    def dev_step(k):
         def f():
             last[k] = provers[k].prove_device(d_traces[k], n, pub, opts)[0]
         return f
 
-    fns = [prover_step(k) for k in range(P)]
-    for f in fns:  # every prover's first proof builds its per-size tables
-        f()
-    # warm-up: W proofs, at least three per prover (the first proofs after the tables pay page faults
-    # and clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms, tools/proof_times.py)
-    run_proofs(fns, max(args.warmup, 3 * P) - P)
-    barrier(pg, local)
-    t0 = time.perf_counter()
-    run_proofs(fns, args.steps)
-    barrier(pg, local)
-    elapsed = max_over_ranks(pg, time.perf_counter() - t0, local)
-    proof = last[0]
-    assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
+    dfns = [dev_step(k) for k in range(P)]
+    run_proofs(dfns, P)
+    dev_s = run_proofs_timed(dfns, cmp_steps, pg, local)
+    assert all(p_ == proof for p_ in last if p_ is not None), "device-resident proof differs"
+    pageable = np.array(trace)  # ordinary (pageable) host memory
+    pfns = [host_step(k, pageable) for k in range(P)]
+    run_proofs(pfns, P)
+    pag_s = run_proofs_timed(pfns, cmp_steps, pg, local)
+    assert all(p_ == proof for p_ in last if p_ is not None), "pageable-trace proof differs"
+    del pageable
     for g in provers[1:]:
         g.close()
-    # per-proof latency breakdown: one proof alone on the GPU
-    gpu.prove_device(d_trace, n, pub, opts)
+    # latency of one prove() call alone on the GPU (host-resident trace), median of 5
+    lat = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        gpu.prove_host(trace, pub, opts)
+        lat.append(time.perf_counter() - t1)
+    latency_ms = 1e3 * sorted(lat)[len(lat) // 2]
     stages = gpu.stage_times()
 
     # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream)
     gpu.profile(True)
-    gpu.prove_device(d_trace, n, pub, opts)
+    gpu.prove_host(trace, pub, opts)
     kstats = gpu.kernel_stats()
     kops = gpu.kernel_ops()
     gpu.profile(False)
@@ -287,6 +329,18 @@ def main():
         verified = orc.verify(proof, opub, min_sec)[0] == 0
     from zkvm_amd.prover import verify as zk_verify
     zk_verified = zk_verify(proof, pub, min_sec)[0] == 0
+    gpu.close()
+    trace = None
+    host.close()
+
+    # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record
+    sharded = None
+    if world > 1 and args.sharded_log_n:
+        import torch
+        if torch.cuda.is_available():
+            sharded = sharded_leg(args, args.sharded_log_n, world, rank, local, pg, steps=10, warmup=3)
+            for k in ("pub", "proof", "n", "min_sec"):
+                sharded.pop(k)
 
     if rank != 0:
         if pg is not None:
@@ -319,42 +373,45 @@ def main():
     value = world * n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "warmup": warm, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f128", "data": "synthetic (seeded VM trace)",
         "config": {"workload": f"configs[{4 if args.config5 else 2}]: 2^{args.log_n}-step READ2/ADD2/SMUL cipher-mix program, "
-                               f"full prove" + (" at 128-bit conjectured security" if args.config5 else ""),
+                               f"full prove from the host-resident trace" +
+                               (" at 128-bit conjectured security" if args.config5 else ""),
                    "trace_len": n, "trace_width": 28, "lde_len": n * opts.blowup_factor,
                    "program_ops": program_ops, "padded_ops": padded_ops,
-                   "options": opts_str, "parallelism": f"independent proofs, {P} in flight per GPU, x{world} GPUs"},
+                   "options": opts_str, "timed_region": "zk_prove_columns: page-locked host trace -> proof bytes",
+                   "parallelism": f"independent proofs, {P} in flight per GPU, x{world} GPUs"},
         "security_bits_checked": min_sec,
+        "latency_ms": round(latency_ms, 3),
+        "device_resident_ms": round(1e3 * dev_s / cmp_steps, 3),
+        "pageable_host_ms": round(1e3 * pag_s / cmp_steps, 3),
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
         "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
     }
+    if sharded is not None:
+        out["sharded"] = sharded
     print(json.dumps(out), flush=True)
     if pg is not None:
         pg.destroy_process_group()
 
 
-def run_sharded(args):
-    world, rank, local, pg = setup_dist(args.gpus)
-    from zkvm_amd import native
+def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=False):
+    """One 2^log_n proof per step with the LDE domain sharded by coset over all ranks (zk_prove_sharded over
+    RCCL): every rank proves the same trace.  Returns (on every rank) the step time and stage split."""
     from zkvm_amd.prover import ProofOptions, make_pub_inputs, vm_trace
     from zkvm_amd.sharded import ShardedProver
-    from zkvm_amd.workloads import make_workload, ops_for_trace_len, padded_length
-
-    native.lib()
-    src = ops_for_trace_len(args.log_n, "cipher")
-    program_ops = sum(1 for ln in src.splitlines() if ln.split("#")[0].strip())
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(log_n, "cipher")
     w = make_workload(src, seed=1000)  # the same trace on every rank: one proof
     t0 = time.perf_counter()
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
     n = trace.shape[1]
-    log(f"[rank {rank}] VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
+    log(f"[rank {rank}] sharded VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
-    opts = ProofOptions(43, 8, 0, 2, 8, 127) if args.config5 else ProofOptions()
-    min_sec = 128 if args.config5 else 95
+    opts = ProofOptions(43, 8, 0, 2, 8, 127) if config5 else ProofOptions()
     uid = ShardedProver.unique_id() if rank == 0 else None
     if pg is not None:
         box = [uid]
@@ -368,35 +425,50 @@ def run_sharded(args):
     def step():
         last["proof"] = sp.prove(None, pub, opts, n=n)[0]
 
-    elapsed = timed_loop(step, args.steps, args.warmup, pg, local)
+    elapsed = timed_loop(step, steps, warmup, pg, local)
     stages = sp.stage_times()
+    proof = last["proof"]
+    sp.close()
+    return {"workload": f"configs[{4 if config5 else 3}]: one 2^{log_n}-step cipher-mix proof, LDE domain sharded by coset",
+            "n_ranks": world, "steps": steps, "warmup": warmup, "ms_per_proof": round(1e3 * elapsed / steps, 3),
+            "trace_steps_per_s": round(n * steps / elapsed, 1), "scaling": "strong",
+            "stage_ms": {k: round(v, 3) for k, v in stages.items()}, "proof_bytes": len(proof),
+            "pub": pub, "proof": proof, "n": n, "min_sec": 128 if config5 else 95}
+
+
+def run_sharded(args):
+    world, rank, local, pg = setup_dist(args.gpus)
+    from zkvm_amd import native
+    from zkvm_amd.workloads import ops_for_trace_len, padded_length
+    native.lib()
+    rec = sharded_leg(args, args.log_n, world, rank, local, pg, args.steps, args.warmup, args.config5)
     verified = None
     if rank == 0 and not args.no_verify:
         import ctypes as C
         from oracle import oracle as orc
         orc.build()
+        pub = rec["pub"]
         opub = orc.PubInputs()
         C.memmove(opub.program_hash, bytes(pub.program_hash), 32)
         C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
         opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
-        verified = orc.verify(last["proof"], opub, min_sec)[0] == 0
-    sp.close()
+        verified = orc.verify(rec["proof"], opub, rec["min_sec"])[0] == 0
     if rank == 0:
+        src = ops_for_trace_len(args.log_n, "cipher")
+        n = rec["n"]
         out = {
-            "metric": METRIC, "value": round(n * args.steps / elapsed, 1), "unit": "trace-steps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "metric": METRIC, "value": rec["trace_steps_per_s"], "unit": "trace-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_proof"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f128",
             "data": "synthetic (seeded VM trace)",
-            "config": {"workload": f"configs[{4 if args.config5 else 3}]: one 2^{args.log_n}-step cipher-mix proof, "
-                                   f"LDE domain sharded by coset",
-                       "trace_len": n, "trace_width": 28, "lde_len": 8 * n,
-                       "program_ops": program_ops, "padded_ops": padded_length(src),
+            "config": {"workload": rec["workload"], "trace_len": n, "trace_width": 28, "lde_len": 8 * n,
+                       "program_ops": sum(1 for ln in src.splitlines() if ln.split("#")[0].strip()),
+                       "padded_ops": padded_length(src),
                        "options": ("ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5
                                    else "ProofOptions(32, 8, 0, None, 8, 127)"),
                        "parallelism": f"coset-sharded x{world} (RCCL all-to-all / all-gather)"},
-            "roofline": None, "cpu_baseline": None,
-            "stage_ms": {k: round(v, 3) for k, v in stages.items()},
-            "proof_bytes": len(last["proof"]), "proof_verified_by_oracle": verified,
+            "roofline": None, "cpu_baseline": None, "stage_ms": rec["stage_ms"],
+            "proof_bytes": rec["proof_bytes"], "proof_verified_by_oracle": verified,
         }
         print(json.dumps(out), flush=True)
     if pg is not None:

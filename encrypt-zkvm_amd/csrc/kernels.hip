@@ -128,18 +128,24 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const int line = pidx >> (LOGM - 2 - LH), grp = pidx & ((M >> (2 + LH)) - 1);
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-        // plain DFT, j = 0 (wave-uniform): w_2h^0 = w_4h^0 = 1, only w_4h^h = w_4 remains
+        // plain DFT, j = 0 (wave-uniform): w_2h^0 = w_4h^0 = 1, only w_4h^h = w_4 remains.  Under LZ the tile
+        // holds lazy (< 2^128, not canonical) values and the skipped multiplies were what made the second
+        // operands of the lazy add/sub canonical, so those waves canonicalise x1, x3 and a2 instead.
         const bool triv = !CT && ZK_NTT_J0 && j == 0;
         fe t1 = x1, t3 = x3;
         if (!triv) {
             const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
             t1 = fe_mul_uniform(x1, W1);
             t3 = fe_mul_uniform(x3, W1);
+        } else if (LZ) {
+            t1 = fe_canon(x1);
+            t3 = fe_canon(x3);
         }
         fe a0, a1, a2, a3;
         addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
         fe u2 = a2;
         if (!triv) u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
+        else if (LZ) u2 = fe_canon(a2);
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
@@ -1544,19 +1550,19 @@ hipError_t upload_rescue_consts(hipStream_t st) {
     if (e == hipSuccess) g_consts_done.set((size_t)dev);
     return e;
 }
-static void upload_rescue(hipStream_t st) { (void)upload_rescue_consts(st); }
 
-void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+hipError_t eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                       const AirConsts *consts_dev, fe *comp, bool bnd, int nce) {
     // (with bnd the kernel reads the boundary divisor planes at stride nce * n: all 8 cosets then)
     if (bnd) nce = 8;
-    eval_constraints_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp,
+    return eval_constraints_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts_dev, comp,
                             bnd);
 }
 
-void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+hipError_t eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                              const fe *divs, const AirConsts *consts_dev, fe *comp, bool bnd) {
-    upload_rescue(st);
+    // the __constant__ MDS tables of this device (normally uploaded by zk_prover_create already)
+    if (const hipError_t e = upload_rescue_consts(st)) return e;
     const size_t CE = (size_t)map.nce << log_n;
     const double bytes = (448.0 * (map.lshift == 0 ? 1 : 2) + (bnd ? 64.0 : 32.0)) * CE;
     if (bnd)
@@ -1565,11 +1571,13 @@ void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap m
     else
         ZK_PROF(st, "eval_constraints", bytes, hipLaunchKernelGGL((k_eval_constraints<1, false>), dim3(cdiv(CE, 256)), dim3(256), 0, st,
                                                                   lde, log_n, map, periodic, divs, consts_dev, consts_dev, (size_t)0, comp));
+    return hipGetLastError();
 }
 
-void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+hipError_t eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                                  const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp, bool bnd) {
-    upload_rescue(st);
+    // the __constant__ MDS tables of this device (normally uploaded by zk_prover_create already)
+    if (const hipError_t e = upload_rescue_consts(st)) return e;
     const size_t CE = (size_t)map.nce << log_n;
     const double bytes = (448.0 * (map.lshift == 0 ? 1 : 2) + (bnd ? 80.0 : 48.0)) * CE;
     if (bnd)
@@ -1578,12 +1586,13 @@ void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalM
     else
         ZK_PROF(st, "eval_constraints_ext", bytes, hipLaunchKernelGGL((k_eval_constraints<2, false>), dim3(cdiv(CE, 256)), dim3(256), 0,
                                                                       st, lde, log_n, map, periodic, divs, consts2_dev, consts2_dev + 1, plane, comp));
+    return hipGetLastError();
 }
 
-void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+hipError_t eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                           const AirConsts *consts2_dev, fe *comp, bool bnd, int nce) {
     if (bnd) nce = 8;
-    eval_constraints_ext_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
+    return eval_constraints_ext_mapped(st, lde, log_n, EvalMap{nce, 0, 1, log_b - 3, 1 << log_b}, periodic, divs, consts2_dev,
                                 (size_t)8 << log_n, comp, bnd);
 }
 
@@ -2532,10 +2541,11 @@ __global__ void __launch_bounds__(256) k_copy_to_host(CopyList L) {
     __threadfence_system();
 }
 
-void copy_to_host(hipStream_t st, const CopyList &L, size_t max_words) {
-    if (L.n <= 0) return;
+hipError_t copy_to_host(hipStream_t st, const CopyList &L, size_t max_words) {
+    if (L.n <= 0) return hipSuccess;
     const unsigned bx = std::max(1u, std::min(cdiv(max_words, 256), 64u));
     hipLaunchKernelGGL(k_copy_to_host, dim3(bx, (unsigned)L.n), dim3(256), 0, st, L);
+    return hipGetLastError();  // a failed launch must not let d2h_flush deliver stale staging bytes
 }
 
 void gather_chunks(hipStream_t st, const uint64_t *addr, size_t k, fe *out) {

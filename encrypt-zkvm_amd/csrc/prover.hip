@@ -265,8 +265,10 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     if (device < 0 || device >= cnt) ZK_FAIL(ZK_ERR_INVALID_ARG, "device index out of range");
     ZK_CHECK_HIP(hipSetDevice(device));
     // The host waits on the prover stream a few times per proof (transcript round trips): spin instead
-    // of yielding (A/B: -0.05 ms per 2^20 proof).  Only takes effect if this is the first use of the
-    // device in the process; ZK_SPIN_WAIT=0 keeps the runtime's default.
+    // of yielding (A/B: -0.05 ms per 2^20 proof).  PROCESS-WIDE side effect (documented at zk_prover_create
+    // in zkvm_gpu.h): hipDeviceScheduleSpin applies to every stream sync of the process on this device, so
+    // each waiting host thread busy-spins.  Only takes effect if this is the first use of the device in the
+    // process; ZK_SPIN_WAIT=0 keeps the runtime's default (yield).
     {
         const char *e = getenv("ZK_SPIN_WAIT");
         if (!e || atoi(e)) {
@@ -280,8 +282,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
-    for (auto &e : p->ev_fork) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+    for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_free, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
     DeviceArena &A = p->arena;
@@ -331,9 +333,9 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamSynchronize(p->st);
     if (p->st2) (void)hipStreamSynchronize(p->st2);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
-    for (auto &e : p->ev_fork)
+    for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
-    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->ev_free) (void)hipEventDestroy(p->ev_free);
     if (p->st2) (void)hipStreamDestroy(p->st2);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
@@ -917,46 +919,71 @@ int zk::deliver_proof(const std::vector<uint8_t> &bytes, unsigned degree_flag, u
 
 // ---------------------------------------------------------------- the single-GPU prove path
 // Coset LDE of the ncols column polynomials at `polys` into the coset-major `lde` and the commitment to
-// its rows (leaves, nodes; the root is read back with the caller's next d2h_flush).  With parts > 1 the
-// cosets go in `parts` groups: the rows of a finished group are hashed on the second stream while the
-// NTT of the next group runs (ZK_PIPE; default 1 = LDE then hashing on one stream: A/B 13.89 ms for 1, 14.05 for 2, 14.38 for 4 parts -- co-resident NTT and BLAKE3 waves do not issue faster than either alone).
-static int pipe_parts(uint32_t B) {
-    static const int parts = [] {
-        const char *e = getenv("ZK_PIPE");
-        const int v = e ? atoi(e) : 1;
-        return v >= 1 && v <= 8 && !(v & (v - 1)) ? v : 1;
-    }();
-    return std::min<int>(parts, (int)B);
-}
+// its rows (leaves, nodes; the root is read back with the caller's next d2h_flush).
 static int lde_commit(zk_prover *p, Plan *pl, const fe *polys, int ncols, fe *lde, uint8_t *leaves, uint8_t *nodes,
                       uint8_t root[32]) {
     const int log_n = pl->log_n, log_b = pl->log_b;
     const size_t n = (size_t)1 << log_n, B = (size_t)1 << log_b;
-    const int parts = pipe_parts((uint32_t)B), per = (int)B / parts, log_per = ilog2((size_t)per);
-    for (int h = 0; h < parts; h++) {
-        ntt_lde(p->st, pl->Tn, pl->ct, polys, n, ncols, h * per, 1, per, lde + (size_t)h * per * n, B * n, n, p->tmp);
-        if (h + 1 < parts) {
-            ZK_CHECK_HIP(hipEventRecord(p->ev_fork[h], p->st));
-            ZK_CHECK_HIP(hipStreamWaitEvent(p->st2, p->ev_fork[h], 0));
-            hash_rows_cosets(p->st2, lde, ncols, log_n, log_b, h * per, log_per, leaves);
-        } else {
-            hash_rows_cosets(p->st, lde, ncols, log_n, log_b, h * per, log_per, leaves);
-        }
-    }
-    if (parts > 1) {
-        ZK_CHECK_HIP(hipEventRecord(p->ev_join, p->st2));
-        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_join, 0));
-    }
+    ntt_lde(p->st, pl->Tn, pl->ct, polys, n, ncols, 0, 1, (int)B, lde, B * n, n, p->tmp);
+    hash_rows_cosets(p->st, lde, ncols, log_n, log_b, 0, log_b, leaves);
     merkle_tree(p->st, leaves, n * B, nodes);
     return d2h_small(p, root, nodes + 32, 32);
 }
 
+// Where the trace comes from: resident in HBM (zk_prove_device), or W host columns (zk_prove,
+// zk_prove_columns, zk_lde_new: the reference's TraceTable / ColMatrix, vm/src/lib.rs:18, 26).
+struct TraceSrc {
+    const fe *dev = nullptr;
+    const uint8_t *const *cols = nullptr;
+};
+
+// Column groups of a host-resident trace upload: 4 groups of 7 columns.  The copy engine streams group
+// g + 1 while the CUs interpolate and extend group g; more groups overlap more of the copy but add a launch
+// drain per NTT pass and group.
+#ifndef ZK_UPLOAD_GROUPS
+#define ZK_UPLOAD_GROUPS 4
+#endif
+static_assert(W % ZK_UPLOAD_GROUPS == 0 && ZK_UPLOAD_GROUPS <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
+
+// hipMemcpyAsync from page-locked memory (zk_host_alloc, zk_host_register, any hipHostMalloc'd or
+// hipHostRegister'ed buffer) is a DMA in stream order; from pageable memory the runtime stages the copy
+// through its own pinned buffers and returns once the source has been read (the host thread copies).
+// Both are correct here; the pinned form is the fast one (DESIGN.md "Host-resident trace").
+static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c0, int nc) {
+    for (int c = c0; c < c0 + nc; c++)
+        ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, src.cols[c], n * sizeof(fe), hipMemcpyHostToDevice, p->st2));
+    return ZK_OK;
+}
+
 // S2: interpolate the 28 trace columns (winter-math interpolate_poly over <w_n>), extend them over the B
-// cosets of the LDE domain (coset r: the coefficients scaled by (3 w_N^r)^k) and commit to the rows
-static int trace_lde_commit(zk_prover *p, Plan *pl, const fe *d_trace, size_t n, uint8_t root[32]) {
-    fe inv_n = h_inv(fe_make(n));
-    ntt(p->st, pl->Tn, d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-    return lde_commit(p, pl, p->polys, W, p->lde, p->leaves, p->nodes, root);
+// cosets of the LDE domain (coset r: the coefficients scaled by (3 w_N^r)^k) and commit to the rows.
+// A host-resident trace goes up on the copy stream in ZK_UPLOAD_GROUPS column groups; each group's
+// event gates that group's interpolation and coset LDE on the compute stream.
+static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
+    const fe inv_n = h_inv(fe_make(n));
+    if (src.dev) {
+        ntt(p->st, pl->Tn, src.dev, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+        return lde_commit(p, pl, p->polys, W, p->lde, p->leaves, p->nodes, root);
+    }
+    const int log_n = pl->log_n, log_b = pl->log_b;
+    const size_t B = (size_t)1 << log_b;
+    // the device trace buffer is free once everything queued before this proof on st is done
+    ZK_CHECK_HIP(hipEventRecord(p->ev_free, p->st));
+    ZK_CHECK_HIP(hipStreamWaitEvent(p->st2, p->ev_free, 0));
+    constexpr int per = W / ZK_UPLOAD_GROUPS;
+    for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
+        ZK_TRY(upload_trace_group(p, src, n, g * per, per));
+        ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->st2));
+    }
+    for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
+        const size_t c0 = (size_t)g * per;
+        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[g], 0));
+        ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
+    }
+    hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
+    merkle_tree(p->st, p->leaves, n * B, p->nodes);
+    return d2h_small(p, root, p->nodes + 32, 32);
 }
 
 static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, size_t n, uint32_t B, uint8_t *dst) {
@@ -1047,10 +1074,19 @@ static int check_ood_identity(const std::vector<fe2> &e, int C, const AirConsts 
     return ZK_OK;
 }
 
-int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
-                    uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
-    if (!p || !d_trace_v || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                      uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
+    if (!p || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
+    // copies from the caller's host columns may still be in flight on an early error return: the caller
+    // may free those columns as soon as this returns (a completed proof has long finished them)
+    struct CopyGuard {
+        zk_prover *p;
+        bool on;
+        ~CopyGuard() {
+            if (on) (void)hipStreamSynchronize(p->st2);
+        }
+    } copy_guard{p, src.cols != nullptr};
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));
@@ -1060,7 +1096,6 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     const int log_n = pl->log_n, log_b = pl->log_b;
     const int C = num_comp_cols(n);
     if (C > 8) ZK_FAIL(ZK_ERR_INVALID_ARG, "composition column count exceeds 8");
-    const fe *d_trace = (const fe *)d_trace_v;
     const fe g = h_root_of_unity(log_n);
     zk_record R;
     memset(&R, 0, sizeof R);
@@ -1075,7 +1110,7 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     Coin coin = seed_coin(n, opt, pub);
 
     // S2: trace LDE + commitment
-    ZK_TRY(trace_lde_commit(p, pl, d_trace, n, R.trace_root));
+    ZK_TRY(trace_lde_commit(p, pl, src, n, R.trace_root));
     ZK_TRY(d2h_flush(p));
     stage_mark(p, "trace_commit");
     HostTimer HT;
@@ -1105,16 +1140,16 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
         ZK_TRY(h2d_small(p, p->air_consts, &Kp[0], sizeof Kp[0]));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp, bnd_rows,
-                         nce);
+        ZK_CHECK_HIP(eval_constraints(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->air_consts, comp,
+                                      bnd_rows, nce));
         HT.stop("air_consts");
     } else {
         draw_air_consts_ext(coin, pub, n, Kp[0], Kp[1], R);
         ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
         const fe *binv = boundary_inverses(p, pl);
         if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-        eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp, bnd_rows,
-                             nce);
+        ZK_CHECK_HIP(eval_constraints_ext(p->st, p->lde, log_n, log_b, pl->periodic, binv, (const AirConsts *)p->x_air, comp,
+                                          bnd_rows, nce));
     }
     stage_mark(p, "constraints");
 
@@ -1349,13 +1384,64 @@ int zk_prove_device(zk_prover *p, const void *d_trace_v, size_t n, const zk_opti
     return deliver_proof(bytes, degree_flag, proof_out, proof_len);
 }
 
+int zk_prove_device(zk_prover *p, const void *d_trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                    uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
+    if (!d_trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    TraceSrc src;
+    src.dev = (const fe *)d_trace;
+    return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+}
+
+int zk_prove_columns_ex(zk_prover *p, const uint8_t *const *columns, size_t n, const zk_options *opt,
+                        const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len, zk_record *rec,
+                        const zk_dump *dump) {
+    if (!columns) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    for (int c = 0; c < W; c++)
+        if (!columns[c]) ZK_FAIL(ZK_ERR_INVALID_ARG, "null trace column");
+    TraceSrc src;
+    src.cols = columns;
+    return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+}
+
+int zk_prove_columns(zk_prover *p, const uint8_t *const *columns, size_t n, const zk_options *opt,
+                     const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len) {
+    return zk_prove_columns_ex(p, columns, n, opt, pub, proof_out, proof_len, nullptr, nullptr);
+}
+
 int zk_prove(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
              uint8_t *proof_out, size_t *proof_len) {
-    if (!p || !trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
-    if (n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "trace longer than max_trace_len");
-    ZK_CHECK_HIP(hipSetDevice(p->device));
-    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
-    return zk_prove_device(p, p->d_trace, n, opt, pub, proof_out, proof_len, nullptr, nullptr);
+    if (!trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    const uint8_t *cols[W];
+    for (int c = 0; c < W; c++) cols[c] = trace + (size_t)c * n * sizeof(fe);
+    return zk_prove_columns(p, cols, n, opt, pub, proof_out, proof_len);
+}
+
+// ---------------------------------------------------------------- page-locked host memory for traces
+int zk_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr || !bytes) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    *ptr = nullptr;
+    const hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *ptr = nullptr;
+        ZK_CHECK_HIP(e);
+    }
+    return ZK_OK;
+}
+
+void zk_host_free(void *ptr) {
+    if (ptr) (void)hipHostFree(ptr);
+}
+
+int zk_host_register(void *ptr, size_t bytes) {
+    if (!ptr || !bytes) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_CHECK_HIP(hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+    return ZK_OK;
+}
+
+int zk_host_unregister(void *ptr) {
+    if (!ptr) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_CHECK_HIP(hipHostUnregister(ptr));
+    return ZK_OK;
 }
 
 // ---------------------------------------------------------------- plug point 1: trace LDE
@@ -1370,10 +1456,15 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     Plan *pl;
     int rc = get_plan(p, n, blowup, &pl);
     if (rc) return rc;
-    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
+    const uint8_t *cols[W];
+    for (int c = 0; c < W; c++) cols[c] = trace + (size_t)c * n * sizeof(fe);
+    TraceSrc src;
+    src.cols = cols;
     uint8_t r[32];
-    if ((rc = trace_lde_commit(p, pl, p->d_trace, n, r))) return rc;
-    if ((rc = d2h_flush(p))) return rc;
+    rc = trace_lde_commit(p, pl, src, n, r);
+    if (!rc) rc = d2h_flush(p);
+    (void)hipStreamSynchronize(p->st2);  // the caller's trace is no longer read once this returns
+    if (rc) return rc;
     if (root) memcpy(root, r, 32);
     *out = new zk_trace_lde{p, n, blowup, W};
     return ZK_OK;
@@ -1455,8 +1546,8 @@ int zk_eval_constraints(zk_trace_lde *h, const zk_pub_inputs *pub, const uint8_t
     ZK_CHECK_HIP(hipMemcpyAsync(p->air_consts, &K, sizeof K, hipMemcpyHostToDevice, p->st));
     const fe *binv = boundary_inverses(p, pl);
     if (!binv) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "boundary divisor table");
-    eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->periodic, binv, (const AirConsts *)p->air_consts,
-                     p->comp);
+    ZK_CHECK_HIP(eval_constraints(p->st, p->lde, pl->log_n, pl->log_b, pl->periodic, binv, (const AirConsts *)p->air_consts,
+                                  p->comp));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     coset_major_rows_to_host(p, p->comp, 1, n, 8, out);
     return ZK_OK;

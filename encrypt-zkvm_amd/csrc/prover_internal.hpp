@@ -40,6 +40,8 @@ extern thread_local std::string g_err;
     } while (0)
 
 static constexpr int W = ZK_TRACE_WIDTH;
+// a host-resident trace is uploaded in up to this many column groups (trace_lde_commit)
+static constexpr int ZK_UPLOAD_GROUPS_MAX = 7;
 static constexpr int NUM_TCONS = 20;
 static constexpr int NUM_ASSERTS = 22;
 
@@ -92,10 +94,10 @@ struct Openings;
 struct zk_prover {
     int device = 0;
     hipStream_t st = nullptr;
-    // second stream: row hashing of finished LDE cosets runs beside the NTT of the next ones (the NTT is
-    // bound by carry-writing VALU issue, BLAKE3 by 3-source ops: co-resident waves fill each other's gaps)
+    // copy stream: a host-resident trace is uploaded here in column groups, each group's event gating its
+    // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it
     hipStream_t st2 = nullptr;
-    hipEvent_t ev_fork[8] = {}, ev_join = nullptr;
+    hipEvent_t ev_up[zk::ZK_UPLOAD_GROUPS_MAX] = {}, ev_free = nullptr;
     size_t max_n = 0;
     uint32_t max_b = 0;
     zk::DeviceArena arena;
@@ -110,7 +112,8 @@ struct zk_prover {
     // Pinned host staging for the small transfers on a proof's critical path (constants up; roots, the
     // degree flag, OOD values, FRI results down).  hipMemcpyAsync from or to pageable memory is staged
     // synchronously by the runtime (~20 us each between kernels); from pinned memory it is a DMA in
-    // stream order.  Bump-allocated and rewound only by d2h_flush, after a stream sync, so no region is
+    // stream order (uploads); reads are copied by one kernel at d2h_flush time, so a read's device source
+    // must stay unchanged from d2h_small until that flush.  Bump-allocated and rewound only by d2h_flush, after a stream sync, so no region is
     // reused while a copy from it may still be in flight.
     struct PendingRead {
         void *dst;              // caller's host destination (written by d2h_flush)
@@ -181,7 +184,8 @@ inline int h2d_small(zk_prover *p, void *dst_dev, const void *src, size_t len) {
 #define ZK_COPY_KERNEL 1  // A/B switch: 0 = one runtime hipMemcpyAsync (blit kernel) per read
 #endif
 // queue a device -> host read of len bytes (len % 4 == 0, src 4-byte aligned); dst is written by the
-// next d2h_flush.  Nothing is enqueued yet: the flush copies every pending read in one kernel.
+// next d2h_flush.  Nothing is enqueued yet: the flush copies every pending read in one kernel, so src_dev must
+// hold the value to read until that flush (no later kernel in the stream may overwrite it before then).
 inline int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
     if ((len & 3) || ((uintptr_t)src_dev & 3)) ZK_FAIL(ZK_ERR_INVALID_ARG, "d2h_small: unaligned read");
     if (p->io_pending.size() >= ZK_COPY_LIST_MAX) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "too many pending reads");
@@ -206,7 +210,13 @@ inline int d2h_flush(zk_prover *p) {
             L.words[i] = (uint32_t)(r.len / 4);
             words = std::max(words, r.len / 4);
         }
-        copy_to_host(p->st, L, words);
+        const hipError_t le = copy_to_host(p->st, L, words);
+        if (le != hipSuccess) {
+            (void)hipStreamSynchronize(p->st);
+            p->io_pending.clear();
+            p->io_used = 0;
+            ZK_CHECK_HIP(le);
+        }
     }
     const hipError_t e = hipStreamSynchronize(p->st);
     if (e == hipSuccess)

@@ -343,12 +343,12 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         const EvalMap em{Bl, X.rank[l], G, 0, Bl};
         if (KX == 1) {
             ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
-            eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                    (const AirConsts *)p->air_consts, p->comp);
+            ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
+                                                 (const AirConsts *)p->air_consts, p->comp));
         } else {
             ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
-            eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                        (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp);
+            ZK_CHECK_HIP(eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
+                                                     (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp));
         }
     }
     stage_mark(P0, "constraints");

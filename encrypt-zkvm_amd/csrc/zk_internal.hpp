@@ -163,7 +163,7 @@ struct CopyList {
     uint32_t *dst[ZK_COPY_LIST_MAX];
     uint32_t words[ZK_COPY_LIST_MAX];
 };
-void copy_to_host(hipStream_t st, const CopyList &L, size_t max_words);
+hipError_t copy_to_host(hipStream_t st, const CopyList &L, size_t max_words);
 void gather_digests(hipStream_t st, const uint8_t *src, const uint64_t *idx, size_t k, uint8_t *out);
 // out[q*ncols + c] = element (c, pos[q]) of a coset-major column set
 void gather_rows(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, const uint64_t *pos, size_t k,
@@ -204,7 +204,7 @@ struct EvalMap {
 // zk_prover_create calls it; the evaluator launches check it again (the plug point may run first).
 hipError_t upload_rescue_consts(hipStream_t st);
 // bnd: the boundary (assertion) terms are evaluated per row (else: boundary_poly_add after interpolation)
-void eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+hipError_t eval_constraints_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                              const fe *divs, const AirConsts *consts_dev, fe *comp, bool bnd = true);
 // Inputs of the cross-coset step for coefficients k0 .. k0+kcount: c[r][kl] = c_r[k0 + kl]; output
 // polys[k2 * pstride + kl].
@@ -220,7 +220,7 @@ void comp_cross_mapped(hipStream_t st, const CrossMap &m, const NttTables &T8n, 
                        fe w8inv, fe inv3n, int ncols, fe *polys, unsigned *nonzero_flag);
 // composition evaluations over the CE domain (8n), written coset-major: comp[r*n + q], i = 8q + r
 // nce: evaluate CE cosets 0 .. nce-1 (8: all; 7: the composition stage derives the last one, bnd = false)
-void eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+hipError_t eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                       const AirConsts *consts_dev, fe *comp, bool bnd = true, int nce = 8);
 // add the boundary terms' quotient polynomial (one coefficient plane K) into col0 (n coefficients);
 // c = g^(n-2); scratch: deep_poly's layout; sets *flag when an assertion fails
@@ -287,10 +287,10 @@ void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev
 void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
                   fe *tab, fe *partials, fe *out);
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
-void eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
+hipError_t eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                           const AirConsts *consts2_dev, fe *comp, bool bnd = true, int nce = 8);
 // ... over the CE cosets of `map` (see eval_constraints_mapped), b plane at comp + plane
-void eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
+hipError_t eval_constraints_ext_mapped(hipStream_t st, const fe *lde, int log_n, EvalMap map, const fe *periodic,
                                  const fe *divs, const AirConsts *consts2_dev, size_t plane, fe *comp, bool bnd = true);
 // out[i] = 1 / (N(x_i - z) N(x_i - zg)), N the norm E -> F (coset-major like batch_inv_pairs)
 void batch_inv_norm_pairs(hipStream_t st, const NttTables &Tn, const fe *xr, int log_b, int log_n, fe2 z, fe2 zg,

@@ -29,7 +29,8 @@ MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 3
 # every symbol include/zkvm_gpu.h declares (checked by tests/test_native_abi.py)
 EXPORTED = (
     "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_destroy", "zk_prover_trace_buffer",
-    "zk_prove", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
+    "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
+    "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_vm_trace",
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_destroy", "zk_prove_sharded",
 )
@@ -90,6 +91,15 @@ def lib():
         L.zk_prover_destroy.restype = None
         L.zk_prover_trace_buffer.argtypes = [vp, C.POINTER(vp)]
         L.zk_prove.argtypes = [vp, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp, C.POINTER(sz)]
+        L.zk_prove_columns.argtypes = [vp, C.POINTER(vp), sz, C.POINTER(Options), C.POINTER(PubInputs), vp,
+                                       C.POINTER(sz)]
+        L.zk_prove_columns_ex.argtypes = [vp, C.POINTER(vp), sz, C.POINTER(Options), C.POINTER(PubInputs), vp,
+                                          C.POINTER(sz), C.POINTER(Record), C.POINTER(Dump)]
+        L.zk_host_alloc.argtypes = [sz, C.POINTER(vp)]
+        L.zk_host_free.argtypes = [vp]
+        L.zk_host_free.restype = None
+        L.zk_host_register.argtypes = [vp, sz]
+        L.zk_host_unregister.argtypes = [vp]
         L.zk_prove_device.argtypes = [vp, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp, C.POINTER(sz),
                                       C.POINTER(Record), C.POINTER(Dump)]
         L.zk_lde_new.argtypes = [vp, vp, sz, sz, u32, C.POINTER(vp), vp]

@@ -85,6 +85,27 @@ class GpuProver:
 
     def prove_device(self, d_trace: int, n: int, pub: PubInputs, options: ProofOptions = REFERENCE_OPTIONS,
                      record: bool = False, dump=(), allow_degree_error=False):
+        """zk_prove_device: the trace is already in this prover's HBM (upload_trace)."""
+        return self._prove(lambda *a: lib().zk_prove_device(self.handle, d_trace, n, *a), n, pub, options, record,
+                           dump, allow_degree_error)
+
+    def prove_host(self, trace: np.ndarray, pub: PubInputs, options: ProofOptions = REFERENCE_OPTIONS,
+                   record: bool = False, dump=(), allow_degree_error=False):
+        """zk_prove_columns_ex: the trace is a (28, n, 2) uint64 host array (pinned -- HostTrace -- or
+        pageable); the library uploads it column group by column group, overlapped with the interpolation."""
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        assert trace.ndim == 3 and trace.shape[0] == 28 and trace.shape[2] == 2
+        n = trace.shape[1]
+        if getattr(self, "_cols", None) is None:
+            self._cols = (C.c_void_p * 28)()
+        cols = self._cols
+        base, stride = trace.ctypes.data, trace.strides[0]
+        for c in range(28):
+            cols[c] = base + c * stride
+        return self._prove(lambda *a: lib().zk_prove_columns_ex(self.handle, cols, n, *a), n, pub, options, record,
+                           dump, allow_degree_error)
+
+    def _prove(self, call, n, pub, options, record, dump, allow_degree_error):
         opt = options.to_c()
         # one proof buffer per prover, reused across proofs (a fresh 4 MiB ctypes buffer per call was
         # ~0.15 ms of zero-fill and page faults between two proofs); only plen bytes are copied out
@@ -104,11 +125,10 @@ class GpuProver:
             for name in dump:
                 held[name] = np.zeros((sizes[name], 2), dtype=np.uint64)
                 setattr(dmp, name, held[name].ctypes.data)
-        rc = lib().zk_prove_device(self.handle, d_trace, n, C.byref(opt), C.byref(pub), buf, C.byref(plen),
-                                   C.byref(rec) if rec is not None else None,
-                                   C.byref(dmp) if dmp is not None else None)
+        rc = call(C.byref(opt), C.byref(pub), buf, C.byref(plen), C.byref(rec) if rec is not None else None,
+                  C.byref(dmp) if dmp is not None else None)
         if not (rc == 0 or (allow_degree_error and rc == native.ZK_ERR_DEGREE)):
-            check(rc, "zk_prove_device")
+            check(rc, "prove")
         return C.string_at(buf, plen.value), rec, held, rc
 
     def upload_trace(self, trace: np.ndarray) -> tuple[int, int]:
@@ -127,8 +147,10 @@ class GpuProver:
         return d, n
 
     def prove(self, trace: np.ndarray, pub: PubInputs, options: ProofOptions = REFERENCE_OPTIONS, **kw):
-        d, n = self.upload_trace(trace)
-        return self.prove_device(d, n, pub, options, **kw)
+        """Prover::prove(trace) with a host-resident trace (the reference's call shape, vm/src/lib.rs:26)."""
+        if trace.shape[1] > self.max_trace_len:
+            raise ZkError(native.ZK_ERR_INVALID_ARG, "trace longer than max_trace_len")
+        return self.prove_host(trace, pub, options, **kw)
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 32)()
@@ -164,6 +186,38 @@ class GpuProver:
         check(lib().zk_prover_kernel_stats(self.handle, names, ms, nl, by, 64, C.byref(cnt)))
         check(lib().zk_prover_kernel_ops(self.handle, mu, ad, 64, C.byref(cnt)))
         return {names[i].decode(): (mu[i], ad[i]) for i in range(min(cnt.value, 64)) if mu[i] or ad[i]}
+
+
+class HostTrace:
+    """A (28, n, 2) uint64 trace array in page-locked host memory (zk_host_alloc): the VM writes into it
+    (vm_trace(..., out=...)) and zk_prove DMAs it at the link rate.  Free with close() (or a with-block)."""
+
+    def __init__(self, n: int):
+        p = C.c_void_p()
+        nbytes = 28 * n * 16
+        check(lib().zk_host_alloc(nbytes, C.byref(p)), "zk_host_alloc")
+        self.ptr = p
+        self.n = n
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=np.uint64).reshape(28, n, 2)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            lib().zk_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _hip_lib = None
@@ -208,9 +262,10 @@ def verify(proof: bytes, pub: PubInputs, min_security: int = 95) -> tuple[int, s
     return rc, msg.value.decode()
 
 
-def vm_trace(source: str, public, secret, server_key, last_row):
+def vm_trace(source: str, public, secret, server_key, last_row, out=None):
     """Processor::run + trace (vm/src/processor/mod.rs:61-95) via the native VM.
-    Returns (trace (28, n, 2) uint64, outputs[16], program_hash[2])."""
+    Returns (trace (28, n, 2) uint64, outputs[16], program_hash[2]).  out: an optional HostTrace (or a
+    C-contiguous (28, n, 2) uint64 array) of exactly the trace's length to write the trace into."""
     L = server_key.lwe_size()
     sec = elems_bytes([v for ct in secret for v in ct])
     nops_hint = 16 * len(source) + 64
@@ -226,7 +281,12 @@ def vm_trace(source: str, public, secret, server_key, last_row):
                            server_key.parameters.delta, elems_bytes(last_row), None, 0, C.byref(n), outputs, h)
     if rc not in (0, native.ZK_ERR_BUFFER_TOO_SMALL):
         raise ZkError(rc, lib().zk_vm_last_error().decode())
-    trace = np.zeros((28, n.value, 2), dtype=np.uint64)
+    if out is None:
+        trace = np.zeros((28, n.value, 2), dtype=np.uint64)
+    else:
+        trace = out.array if isinstance(out, HostTrace) else out
+        if trace.shape != (28, n.value, 2) or trace.dtype != np.uint64 or not trace.flags.c_contiguous:
+            raise ZkError(native.ZK_ERR_INVALID_ARG, f"out must be a contiguous (28, {n.value}, 2) uint64 array")
     rc = lib().zk_vm_trace(source.encode(), bytes(public), len(public), sec, len(secret), L,
                            server_key.parameters.delta, elems_bytes(last_row), trace.ctypes.data, n.value,
                            C.byref(n), outputs, h)

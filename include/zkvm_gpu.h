@@ -49,7 +49,8 @@ extern "C" {
 
 /* ProofOptions::new(num_queries, blowup, grinding, field_extension, fri_folding, fri_rem_max_deg)
  * -- the reference hard-codes (32, 8, 0, None, 8, 127) at vm/src/lib.rs:20.
- * field_extension: 1 = FieldExtension::None (the only value this build accepts). */
+ * field_extension: 1 = FieldExtension::None, 2 = FieldExtension::Quadratic; 3 (Cubic) is refused
+ * with ZK_ERR_INVALID_ARG (winter-math implements no cubic extension of f128). */
 typedef struct {
     uint32_t num_queries;
     uint32_t blowup;
@@ -111,7 +112,11 @@ typedef struct zk_trace_lde zk_trace_lde;
 const char *zk_last_error(void);
 int zk_device_count(int *count);
 
-/* ---- prover object: device memory sized for traces up to max_trace_len rows ---- */
+/* ---- prover object: device memory sized for traces up to max_trace_len rows ----
+ * Process-wide side effect: the first zk_prover_create on a device that the process has not used yet
+ * sets hipDeviceScheduleSpin for that device, so every host thread waiting on a stream of that device
+ * (this library's transcript round trips, and any other code's syncs) busy-spins instead of yielding
+ * (-0.05 ms per 2^20 proof).  Set ZK_SPIN_WAIT=0 in the environment to keep the runtime's default. */
 int zk_prover_create(int device, size_t max_trace_len, uint32_t max_blowup, zk_prover **out);
 void zk_prover_destroy(zk_prover *p);
 /* device pointer to a scratch region large enough for a 28 x max_trace_len trace (so callers can
@@ -119,9 +124,27 @@ void zk_prover_destroy(zk_prover *p);
 int zk_prover_trace_buffer(zk_prover *p, void **d_trace);
 
 /* Prover::prove (vm/src/lib.rs:26 -> winterfell generate_proof), whole proof.
- * Host trace variant: trace is 28 x n, column-major, host memory. */
+ * Host trace variant: trace is 28 x n, column-major, host memory.  The trace goes up in column groups on
+ * a copy stream, each group's interpolation and coset LDE starting as soon as it is in HBM.  From
+ * page-locked memory (zk_host_alloc / zk_host_register) the copies are DMAs at the link rate; pageable
+ * memory works too, staged by the HIP runtime at a lower rate.  The trace is not read after return. */
 int zk_prove(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
              uint8_t *proof_out, size_t *proof_len);
+/* The same with one pointer per column (n * 16 bytes each): winterfell's ColMatrix / TraceTable keeps
+ * every column in its own Vec<f128> (vm/src/lib.rs:18), which binds here without a flattening copy. */
+int zk_prove_columns(zk_prover *p, const uint8_t *const *columns, size_t n, const zk_options *opt,
+                     const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len);
+/* ... with the optional record / dumps of zk_prove_device */
+int zk_prove_columns_ex(zk_prover *p, const uint8_t *const *columns, size_t n, const zk_options *opt,
+                        const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len, zk_record *rec,
+                        const zk_dump *dump);
+/* Page-locked host memory for traces (hipHostMalloc, usable from every device), e.g. the buffer the
+ * VM writes its trace into (zk_vm_trace), and page-locking of a caller's own buffer (hipHostRegister:
+ * costs about as much as one copy of it, so register buffers that are reused). */
+int zk_host_alloc(size_t bytes, void **ptr);
+void zk_host_free(void *ptr);
+int zk_host_register(void *ptr, size_t bytes);
+int zk_host_unregister(void *ptr);
 /* Device trace variant (trace already resident in HBM on this prover's device), with optional
  * record / dumps.  proof_len is in/out: capacity in, bytes written out; ZK_ERR_BUFFER_TOO_SMALL
  * reports the needed size. */

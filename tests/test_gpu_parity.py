@@ -122,6 +122,29 @@ def test_ntt_four_step_splits(oracle, log_n):
     assert out.raw == buf.raw, "inverse NTT differs"
 
 
+@pytest.mark.parametrize("log_n", [20, 21, 22])
+def test_ntt_lazy_edge_values(oracle, log_n):
+    """Columns drawn from {0, 1, 2, p - 2, p - 1}: pass-1 butterfly sums such as (p - 1) + 2 = p + 1 stay
+    partially reduced in the tile (ZK_NTT_LAZY), and the wave-uniform j = 0 rounds, which skip their unit
+    twiddle multiplies, must still hand canonical second operands to the lazy add / subtract (a
+    later j = 0 wave computed 0 - (p + 1) wrongly).  Random canonical data almost never reaches those values,
+    so the inverse (trace interpolation) and the forward coset transform are checked on such columns."""
+    n = 1 << log_n
+    rng = np.random.default_rng(100 + log_n)
+    pick = np.array([[0, 0], [1, 0], [2, 0], [(P - 2) % 2**64, (P - 2) >> 64], [(P - 1) % 2**64, (P - 1) >> 64]],
+                    dtype=np.uint64)
+    vals = pick[rng.integers(0, 5, size=n)].tobytes()
+    out = C.create_string_buffer(16 * n)
+    native.check(native.lib().zk_diag_ntt(0, vals, n, 1, 1, None, out))
+    buf = C.create_string_buffer(vals, 16 * n)
+    assert oracle.lib().or_interp_coset(buf, n, elems_bytes([1])) == 0
+    assert out.raw == buf.raw, "inverse NTT differs on edge-valued input"
+    native.check(native.lib().zk_diag_ntt(0, vals, n, 1, 0, elems_bytes([3]), out))
+    ref = C.create_string_buffer(16 * n)
+    assert oracle.lib().or_eval_coset(vals, n, n, elems_bytes([3]), ref) == 0
+    assert out.raw == ref.raw, "forward coset NTT differs on edge-valued input"
+
+
 def workload_trace(source, seed=3):
     w = make_workload(source, seed=seed)
     trace, outputs, h = vm_trace(source, w.public, w.secret, w.server_key, w.last_row)

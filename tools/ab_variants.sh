@@ -7,12 +7,13 @@ O=gpurun_out
 mkdir -p "$O"
 for v in "$@"; do
   if [ "$v" = base ]; then lib=encrypt-zkvm_amd/lib/libzkvm_gpu.so; else lib=encrypt-zkvm_amd/lib/libzkvm_gpu_$v.so; fi
-  ZKVM_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-verify --steps 5 --warmup 2 ${BENCH_ARGS:-} \
+  ZKVM_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-verify --steps ${AB_STEPS:-20} --warmup 6 ${BENCH_ARGS:-} \
     > "$O/ab_$v.json" 2> "$O/ab_$v.err" || { echo "$v FAILED"; tail -5 "$O/ab_$v.err"; exit 1; }
   python3 - "$v" "$O/ab_$v.json" <<'PY'
 import json, sys
 b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 k = b.get("kernel_ms", {})
-print(f"{sys.argv[1]:>12} {b['ms_per_step']:8.3f} ms  " + " ".join(f"{n}={v}" for n, v in list(k.items())[:6]))
+print(f"{sys.argv[1]:>12} {b['ms_per_step']:8.3f} ms  latency {b.get('latency_ms')} device {b.get('device_resident_ms')} "
+      f"pageable {b.get('pageable_host_ms')}  " + " ".join(f"{n}={v}" for n, v in list(k.items())[:4]))
 PY
 done
