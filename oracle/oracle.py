@@ -14,7 +14,8 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "liboracle.so"
+# ORACLE_LIB selects another build of the same sources (tests/test_asan.py: the sanitizer build)
+LIB_PATH = Path(os.environ.get("ORACLE_LIB", HERE / "liboracle.so"))
 P = 2**128 - 45 * 2**40 + 1
 MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 32, 16, 16, 256, 255
 
@@ -52,6 +53,8 @@ class Dump(C.Structure):
 
 
 def build(force: bool = False) -> Path:
+    if "ORACLE_LIB" in os.environ:
+        return LIB_PATH
     if force or not LIB_PATH.exists() or any(
             p.stat().st_mtime > LIB_PATH.stat().st_mtime for p in HERE.glob("*.[ch]")):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)

@@ -1,0 +1,96 @@
+"""Sanitizer build of the host code that parses untrusted input.
+
+`make asan` (encrypt-zkvm_amd/ and oracle/) builds the proof verifier and the assembler / VM with
+AddressSanitizer + UndefinedBehaviorSanitizer: csrc/verifier.cpp and csrc/vm.cpp inside a drop-in copy of the
+library (lib/libzkvm_host_asan.so) and all of oracle/*.c (liboracle_asan.so), plus one fuzz driver per target
+(tools/asan/fuzz_verify.c).  Here, on the CPU:
+  * every golden proof (tests/golden, and the full-size pins under tests/golden/large) goes through zk_verify and
+    or_verify whole, truncated at every length up to 4 KiB and at a stride beyond, with random single-byte
+    changes and as random garbage -- the originals must verify, nothing else may, and no sanitizer may fire;
+  * mutated program texts go through the assembler and the VM of both;
+  * the CPU tests that exercise those parsers (golden proofs, wire formats, oracle VM / AIR) run again with the
+    sanitized libraries loaded in place of the normal ones.
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "encrypt-zkvm_amd"
+GOLD = ROOT / "tests" / "golden"
+SAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1:abort_on_error=0",
+           "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+
+
+def _asan_runtime():
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    try:
+        out = subprocess.run([hipcc, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True, text=True,
+                             timeout=60).stdout.strip()
+    except (OSError, subprocess.TimeoutExpired):
+        return None
+    return out if out and Path(out).is_file() else None
+
+
+@pytest.fixture(scope="module")
+def asan_builds():
+    rt = _asan_runtime()
+    if rt is None:
+        pytest.skip("no clang AddressSanitizer runtime in this image")
+    subprocess.run(["make", "-s", "-C", str(PKG), "-j", "4", "asan"], check=True, timeout=1800)
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "asan"], check=True, timeout=600)
+    return rt
+
+
+def _pub_bytes(program_hash, stack_outputs, lwe_size=5, delta=16) -> bytes:
+    b = b"".join(int(v, 16).to_bytes(16, "little") for v in program_hash)
+    b += b"".join(int(v, 16).to_bytes(16, "little") for v in stack_outputs[:16])
+    return b + lwe_size.to_bytes(4, "little") + delta.to_bytes(4, "little")
+
+
+def _cases_file(tmp: Path) -> Path:
+    lines = []
+    small = json.loads((GOLD / "cases.json").read_text())["cases"]
+    for c in small:
+        pub = tmp / f"{c['name']}.pub"
+        pub.write_bytes(_pub_bytes(c["program_hash"], c["stack_outputs"], c["lwe_size"], c["delta"]))
+        lines.append(f"{GOLD / (c['name'] + '.proof')} {pub} 0")
+    large = GOLD / "large" / "cases.json"
+    if large.exists():
+        for c in json.loads(large.read_text())["cases"]:
+            pub = tmp / f"{c['name']}.pub"
+            pub.write_bytes(_pub_bytes(c["program_hash"], c["stack_outputs"]))
+            lines.append(f"{GOLD / 'large' / (c['name'] + '.proof')} {pub} {c['min_security']}")
+    f = tmp / "cases.txt"
+    f.write_text("\n".join(lines) + "\n")
+    return f
+
+
+@pytest.mark.parametrize("target", ["product", "oracle"])
+def test_fuzz_verifier_and_assembler_under_sanitizers(asan_builds, tmp_path, target):
+    exe = PKG / "build_asan" / "fuzz_verify" if target == "product" else ROOT / "oracle" / "fuzz_verify_asan"
+    cases = _cases_file(tmp_path)
+    r = subprocess.run([str(exe), str(cases), "20261017", "40"], capture_output=True, text=True, timeout=900,
+                       env={**os.environ, **SAN_ENV})
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "fuzz_verify: ok" in r.stdout and "ERROR: AddressSanitizer" not in out and "runtime error" not in out, \
+        out[-4000:]
+
+
+def test_cpu_suite_under_sanitizers(asan_builds):
+    """The parser-facing CPU tests with the sanitized libraries loaded in place of the normal ones."""
+    env = {**os.environ, **SAN_ENV, "LD_PRELOAD": asan_builds,
+           "ZKVM_GPU_LIB": str(PKG / "lib" / "libzkvm_host_asan.so"),
+           "ORACLE_LIB": str(ROOT / "oracle" / "liboracle_asan.so")}
+    tests = ["tests/test_golden.py", "tests/test_wire.py", "tests/test_oracle_vm_air.py", "tests/test_oracle_core.py"]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider", *tests],
+                       cwd=ROOT, capture_output=True, text=True, timeout=1800, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-6000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out, out[-6000:]
