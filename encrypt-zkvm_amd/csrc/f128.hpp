@@ -556,13 +556,10 @@ __device__ __forceinline__ fe fe_mul(fe a, fe b) { return fe_mul_asm(a, b); }
 // host: unsigned __int128 with the same two folds
 __host__ static inline fe fe_from_u128(unsigned __int128 v) { return fe{(uint64_t)v, (uint64_t)(v >> 64)}; }
 __host__ static inline unsigned __int128 fe_to_u128(fe a) { return ((unsigned __int128)a.hi << 64) | a.lo; }
-__host__ static inline fe fe_mul(fe a, fe b) {
+// hi * 2^128 + lo (mod p) for any 256-bit value
+__host__ static inline fe fe_reduce_wide(unsigned __int128 lo, unsigned __int128 hi) {
     typedef unsigned __int128 u128;
     const u128 P = ((u128)ZK_P_HI << 64) | ZK_P_LO;
-    const u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
-    const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
-    const u128 lo = (mid << 64) | (uint64_t)p00;
-    const u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);  // product = hi * 2^128 + lo
     // 2^128 = C (mod p), C < 2^46: lo + hi*C = s2 + top * 2^128 with top < 2^47, then fold once more
     const u128 t0 = (u128)(uint64_t)hi * ZK_C, t1 = (u128)(uint64_t)(hi >> 64) * ZK_C;
     const u128 s1 = lo + t0;
@@ -572,6 +569,23 @@ __host__ static inline fe fe_mul(fe a, fe b) {
     if (r < s2) r += ZK_C;  // wrapped past 2^128: + 2^128 = + C (mod p); cannot wrap again
     if (r >= P) r -= P;
     return fe_from_u128(r);
+}
+__host__ static inline fe fe_mul(fe a, fe b) {
+    typedef unsigned __int128 u128;
+    const u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
+    const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+    const u128 lo = (mid << 64) | (uint64_t)p00;
+    const u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);  // product = hi * 2^128 + lo
+    return fe_reduce_wide(lo, hi);
+}
+// a^2 with three 64 x 64 products (the cross product once, doubled)
+__host__ static inline fe fe_sqr_host(fe a) {
+    typedef unsigned __int128 u128;
+    const u128 p00 = (u128)a.lo * a.lo, p01 = (u128)a.lo * a.hi, p11 = (u128)a.hi * a.hi;
+    const u128 mid = (p00 >> 64) + (u128)(uint64_t)p01 * 2;  // < 3 * 2^64
+    const u128 lo = (mid << 64) | (uint64_t)p00;
+    const u128 hi = p11 + (p01 >> 64) * 2 + (mid >> 64);
+    return fe_reduce_wide(lo, hi);
 }
 
 ZK_HD fe fe_sqr(fe a) { return fe_mul(a, a); }

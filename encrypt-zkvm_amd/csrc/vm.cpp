@@ -11,7 +11,12 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <stdlib.h>
+
+#include <algorithm>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zkvm_gpu.h"
@@ -54,7 +59,7 @@ fe mds(const uint64_t m[16][2], int i) { return fe_make(m[i][0], m[i][1]); }
 // multiply chains (~4.4 ns per product instead of ~10 for one chain).
 __attribute__((noinline)) void sqn4(fe v[4], int k) {  // v^(2^k)
     for (int t = 0; t < k; t++)
-        for (int i = 0; i < 4; i++) v[i] = fe_mul(v[i], v[i]);
+        for (int i = 0; i < 4; i++) v[i] = fe_sqr_host(v[i]);
 }
 __attribute__((noinline)) void mul4(fe v[4], const fe w[4]) {
     for (int i = 0; i < 4; i++) v[i] = fe_mul(v[i], w[i]);
@@ -224,121 +229,244 @@ int compile(const std::string &src, std::vector<Op> &code) {
     return ZK_OK;
 }
 
-// Processor::run -> trace.  Column-major output (28 x n).
-struct Processor {
+// ---------------------------------------------------------------- compiled program (Program::compile)
+// The chiplet's sponge (columns 7-10 of the trace) absorbs (op code, op value) of every step and nothing else
+// (vm/src/processor/chiplets.rs; crypto/src/rescue.rs:102-118): it is a function of the compiled code alone, and
+// its final state is Program::compile's hash (vm/src/program/mod.rs:88-95).  The reference hashes the code at
+// compile time and runs the same sponge again inside every Processor::run; here the compiled program keeps the
+// per-step states it computed for the hash, so a run of the program on new inputs (the per-proof step) is the
+// stack machine and the column writes only, split over threads.
+struct CompiledProgram {
+    std::vector<Op> code;
+    std::vector<fe> sponge[4];  // state after step k (k = 0..len; k = 0 is the zero state), per lane
+    fe hash[2];
+    size_t chiplet_err = 0;     // 1-based step of a non-noop op on a non-round step (0: none)
+    size_t trace_len = 0;       // Processor::trace length (power of two)
+};
+
+int build_program(const char *source, CompiledProgram &P) {
+    int rc = compile(source, P.code);
+    if (rc) return rc;
+    const size_t len = P.code.size();
+    for (auto &v : P.sponge) v.resize(len + 1);
+    for (int i = 0; i < 4; i++) P.sponge[i][0] = fe_zero();
+    Rescue r;
+    for (size_t k = 0; k < len; k++) {
+        const Op o = P.code[k];
+        if (!r.is_round() && o.code != NOOP && !P.chiplet_err) P.chiplet_err = k + 1;
+        r.update(o.code, o.value);
+        for (int i = 0; i < 4; i++) P.sponge[i][k + 1] = r.s[i];
+    }
+    P.hash[0] = r.s[0];
+    P.hash[1] = r.s[1];
+    // Processor::grow doubles the capacity past clk; trace_len() is the next power of two above it
     size_t cap = MIN_TRACE;
-    size_t clk = 0, depth = 0;
-    std::vector<std::vector<fe>> reg = std::vector<std::vector<fe>>(MAX_STACK, std::vector<fe>(MIN_TRACE, fe_zero()));
-    std::vector<fe> helper = std::vector<fe>(MIN_TRACE, fe_zero());
-    std::vector<std::vector<fe>> bits = std::vector<std::vector<fe>>(5, std::vector<fe>(MIN_TRACE, fe_zero()));
-    std::vector<fe> hflag = std::vector<fe>(MIN_TRACE, fe_zero());
-    std::vector<std::vector<fe>> sponge = std::vector<std::vector<fe>>(4, std::vector<fe>(MIN_TRACE, fe_zero()));
-    Rescue rescue;
+    while (len >= cap) cap *= 2;
+    size_t n = 1;
+    while (n < cap + 1) n *= 2;
+    P.trace_len = n;
+    return ZK_OK;
+}
 
-    void grow() {
-        if (clk < cap) return;
-        cap *= 2;
-        for (auto &c : reg) c.resize(cap, fe_zero());
-        helper.resize(cap, fe_zero());
-        for (auto &c : bits) c.resize(cap, fe_zero());
-        hflag.resize(cap, fe_zero());
-        for (auto &c : sponge) c.resize(cap, fe_zero());
-    }
+// ---------------------------------------------------------------- Processor::run -> trace
+// The stack machine (vm/src/processor/stack.rs; the ciphertext ops of fhe/src/server_key.rs:89-124) on a small
+// register file.  Pass 1 runs it once over the whole program, sequentially (each step reads the previous one),
+// checks every error the reference raises and keeps the state at chunk boundaries; pass 2 replays the chunks on
+// T threads, each writing its own rows of all 28 columns straight into the caller's column-major trace.
+struct StackState {
+    fe reg[MAX_STACK];
+    size_t depth = 0, ta = 0, tb = 0;
+};
 
-    int run(const std::vector<Op> &code, const uint8_t *pub, size_t npub, const fe *sec, size_t nsec, uint32_t L,
-            uint32_t delta) {
-        size_t ta = 0, tb = 0;
-        for (const Op &o : code) {
-            clk++;
-            grow();
-            auto R = [&](size_t i, size_t c) -> fe & { return reg[i][c]; };
-            auto stack_err = [&](const char *what) {
-                vm_err = "stack error at " + std::to_string(clk) + ": " + what;
-                return ZK_ERR_STACK;
-            };
-            switch (o.code) {
-            case NOOP:
-                for (size_t i = 0; i < depth; i++) R(i, clk) = R(i, clk - 1);
-                break;
-            case PUSH:
-            case READ:
-            case READ2: {
-                size_t cnt = o.code == READ2 ? L : 1;
-                if (o.code == READ2 && tb >= nsec) return stack_err(("no more inputs to " + op_str(o)).c_str());
-                depth += cnt;
-                if (depth > (size_t)MAX_STACK) return stack_err((op_str(o) + " operation stack overflow").c_str());
-                if (o.code == READ && ta >= npub) return stack_err(("no more inputs to " + op_str(o)).c_str());
-                for (size_t i = 0; i < depth - cnt; i++) R(i + cnt, clk) = R(i, clk - 1);
-                if (o.code == PUSH) R(0, clk) = fe_make(o.value);
-                else if (o.code == READ) R(0, clk) = fe_make(pub[ta++]);
-                else {
-                    for (size_t i = 0; i < L; i++) R(i, clk) = sec[tb * L + i];
-                    tb++;
-                }
-                break;
+struct Machine {
+    const uint8_t *pub;
+    size_t npub;
+    const fe *sec;
+    size_t nsec;
+    uint32_t L, delta;
+
+    // one step (clk is the 1-based step of op o, for the error texts); next := state after o
+    int step(const StackState &cur, StackState &nx, Op o, size_t clk) const {
+        auto stack_err = [&](const std::string &what) {
+            vm_err = "stack error at " + std::to_string(clk) + ": " + what;
+            return ZK_ERR_STACK;
+        };
+        nx.ta = cur.ta;
+        nx.tb = cur.tb;
+        size_t depth = cur.depth;
+        switch (o.code) {
+        case NOOP:
+            for (size_t i = 0; i < depth; i++) nx.reg[i] = cur.reg[i];
+            break;
+        case PUSH:
+        case READ:
+        case READ2: {
+            const size_t cnt = o.code == READ2 ? L : 1;
+            if (o.code == READ2 && cur.tb >= nsec) return stack_err("no more inputs to " + op_str(o));
+            depth += cnt;
+            if (depth > (size_t)MAX_STACK) return stack_err(op_str(o) + " operation stack overflow");
+            if (o.code == READ && cur.ta >= npub) return stack_err("no more inputs to " + op_str(o));
+            for (size_t i = 0; i < depth - cnt; i++) nx.reg[i + cnt] = cur.reg[i];
+            if (o.code == PUSH) nx.reg[0] = fe_make(o.value);
+            else if (o.code == READ) nx.reg[0] = fe_make(pub[nx.ta++]);
+            else {
+                for (size_t i = 0; i < L; i++) nx.reg[i] = sec[cur.tb * L + i];
+                nx.tb++;
             }
-            default: {
-                size_t need = (o.code == ADD || o.code == MUL) ? 2 : o.code == ADD2 ? 2 * L : L + 1;
-                size_t pos = o.code == ADD2 ? L : 1;
-                if (depth < need) return stack_err((op_str(o) + " operation stack underflow").c_str());
-                fe s0 = R(0, clk - 1);
-                if (o.code == ADD) R(0, clk) = fe_add(s0, R(1, clk - 1));
-                else if (o.code == MUL) R(0, clk) = fe_mul(s0, R(1, clk - 1));
-                else if (o.code == SADD) {  // ServerKey::scalar_add (fhe/src/server_key.rs:104-114)
-                    for (size_t i = 0; i < L; i++) {
-                        fe v = R(1 + i, clk - 1);
-                        if (i == L - 1) v = fe_add(v, fe_mul(fe_make(delta), s0));
-                        R(i, clk) = v;
-                    }
-                } else if (o.code == SMUL) {  // ServerKey::scalar_mul (server_key.rs:116-124)
-                    for (size_t i = 0; i < L; i++) R(i, clk) = fe_mul(R(1 + i, clk - 1), s0);
-                } else {  // ServerKey::add (server_key.rs:89-102)
-                    for (size_t i = 0; i < L; i++) R(i, clk) = fe_add(R(i, clk - 1), R(i + L, clk - 1));
-                }
-                for (size_t i = need; i < depth; i++) R(i - pos, clk) = R(i, clk - 1);  // shift_left
-                for (size_t i = depth - pos; i < depth; i++) R(i, clk) = fe_zero();
-                depth -= pos;
-            }
-            }
-            helper[clk] = fe_make(depth);
-            for (int i = 0; i < 5; i++) bits[i][clk - 1] = fe_make((o.code >> i) & 1);
-            if (!rescue.is_round() && o.code != NOOP) {
-                vm_err = "chiplets error at " + std::to_string(clk) + ": expected noop but was " + op_str(o);
-                return ZK_ERR_CHIPLETS;
-            }
-            rescue.update(o.code, o.value);
-            hflag[clk - 1] = fe_one();
-            for (int i = 0; i < 4; i++) sponge[i][clk] = rescue.s[i];
+            break;
         }
-        if (clk % CYCLE) {
-            vm_err = "chiplets error at " + std::to_string(clk) + ": trace length should be a multiple of 16, but was " +
-                     std::to_string(clk);
-            return ZK_ERR_CHIPLETS;
+        default: {
+            const size_t need = (o.code == ADD || o.code == MUL) ? 2 : o.code == ADD2 ? 2 * L : L + 1;
+            const size_t pos = o.code == ADD2 ? L : 1;
+            if (depth < need) return stack_err(op_str(o) + " operation stack underflow");
+            const fe s0 = cur.reg[0];
+            if (o.code == ADD) nx.reg[0] = fe_add(s0, cur.reg[1]);
+            else if (o.code == MUL) nx.reg[0] = fe_mul(s0, cur.reg[1]);
+            else if (o.code == SADD) {  // ServerKey::scalar_add (fhe/src/server_key.rs:104-114)
+                for (size_t i = 0; i < L; i++) {
+                    fe v = cur.reg[1 + i];
+                    if (i == L - 1) v = fe_add(v, fe_mul(fe_make(delta), s0));
+                    nx.reg[i] = v;
+                }
+            } else if (o.code == SMUL) {  // ServerKey::scalar_mul (server_key.rs:116-124)
+                for (size_t i = 0; i < L; i++) nx.reg[i] = fe_mul(cur.reg[1 + i], s0);
+            } else {  // ServerKey::add (server_key.rs:89-102)
+                for (size_t i = 0; i < L; i++) nx.reg[i] = fe_add(cur.reg[i], cur.reg[i + L]);
+            }
+            for (size_t i = need; i < depth; i++) nx.reg[i - pos] = cur.reg[i];  // shift_left
+            for (size_t i = depth - pos; i < depth; i++) nx.reg[i] = fe_zero();
+            depth -= pos;
         }
+        }
+        for (size_t i = depth; i < (size_t)MAX_STACK; i++) nx.reg[i] = fe_zero();
+        nx.depth = depth;
         return ZK_OK;
-    }
-
-    size_t trace_len() const {
-        size_t n = 1;
-        while (n < cap + 1) n *= 2;
-        return n;
-    }
-
-    void write(fe *t, size_t n, const fe *last) const {
-        for (size_t r = 0; r < n; r++) {
-            size_t rr = r <= clk ? r : clk;
-            t[r] = fe_make(r);
-            for (int i = 0; i < 5; i++) t[(1 + i) * n + r] = r <= clk ? bits[i][r] : fe_zero();
-            t[6 * n + r] = r <= clk ? hflag[r] : fe_zero();
-            for (int i = 0; i < 4; i++) t[(7 + i) * n + r] = sponge[i][rr];
-            t[11 * n + r] = helper[rr];
-            for (int i = 0; i < MAX_STACK; i++) t[(12 + i) * n + r] = reg[i][rr];
-        }
-        for (int c = 0; c < 28; c++) t[c * n + n - 1] = last[c];
     }
 };
 
+int vm_threads() {
+    const char *e = getenv("ZK_VM_THREADS");
+    if (!e) e = getenv("OMP_NUM_THREADS");
+    int t = e ? atoi(e) : 0;
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 64));
+}
+
+// rows [r0, r1) of the trace: row r holds clk = r (column 0), the bits / hash flag of op r (r < len), and the
+// sponge / depth / stack after step min(r, len); the last row is the caller's random row (processor/mod.rs:86-92)
+void write_rows(const CompiledProgram &P, const Machine &M, StackState st, size_t r0, size_t r1, fe *t, size_t n,
+                const fe *last) {
+    const size_t len = P.code.size();
+    StackState nx;
+    for (size_t r = r0; r < r1; r++) {
+        if (r == n - 1) {
+            for (int c = 0; c < 28; c++) t[c * n + r] = last[c];
+            continue;
+        }
+        if (r >= 1 && r <= len) {  // the state after step r
+            (void)M.step(st, nx, P.code[r - 1], r);  // pass 1 already ran every step without error
+            st = nx;
+        }
+        const size_t rr = r <= len ? r : len;
+        const Op o = r < len ? P.code[r] : Op{NOOP, 0};
+        t[r] = fe_make(r);
+        for (int i = 0; i < 5; i++) t[(1 + i) * n + r] = fe_make(r < len ? (o.code >> i) & 1 : 0);
+        t[6 * n + r] = r < len ? fe_one() : fe_zero();
+        for (int i = 0; i < 4; i++) t[(7 + i) * n + r] = P.sponge[i][rr];
+        t[11 * n + r] = fe_make(st.depth);
+        for (int i = 0; i < MAX_STACK; i++) t[(12 + i) * n + r] = st.reg[i];
+    }
+}
+
+int run_program(const CompiledProgram &P, const Machine &M, fe *t, size_t n, const fe *last, fe *outputs) {
+    const size_t len = P.code.size();
+    const int T = (int)std::min<size_t>((size_t)vm_threads(), std::max<size_t>(1, n / 4096));
+    // chunk c covers rows [bnd[c], bnd[c + 1]); pass 1 records the state after step bnd[c] - 1 ... i.e. the
+    // state row bnd[c] - 1 shows, from which write_rows steps forward
+    std::vector<size_t> bnd(T + 1);
+    for (int c = 0; c <= T; c++) bnd[c] = n * (size_t)c / (size_t)T;
+    std::vector<StackState> start(T);
+    StackState st, nx;
+    int c = 1;
+    for (size_t k = 1; k <= len; k++) {  // state after step k (row k)
+        while (c < T && bnd[c] - 1 < k) start[c++] = st;
+        int rc = M.step(st, nx, P.code[k - 1], k);
+        if (rc) return rc;
+        st = nx;
+        if (P.chiplet_err == k) {
+            vm_err = "chiplets error at " + std::to_string(k) + ": expected noop but was " + op_str(P.code[k - 1]);
+            return ZK_ERR_CHIPLETS;
+        }
+    }
+    while (c < T) start[c++] = st;
+    if (len % CYCLE) {
+        vm_err = "chiplets error at " + std::to_string(len) + ": trace length should be a multiple of 16, but was " +
+                 std::to_string(len);
+        return ZK_ERR_CHIPLETS;
+    }
+    if (outputs)
+        for (int i = 0; i < MAX_STACK; i++) outputs[i] = st.reg[i];
+    if (!t) return ZK_OK;
+    // chunk c starts at row bnd[c] with the state of row bnd[c] - 1 (write_rows steps once before writing
+    // a row in [1, len]); chunk 0 starts from the zero state at row 0
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; k++) th.emplace_back(write_rows, std::cref(P), std::cref(M), start[k], bnd[k], bnd[k + 1], t, n, last);
+    write_rows(P, M, StackState(), 0, bnd[1], t, n, last);
+    for (auto &x : th) x.join();
+    return ZK_OK;
+}
+
+int parse_inputs(const uint8_t *secret, size_t num_secret, uint32_t lwe_size, std::vector<fe> &sec) {
+    sec.resize(num_secret * lwe_size);
+    for (size_t i = 0; i < sec.size(); i++) sec[i] = fe_from_bytes(secret + 16 * i);
+    return ZK_OK;
+}
+
 }  // namespace
+
+struct zk_program {
+    CompiledProgram P;
+};
+
+extern "C" int zk_program_compile(const char *source, zk_program **out, uint8_t *program_hash, size_t *trace_len) {
+    if (!source || !out) return ZK_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto prog = std::make_unique<zk_program>();
+    const int rc = build_program(source, prog->P);
+    if (rc) return rc;
+    if (program_hash) {
+        fe_to_bytes(prog->P.hash[0], program_hash);
+        fe_to_bytes(prog->P.hash[1], program_hash + 16);
+    }
+    if (trace_len) *trace_len = prog->P.trace_len;
+    *out = prog.release();
+    return ZK_OK;
+}
+
+extern "C" void zk_program_free(zk_program *prog) { delete prog; }
+
+extern "C" int zk_program_trace(const zk_program *prog, const uint8_t *public_in, size_t num_public,
+                                const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                                const uint8_t *last_row, uint8_t *trace_out, size_t cap_rows, size_t *n_out,
+                                uint8_t *outputs) {
+    if (!prog || !last_row || !n_out || lwe_size == 0 || lwe_size > 15 || (num_secret && !secret) ||
+        (num_public && !public_in))
+        return ZK_ERR_INVALID_ARG;
+    const CompiledProgram &P = prog->P;
+    const size_t n = P.trace_len;
+    *n_out = n;
+    if (trace_out && n > cap_rows) return ZK_ERR_BUFFER_TOO_SMALL;
+    std::vector<fe> sec;
+    parse_inputs(secret, num_secret, lwe_size, sec);
+    const Machine M{public_in, num_public, sec.data(), num_secret, lwe_size, delta};
+    fe last[28], outs[MAX_STACK];
+    for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
+    const int rc = run_program(P, M, reinterpret_cast<fe *>(trace_out), n, last, outs);
+    if (rc) return rc;
+    if (outputs)
+        for (int i = 0; i < MAX_STACK; i++) fe_to_bytes(outs[i], outputs + 16 * i);
+    return trace_out ? ZK_OK : ZK_ERR_BUFFER_TOO_SMALL;
+}
 
 extern "C" int zk_vm_trace(const char *source, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
                            size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row,
@@ -346,12 +474,11 @@ extern "C" int zk_vm_trace(const char *source, const uint8_t *public_in, size_t 
                            uint8_t *program_hash) {
     if (!source || !last_row || !n_out || lwe_size == 0 || lwe_size > 15 || (num_secret && !secret))
         return ZK_ERR_INVALID_ARG;
-    std::vector<Op> code;
-    int rc = compile(source, code);
-    if (rc) return rc;
     if (!trace_out) {
         // size query: one clock per compiled op, so the length follows from the program alone
-        // (Processor::grow doubles the capacity past clk; trace_len() is the next power of two above it)
+        std::vector<Op> code;
+        const int rc = compile(source, code);
+        if (rc) return rc;
         size_t cap = MIN_TRACE;
         while (code.size() >= cap) cap *= 2;
         size_t n = 1;
@@ -359,24 +486,13 @@ extern "C" int zk_vm_trace(const char *source, const uint8_t *public_in, size_t 
         *n_out = n;
         return ZK_ERR_BUFFER_TOO_SMALL;
     }
-    std::vector<fe> sec(num_secret * lwe_size);
-    for (size_t i = 0; i < sec.size(); i++) sec[i] = fe_from_bytes(secret + 16 * i);
-    Processor P;
-    rc = P.run(code, public_in, num_public, sec.data(), num_secret, lwe_size, delta);
+    zk_program *prog = nullptr;
+    int rc = zk_program_compile(source, &prog, program_hash, nullptr);
     if (rc) return rc;
-    size_t n = P.trace_len();
-    *n_out = n;
-    if (!trace_out || n > cap_rows) return ZK_ERR_BUFFER_TOO_SMALL;
-    std::vector<fe> last(28);
-    for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
-    P.write(reinterpret_cast<fe *>(trace_out), n, last.data());
-    if (outputs)
-        for (int i = 0; i < MAX_STACK; i++) fe_to_bytes(P.reg[i][P.clk], outputs + 16 * i);
-    if (program_hash) {  // Program::compile's hash = the chiplet's sponge after the whole program
-        fe_to_bytes(P.rescue.s[0], program_hash);
-        fe_to_bytes(P.rescue.s[1], program_hash + 16);
-    }
-    return ZK_OK;
+    rc = zk_program_trace(prog, public_in, num_public, secret, num_secret, lwe_size, delta, last_row, trace_out,
+                          cap_rows, n_out, outputs);
+    zk_program_free(prog);
+    return rc;
 }
 
 extern "C" const char *zk_vm_last_error(void) { return vm_err.c_str(); }

@@ -33,6 +33,7 @@ EXPORTED = (
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_vm_trace",
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_destroy", "zk_prove_sharded",
+    "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error",
 )
 
 
@@ -127,6 +128,10 @@ def lib():
                                        C.POINTER(sz), C.POINTER(Record)]
         L.zk_vm_trace.argtypes = [C.c_char_p, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp, vp]
         L.zk_vm_last_error.restype = C.c_char_p
+        L.zk_program_compile.argtypes = [C.c_char_p, C.POINTER(vp), vp, C.POINTER(sz)]
+        L.zk_program_trace.argtypes = [vp, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp]
+        L.zk_program_free.argtypes = [vp]
+        L.zk_program_free.restype = None
         L.zk_diag_mul_limbs_host.argtypes = [vp, vp, vp, sz]
         L.zk_diag_mul_limbs_host.restype = None
         L.zk_diag_dot_host.argtypes = [vp, vp, sz, vp]

@@ -295,6 +295,53 @@ def vm_trace(source: str, public, secret, server_key, last_row, out=None):
     return trace, bytes_elems(outputs.raw), bytes_elems(h.raw)
 
 
+class Program:
+    """Program::compile (vm/src/program/mod.rs:37-131) through zk_program_compile: parse, pad, hash.  The handle
+    keeps the chiplet's per-step sponge states (a function of the code alone), so trace() -- Processor::run +
+    trace on given inputs (vm/src/processor/mod.rs:61-95) -- is the stack machine plus threaded row writes."""
+
+    def __init__(self, source: str):
+        h = C.c_void_p()
+        hb = C.create_string_buffer(32)
+        n = C.c_size_t(0)
+        rc = lib().zk_program_compile(source.encode(), C.byref(h), hb, C.byref(n))
+        if rc:
+            raise ZkError(rc, lib().zk_vm_last_error().decode())
+        self.handle = h
+        self.hash = bytes_elems(hb.raw)
+        self.trace_len = n.value
+
+    def trace(self, public, secret, server_key, last_row, out=None):
+        """Returns (trace (28, n, 2) uint64, outputs[16]); out: an optional HostTrace / array of length n."""
+        n = self.trace_len
+        if out is None:
+            trace = np.zeros((28, n, 2), dtype=np.uint64)
+        else:
+            trace = out.array if isinstance(out, HostTrace) else out
+            if trace.shape != (28, n, 2) or trace.dtype != np.uint64 or not trace.flags.c_contiguous:
+                raise ZkError(native.ZK_ERR_INVALID_ARG, f"out must be a contiguous (28, {n}, 2) uint64 array")
+        sec = elems_bytes([v for ct in secret for v in ct])
+        outputs = C.create_string_buffer(256)
+        nn = C.c_size_t(0)
+        rc = lib().zk_program_trace(self.handle, bytes(public), len(public), sec, len(secret), server_key.lwe_size(),
+                                    server_key.parameters.delta, elems_bytes(last_row), trace.ctypes.data, n,
+                                    C.byref(nn), outputs)
+        if rc:
+            raise ZkError(rc, lib().zk_vm_last_error().decode())
+        return trace, bytes_elems(outputs.raw)
+
+    def close(self):
+        if self.handle:
+            lib().zk_program_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def prove(source: str, public, secret, server_key, last_row, options: ProofOptions = REFERENCE_OPTIONS,
           gpu: GpuProver | None = None):
     """vm::prove (vm/src/lib.rs:13-29): run -> output -> trace -> options -> hash -> prove."""

@@ -231,6 +231,19 @@ int zk_prover_kernel_ops(zk_prover *p, double *total_muls, double *total_addsubs
 int zk_vm_trace(const char *source, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
                 size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, uint8_t *trace_out,
                 size_t cap_rows, size_t *n_out, uint8_t *outputs, uint8_t *program_hash);
+/* The same in the reference's two steps.  zk_program_compile = Program::compile (vm/src/program/mod.rs:37-131):
+ * parse, pad, hash; the handle keeps the chiplet's per-step sponge states the hash computation produced (they
+ * depend on the code alone).  zk_program_trace = Processor::run + trace (vm/src/processor/mod.rs:61-95) of that
+ * program on these inputs: the stack machine runs once sequentially (errors, chunk states), then threads
+ * (ZK_VM_THREADS, else OMP_NUM_THREADS, else all cores) write the rows.  trace_out = NULL runs the program and
+ * reports n (ZK_ERR_BUFFER_TOO_SMALL).  A compiled program may be traced from several threads at once. */
+typedef struct zk_program zk_program;
+int zk_program_compile(const char *source, zk_program **out, uint8_t *program_hash, size_t *trace_len);
+int zk_program_trace(const zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
+                     size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row,
+                     uint8_t *trace_out, size_t cap_rows, size_t *n_out, uint8_t *outputs);
+void zk_program_free(zk_program *prog);
+const char *zk_vm_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -461,3 +461,24 @@ def test_provers_on_every_device_agree(oracle):
         finally:
             g.close()
         assert rc == 0 and proof == oproof, f"device {dev}"
+
+
+# ---------------------------------------------------------------- full-size pins (BASELINE configs[2], [3], [4])
+from golden_large import LARGE_CASES, check_large_proof, large_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in LARGE_CASES])
+def test_full_size_proof_matches_oracle_pin(oracle, name):
+    """configs[2] (2^20, reference options), configs[4] (2^20, 43 queries over the quadratic extension, 128 bits)
+    and configs[3]'s 2^22 trace on one GPU: the proof from the host-resident trace is byte-identical to the
+    oracle's (sha256, roots, query positions) and both verifiers accept it at the config's security."""
+    c = next(c for c in LARGE_CASES if c["name"] == name)
+    ht, trace, pub, opts = large_inputs(c)
+    g = GpuProver(0, max_trace_len=1 << c["log_n"])
+    try:
+        proof, rec, _, rc = g.prove(trace, pub, opts, record=True)
+    finally:
+        g.close()
+        ht.close()
+    assert rc == 0
+    check_large_proof(c, proof, rec, pub, oracle)

@@ -115,3 +115,23 @@ def test_sharded_rejects_bad_world():
     import ctypes as C
     comm = C.c_void_p()
     assert native.lib().zk_comm_create_loopback(3, C.byref(comm)) == native.ZK_ERR_INVALID_ARG
+
+
+# ---------------------------------------------------------------- full-size pins, sharded
+from golden_large import LARGE_CASES, check_large_proof, large_inputs  # noqa: E402
+# (case, world): every loopback rank holds its own prover on the one test GPU
+LARGE_SHARDED = [(c, w) for c in LARGE_CASES for w in ((8,) if c["log_n"] <= 20 else (2,))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,world", LARGE_SHARDED, ids=[f"{c['name']}-w{w}" for c, w in LARGE_SHARDED])
+def test_sharded_full_size_matches_oracle_pin(oracle, c, world):
+    """The coset-sharded prover (loopback ranks) on the full-size configs: proof bytes equal the oracle's pin."""
+    ht, trace, pub, opts = large_inputs(c)
+    sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
+    try:
+        proof, rec = sp.prove(trace, pub, opts, record=True)
+    finally:
+        sp.close()
+        ht.close()
+    check_large_proof(c, proof, rec, pub, oracle)
