@@ -215,6 +215,24 @@ def run_proofs_timed(fns, count: int, pg, local: int) -> float:
     return max_over_ranks(pg, time.perf_counter() - t0, local)
 
 
+def pmc_valu(kernel: str):
+    """Hardware VALU issue of the kernel from the committed rocprofv3 SQ/GRBM pass (tools/pmc_valu.py):
+    SQ_INSTS_VALU over the 1024 SIMDs' 2-cycle issue slots (a plain wave64 VALU instruction takes one) --
+    the hardware roofline of an integer-VALU-bound kernel, independent of this build's own field ops."""
+    f = ROOT / "profiles" / "pmc_valu.json"
+    if not f.exists():
+        return None
+    try:
+        k = json.loads(f.read_text())["kernels"].get(kernel)
+    except Exception:
+        return None
+    if not k:
+        return None
+    return {"bound": "valu-issue", "slot_util": round(k["slot_util"], 3), "clock_ghz": round(k["clock_ghz"], 2),
+            "valu_instr_per_launch": k["valu_instr"] / k["launches"], "peak": "1024 SIMDs x 1 wave64 VALU instr / 2 cycles",
+            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE, tools/pmc_valu.py)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +248,8 @@ def main():
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
     ap.add_argument("--sharded-log-n", type=int, default=22,
                     help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="skip the device-resident / pageable / latency comparison legs (profiler passes)")
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
@@ -282,32 +302,35 @@ def main():
     # ---- comparison legs (same provers, same count, outside the headline): the trace already in HBM
     # (zk_prove_device), and the host trace in pageable memory (runtime-staged copies)
     cmp_steps = max(2 * P, min(args.steps, 10))
-    d_traces = [g.upload_trace(trace)[0] for g in provers]
+    dev_s = pag_s = latency_ms = None
+    if not args.no_compare:
+        d_traces = [g.upload_trace(trace)[0] for g in provers]
 
-    def dev_step(k):
-        def f():
-            last[k] = provers[k].prove_device(d_traces[k], n, pub, opts)[0]
-        return f
+        def dev_step(k):
+            def f():
+                last[k] = provers[k].prove_device(d_traces[k], n, pub, opts)[0]
+            return f
 
-    dfns = [dev_step(k) for k in range(P)]
-    run_proofs(dfns, P)
-    dev_s = run_proofs_timed(dfns, cmp_steps, pg, local)
-    assert all(p_ == proof for p_ in last if p_ is not None), "device-resident proof differs"
-    pageable = np.array(trace)  # ordinary (pageable) host memory
-    pfns = [host_step(k, pageable) for k in range(P)]
-    run_proofs(pfns, P)
-    pag_s = run_proofs_timed(pfns, cmp_steps, pg, local)
-    assert all(p_ == proof for p_ in last if p_ is not None), "pageable-trace proof differs"
-    del pageable
+        dfns = [dev_step(k) for k in range(P)]
+        run_proofs(dfns, P)
+        dev_s = run_proofs_timed(dfns, cmp_steps, pg, local)
+        assert all(p_ == proof for p_ in last if p_ is not None), "device-resident proof differs"
+        pageable = np.array(trace)  # ordinary (pageable) host memory
+        pfns = [host_step(k, pageable) for k in range(P)]
+        run_proofs(pfns, P)
+        pag_s = run_proofs_timed(pfns, cmp_steps, pg, local)
+        assert all(p_ == proof for p_ in last if p_ is not None), "pageable-trace proof differs"
+        del pageable
     for g in provers[1:]:
         g.close()
-    # latency of one prove() call alone on the GPU (host-resident trace), median of 5
-    lat = []
-    for _ in range(5):
-        t1 = time.perf_counter()
-        gpu.prove_host(trace, pub, opts)
-        lat.append(time.perf_counter() - t1)
-    latency_ms = 1e3 * sorted(lat)[len(lat) // 2]
+    if not args.no_compare:
+        # latency of one prove() call alone on the GPU (host-resident trace), median of 5
+        lat = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            gpu.prove_host(trace, pub, opts)
+            lat.append(time.perf_counter() - t1)
+        latency_ms = 1e3 * sorted(lat)[len(lat) // 2]
     stages = gpu.stage_times()
 
     # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream)
@@ -367,6 +390,7 @@ def main():
         roofline["valu"] = {"bound": "valu", "fe_mul_equiv_per_launch": muls / launches, "fe_addsub_per_launch": addsubs / launches,
                             "achieved_fe_mul_per_s": round(muls / (tot_ms / 1e3), 1), "peak_fe_mul_per_s": FE_MUL_PEAK,
                             "floor_ms_per_launch": round(floor_ms / launches, 4), "frac": round(floor_ms / tot_ms, 4)}
+    roofline["valu_hw"] = pmc_valu(name)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_log_n, args.config5, host_cores(args.cpu_cores))
@@ -383,9 +407,9 @@ def main():
                    "options": opts_str, "timed_region": "zk_prove_columns: page-locked host trace -> proof bytes",
                    "parallelism": f"independent proofs, {P} in flight per GPU, x{world} GPUs"},
         "security_bits_checked": min_sec,
-        "latency_ms": round(latency_ms, 3),
-        "device_resident_ms": round(1e3 * dev_s / cmp_steps, 3),
-        "pageable_host_ms": round(1e3 * pag_s / cmp_steps, 3),
+        "latency_ms": round(latency_ms, 3) if latency_ms is not None else None,
+        "device_resident_ms": round(1e3 * dev_s / cmp_steps, 3) if dev_s is not None else None,
+        "pageable_host_ms": round(1e3 * pag_s / cmp_steps, 3) if pag_s is not None else None,
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},

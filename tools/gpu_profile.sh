@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-BENCH_ARGS="--steps 4 --warmup 2 --inflight 1 --no-cpu-baseline --no-verify"
+BENCH_ARGS="--steps 4 --warmup 2 --inflight 1 --no-cpu-baseline --no-verify --no-compare"
 
 if [ "${2:-tests}" = "tests" ]; then
   (cd "$R" && timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$O/gpu_tests_$TAG.log" 2>&1)
@@ -18,18 +18,19 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
   python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench_$TAG.json" 2> "$O/prof_bench_$TAG.err"
 echo "kernel trace ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o f -- \
-  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_fetch_$TAG.err"
+  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify --no-compare > /dev/null 2> "$O/pmc_fetch_$TAG.err"
 echo "pmc fetch ok"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write_$TAG" -o w -- \
-  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_write_$TAG.err"
+  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify --no-compare > /dev/null 2> "$O/pmc_write_$TAG.err"
 echo "pmc write ok"
 python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -o "$O/pmc_traffic_$TAG.json"
 cp "$O/pmc_traffic_$TAG.json" "$R/profiles/pmc_traffic.json"
 # VALU issue rate: 6 SQ + 2 GRBM counters, one pass of its own
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_LDS SQ_BUSY_CYCLES \
   SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$O/pmc_sq_$TAG" -o sq -- \
-  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_sq_$TAG.err"
-python3 "$R/tools/pmc_valu.py" "$O/pmc_sq_$TAG" -o "$O/pmc_valu_$TAG.md"
+  python3 "$R/bench.py" --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify --no-compare > /dev/null 2> "$O/pmc_sq_$TAG.err"
+python3 "$R/tools/pmc_valu.py" "$O/pmc_sq_$TAG" -o "$O/pmc_valu_$TAG.md" -j "$O/pmc_valu_$TAG.json"
+cp "$O/pmc_valu_$TAG.json" "$R/profiles/pmc_valu.json"
 echo "pmc sq ok"
 # keep only the summaries (the per-dispatch counter CSVs are large)
 find "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
@@ -40,9 +41,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
   python3 "$R/bench.py" --config5 $BENCH_ARGS > "$O/prof_bench_c5_$TAG.json" 2> "$O/prof_bench_c5_$TAG.err"
 echo "config5 kernel trace ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_c5_$TAG" -o f -- \
-  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_fetch_c5_$TAG.err"
+  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify --no-compare > /dev/null 2> "$O/pmc_fetch_c5_$TAG.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write_c5_$TAG" -o w -- \
-  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_write_c5_$TAG.err"
+  python3 "$R/bench.py" --config5 --steps 1 --warmup 0 --inflight 1 --no-cpu-baseline --no-verify --no-compare > /dev/null 2> "$O/pmc_write_c5_$TAG.err"
 python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" -o "$O/pmc_traffic_c5_$TAG.json"
 find "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
 echo "config5 pmc ok"

@@ -39,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("-o", default=None)
+    ap.add_argument("-j", default=None, help="also write the table as JSON (bench.py reads profiles/pmc_valu.json)")
     args = ap.parse_args()
     path = args.csv
     if os.path.isdir(path):  # rocprofv3 -d DIR: the CSV may sit in a host/pid subdirectory
@@ -63,10 +64,13 @@ def main():
     lines = ["| kernel | launches | time (ms) | clock (GHz) | VALU instr (G) | slot_util |",
              "|---|---|---|---|---|---|"]
     tot = collections.Counter()
+    js = {"source": os.path.abspath(path), "n_xcd": N_XCD, "simds": SIMDS, "kernels": {}}
     for g, a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
         cyc = a["GRBM_GUI_ACTIVE"] / N_XCD
         issue = a["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc) if cyc else 0.0
         clock = cyc / a["ns"] if a["ns"] else 0.0
+        js["kernels"][g] = {"launches": a["n"], "ms": a["ns"] / 1e6, "clock_ghz": clock,
+                            "valu_instr": a["SQ_INSTS_VALU"], "slot_util": issue}
         lines.append(f"| {g} | {a['n']} | {a['ns'] / 1e6:.3f} | {clock:.2f} | {a['SQ_INSTS_VALU'] / 1e9:.2f} | "
                      f"{issue:.2f} |")
         tot.update(a)
@@ -76,6 +80,9 @@ def main():
     out = "\n".join(lines) + "\n"
     if args.o:
         open(args.o, "w").write(out)
+    if args.j:
+        import json
+        open(args.j, "w").write(json.dumps(js, indent=1) + "\n")
     print(out)
 
 
