@@ -257,9 +257,9 @@ int zk_device_count(int *count) {
     return ZK_OK;
 }
 
-int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) {
-    if (!out || max_n < 16 || (max_n & (max_n - 1)) || max_b < 8 || (max_b & (max_b - 1)) || max_b > 64)
-        ZK_FAIL(ZK_ERR_INVALID_ARG, "zk_prover_create: max_trace_len must be a power of two >= 16, blowup in [8, 64]");
+// world = 0: a full prover; world = G: one rank of a G-way coset-sharded proof (blowup 8), whose LDE-domain
+// buffers (trace / composition LDE, DEEP, NTT scratch, Merkle subtrees) hold N / G points instead of N
+static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk_prover **out) {
     int cnt = 0;
     if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) ZK_FAIL(ZK_ERR_DEVICE, "no HIP device available");
     if (device < 0 || device >= cnt) ZK_FAIL(ZK_ERR_INVALID_ARG, "device index out of range");
@@ -280,32 +280,36 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     p->device = device;
     p->max_n = max_n;
     p->max_b = max_b;
+    p->shard_world = world;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
-    for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_free, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
+    // Nl: LDE-domain points this prover holds (all N, or the N / G of one sharded rank)
+    const size_t Nl = world ? N / (size_t)world : N;
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
     ZK_CHECK_HIP(A.alloc(&p->polys, (size_t)W * n));
-    // NTT scratch: the four-step intermediate of a whole 8-coset LDE of the trace (28 x 8 x n)
-    ZK_CHECK_HIP(A.alloc(&p->tmp, (size_t)W * 8 * n));
-    ZK_CHECK_HIP(A.alloc(&p->lde, (size_t)W * N));
+    // NTT scratch: the four-step intermediate of a whole 8-coset LDE of the trace (28 x 8 x n; a sharded rank's
+    // cosets: 28 x 8/G x n, at least the 28 x n of the interpolation)
+    ZK_CHECK_HIP(A.alloc(&p->tmp, (size_t)W * (world ? std::max<size_t>(n, Nl) : 8 * n)));
+    ZK_CHECK_HIP(A.alloc(&p->lde, (size_t)W * Nl));
     ZK_CHECK_HIP(A.alloc(&p->comp, CE));
     ZK_CHECK_HIP(A.alloc(&p->ctmp, CE));
     ZK_CHECK_HIP(A.alloc(&p->cpolys, (size_t)ZK_MAX_CCOLS * n));
-    ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * N));
-    ZK_CHECK_HIP(A.alloc(&p->deep, N));
-    ZK_CHECK_HIP(A.alloc(&p->ulde, N));
+    ZK_CHECK_HIP(A.alloc(&p->clde, (size_t)8 * Nl));
+    ZK_CHECK_HIP(A.alloc(&p->deep, Nl));
+    if (!world) ZK_CHECK_HIP(A.alloc(&p->ulde, N));  // the single path's DEEP LDE
     ZK_CHECK_HIP(A.alloc(&p->dscratch, 4 * (2048 + n / 2048 + 2) + 3 * n + 2 * (n / 256 + 1)));
     // FRI layers: sum over layers of L/fold values and 2*L/fold digests; worst case fold = 2
     ZK_CHECK_HIP(A.alloc(&p->fri, N + 16));
-    ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * N));
-    ZK_CHECK_HIP(A.alloc(&p->nodes, 32 * N));
-    ZK_CHECK_HIP(A.alloc(&p->cleaves, 32 * N));
-    ZK_CHECK_HIP(A.alloc(&p->cnodes, 32 * N));
-    ZK_CHECK_HIP(A.alloc(&p->fri_dig, 64 * N + 64));
+    ZK_CHECK_HIP(A.alloc(&p->leaves, 32 * Nl));
+    ZK_CHECK_HIP(A.alloc(&p->nodes, 32 * Nl));
+    ZK_CHECK_HIP(A.alloc(&p->cleaves, 32 * Nl));
+    ZK_CHECK_HIP(A.alloc(&p->cnodes, 32 * Nl));
+    // digest scratch: a sharded rank's all-to-all send + receive areas (64 B per local point), and the digests of
+    // the FRI layers >= 1 (at most 32 B per point of the whole domain, fold 2)
+    ZK_CHECK_HIP(A.alloc(&p->fri_dig, (world ? std::max<size_t>(64 * Nl, 32 * N) : 64 * N) + 64));
     ZK_CHECK_HIP(A.alloc(&p->partials, (size_t)(2 * ZK_MAX_COLS + ZK_MAX_CCOLS) * ood_waves(max_n)));
     ZK_CHECK_HIP(A.alloc(&p->ood_tab, (size_t)128 + 2 * ood_waves(max_n)));
     ZK_CHECK_HIP(A.alloc(&p->ood, 256));
@@ -318,6 +322,8 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_idx, ZK_GATHER_CAP * sizeof(uint64_t), hipHostMallocDefault));
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_out, ZK_GATHER_CAP * sizeof(fe), hipHostMallocDefault));
     ZK_CHECK_HIP(A.alloc(&p->flag, 4));
+    ZK_CHECK_HIP(A.alloc(&p->up_flag, 16));
+    ZK_CHECK_HIP(hipMemset(p->up_flag, 0, 64));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->fold_consts, sizeof(FoldConsts)));
@@ -327,15 +333,24 @@ int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) 
     return ZK_OK;
 }
 
+int zk_prover_create(int device, size_t max_n, uint32_t max_b, zk_prover **out) {
+    if (!out || max_n < 16 || (max_n & (max_n - 1)) || max_b < 8 || (max_b & (max_b - 1)) || max_b > 64)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "zk_prover_create: max_trace_len must be a power of two >= 16, blowup in [8, 64]");
+    return create_prover(device, max_n, max_b, 0, out);
+}
+
+int zk_prover_create_shard(int device, size_t max_n, int world, zk_prover **out) {
+    if (!out || max_n < 16 || (max_n & (max_n - 1)) || (world != 1 && world != 2 && world != 4 && world != 8))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "zk_prover_create_shard: max_trace_len a power of two >= 16, world 1, 2, 4 or 8");
+    return create_prover(device, max_n, 8, world, out);
+}
+
 void zk_prover_destroy(zk_prover *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     (void)hipStreamSynchronize(p->st);
     if (p->st2) (void)hipStreamSynchronize(p->st2);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
-    for (auto &e : p->ev_up)
-        if (e) (void)hipEventDestroy(e);
-    if (p->ev_free) (void)hipEventDestroy(p->ev_free);
     if (p->st2) (void)hipStreamDestroy(p->st2);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
@@ -967,17 +982,18 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     }
     const int log_n = pl->log_n, log_b = pl->log_b;
     const size_t B = (size_t)1 << log_b;
-    // the device trace buffer is free once everything queued before this proof on st is done
-    ZK_CHECK_HIP(hipEventRecord(p->ev_free, p->st));
-    ZK_CHECK_HIP(hipStreamWaitEvent(p->st2, p->ev_free, 0));
+    // The device trace buffer is free: the previous proof on this prover returned only after its stream drained
+    // (and the trace is read by the interpolation alone).  Group g of proof s is in HBM once *up_flag reaches
+    // s * 8 + g + 1 (monotonic, so a flag left by an earlier proof never satisfies a later wait).
+    const uint32_t base = (++p->up_seq) * 8u;
     constexpr int per = W / ZK_UPLOAD_GROUPS;
     for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
         ZK_TRY(upload_trace_group(p, src, n, g * per, per));
-        ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->st2));
+        ZK_CHECK_HIP(hipStreamWriteValue32(p->st2, p->up_flag, base + (uint32_t)g + 1u, 0));
     }
     for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
         const size_t c0 = (size_t)g * per;
-        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[g], 0));
+        ZK_CHECK_HIP(hipStreamWaitValue32(p->st, p->up_flag, base + (uint32_t)g + 1u, hipStreamWaitValueGte, 0xffffffffu));
         ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
     }
@@ -1001,18 +1017,19 @@ static void coset_major_rows_to_host(zk_prover *p, const fe *base, int ncols, si
 int zk::ensure_ext(zk_prover *p) {
     if (p->x_comp) return ZK_OK;
     const size_t n = p->max_n, N = n * p->max_b, CE = 8 * n;
+    const size_t Nl = p->shard_world ? N / (size_t)p->shard_world : N;  // LDE points held (see create_prover)
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->x_comp, 2 * CE));
     ZK_CHECK_HIP(A.alloc(&p->x_ctmp, 2 * CE));
-    ZK_CHECK_HIP(A.alloc(&p->x_clde, (size_t)2 * 8 * N));  // C <= 8 E columns
-    ZK_CHECK_HIP(A.alloc(&p->x_deep, 2 * N));
+    ZK_CHECK_HIP(A.alloc(&p->x_clde, (size_t)2 * 8 * Nl));  // C <= 8 E columns
+    ZK_CHECK_HIP(A.alloc(&p->x_deep, 2 * Nl));
     ZK_CHECK_HIP(A.alloc(&p->x_fri, 2 * (N + 16)));
     ZK_CHECK_HIP(A.alloc(&p->x_partials, (size_t)2 * (2 * ZK_MAX_COLS + ZK_MAX_CCOLS) * ood_waves(n)));
     ZK_CHECK_HIP(A.alloc(&p->x_tab, (size_t)2 * (128 + 2 * ood_waves(n))));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_air, 2 * sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_deep_consts, sizeof(DeepConstsE)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->x_fold_consts, sizeof(FoldConstsE)));
-    ZK_CHECK_HIP(A.alloc(&p->x_ulde, 2 * N));
+    if (!p->shard_world) ZK_CHECK_HIP(A.alloc(&p->x_ulde, 2 * N));
     ZK_CHECK_HIP(A.alloc(&p->x_dscratch, 8 * (2048 + n / 2048 + 2) + 6 * n + 4 * (n / 256 + 1)));
     return ZK_OK;
 }
@@ -1077,6 +1094,7 @@ static int check_ood_identity(const std::vector<fe2> &e, int C, const AirConsts 
 static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     if (!p || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_REQUIRE_FULL_PROVER(p);
     ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
     // copies from the caller's host columns may still be in flight on an early error return: the caller
     // may free those columns as soon as this returns (a completed proof has long finished them)
@@ -1448,6 +1466,7 @@ int zk_host_unregister(void *ptr) {
 int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint32_t blowup, zk_trace_lde **out,
                uint8_t root[32]) {
     if (!p || !trace || !out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_REQUIRE_FULL_PROVER(p);
     if (width != (size_t)W) ZK_FAIL(ZK_ERR_INVALID_ARG, "ProcessorAir traces have 28 columns");
     if (n < 16 || (n & (n - 1)) || n > p->max_n || blowup < 8 || (blowup & (blowup - 1)) || blowup > p->max_b)
         ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid trace length or blowup");

@@ -45,6 +45,13 @@ static constexpr int ZK_UPLOAD_GROUPS_MAX = 7;
 static constexpr int NUM_TCONS = 20;
 static constexpr int NUM_ASSERTS = 22;
 
+// single-GPU entry points refuse a prover sized for one rank of a sharded proof
+#define ZK_REQUIRE_FULL_PROVER(p)                                                                                  \
+    do {                                                                                                          \
+        if ((p)->shard_world)                                                                                     \
+            ZK_FAIL(ZK_ERR_INVALID_ARG, "this prover was created for one rank of a sharded proof (zk_prover_create_shard)"); \
+    } while (0)
+
 inline int ilog2(size_t n) {
     int r = 0;
     while (((size_t)1 << r) < n) r++;
@@ -97,8 +104,17 @@ struct zk_prover {
     // copy stream: a host-resident trace is uploaded here in column groups, each group's event gating its
     // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it
     hipStream_t st2 = nullptr;
-    hipEvent_t ev_up[zk::ZK_UPLOAD_GROUPS_MAX] = {}, ev_free = nullptr;
+    // ... ordered by a device word the copy stream writes after each group (hipStreamWriteValue32) and the compute
+    // stream waits on (hipStreamWaitValue32): measured (tools/ubench/upload_probe.hip), an event recorded between
+    // the column copies of one stream halves their rate (29.7 vs 55 GB/s), a cross-stream event wait ahead of them
+    // costs 25 %, the value writes cost nothing
+    uint32_t *up_flag = nullptr;
+    uint32_t up_seq = 0;
     size_t max_n = 0;
+    // 0: a full prover (every entry point).  G in {1, 2, 4, 8}: sized for one rank of a G-way coset-sharded proof
+    // (zk_prover_create_shard): the LDE-domain buffers hold the rank's 8/G cosets only, so it serves
+    // zk_prove_sharded with that world size and nothing else
+    int shard_world = 0;
     uint32_t max_b = 0;
     zk::DeviceArena arena;
     fe *d_trace = nullptr, *polys = nullptr, *tmp = nullptr, *lde = nullptr, *comp = nullptr, *ctmp = nullptr,

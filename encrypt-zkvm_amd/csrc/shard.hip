@@ -769,6 +769,8 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
     for (int l = 0; l < nlocal; l++) {
         zk_prover *p = provers[l];
         if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+        if (p->shard_world && p->shard_world != X.G)
+            ZK_FAIL(ZK_ERR_INVALID_ARG, "prover was created for a sharded proof over a different number of ranks");
         ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
         X.P.push_back(p);
         X.rank.push_back(comm->loopback() ? l : comm->rank);

@@ -36,9 +36,9 @@ class ShardedProver:
         comm = C.c_void_p()
         check(lib().zk_comm_create_loopback(world, C.byref(comm)), "zk_comm_create_loopback")
         provers = []
-        for _ in range(world):
+        for _ in range(world):  # one rank's share of the LDE domain each (zk_prover_create_shard)
             p = C.c_void_p()
-            check(lib().zk_prover_create(device, max_trace_len, 8, C.byref(p)), "zk_prover_create")
+            check(lib().zk_prover_create_shard(device, max_trace_len, world, C.byref(p)), "zk_prover_create_shard")
             provers.append(p)
         return cls(comm, provers, 0, world)
 
@@ -47,7 +47,7 @@ class ShardedProver:
         comm = C.c_void_p()
         check(lib().zk_comm_create_rccl(uid, rank, world, device, C.byref(comm)), "zk_comm_create_rccl")
         p = C.c_void_p()
-        check(lib().zk_prover_create(device, max_trace_len, 8, C.byref(p)), "zk_prover_create")
+        check(lib().zk_prover_create_shard(device, max_trace_len, world, C.byref(p)), "zk_prover_create_shard")
         return cls(comm, [p], rank, world)
 
     def upload_trace(self, trace: np.ndarray) -> int:

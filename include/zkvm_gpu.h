@@ -118,6 +118,11 @@ int zk_device_count(int *count);
  * (this library's transcript round trips, and any other code's syncs) busy-spins instead of yielding
  * (-0.05 ms per 2^20 proof).  Set ZK_SPIN_WAIT=0 in the environment to keep the runtime's default. */
 int zk_prover_create(int device, size_t max_trace_len, uint32_t max_blowup, zk_prover **out);
+/* A prover sized for ONE rank of a `world`-way coset-sharded proof (zk_prove_sharded, blowup 8): the buffers of
+ * the LDE domain (trace and composition LDE, DEEP, NTT scratch, Merkle subtrees) hold the rank's 8/world cosets
+ * only -- about 12.6 GB per rank at 2^22, world 8, against 50 GB for a full prover.  It serves zk_prove_sharded
+ * with that world size; every single-GPU entry point refuses it (ZK_ERR_INVALID_ARG). */
+int zk_prover_create_shard(int device, size_t max_trace_len, int world, zk_prover **out);
 void zk_prover_destroy(zk_prover *p);
 /* device pointer to a scratch region large enough for a 28 x max_trace_len trace (so callers can
  * stage a device-resident trace without their own allocator) */

@@ -119,8 +119,9 @@ def test_sharded_rejects_bad_world():
 
 # ---------------------------------------------------------------- full-size pins, sharded
 from golden_large import LARGE_CASES, check_large_proof, large_inputs  # noqa: E402
-# (case, world): every loopback rank holds its own prover on the one test GPU
-LARGE_SHARDED = [(c, w) for c in LARGE_CASES for w in ((8,) if c["log_n"] <= 20 else (2,))]
+# (case, world): every loopback rank holds its own rank-sized prover (zk_prover_create_shard) on the one test GPU:
+# 2^22 at world 8 is 8 x ~12.6 GB
+LARGE_SHARDED = [(c, w) for c in LARGE_CASES for w in ((8,) if c["log_n"] <= 20 else (2, 8))]
 
 
 @pytest.mark.gpu
@@ -135,3 +136,36 @@ def test_sharded_full_size_matches_oracle_pin(oracle, c, world):
         sp.close()
         ht.close()
     check_large_proof(c, proof, rec, pub, oracle)
+
+
+@pytest.mark.gpu
+def test_shard_prover_refuses_single_gpu_calls():
+    """A prover sized for one rank of a sharded proof holds 1/world of the LDE domain: the single-GPU entry
+    points refuse it, and zk_prove_sharded refuses it for another world size."""
+    import ctypes as C
+    from zkvm_amd.prover import GpuProver
+    c = CASES[0]
+    trace, proof, pub, opts = case_inputs(c)
+    n = trace.shape[1]
+    L = native.lib()
+    h = C.c_void_p()
+    native.check(L.zk_prover_create_shard(0, n, 4, C.byref(h)))
+    try:
+        g = GpuProver.__new__(GpuProver)
+        g.handle, g.max_trace_len, g.device = h, n, 0
+        with pytest.raises(native.ZkError) as e:
+            g.prove(trace, pub, opts)
+        assert e.value.code == native.ZK_ERR_INVALID_ARG and "sharded" in str(e.value)
+        g.handle = None  # the handle is destroyed below, not by the wrapper
+        comm = C.c_void_p()
+        native.check(L.zk_comm_create_loopback(2, C.byref(comm)))
+        arr = (C.c_void_p * 2)(h.value, h.value)
+        plen = C.c_size_t(1 << 20)
+        buf = C.create_string_buffer(1 << 20)
+        opt = opts.to_c()
+        rc = L.zk_prove_sharded(comm, arr, 2, trace.ctypes.data, n, C.byref(opt), C.byref(pub), buf, C.byref(plen), None)
+        assert rc == native.ZK_ERR_INVALID_ARG
+        L.zk_comm_destroy(comm)
+    finally:
+        L.zk_prover_destroy(h)
+
