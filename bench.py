@@ -244,7 +244,7 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=-1,
                     help="threads of the all-cores CPU sample (-1: the host share, at most 16; 0: skip it)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2, help="independent provers (proofs in flight) per GPU")
+    ap.add_argument("--inflight", type=int, default=3, help="independent provers (proofs in flight) per GPU")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
     ap.add_argument("--sharded-log-n", type=int, default=22,
                     help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
@@ -253,6 +253,11 @@ def main():
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
+    # Each prover drives two streams (compute, trace upload); with HIP's default of 4 hardware queues per process the
+    # streams of 3 provers share queues, and a compute stream parked on its upload's wait-value packet then holds
+    # up the kernels of another prover queued behind it (A/B: 16.1 ms per proof at 4 queues, 14.3 at 8, 12.9 with 3
+    # provers at 16 -- device-resident 12.5).  Set before the first HIP call of the process (torch.distributed too).
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     if args.sharded:
         return run_sharded(args)
 

@@ -398,94 +398,14 @@ __device__ __forceinline__ fe fe_mul_w2(fe A, const fe_w2 &W) {
     return ws_fold(d0, e1, e2, e3, e4, 0u);
 }
 
-// ---- two butterflies' sums and differences at once: (a + b, a - b, c + d, c - d) mod p.  The compiler routes
-// every carry through VCC, so each dependent step of a chain waits out the 2 wait states gfx950 needs between a
-// VALU writing an SGPR and a VALU reading it (s_nop 1 per step).  Here the eight chains (sum, sum + C, difference,
-// difference fix-up, for each pair) carry through their own SGPR pairs and are interleaved so that every carry is
-// read at least 3 instructions after it was written: no wait-state padding.  Same algorithm as fe_add / fe_sub.
-#ifndef ZK_ADDSUB_ASM
-#define ZK_ADDSUB_ASM 0  // A/B on one box: no gain in the NTT (13.09-13.30 vs 13.13-13.22 ms): at 8 waves per SIMD the wait states are hidden
-#endif
+// ---- two butterflies' sums and differences at once: (a + b, a - b, c + d, c - d) mod p.  (A hand-interleaved
+// asm form with a separate SGPR carry pair per chain measured no faster inside the NTT: tools/ubench/fadd_lab.hip,
+// DESIGN.md "Measured dead ends".)
 __device__ __forceinline__ void fe_addsub2(fe a, fe b, fe c, fe d, fe &apb, fe &amb, fe &cpd, fe &cmd) {
-#if ZK_ADDSUB_ASM
-    // a's words become a - b in place, b's words s + C; likewise c, d (register pressure: 12 new VGPRs)
-    uint32_t a0 = lo32(a.lo), a1 = hi32(a.lo), a2 = lo32(a.hi), a3 = hi32(a.hi);
-    uint32_t b0 = lo32(b.lo), b1 = hi32(b.lo), b2 = lo32(b.hi), b3 = hi32(b.hi);
-    uint32_t c0 = lo32(c.lo), c1 = hi32(c.lo), c2 = lo32(c.hi), c3 = hi32(c.hi);
-    uint32_t d0 = lo32(d.lo), d1 = hi32(d.lo), d2 = lo32(d.hi), d3 = hi32(d.hi);
-    uint32_t sA0, sA1, sA2, sA3, sB0, sB1, sB2, sB3, mA, mB, hA, hB;
-    uint64_t cSA, cUA, cDA, cRA, cSB, cUB, cDB, cRB, selA, selB;
-    const uint32_t K1 = 0x2cffu;
-    asm("v_add_co_u32 %[sA0], %[cSA], %[a0], %[b0]\n\t"
-        "v_sub_co_u32 %[a0], %[cDA], %[a0], %[b0]\n\t"
-        "v_add_co_u32 %[sB0], %[cSB], %[c0], %[d0]\n\t"
-        "v_sub_co_u32 %[c0], %[cDB], %[c0], %[d0]\n\t"
-        "v_add_co_u32 %[b0], %[cUA], %[sA0], -1\n\t"
-        "v_add_co_u32 %[d0], %[cUB], %[sB0], -1\n\t"
-        "v_addc_co_u32 %[sA1], %[cSA], %[a1], %[b1], %[cSA]\n\t"
-        "v_subb_co_u32 %[a1], %[cDA], %[a1], %[b1], %[cDA]\n\t"
-        "v_addc_co_u32 %[sB1], %[cSB], %[c1], %[d1], %[cSB]\n\t"
-        "v_subb_co_u32 %[c1], %[cDB], %[c1], %[d1], %[cDB]\n\t"
-        "v_addc_co_u32 %[b1], %[cUA], %[sA1], %[K1], %[cUA]\n\t"
-        "v_addc_co_u32 %[d1], %[cUB], %[sB1], %[K1], %[cUB]\n\t"
-        "v_addc_co_u32 %[sA2], %[cSA], %[a2], %[b2], %[cSA]\n\t"
-        "v_subb_co_u32 %[a2], %[cDA], %[a2], %[b2], %[cDA]\n\t"
-        "v_addc_co_u32 %[sB2], %[cSB], %[c2], %[d2], %[cSB]\n\t"
-        "v_subb_co_u32 %[c2], %[cDB], %[c2], %[d2], %[cDB]\n\t"
-        "v_addc_co_u32 %[b2], %[cUA], %[sA2], 0, %[cUA]\n\t"
-        "v_addc_co_u32 %[d2], %[cUB], %[sB2], 0, %[cUB]\n\t"
-        "v_addc_co_u32 %[sA3], %[cSA], %[a3], %[b3], %[cSA]\n\t"
-        "v_subb_co_u32 %[a3], %[cDA], %[a3], %[b3], %[cDA]\n\t"
-        "v_addc_co_u32 %[sB3], %[cSB], %[c3], %[d3], %[cSB]\n\t"
-        "v_subb_co_u32 %[c3], %[cDB], %[c3], %[d3], %[cDB]\n\t"
-        "v_addc_co_u32 %[b3], %[cUA], %[sA3], 0, %[cUA]\n\t"
-        "v_addc_co_u32 %[d3], %[cUB], %[sB3], 0, %[cUB]\n\t"
-        // differences: the final borrow becomes a mask m, then d - (m & C) with its own borrow chain
-        "v_cndmask_b32 %[mA], 0, -1, %[cDA]\n\t"
-        "v_cndmask_b32 %[mB], 0, -1, %[cDB]\n\t"
-        // sums: a + b >= p  <=>  carry(a + b) or carry(a + b + C)
-        "s_or_b64 %[selA], %[cSA], %[cUA]\n\t"
-        "s_or_b64 %[selB], %[cSB], %[cUB]\n\t"
-        "v_sub_co_u32 %[a0], %[cRA], %[a0], %[mA]\n\t"
-        "v_and_b32 %[hA], %[K1], %[mA]\n\t"
-        "v_sub_co_u32 %[c0], %[cRB], %[c0], %[mB]\n\t"
-        "v_and_b32 %[hB], %[K1], %[mB]\n\t"
-        "v_cndmask_b32 %[sA0], %[sA0], %[b0], %[selA]\n\t"
-        "v_subb_co_u32 %[a1], %[cRA], %[a1], %[hA], %[cRA]\n\t"
-        "v_cndmask_b32 %[sA1], %[sA1], %[b1], %[selA]\n\t"
-        "v_subb_co_u32 %[c1], %[cRB], %[c1], %[hB], %[cRB]\n\t"
-        "v_cndmask_b32 %[sA2], %[sA2], %[b2], %[selA]\n\t"
-        "v_subb_co_u32 %[a2], %[cRA], %[a2], 0, %[cRA]\n\t"
-        "v_cndmask_b32 %[sA3], %[sA3], %[b3], %[selA]\n\t"
-        "v_subb_co_u32 %[c2], %[cRB], %[c2], 0, %[cRB]\n\t"
-        "v_cndmask_b32 %[sB0], %[sB0], %[d0], %[selB]\n\t"
-        "v_subb_co_u32 %[a3], %[cRA], %[a3], 0, %[cRA]\n\t"
-        "v_cndmask_b32 %[sB1], %[sB1], %[d1], %[selB]\n\t"
-        "v_subb_co_u32 %[c3], %[cRB], %[c3], 0, %[cRB]\n\t"
-        "v_cndmask_b32 %[sB2], %[sB2], %[d2], %[selB]\n\t"
-        "v_cndmask_b32 %[sB3], %[sB3], %[d3], %[selB]"
-        : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3),
-          [b0] "+v"(b0), [b1] "+v"(b1), [b2] "+v"(b2), [b3] "+v"(b3),
-          [c0] "+v"(c0), [c1] "+v"(c1), [c2] "+v"(c2), [c3] "+v"(c3),
-          [d0] "+v"(d0), [d1] "+v"(d1), [d2] "+v"(d2), [d3] "+v"(d3),
-          [sA0] "=&v"(sA0), [sA1] "=&v"(sA1), [sA2] "=&v"(sA2), [sA3] "=&v"(sA3),
-          [sB0] "=&v"(sB0), [sB1] "=&v"(sB1), [sB2] "=&v"(sB2), [sB3] "=&v"(sB3),
-          [mA] "=&v"(mA), [mB] "=&v"(mB), [hA] "=&v"(hA), [hB] "=&v"(hB),
-          [cSA] "=&s"(cSA), [cUA] "=&s"(cUA), [cDA] "=&s"(cDA), [cRA] "=&s"(cRA),
-          [cSB] "=&s"(cSB), [cUB] "=&s"(cUB), [cDB] "=&s"(cDB), [cRB] "=&s"(cRB),
-          [selA] "=&s"(selA), [selB] "=&s"(selB)
-        : [K1] "v"(K1)
-        : "scc");
-    apb = fe{join32(sA0, sA1), join32(sA2, sA3)};
-    amb = fe{join32(a0, a1), join32(a2, a3)};
-    cpd = fe{join32(sB0, sB1), join32(sB2, sB3)};
-    cmd = fe{join32(c0, c1), join32(c2, c3)};
-#else
     apb = fe_add(a, b);
     amb = fe_sub(a, b);
     cpd = fe_add(c, d);
     cmd = fe_sub(c, d);
-#endif
 }
 // the same with lazy sums (fe_add_lazy's contract: a, c any value < 2^128; b, d canonical)
 template <bool LZ>

@@ -55,9 +55,6 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 #ifndef ZK_NTT_LAZY
 #define ZK_NTT_LAZY 1  // fused UNI pass-1 rounds keep butterfly sums partially reduced (fe_add_lazy); the pass
 #endif                 // twiddle multiply makes the stored values canonical (A/B: pass 1 -0.09 ms per proof)
-#ifndef ZK_NTT_LAZY2
-#define ZK_NTT_LAZY2 0  // the same in pass 2, with fe_canon at the store: +0.1 ms per proof (A/B), off
-#endif
 #ifndef ZK_NTT_J0
 #define ZK_NTT_J0 1  // plain-DFT wave-uniform rounds: the waves with j = 0 skip their three unit-twiddle multiplies
 #endif
@@ -501,12 +498,11 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const fe *in = a.in + b * a.in_stride;
     if constexpr (Fuse<LOGM, TILE>::OK) {
         fe *out = a.out_of(b);
-        first_round_from<LOGM, TILE, false, ZK_NTT_LAZY2>(
+        first_round_from<LOGM, TILE, false, false>(
             s, [&](int line, int k1) { return in[(size_t)k1 * n2 + j2_0 + line]; }, a.tw_ws);
-        r4_rounds<LOGM, TILE, 3, false, LOGM - 2, ZK_NTT_LAZY2>(s, a.tw4096, a.tw_ws, a.tw_w2);
-        last_round_to<LOGM, TILE, false, ZK_NTT_LAZY2>(s, a.tw_w2, [&](int line, int j1, fe v) {
+        r4_rounds<LOGM, TILE, 3, false, LOGM - 2, false>(s, a.tw4096, a.tw_ws, a.tw_w2);
+        last_round_to<LOGM, TILE, false, false>(s, a.tw_w2, [&](int line, int j1, fe v) {
             if (a.has_post) v = fe_mul(v, a.post);
-            else if (ZK_NTT_LAZY2) v = fe_canon(v);
             out[n2 * (size_t)j1 + j2_0 + line] = v;
         });
         return;
@@ -609,12 +605,8 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
 void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp);
 
 int ntt_log_n2(int L) {
-    static const bool balanced = [] {
-        const char *e = getenv("ZK_NTT_SPLIT");
-        return e && !strcmp(e, "balanced");
-    }();
     const int bal = (L + 1) / 2;
-    if (balanced || L < 20) return bal;
+    if (L < 20) return bal;
     return std::min(12, L - 10);  // pass-2 lines of 1024 while pass-1 lines fit a 4096-element tile
 }
 

@@ -1147,11 +1147,7 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     // caller dumps the composition values, which must then include them).
     const bool bnd_rows = dump && dump->composition;
     // CE cosets evaluated: 7 when the composition has at most 7 columns (the stage derives the 8th)
-    static const bool ce7 = [] {
-        const char *e = getenv("ZK_CE7");
-        return !e || atoi(e) != 0;
-    }();
-    const int nce = (ce7 && !bnd_rows && C <= 7) ? 7 : 8;
+    const int nce = (!bnd_rows && C <= 7) ? 7 : 8;
     AirConsts Kp[2];
     if (KX == 1) {
         draw_air_consts(coin, pub, n, Kp[0], R);

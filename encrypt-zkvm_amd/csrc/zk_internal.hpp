@@ -88,7 +88,7 @@ struct NttTables {
 // at L = 22 the balanced 11/11 split leaves pass 2 with 32-B segments (2 lines of 2048 per
 // 4096-element tile) and an extra radix-2 LDS stage; 12/10 gives it the 64-B segments of 2^20.
 // Every table builder and the NTT dispatcher use this one function, so they always agree.
-// ZK_NTT_SPLIT=balanced restores the ceil(L/2) split (A/B runs); read once per process.
+// (the balanced ceil(L/2) split measured slower at 2^22: DESIGN.md "NTT")
 int ntt_log_n2(int L);
 // fill NttTables::fwd_pass / inv_pass (allocated by the caller, n elements each)
 void make_pass_twiddles(hipStream_t st, NttTables &T);

@@ -15,6 +15,6 @@ for v in "$@"; do
   python3 - "$v" "$O/abenv_$i.json" <<'PY'
 import json, sys
 b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(f"{sys.argv[1]:>24} {b['ms_per_step']:8.3f} ms")
+print(f"{sys.argv[1]:>24} {b['ms_per_step']:8.3f} ms  latency {b.get('latency_ms')} device {b.get('device_resident_ms')}")
 PY
 done
