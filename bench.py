@@ -11,10 +11,11 @@ on a copy stream, overlapped with the interpolation and, with two provers in fli
 kernels.  Beside `value` the line reports device_resident_ms (the trace already in HBM), pageable_host_ms
 (the trace in ordinary pageable memory) and latency_ms (one prove() call alone on the GPU).
 
-Proofs in flight (--inflight P, default 2): each GPU holds P independent provers (own HBM buffers and
-stream, zk_prover objects) driven by P host threads, so one prover's host-side transcript round trips and
-proof tail overlap the other's kernels (tools/dual_prover.py: 13.90 -> 13.46 ms per proof at P = 2).  The
-K timed steps are K complete proofs, dealt round-robin to the provers; per-proof latency is stage_ms.
+Proofs in flight (--inflight P, default 3): each GPU holds P independent provers (own HBM buffers and
+streams, zk_prover objects) driven by P host threads, so one prover's trace upload, host-side transcript round
+trips and proof tail overlap the others' kernels (host-resident trace: 16.1 ms per proof at P = 2 with HIP's 4
+hardware queues, 12.9 ms at P = 3 with 16; device-resident 12.5).  The K timed steps are K complete proofs, dealt
+round-robin to the provers; per-proof latency is stage_ms.
 
 Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
 scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
