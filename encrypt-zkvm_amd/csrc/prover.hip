@@ -280,12 +280,13 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     p->device = device;
     p->max_n = max_n;
     p->max_b = max_b;
-    p->shard_world = world;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
     // Nl: LDE-domain points this prover holds (all N, or the N / G of one sharded rank)
+    if (world == 1) world = 0;  // one rank holds the whole domain: a full prover
+    p->shard_world = world;
     const size_t Nl = world ? N / (size_t)world : N;
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
@@ -1404,6 +1405,19 @@ int zk_prove_device(zk_prover *p, const void *d_trace, size_t n, const zk_option
     TraceSrc src;
     src.dev = (const fe *)d_trace;
     return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+}
+
+int zk::prove_single(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                     uint8_t *proof_out, size_t *proof_len, zk_record *rec) {
+    const uint8_t *cols[W];
+    TraceSrc src;
+    if (trace) {
+        for (int c = 0; c < W; c++) cols[c] = trace + (size_t)c * n * sizeof(fe);
+        src.cols = cols;
+    } else {
+        src.dev = p->d_trace;
+    }
+    return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, nullptr);
 }
 
 int zk_prove_columns_ex(zk_prover *p, const uint8_t *const *columns, size_t n, const zk_options *opt,

@@ -48,7 +48,7 @@ static constexpr int NUM_ASSERTS = 22;
 // single-GPU entry points refuse a prover sized for one rank of a sharded proof
 #define ZK_REQUIRE_FULL_PROVER(p)                                                                                  \
     do {                                                                                                          \
-        if ((p)->shard_world)                                                                                     \
+        if ((p)->shard_world > 1)                                                                                 \
             ZK_FAIL(ZK_ERR_INVALID_ARG, "this prover was created for one rank of a sharded proof (zk_prover_create_shard)"); \
     } while (0)
 
@@ -111,9 +111,9 @@ struct zk_prover {
     uint32_t *up_flag = nullptr;
     uint32_t up_seq = 0;
     size_t max_n = 0;
-    // 0: a full prover (every entry point).  G in {1, 2, 4, 8}: sized for one rank of a G-way coset-sharded proof
+    // 0: a full prover (every entry point).  G in {2, 4, 8}: sized for one rank of a G-way coset-sharded proof
     // (zk_prover_create_shard): the LDE-domain buffers hold the rank's 8/G cosets only, so it serves
-    // zk_prove_sharded with that world size and nothing else
+    // zk_prove_sharded with that world size and nothing else.  (G = 1 is a full prover.)
     int shard_world = 0;
     uint32_t max_b = 0;
     zk::DeviceArena arena;
@@ -179,6 +179,11 @@ struct zk_prover {
 };
 
 namespace zk {
+
+// the single-GPU prove path (prover.hip) for a sharded proof over one rank: trace = host column-major trace, or
+// NULL when it already sits in p->d_trace
+int prove_single(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                 uint8_t *proof_out, size_t *proof_len, zk_record *rec);
 
 // ---- small transfers through the pinned staging area (zk_prover::h_io)
 inline uint8_t *io_take(zk_prover *p, size_t len) {
