@@ -282,6 +282,7 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+    for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
     // Nl: LDE-domain points this prover holds (all N, or the N / G of one sharded rank)
@@ -323,8 +324,6 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_idx, ZK_GATHER_CAP * sizeof(uint64_t), hipHostMallocDefault));
     ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_gather_out, ZK_GATHER_CAP * sizeof(fe), hipHostMallocDefault));
     ZK_CHECK_HIP(A.alloc(&p->flag, 4));
-    ZK_CHECK_HIP(A.alloc(&p->up_flag, 16));
-    ZK_CHECK_HIP(hipMemset(p->up_flag, 0, 64));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->air_consts, sizeof(AirConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->deep_consts, sizeof(DeepConsts)));
     ZK_CHECK_HIP(A.alloc((uint8_t **)&p->fold_consts, sizeof(FoldConsts)));
@@ -352,6 +351,8 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamSynchronize(p->st);
     if (p->st2) (void)hipStreamSynchronize(p->st2);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
+    for (auto &e : p->ev_up)
+        if (e) (void)hipEventDestroy(e);
     if (p->st2) (void)hipStreamDestroy(p->st2);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
@@ -965,9 +966,16 @@ static_assert(W % ZK_UPLOAD_GROUPS == 0 && ZK_UPLOAD_GROUPS <= ZK_UPLOAD_GROUPS_
 // hipHostRegister'ed buffer) is a DMA in stream order; from pageable memory the runtime stages the copy
 // through its own pinned buffers and returns once the source has been read (the host thread copies).
 // Both are correct here; the pinned form is the fast one (DESIGN.md "Host-resident trace").
+// Columns that are contiguous in host memory (zk_prove's single buffer) go up as one copy per run.
 static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c0, int nc) {
-    for (int c = c0; c < c0 + nc; c++)
-        ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, src.cols[c], n * sizeof(fe), hipMemcpyHostToDevice, p->st2));
+    const size_t col = n * sizeof(fe);
+    for (int c = c0; c < c0 + nc;) {
+        int e = c + 1;
+        while (e < c0 + nc && src.cols[e] == src.cols[e - 1] + col) e++;
+        ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, src.cols[c], (size_t)(e - c) * col, hipMemcpyHostToDevice,
+                                    p->st2));
+        c = e;
+    }
     return ZK_OK;
 }
 
@@ -984,17 +992,16 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     const int log_n = pl->log_n, log_b = pl->log_b;
     const size_t B = (size_t)1 << log_b;
     // The device trace buffer is free: the previous proof on this prover returned only after its stream drained
-    // (and the trace is read by the interpolation alone).  Group g of proof s is in HBM once *up_flag reaches
-    // s * 8 + g + 1 (monotonic, so a flag left by an earlier proof never satisfies a later wait).
-    const uint32_t base = (++p->up_seq) * 8u;
+    // (and the trace is read by the interpolation alone).
+    // Group by group: its copies, then its kernels.  From page-locked memory every call returns at once (the
+    // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
+    // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
     constexpr int per = W / ZK_UPLOAD_GROUPS;
     for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
         ZK_TRY(upload_trace_group(p, src, n, g * per, per));
-        ZK_CHECK_HIP(hipStreamWriteValue32(p->st2, p->up_flag, base + (uint32_t)g + 1u, 0));
-    }
-    for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
+        ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->st2));
         const size_t c0 = (size_t)g * per;
-        ZK_CHECK_HIP(hipStreamWaitValue32(p->st, p->up_flag, base + (uint32_t)g + 1u, hipStreamWaitValueGte, 0xffffffffu));
+        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[g], 0));
         ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
     }

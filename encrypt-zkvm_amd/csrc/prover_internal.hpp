@@ -104,12 +104,12 @@ struct zk_prover {
     // copy stream: a host-resident trace is uploaded here in column groups, each group's event gating its
     // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it
     hipStream_t st2 = nullptr;
-    // ... ordered by a device word the copy stream writes after each group (hipStreamWriteValue32) and the compute
-    // stream waits on (hipStreamWaitValue32): measured (tools/ubench/upload_probe.hip), an event recorded between
-    // the column copies of one stream halves their rate (29.7 vs 55 GB/s), a cross-stream event wait ahead of them
-    // costs 25 %, the value writes cost nothing
-    uint32_t *up_flag = nullptr;
-    uint32_t up_seq = 0;
+    // ... each group's event gating its kernels on st.  Measured (tools/ubench/upload_probe.hip): an event recorded
+    // between the 16 MiB column copies of one stream halves their rate (29.7 vs 55 GB/s), but not between 112 MiB
+    // copies (56.8 GB/s), so contiguous columns go up as one copy per group.  (Stream write / wait-value packets
+    // avoid the slowdown too, but a compute stream parked on a wait-value packet can deadlock the copy stream's
+    // write when the runtime maps both streams onto one hardware queue -- it hung under rocprofv3 --pmc.)
+    hipEvent_t ev_up[zk::ZK_UPLOAD_GROUPS_MAX] = {};
     size_t max_n = 0;
     // 0: a full prover (every entry point).  G in {2, 4, 8}: sized for one rank of a G-way coset-sharded proof
     // (zk_prover_create_shard): the LDE-domain buffers hold the rank's 8/G cosets only, so it serves

@@ -32,6 +32,47 @@ __global__ void __launch_bounds__(256) k_tput(uint64_t *out, uint32_t seed, cons
     for (int i = 0; i < 4; i++) s ^= a[i].lo ^ a[i].hi;
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
+// Lower bound of an unsaturated representation: 5 limbs of 26 bits (130 bits), the 25 partial
+// products accumulated per column in 64 bits (each column < 5 * 2^52, so no carry ever leaves a column: no SGPR
+// carry chains), then the 9 columns normalised back to 26-bit limbs.  This is NOT a field multiply -- the reduction
+// mod p (2^130 = 4C, C = 45 * 2^40 - 1, a second limb product and normalisation) and the conversion to and from the
+// 4 x 32-bit storage form are left out -- so its slot count bounds the form from below.
+__device__ __forceinline__ void unsat_mul_norm(uint32_t a[5], const uint32_t b[5]) {
+    uint64_t col[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) col[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+#pragma unroll
+        for (int j = 0; j < 5; j++) col[i + j] += (uint64_t)a[i] * b[j];
+    uint64_t carry = 0;
+    uint32_t t[10];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint64_t c = col[k] + carry;
+        t[k] = (uint32_t)c & 0x3ffffffu;
+        carry = c >> 26;
+    }
+    t[9] = (uint32_t)carry;
+    // feed the product back (a dependency chain); the high limbs are folded in with plain xors to keep them live
+#pragma unroll
+    for (int i = 0; i < 5; i++) a[i] = (t[i] ^ t[i + 5]) & 0x3ffffffu;
+}
+__global__ void __launch_bounds__(256) k_tput_unsat(uint64_t *out, uint32_t seed) {
+    uint32_t a[4][5], b[5];
+    for (int i = 0; i < 5; i++) b[i] = (threadIdx.x * 2654435761u + seed + i) & 0x3ffffffu;
+    for (int c = 0; c < 4; c++)
+        for (int i = 0; i < 5; i++) a[c][i] = (blockIdx.x + c * 7 + i) & 0x3ffffffu;
+    for (int it = 0; it < 1024; it++) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) unsat_mul_norm(a[c], b);
+    }
+    uint64_t s = 0;
+    for (int c = 0; c < 4; c++)
+        for (int i = 0; i < 5; i++) s ^= a[c][i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ void k_add(uint64_t *out, uint32_t seed) {
     uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const uint32_t x = seed;
@@ -135,5 +176,9 @@ int main() {
     (void)hipMemcpy(da, ha.data(), n * sizeof(fe), hipMemcpyHostToDevice);
     (void)hipMemcpy(db, hb.data(), n * sizeof(fe), hipMemcpyHostToDevice);
     const float tadd = tk(k_add, out, 256 * 8);
-    return run_all<0>(out, da, db, dout, ha, hb, tadd);
+    const int rc = run_all<0>(out, da, db, dout, ha, hb, tadd);
+    const float tu = tk(k_tput_unsat, out, 256 * 8);
+    printf("unsaturated 5 x 26-bit limbs, product + normalisation only (no reduction, no conversion; a lower bound): "
+           "%.1f add-equivalents per multiply\n", tu / tadd * (8192.0 * 8) / (1024.0 * 4));
+    return rc;
 }
