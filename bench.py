@@ -11,11 +11,11 @@ on a copy stream, overlapped with the interpolation and, with two provers in fli
 kernels.  Beside `value` the line reports device_resident_ms (the trace already in HBM), pageable_host_ms
 (the trace in ordinary pageable memory) and latency_ms (one prove() call alone on the GPU).
 
-Proofs in flight (--inflight P, default 3): each GPU holds P independent provers (own HBM buffers and
+Proofs in flight (--inflight P, default 4): each GPU holds P independent provers (own HBM buffers and
 streams, zk_prover objects) driven by P host threads, so one prover's trace upload, host-side transcript round
-trips and proof tail overlap the others' kernels (host-resident trace: 16.1 ms per proof at P = 2 with HIP's 4
-hardware queues, 12.9 ms at P = 3 with 16; device-resident 12.5).  The K timed steps are K complete proofs, dealt
-round-robin to the provers; per-proof latency is stage_ms.
+trips and proof tail overlap the others' kernels (host-resident trace, one box: 13.6-13.8 ms per proof at P = 3,
+13.2-13.4 at P = 4, device-resident 12.7-12.9; 16.1 ms at P = 2 with HIP's default 4 hardware queues).  The K timed
+steps are K complete proofs, dealt round-robin to the provers; per-proof latency is stage_ms.
 
 Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
 scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
@@ -245,7 +245,7 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=-1,
                     help="threads of the all-cores CPU sample (-1: the host share, at most 16; 0: skip it)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3, help="independent provers (proofs in flight) per GPU")
+    ap.add_argument("--inflight", type=int, default=4, help="independent provers (proofs in flight) per GPU")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
     ap.add_argument("--sharded-log-n", type=int, default=22,
                     help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
@@ -255,9 +255,9 @@ def main():
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
     # Each prover drives two streams (compute, trace upload); with HIP's default of 4 hardware queues per process the
-    # streams of 3 provers share queues, and a compute stream parked on its upload's wait-value packet then holds
-    # up the kernels of another prover queued behind it (A/B: 16.1 ms per proof at 4 queues, 14.3 at 8, 12.9 with 3
-    # provers at 16 -- device-resident 12.5).  Set before the first HIP call of the process (torch.distributed too).
+    # streams of several provers share queues, and a compute stream parked on its upload's event then holds up the
+    # kernels of another prover queued behind it (A/B, 2 provers: 16.1 ms per proof at 4 queues, 14.3 at 8, 13.8 at
+    # 16).  Set before the first HIP call of the process (torch.distributed's included).
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     if args.sharded:
         return run_sharded(args)

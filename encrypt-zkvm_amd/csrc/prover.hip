@@ -954,11 +954,12 @@ struct TraceSrc {
     const uint8_t *const *cols = nullptr;
 };
 
-// Column groups of a host-resident trace upload: 4 groups of 7 columns.  The copy engine streams group
-// g + 1 while the CUs interpolate and extend group g; more groups overlap more of the copy but add a launch
-// drain per NTT pass and group.
+// Column groups of a host-resident trace upload: 7 groups of 4 columns.  The copy engine streams group g + 1 while
+// the CUs interpolate and extend group g; more groups overlap more of the copy but add a launch drain per NTT pass
+// and group.  A/B on one box (3 provers in flight): 1 group 12.73-13.02 ms per proof at 22.7 ms latency, 2 groups
+// 13.15-13.24 / 18.7, 4 groups 13.16-13.32 / 16.8, 7 groups 13.02-13.04 / 15.9 (device-resident 12.15-12.32).
 #ifndef ZK_UPLOAD_GROUPS
-#define ZK_UPLOAD_GROUPS 4
+#define ZK_UPLOAD_GROUPS 7
 #endif
 static_assert(W % ZK_UPLOAD_GROUPS == 0 && ZK_UPLOAD_GROUPS <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
 
