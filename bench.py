@@ -372,20 +372,48 @@ def main():
     trace = None
     host.close()
 
-    # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record
-    sharded = None
+    out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
+                     latency_ms, dev_s, pag_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
+                     zk_verified) if rank == 0 else None
+
+    # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A
+    # watchdog bounds it: should a collective never complete, rank 0 still prints the line (with the error) and
+    # every rank exits, so the replica measurement above is never lost.
     if world > 1 and args.sharded_log_n:
         import torch
         if torch.cuda.is_available():
-            sharded = sharded_leg(args, args.sharded_log_n, world, rank, local, pg, steps=10, warmup=3)
-            for k in ("pub", "proof", "n", "min_sec"):
-                sharded.pop(k)
+            done = threading.Event()
 
-    if rank != 0:
-        if pg is not None:
-            pg.destroy_process_group()
-        return
+            def watchdog():
+                if not done.wait(SHARDED_TIMEOUT_S):
+                    if out is not None:
+                        out["sharded"] = {"error": f"the sharded proof did not finish within {SHARDED_TIMEOUT_S} s"}
+                        print(json.dumps(out), flush=True)
+                    os._exit(0)
 
+            threading.Thread(target=watchdog, daemon=True).start()
+            try:
+                rec = sharded_leg(args, args.sharded_log_n, world, rank, local, pg, steps=10, warmup=3)
+                for k in ("pub", "proof", "n", "min_sec"):
+                    rec.pop(k)
+            except Exception as e:  # reported in the line; the replica value stands
+                rec = {"error": repr(e)}
+            done.set()
+            if out is not None:
+                out["sharded"] = rec
+
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+SHARDED_TIMEOUT_S = 240
+
+
+def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops, latency_ms,
+               dev_s, pag_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified):
+    """rank 0's JSON line (the driver's contract) from the measurements of main()."""
     dom = max(kstats.items(), key=lambda kv: kv[1][0])
     name, (tot_ms, launches, tot_bytes) = dom
     avg_ms = tot_ms / launches
@@ -432,11 +460,7 @@ def main():
         "vm": vm_rec,
         "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
     }
-    if sharded is not None:
-        out["sharded"] = sharded
-    print(json.dumps(out), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    return out
 
 
 def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=False):
