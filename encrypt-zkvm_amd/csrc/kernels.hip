@@ -1698,8 +1698,8 @@ __global__ void k_ood_tables(fe z, fe zg, uint64_t chunk, int nw, fe *tab) {
 
 template <int E>
 __global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const fe *cpolys, int C, size_t n,
-                                                  const fe *tab, int nw, fe *partials) {
-    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+                                                  const fe *tab, int nw, int w0, int w1, fe *partials) {
+    const int gw = w0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // waves [w0, w1) of nw
     const int lane = threadIdx.x & 63;
     const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
     const int g = blockIdx.y;
@@ -1716,7 +1716,7 @@ __global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const
         Y[which][e] = fe_exp(y, (uint64_t)e);
     }
     __syncthreads();
-    if (gw >= nw) return;
+    if (gw >= w1) return;
     const fe wz = fe_mul(tab[lane], tab[128 + gw]);
     const fe wzg = comp ? fe_zero() : fe_mul(tab[64 + lane], tab[128 + nw + gw]);
     for (int p = p0; p < p1; p++) {
@@ -1744,15 +1744,18 @@ __global__ void __launch_bounds__(256) k_ood_eval(const fe *tpolys, int W, const
 
 int ood_waves(size_t n) { return (int)std::max<size_t>(1, n / 1024); }
 
+// part = (rank, G): only this rank's share of the coefficient range (waves [rank nw / G, (rank + 1) nw / G)), so that
+// the G partial sums of each value add up to it (the sharded prover all-gathers them); (0, 1) = the whole range
 void ood_eval(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe z, fe zg, fe *tab,
-              fe *partials, fe *out) {
+              fe *partials, fe *out, int rank, int G) {
     const size_t n = (size_t)1 << log_n;
     const int E = n >= 1024 ? 16 : std::max<int>(1, (int)(n / 64));
     const int nw = (int)((n + 64 * E - 1) / (64 * E));
+    const int w0 = (int)((int64_t)nw * rank / G), w1 = (int)((int64_t)nw * (rank + 1) / G);
     hipLaunchKernelGGL(k_ood_tables, dim3(cdiv(128 + 2 * nw, 256)), dim3(256), 0, st, z, zg, (uint64_t)64 * E, nw, tab);
-    const dim3 grid(cdiv(nw, 4), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
-#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, tab, nw, partials)
-    const double bytes = 16.0 * (W + C) * n;
+    const dim3 grid(std::max(1u, cdiv(w1 - w0, 4)), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
+#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, tab, nw, w0, w1, partials)
+    const double bytes = 16.0 * (W + C) * (double)n * (w1 - w0) / nw;
     switch (E) {
         case 16: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(16)); break;
         case 8: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(8)); break;
@@ -1761,13 +1764,13 @@ void ood_eval(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, 
         default: ZK_PROF(st, "ood_eval", bytes, ZK_OOD(1)); break;
     }
 #undef ZK_OOD
-    sum_partials(st, partials, 2 * W + C, nw, out);
+    sum_partials(st, partials, 2 * W + C, nw, out, w0, w1);
 }
 
-__global__ void k_sum_partials(const fe *partials, int nblk, fe *out) {
+__global__ void k_sum_partials(const fe *partials, int nblk, int b0, int b1, fe *out) {
     __shared__ fe red[256];
     fe acc = fe_zero();
-    for (int b = threadIdx.x; b < nblk; b += blockDim.x) acc = fe_add(acc, partials[(size_t)blockIdx.x * nblk + b]);
+    for (int b = b0 + (int)threadIdx.x; b < b1; b += blockDim.x) acc = fe_add(acc, partials[(size_t)blockIdx.x * nblk + b]);
     red[threadIdx.x] = acc;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -1777,8 +1780,9 @@ __global__ void k_sum_partials(const fe *partials, int nblk, fe *out) {
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
-void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out) {
-    hipLaunchKernelGGL(k_sum_partials, dim3(npolys), dim3(256), 0, st, partials, nblk, out);
+void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out, int b0, int b1) {
+    if (b1 < 0) b1 = nblk;
+    hipLaunchKernelGGL(k_sum_partials, dim3(npolys), dim3(256), 0, st, partials, nblk, b0, b1, out);
 }
 
 // ================================================================ DEEP composition (K6)
@@ -2338,8 +2342,8 @@ __device__ __forceinline__ fe2 dot_base_ext(const fe *v, const fe2 *y) {
 
 template <int E>
 __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, const fe *cpolys, int C, size_t n,
-                                                      const fe2 *tab, int nw, fe *partials) {
-    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+                                                      const fe2 *tab, int nw, int w0, int w1, fe *partials) {
+    const int gw = w0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // waves [w0, w1) of nw
     const int lane = threadIdx.x & 63;
     const int np = 2 * W + C;
     const int tgroups = (W + OOD_GROUP - 1) / OOD_GROUP;
@@ -2356,7 +2360,7 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
         Y[which][e] = fe2_exp(y, (uint64_t)e);
     }
     __syncthreads();
-    if (gw >= nw) return;
+    if (gw >= w1) return;
     const fe2 wz = fe2_mul(tab[lane], tab[128 + gw]);
     const fe2 wzg = comp ? fe2_zero() : fe2_mul(tab[64 + lane], tab[128 + nw + gw]);
     for (int p = p0; p < p1; p++) {
@@ -2386,15 +2390,16 @@ __global__ void __launch_bounds__(256) k_ood_eval_ext(const fe *tpolys, int W, c
 }
 
 void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
-                  fe *tab, fe *partials, fe *out) {
+                  fe *tab, fe *partials, fe *out, int rank, int G) {
     const size_t n = (size_t)1 << log_n;
     const int E = n >= 1024 ? 16 : std::max<int>(1, (int)(n / 64));
     const int nw = (int)((n + 64 * E - 1) / (64 * E));
+    const int w0 = (int)((int64_t)nw * rank / G), w1 = (int)((int64_t)nw * (rank + 1) / G);
     fe2 *t2 = reinterpret_cast<fe2 *>(tab);
     hipLaunchKernelGGL(k_ood_tables_ext, dim3(cdiv(128 + 2 * nw, 256)), dim3(256), 0, st, z, zg, (uint64_t)64 * E, nw, t2);
-    const dim3 grid(cdiv(nw, 4), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
-#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval_ext<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, t2, nw, partials)
-    const double bytes = 16.0 * (W + C) * n;
+    const dim3 grid(std::max(1u, cdiv(w1 - w0, 4)), (W + OOD_GROUP - 1) / OOD_GROUP + 1);
+#define ZK_OOD(EE) hipLaunchKernelGGL((k_ood_eval_ext<EE>), grid, dim3(256), 0, st, tpolys, W, cpolys, C, n, t2, nw, w0, w1, partials)
+    const double bytes = 16.0 * (W + C) * (double)n * (w1 - w0) / nw;
     switch (E) {
         case 16: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(16)); break;
         case 8: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(8)); break;
@@ -2403,7 +2408,7 @@ void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int
         default: ZK_PROF(st, "ood_eval_ext", bytes, ZK_OOD(1)); break;
     }
 #undef ZK_OOD
-    sum_partials(st, partials, 2 * (2 * W + C), nw, out);
+    sum_partials(st, partials, 2 * (2 * W + C), nw, out, w0, w1);
 }
 
 // 1 / (N(x - z) N(x - zg)): N(x - z) = (x - z.a)(x - z.a - z.b) - z.b^2 (the norm of x - z, X^2 = X + 1)

@@ -426,16 +426,36 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     coin.reseed(R.constraint_root);
 
-    // S5: OOD frame (every process evaluates the replicated polynomials), DEEP over the local cosets
+    // S5: OOD frame -- every rank evaluates its 1/G of the coefficient range of the (replicated) polynomials, the
+    // partial sums are all-gathered and added on the host -- then DEEP over the local cosets
     std::vector<fe> h;  // the OOD frame, flattened (k base elements per E value)
-    ZK_CHECK_HIP(hipSetDevice(P0->device));
+    // nv values per rank (ood_eval / ood_eval_ext output); the frame value v is sum over ranks of part[rank][v]
+    auto ood_parts = [&](int nv, auto launch, std::vector<fe> &sum) -> int {
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            launch(p, X.rank[l]);
+            snd[l] = p->ood;
+            rcv[l] = p->sh_buf;
+        }
+        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)nv * sizeof(fe)));
+        std::vector<fe> parts((size_t)G * nv);
+        ZK_CHECK_HIP(hipSetDevice(P0->device));
+        ZK_TRY(d2h_small(P0, parts.data(), P0->sh_buf, parts.size() * sizeof(fe)));
+        ZK_TRY(d2h_flush(P0));
+        sum.assign(nv, fe_zero());
+        for (int d = 0; d < G; d++)
+            for (int v = 0; v < nv; v++) sum[v] = fe_add(sum[v], parts[(size_t)d * nv + v]);
+        return ZK_OK;
+    };
     if (KX == 1) {
         const fe z = coin.draw(), zg = fe_mul(z, g);
         fe_to_bytes(z, R.z);
-        h.resize(2 * W + C);
-        ood_eval(P0->st, P0->polys, W, P0->cpolys, C, log_n, z, zg, P0->ood_tab, P0->partials, P0->ood);
-        ZK_TRY(d2h_small(P0, h.data(), P0->ood, (2 * W + C) * sizeof(fe)));
-        ZK_TRY(d2h_flush(P0));
+        ZK_TRY(ood_parts(2 * W + C, [&](zk_prover *p, int rank) {
+            ood_eval(p->st, p->polys, W, p->cpolys, C, log_n, z, zg, p->ood_tab, p->partials, p->ood, rank, G);
+        }, h));
         ood_reseed(coin, h.data(), C, R);
         stage_mark(P0, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
@@ -452,10 +472,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
         fe_to_bytes(z.a, R.z);
         const int np = 2 * W + CK;
-        ood_eval_ext(P0->st, P0->polys, W, P0->cpolys, CK, log_n, z, zg, P0->x_tab, P0->x_partials, P0->ood);
-        std::vector<fe> hv(2 * np);
-        ZK_TRY(d2h_small(P0, hv.data(), P0->ood, hv.size() * sizeof(fe)));
-        ZK_TRY(d2h_flush(P0));
+        std::vector<fe> hv;
+        ZK_TRY(ood_parts(2 * np, [&](zk_prover *p, int rank) {
+            ood_eval_ext(p->st, p->polys, W, p->cpolys, CK, log_n, z, zg, p->x_tab, p->x_partials, p->ood, rank, G);
+        }, hv));
         std::vector<fe2> e;
         ood_reseed_ext(coin, hv, C, R, e, h);
         stage_mark(P0, "ood");
@@ -566,8 +586,21 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         layer_vals[1] = FRI(P0);
         layer_len[1] = rows0;
         {
+            // layers >= 1 are replicated on local rank 0: their coins run on the device as in the single-GPU path
+            // (fri_coin_launch: no host round trip per layer), the host replays the transcript after one flush
             fe *next = FRI(P0) + KX * rows0;
             uint8_t *dig = P0->fri_dig;  // the all-to-all scratch is free once layer 0 is committed
+            fe *alpha_dev = nullptr;
+            if (KX == 1) {
+                const FoldConsts F = fold_consts(fe_zero(), fold);
+                ZK_TRY(h2d_small(P0, P0->fold_consts, &F, sizeof F));
+                alpha_dev = &((FoldConsts *)P0->fold_consts)->alpha;
+            } else {
+                const FoldConstsE F = fold_consts_ext(fe2_zero(), fold);
+                ZK_TRY(h2d_small(P0, P0->x_fold_consts, &F, sizeof F));
+                alpha_dev = &((FoldConstsE *)P0->x_fold_consts)->alpha.a;
+            }
+            ZK_TRY(h2d_small(P0, P0->fri_seed, coin.seed, 32));  // reseeded with layer 0's root: the counter restarts
             for (int l = 1; l < nl; l++) {
                 const size_t L = layer_len[l], rows = L / fold;
                 layer_leaves[l] = dig;
@@ -575,30 +608,26 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 dig += 64 * rows;
                 if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
                 else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-                ZK_TRY(d2h_small(P0, R.fri_roots[l], layer_nodes[l] + 32, 32));
-                ZK_TRY(d2h_flush(P0));
-                coin.reseed(R.fri_roots[l]);
-                if (KX == 1) {
-                    const fe alpha = coin.draw();
-                    fe_to_bytes(alpha, R.fri_alphas[l]);
-                    const FoldConsts F = fold_consts(alpha, fold);
-                    ZK_TRY(h2d_small(P0, P0->fold_consts, &F, sizeof F));
-                    fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
-                } else {
-                    const fe2 alpha = coin.draw_ext(2);
-                    fe_to_bytes(alpha.a, R.fri_alphas[l]);
-                    const FoldConstsE F = fold_consts_ext(alpha, fold);
-                    ZK_TRY(h2d_small(P0, P0->x_fold_consts, &F, sizeof F));
-                    fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L,
-                                        next);
-                }
+                fri_coin_launch(P0->st, (uint32_t *)P0->fri_seed, layer_nodes[l] + 32, KX, alpha_dev, P0->fri_alphas + 2 * l);
+                if (KX == 1) fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
+                else fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L, next);
                 layer_vals[l + 1] = next;
                 layer_len[l + 1] = rows;
                 next += KX * rows;
             }
-            std::vector<fe> rv(KX * layer_len[nl]);
+            // one round trip: roots and device alphas of layers >= 1, the last layer
+            std::vector<fe> rv(KX * layer_len[nl]), dalpha(2 * nl);
+            for (int l = 1; l < nl; l++) ZK_TRY(d2h_small(P0, R.fri_roots[l], layer_nodes[l] + 32, 32));
+            if (nl > 1) ZK_TRY(d2h_small(P0, dalpha.data() + 2, P0->fri_alphas + 2, 2 * (nl - 1) * sizeof(fe)));
             ZK_TRY(d2h_small(P0, rv.data(), layer_vals[nl], rv.size() * sizeof(fe)));
             ZK_TRY(d2h_flush(P0));
+            for (int l = 1; l < nl; l++) {  // host replay of the same transcript
+                coin.reseed(R.fri_roots[l]);
+                const fe2 alpha = KX == 1 ? fe2{coin.draw(), fe_zero()} : coin.draw_ext(2);
+                fe_to_bytes(alpha.a, R.fri_alphas[l]);
+                if (!fe_eq(alpha.a, dalpha[2 * l]) || (KX == 2 && !fe_eq(alpha.b, dalpha[2 * l + 1])))
+                    ZK_FAIL(ZK_ERR_DEVICE, "device FRI transcript diverged from the host transcript");
+            }
             ZK_TRY(remainder(rv));
         }
     }

@@ -238,8 +238,8 @@ void comp_cross_coset(hipStream_t st, const fe *c, int log_n, const NttTables &T
 // elements, partials: (2W + C) * ood_waves(n) elements of scratch.
 int ood_waves(size_t n);
 void ood_eval(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe z, fe zg, fe *tab,
-              fe *partials, fe *out);
-void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out);
+              fe *partials, fe *out, int rank = 0, int G = 1);
+void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *out, int b0 = 0, int b1 = -1);
 // DEEP over the LDE domain, natural order (consts: DeepConsts in device memory)
 struct DeepConsts {
     fe alpha_t[32];
@@ -285,7 +285,7 @@ void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev
 // OOD frame over E points: out[j*np + P], np = 2W + C, component j of poly P's value (T(z), T(zg), H(z));
 // tab: 2 * (128 + 2 * ood_waves(n)) fe, partials: 2 * np * ood_waves(n) fe.
 void ood_eval_ext(hipStream_t st, const fe *tpolys, int W, const fe *cpolys, int C, int log_n, fe2 z, fe2 zg,
-                  fe *tab, fe *partials, fe *out);
+                  fe *tab, fe *partials, fe *out, int rank = 0, int G = 1);
 // composition over E: consts2_dev = {a components, b components}; planes comp[0, 8n), comp[8n, 16n)
 hipError_t eval_constraints_ext(hipStream_t st, const fe *lde, int log_n, int log_b, const fe *periodic, const fe *divs,
                           const AirConsts *consts2_dev, fe *comp, bool bnd = true, int nce = 8);
