@@ -1,0 +1,61 @@
+"""Measured decomposition of the coset-sharded prover's per-rank time.
+
+Loopback ranks run every rank of a G-way sharded proof on ONE GPU, so the wall time of a loopback proof is
+    T_loop(G) = G * R + S + X(G)
+with R the work every rank repeats (interpolation, DEEP coefficients, FRI layers >= 1, host steps), S the work that
+is divided among the ranks (LDEs, evaluation, hashing, layer 0) and X the in-process exchange copies (device-local,
+small).  From G = 2, 4, 8 this fits R and S (least squares); the per-rank time on G separate GPUs is then
+R + S / G + exchange(G), the exchange priced from its volume at an assumed xGMI rate.
+    python3 tools/shard_model.py [log_n] [steps]      (GPU box; prints one JSON object)
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "encrypt-zkvm_amd"))
+
+from zkvm_amd.prover import ProofOptions, make_pub_inputs, vm_trace  # noqa: E402
+from zkvm_amd.sharded import ShardedProver  # noqa: E402
+from zkvm_amd.workloads import make_workload, ops_for_trace_len  # noqa: E402
+
+
+def main():
+    log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 22
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    src = ops_for_trace_len(log_n, "cipher")
+    w = make_workload(src, seed=1000)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    n = trace.shape[1]
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    res = {"log_n": log_n, "steps": steps, "loopback_ms": {}, "stage_ms": {}}
+    proofs = set()
+    for G in (2, 4, 8):
+        sp = ShardedProver.loopback(G, max_trace_len=n)
+        try:
+            sp.upload_trace(trace)
+            for _ in range(2):
+                proofs.add(sp.prove(None, pub, ProofOptions(), n=n)[0])
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                proofs.add(sp.prove(None, pub, ProofOptions(), n=n)[0])
+            res["loopback_ms"][G] = 1e3 * (time.perf_counter() - t0) / steps
+            res["stage_ms"][G] = {k: round(v, 3) for k, v in sp.stage_times().items()}
+        finally:
+            sp.close()
+        print(f"G={G}: {res['loopback_ms'][G]:.2f} ms per loopback proof", file=sys.stderr, flush=True)
+    assert len(proofs) == 1, "loopback world sizes disagree on the proof bytes"
+    Gs = np.array([2.0, 4.0, 8.0])
+    T = np.array([res["loopback_ms"][g] for g in (2, 4, 8)])
+    A = np.stack([Gs, np.ones(3)], axis=1)
+    (R, S), *_ = np.linalg.lstsq(A, T, rcond=None)
+    res["fit"] = {"replicated_ms_R": round(float(R), 3), "divided_ms_S": round(float(S), 3),
+                  "residuals_ms": [round(float(x), 3) for x in (T - A @ np.array([R, S]))]}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
