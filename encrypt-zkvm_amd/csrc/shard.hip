@@ -58,6 +58,38 @@ struct LoopbackComm : zk_comm {
     }
 };
 
+// ---------------------------------------------------------------- caller-transport communicator
+// One rank per process, exchanges through a caller callback over host memory (MPI, gloo, TCP across nodes).  The
+// staging is synchronous: device chunk -> host, callback, host -> device, in stream order of this rank's prover.
+struct HostComm : zk_comm {
+    zk_exchange_fn fn = nullptr;
+    void *ctx = nullptr;
+    std::vector<uint8_t> sbuf, rbuf;
+    bool loopback() const override { return false; }
+    int run(const std::vector<zk_prover *> &P, int op, const void *send, size_t sbytes, void *recv, size_t bytes) {
+        if (P.size() != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "a host-exchange communicator drives exactly one local rank");
+        zk_prover *p = P[0];
+        const size_t rbytes = bytes * (size_t)world;
+        sbuf.resize(std::max<size_t>(sbytes, 1));
+        rbuf.resize(std::max<size_t>(rbytes, 1));
+        if (sbytes) ZK_CHECK_HIP(hipMemcpyAsync(sbuf.data(), send, sbytes, hipMemcpyDeviceToHost, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        const int rc = fn(ctx, op, sbuf.data(), rbuf.data(), bytes);
+        if (rc != 0) ZK_FAIL(ZK_ERR_DEVICE, "exchange callback failed (" + std::to_string(rc) + ")");
+        if (rbytes) ZK_CHECK_HIP(hipMemcpyAsync(recv, rbuf.data(), rbytes, hipMemcpyHostToDevice, p->st));
+        ZK_CHECK_HIP(hipStreamSynchronize(p->st));  // rbuf is reused by the next exchange
+        return ZK_OK;
+    }
+    int all_to_all(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
+                   const std::vector<void *> &recv, size_t bytes) override {
+        return run(P, ZK_XCHG_ALL_TO_ALL, send.at(0), bytes * (size_t)world, recv.at(0), bytes);
+    }
+    int all_gather(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
+                   const std::vector<void *> &recv, size_t bytes) override {
+        return run(P, ZK_XCHG_ALL_GATHER, send.at(0), bytes, recv.at(0), bytes);
+    }
+};
+
 // ---------------------------------------------------------------- local-coset kernels
 __device__ __forceinline__ void st_digest(uint8_t *dst, const uint32_t h[8]) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
@@ -782,6 +814,18 @@ int zk_comm_create_rccl(const uint8_t id[128], int rank, int world, int device, 
     return zk_make_rccl_comm(id, rank, world, device, out);
 }
 
+int zk_comm_create_host(int rank, int world, zk_exchange_fn fn, void *ctx, zk_comm **out) {
+    if (!fn || !out || rank < 0 || rank >= world || (world != 1 && world != 2 && world != 4 && world != 8))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "invalid rank / world (world must be 1, 2, 4 or 8) or null callback");
+    auto *c = new HostComm();
+    c->world = world;
+    c->rank = rank;
+    c->fn = fn;
+    c->ctx = ctx;
+    *out = c;
+    return ZK_OK;
+}
+
 void zk_comm_destroy(zk_comm *c) { delete c; }
 
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
@@ -789,7 +833,8 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
                      zk_record *rec) {
     if (!comm || !provers || !proof_len || nlocal <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     if (comm->loopback() ? nlocal != comm->world : nlocal != 1)
-        ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator needs one prover per rank, an RCCL one exactly one");
+        ZK_FAIL(ZK_ERR_INVALID_ARG,
+                "a loopback communicator needs one prover per rank, an RCCL or host-exchange one exactly one");
     Ctx X;
     X.comm = comm;
     X.G = comm->world;

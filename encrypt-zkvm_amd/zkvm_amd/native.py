@@ -32,9 +32,14 @@ EXPORTED = (
     "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_vm_trace",
-    "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_destroy", "zk_prove_sharded",
+    "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_prove_sharded",
     "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error",
 )
+
+
+# zk_exchange_fn (include/zkvm_gpu.h): int fn(void *ctx, int op, const void *send, void *recv, size_t bytes)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+XCHG_ALL_TO_ALL, XCHG_ALL_GATHER = 0, 1
 
 
 class ZkError(RuntimeError):
@@ -123,6 +128,7 @@ def lib():
         L.zk_comm_create_loopback.argtypes = [i32, C.POINTER(vp)]
         L.zk_comm_unique_id.argtypes = [vp]
         L.zk_comm_create_rccl.argtypes = [vp, i32, i32, i32, C.POINTER(vp)]
+        L.zk_comm_create_host.argtypes = [i32, i32, EXCHANGE_FN, vp, C.POINTER(vp)]
         L.zk_comm_destroy.argtypes = [vp]
         L.zk_comm_destroy.restype = None
         L.zk_prove_sharded.argtypes = [vp, C.POINTER(vp), i32, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp,

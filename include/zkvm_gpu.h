@@ -204,6 +204,15 @@ typedef struct zk_comm zk_comm;
 int zk_comm_create_loopback(int world, zk_comm **out);
 int zk_comm_unique_id(uint8_t id[128]);
 int zk_comm_create_rccl(const uint8_t id[128], int rank, int world, int device, zk_comm **out);
+/* A communicator over a caller-supplied transport (MPI, gloo, TCP; also across nodes): one rank per process.
+ * For every exchange the library copies this rank's device chunk(s) to host memory, calls fn, and copies recv
+ * back to the device.  op ZK_XCHG_ALL_TO_ALL: send holds `world` chunks of `bytes` (chunk d is for rank d), recv
+ * receives `world` chunks (chunk s came from rank s); op ZK_XCHG_ALL_GATHER: send is one chunk of `bytes`, recv
+ * receives the `world` chunks in rank order.  fn returns 0 on success (anything else fails the proof with
+ * ZK_ERR_DEVICE); every rank calls it the same number of times with the same op and bytes. */
+typedef int (*zk_exchange_fn)(void *ctx, int op, const void *send, void *recv, size_t bytes);
+enum { ZK_XCHG_ALL_TO_ALL = 0, ZK_XCHG_ALL_GATHER = 1 };
+int zk_comm_create_host(int rank, int world, zk_exchange_fn fn, void *ctx, zk_comm **out);
 void zk_comm_destroy(zk_comm *comm);
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,

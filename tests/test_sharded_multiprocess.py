@@ -1,0 +1,78 @@
+"""The sharded prover with one rank per PROCESS (zk_comm_create_host + a gloo transport), as an RCCL job runs it.
+
+The loopback tests (tests/test_sharded.py) drive every rank from one process; here `world` separate processes on
+the one test GPU each hold a single rank-sized prover, so every rank-dependent branch of shard.hip (coset ownership,
+the openings each rank serves, FRI layers >= 1 on rank 0, the per-process transcript) runs as in a multi-GPU job --
+only the transport differs (gloo over 127.0.0.1 instead of RCCL over xGMI).  The CPU tests check the exchange
+callback's chunk order at world 2 with gloo, and the communicator's argument checks.
+"""
+import ctypes as C
+import json
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from zkvm_amd import native
+
+WORKER = Path(__file__).resolve().parent / "sharded_worker.py"
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return str(s.getsockname()[1])
+
+
+def run_ranks(world, out, mode="prove", timeout=240):
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, "-u", str(WORKER), str(r), str(world), port, str(out), mode],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=timeout)[0])
+    finally:
+        for p in procs:  # only the processes started here
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r] if r < len(logs) else ''}"
+    return [json.loads((out / f"rank{r}.json").read_text()) for r in range(world)]
+
+
+def test_host_exchange_callback_gloo_world2(tmp_path):
+    res = run_ranks(2, tmp_path, "selftest", timeout=120)
+    nb, world = 5, 2
+    for r, x in enumerate(res):
+        # all-to-all: chunk s of rank r's recv is chunk r of rank s's send (value 16 s + r)
+        assert x["a2a"] == [16 * s + r for s in range(world) for _ in range(nb)]
+        assert x["ag"] == [100 + s for s in range(world) for _ in range(nb)]
+        assert x["bad_op_rc"] != 0
+
+
+def test_host_comm_argument_checks():
+    L = native.lib()
+    comm = C.c_void_p()
+    fn = native.EXCHANGE_FN(lambda *a: 0)
+    assert L.zk_comm_create_host(0, 3, fn, None, C.byref(comm)) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_comm_create_host(2, 2, fn, None, C.byref(comm)) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_comm_create_host(0, 2, native.EXCHANGE_FN(), None, C.byref(comm)) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_comm_create_host(1, 4, fn, None, C.byref(comm)) == native.ZK_OK
+    L.zk_comm_destroy(comm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_one_rank_per_process(tmp_path, world):
+    res = run_ranks(world, tmp_path)
+    names = sorted(res[0])
+    assert len(names) >= 3 and all(sorted(x) == names for x in res)
+    for name in names:
+        want = res[0][name]["want"]  # golden sha, or rank 0's single-GPU proof for the generated traces
+        assert want, name
+        for r, x in enumerate(res):
+            assert x[name]["sha256"] == want, (name, r)
