@@ -291,7 +291,9 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     const size_t Nl = world ? N / (size_t)world : N;
     DeviceArena &A = p->arena;
     ZK_CHECK_HIP(A.alloc(&p->d_trace, (size_t)W * n));
-    ZK_CHECK_HIP(A.alloc(&p->polys, (size_t)W * n));
+    // trace polynomials; as a rank of a sharded proof, G slices of ceil(W / G) columns (the in-place all-gather of
+    // shard.hip): 8 ceil(W / 8) columns cover G = 1, 2, 4, 8
+    ZK_CHECK_HIP(A.alloc(&p->polys, (size_t)8 * ((W + 7) / 8) * n));
     // NTT scratch: the four-step intermediate of a whole 8-coset LDE of the trace (28 x 8 x n; a sharded rank's
     // cosets: 28 x 8/G x n, at least the 28 x n of the interpolation)
     ZK_CHECK_HIP(A.alloc(&p->tmp, (size_t)W * (world ? std::max<size_t>(n, Nl) : 8 * n)));

@@ -40,8 +40,9 @@ extern thread_local std::string g_err;
     } while (0)
 
 static constexpr int W = ZK_TRACE_WIDTH;
-// a host-resident trace is uploaded in up to this many column groups (trace_lde_commit)
-static constexpr int ZK_UPLOAD_GROUPS_MAX = 7;
+// a host-resident trace is uploaded in up to this many column groups (trace_lde_commit; shard.hip: one per round
+// of its column split, ceil(W / G) rounds)
+static constexpr int ZK_UPLOAD_GROUPS_MAX = 14;
 static constexpr int NUM_TCONS = 20;
 static constexpr int NUM_ASSERTS = 22;
 

@@ -1,7 +1,8 @@
 // shard.hip -- one proof with the LDE domain sharded by coset over `world` GPUs.
 //
 // Rank g of G owns the LDE cosets r = g + G*j, j < Bl = 8/G (blowup 8).  Per stage:
-//   trace interpolation          replicated (every rank holds the trace)
+//   trace interpolation          host trace: split by column (a rank uploads and interpolates W/G columns,
+//                                round robin), in-place all-gathers of the coefficients; device trace: replicated
 //   trace LDE, constraint eval,  local: a coset's LDE is an independent size-n NTT, and constraint
 //   DEEP, first FRI fold         row i+8 / a fold row {e[r' + k N/fold]} stay inside one coset
 //   Merkle trees                 all-to-all of leaf digests into contiguous leaf ranges, a local
@@ -53,7 +54,8 @@ struct LoopbackComm : zk_comm {
         ZK_TRY(sync(P));
         for (int d = 0; d < world; d++)
             for (int s = 0; s < world; s++)
-                ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, send[s], bytes, hipMemcpyDefault, P[d]->st));
+                if ((uint8_t *)recv[d] + s * bytes != send[s])  // in place: a rank's own chunk is already there
+                    ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, send[s], bytes, hipMemcpyDefault, P[d]->st));
         return sync(P);
     }
 };
@@ -326,15 +328,57 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     stage_mark(P0, "start");
     Coin coin = seed_coin(n, opt, pub);
 
-    // S2: replicated interpolation, local coset LDE, distributed commitment
+    // S2: the trace polynomials on every rank, then the local coset LDE and the distributed commitment.
+    //  * host trace: split by column, round robin -- in round k rank g uploads (copy stream) and interpolates column
+    //    c = g + G k, and an in-place all-gather fills columns [G k, G k + G) on every rank (p->polys holds
+    //    8 ceil(W / 8) columns; a column past W is padding).  Each rank moves 1/G of the trace over its PCIe link
+    //    instead of all of it, and round k + 1's upload overlaps round k's interpolation and all-gather;
+    //  * trace already in every rank's HBM (trace = NULL): each rank interpolates all W columns itself, which costs
+    //    less than receiving (G-1)/G of the coefficients over xGMI.
     const fe inv_n = h_inv(fe_make(n));
+    if (trace) {
+        const int rounds = (W + G - 1) / G;
+        static_assert((W + 1) / 2 <= ZK_UPLOAD_GROUPS_MAX, "one upload event per round at G = 2");
+        const size_t col = n * sizeof(fe);
+        auto upload = [&](int k) -> int {
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                const int c = X.rank[l] + G * k;
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                if (c < W)
+                    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, trace + (size_t)c * col, col,
+                                                hipMemcpyHostToDevice, p->st2));
+                ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->st2));
+            }
+            return ZK_OK;
+        };
+        ZK_TRY(upload(0));
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int k = 0; k < rounds; k++) {
+            if (k + 1 < rounds) ZK_TRY(upload(k + 1));
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                const size_t c = (size_t)X.rank[l] + (size_t)G * k;
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[k], 0));
+                if (c < (size_t)W) ntt(p->st, X.pl[l]->Tn, p->d_trace + c * n, n, p->polys + c * n, n, 1, true, nullptr, &inv_n, p->tmp);
+                snd[l] = p->polys + c * n;
+                rcv[l] = p->polys + (size_t)G * k * n;
+            }
+            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, col));
+        }
+    } else {
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ntt(p->st, X.pl[l]->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+        }
+    }
     for (int l = 0; l < nlp; l++) {
         zk_prover *p = X.P[l];
-        Plan *pl = X.pl[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        if (trace) ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace, trace, (size_t)W * n * 16, hipMemcpyHostToDevice, p->st));
-        ntt(p->st, pl->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-        ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
+        ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
     }
     stage_mark(P0, "trace_lde");
     std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);

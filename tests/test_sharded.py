@@ -111,6 +111,24 @@ def test_sharded_rccl_world1_and_device_trace():
         sp.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_device_trace(world):
+    """Every rank's device trace buffer already holds the trace (zk_prove_sharded with trace = NULL): each rank
+    interpolates its slice of the columns from it; same proof bytes as from the host trace."""
+    c = next(c for c in CASES if c["name"] == "cipher20")
+    trace, proof, pub, opts = case_inputs(c)
+    sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
+    try:
+        n = sp.upload_trace(trace)
+        got, _ = sp.prove(None, pub, opts, n=n)
+        assert got == proof
+        got2, _ = sp.prove(trace, pub, opts)
+        assert got2 == proof
+    finally:
+        sp.close()
+
+
 def test_sharded_rejects_bad_world():
     import ctypes as C
     comm = C.c_void_p()
