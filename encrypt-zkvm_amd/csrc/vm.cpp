@@ -54,12 +54,29 @@ std::string op_str(Op o) {
 
 fe mds(const uint64_t m[16][2], int i) { return fe_make(m[i][0], m[i][1]); }
 
+// a^2 (mod p) as any 128-bit representative (a itself may be one): fe_reduce_wide without the final
+// conditional subtraction of p, which sits on the critical path of the squaring chains below; the
+// multiplies that close each chain (fe_mul) return the canonical value.
+inline fe sqr_lazy(fe a) {
+    typedef unsigned __int128 u128;
+    const u128 p00 = (u128)a.lo * a.lo, p01 = (u128)a.lo * a.hi, p11 = (u128)a.hi * a.hi;
+    const u128 mid = (p00 >> 64) + (u128)(uint64_t)p01 * 2;
+    const u128 lo = (mid << 64) | (uint64_t)p00;
+    const u128 hi = p11 + (p01 >> 64) * 2 + (mid >> 64);
+    const u128 t0 = (u128)(uint64_t)hi * ZK_C, t1 = (u128)(uint64_t)(hi >> 64) * ZK_C;
+    const u128 s1 = lo + t0, s2 = s1 + (t1 << 64);
+    const uint64_t top = (uint64_t)(t1 >> 64) + (uint64_t)(s1 < lo) + (uint64_t)(s2 < s1);
+    u128 r = s2 + (u128)top * ZK_C;
+    if (r < s2) r += ZK_C;
+    return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+
 // The S-box chains of the four state elements are independent: each step below runs the four
 // lanes back to back (lane loop innermost), which lets the out-of-order core overlap the four
 // multiply chains (~4.4 ns per product instead of ~10 for one chain).
-__attribute__((noinline)) void sqn4(fe v[4], int k) {  // v^(2^k)
+__attribute__((noinline)) void sqn4(fe v[4], int k) {  // v^(2^k), lazy representatives
     for (int t = 0; t < k; t++)
-        for (int i = 0; i < 4; i++) v[i] = fe_sqr_host(v[i]);
+        for (int i = 0; i < 4; i++) v[i] = sqr_lazy(v[i]);
 }
 __attribute__((noinline)) void mul4(fe v[4], const fe w[4]) {
     for (int i = 0; i < 4; i++) v[i] = fe_mul(v[i], w[i]);
