@@ -197,9 +197,11 @@ void zk_comp_free(zk_comp_commit *comp);
  * r = g (mod world).  Exchanges (leaf digests, composition coefficient slices, FRI layer 1, openings)
  * go through a zk_comm: RCCL over xGMI with one process per GPU (zk_comm_unique_id on rank 0,
  * shared out of band, then zk_comm_create_rccl on every rank), or an in-process loopback that drives
- * every rank from one process (tests; one prover per rank).  Every rank passes the same host trace
- * (or NULL: the trace already sits in each prover's zk_prover_trace_buffer); every rank receives the
- * same proof bytes, identical to zk_prove's. */
+ * every rank from one process (tests; one prover per rank), or a caller transport (zk_comm_create_host).
+ * Every rank passes the same host trace (column-major, 28 x n x 16 B; rank g reads and uploads only
+ * columns g, g + world, g + 2 world, ... and receives the other columns' polynomials from their owners),
+ * or NULL: the whole trace already sits in each prover's zk_prover_trace_buffer.  Every rank receives
+ * the same proof bytes, identical to zk_prove's. */
 typedef struct zk_comm zk_comm;
 int zk_comm_create_loopback(int world, zk_comm **out);
 int zk_comm_unique_id(uint8_t id[128]);
