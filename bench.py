@@ -70,9 +70,49 @@ def setup_dist(n_gpus):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
+            if os.environ.get("ZK_NUMA_BIND", "1") != "0":
+                HOST["numa_node"] = bind_to_gpu_numa_node(local)
+                log(f"[rank {rank}] GPU {local}: host threads on NUMA node {HOST['numa_node']}")
         dist.init_process_group(backend=backend)
         pg = dist
+    elif os.environ.get("ZK_NUMA_BIND", "1") != "0":
+        import torch
+        if torch.cuda.is_available():
+            HOST["numa_node"] = bind_to_gpu_numa_node(local)
     return world, rank, local, pg
+
+
+HOST = {"numa_node": None}  # the NUMA node this process's host threads were pinned to (bind_to_gpu_numa_node)
+
+
+def _cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def bind_to_gpu_numa_node(local):
+    """Pin this rank's host threads to the NUMA node its GPU hangs off (with several GPUs per host): the page-locked
+    trace is then allocated and written on that node, and each upload reads memory behind its own PCIe root rather
+    than across the socket link.  Threads started later (the VM's) inherit it.  Returns the node, or None where the
+    topology is not exposed (nothing changes then)."""
+    try:
+        import torch
+        pr = torch.cuda.get_device_properties(local)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = _cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()) & os.sched_getaffinity(0)
+        if not cpus:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return node
+    except Exception:
+        return None
 
 
 def barrier(pg, local):
@@ -449,7 +489,8 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
                    "trace_len": n, "trace_width": 28, "lde_len": n * opts.blowup_factor,
                    "program_ops": program_ops, "padded_ops": padded_ops,
                    "options": opts_str, "timed_region": "zk_prove_columns: page-locked host trace -> proof bytes",
-                   "parallelism": f"independent proofs, {P} in flight per GPU, x{world} GPUs"},
+                   "parallelism": f"independent proofs, {P} in flight per GPU, x{world} GPUs",
+                   "host_numa_node": HOST["numa_node"]},
         "security_bits_checked": min_sec,
         "latency_ms": round(latency_ms, 3) if latency_ms is not None else None,
         "device_resident_ms": round(1e3 * dev_s / cmp_steps, 3) if dev_s is not None else None,
