@@ -336,6 +336,19 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     //  * trace already in every rank's HBM (trace = NULL): each rank interpolates all W columns itself, which costs
     //    less than receiving (G-1)/G of the coefficients over xGMI.
     const fe inv_n = h_inv(fe_make(n));
+    // on an early error return, copies from the caller's host trace may still be in flight: the caller may free it
+    // as soon as this returns (the rounds of a completed S2 have waited for every copy)
+    struct CopyGuard {
+        const std::vector<zk_prover *> &P;
+        bool on;
+        ~CopyGuard() {
+            if (!on) return;
+            for (zk_prover *p : P) {
+                (void)hipSetDevice(p->device);
+                (void)hipStreamSynchronize(p->st2);
+            }
+        }
+    } copy_guard{X.P, trace != nullptr};
     if (trace) {
         const int rounds = (W + G - 1) / G;
         static_assert((W + 1) / 2 <= ZK_UPLOAD_GROUPS_MAX, "one upload event per round at G = 2");
