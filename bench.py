@@ -19,7 +19,8 @@ steps are K complete proofs, dealt round-robin to the provers; per-proof latency
 
 Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
 scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
-whole-job rate.  rank 0 prints one JSON line.
+whole-job rate.  rank 0 prints one JSON line.  Each process pins its host threads to the NUMA node of its
+GPU (bind_to_gpu_numa_node; ZK_NUMA_BIND=0 turns it off), so its page-locked trace lives behind its own PCIe root.
 
 --config5 (BASELINE.json configs[4]): the same workload at 128-bit conjectured security,
 ProofOptions(43, 8, 0, Quadratic, 8, 127): composition, OOD, DEEP and FRI over the quadratic extension.

@@ -67,3 +67,14 @@ def test_workload_seeds_differ_per_rank():
     src = cipher_mix_program(4)[0]
     a, b = make_workload(src, seed=1000), make_workload(src, seed=1001)
     assert a.secret != b.secret and a.last_row != b.last_row
+
+
+def test_numa_cpulist_parsing():
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench._cpulist("") == set()
+    # no GPU here: the binding is a no-op and leaves the affinity alone
+    before = os.sched_getaffinity(0)
+    assert bench.bind_to_gpu_numa_node(0) is None
+    assert os.sched_getaffinity(0) == before
