@@ -482,3 +482,34 @@ def test_full_size_proof_matches_oracle_pin(oracle, name):
         ht.close()
     assert rc == 0
     check_large_proof(c, proof, rec, pub, oracle)
+
+
+def test_largest_single_gpu_trace_2p23(oracle):
+    """The largest trace this build proves on one GPU: 2^23 steps (a ~100 GB full prover of the 288 GB HBM; every
+    LDE-domain index of 28 x 2^26 elements still fits the kernels' 32-bit grid arithmetic).  No oracle pin at this
+    size (the CPU oracle would need ~30 GB and ~15 min): the proof from the page-locked host trace must verify with
+    both verifiers, and its trace root must not depend on the upload path (device-resident proof: same bytes)."""
+    from golden_large import oracle_pub
+    from zkvm_amd.prover import HostTrace, Program, verify
+    src = ops_for_trace_len(23, "cipher")
+    w = make_workload(src, seed=2300)
+    prog = Program(src)
+    ht = HostTrace(prog.trace_len)
+    g = None
+    try:
+        trace, outputs = prog.trace(w.public, w.secret, w.server_key, w.last_row, out=ht)
+        assert trace.shape[1] == 1 << 23
+        pub = make_pub_inputs(prog.hash, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+        g = GpuProver(0, max_trace_len=1 << 23)
+        proof, _, _, rc = g.prove(trace, pub, ProofOptions())
+        assert rc == 0
+        d, _ = g.upload_trace(trace)
+        proof_dev, _, _, rc2 = g.prove_device(d, 1 << 23, pub, ProofOptions())
+        assert rc2 == 0 and proof_dev == proof
+    finally:
+        if g is not None:
+            g.close()
+        prog.close()
+        ht.close()
+    assert verify(proof, pub, 95) == (0, "")
+    assert oracle.verify(proof, oracle_pub(oracle, pub), 95) == (0, "")

@@ -7,7 +7,7 @@ The small fixtures (tools/gen_golden.py) store whole traces and proofs; at 2^20 
 regenerate the trace with the product VM, require its sha256, prove on the GPU and require the proof's
 sha256 to equal the oracle's (tests/test_gpu_parity.py::test_full_size_golden, test_sharded.py).
 
-    python tools/gen_golden_large.py [name ...]     # ~100 s (2^20), ~150 s (2^20 quadratic), ~8 min (2^22)
+    python tools/gen_golden_large.py [name ...]     # ~100 s (2^20), ~150 s (2^20 quadratic), ~8 min (2^22), ~4 min (2^21)
 """
 from __future__ import annotations
 
@@ -31,6 +31,9 @@ CASES = [
     ("c2_cipher_2p20", 20, "cipher", 1000, {}, "configs[2]"),
     ("c4_cipher_2p20_quad", 20, "cipher", 1000, {"num_queries": 43, "field_extension": 2}, "configs[4]"),
     ("c3_cipher_2p22", 22, "cipher", 1000, {}, "configs[3]"),
+    # not a BASELINE config: the odd four-step split (pass-1 lines of 2^11 with a trailing radix-2 stage, pass-2
+    # lines of 2^10) at full scale
+    ("x_cipher_2p21", 21, "cipher", 2100, {}, "odd split 2^21"),
 ]
 
 
