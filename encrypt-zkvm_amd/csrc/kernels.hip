@@ -47,9 +47,6 @@ __device__ __forceinline__ fe pow_split(const fe *lo, const fe *hi, size_t t) {
 #ifndef ZK_NTT_WAVES
 #define ZK_NTT_WAVES 8  // waves per SIMD: two 1024-thread blocks per CU (the LDS limit) need <= 64 VGPRs
 #endif
-#ifndef ZK_NTT_PASS_TABLE
-#define ZK_NTT_PASS_TABLE 1  // inter-pass twiddles from a full table (0: split tables, one multiply more)
-#endif
 constexpr int NTT_THREADS = ZK_NTT_THREADS;
 
 #ifndef ZK_NTT_LAZY
@@ -640,11 +637,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.pre_hi = pre ? pre->hi : nullptr;
     a.pre_full = pre ? pre->full : nullptr;
     a.pre_stride = 0;
-#if ZK_NTT_PASS_TABLE
-    a.pass_tw = inverse ? T.inv_pass : T.fwd_pass;
-#else
-    a.pass_tw = nullptr;
-#endif
+    a.pass_tw = inverse ? T.inv_pass : T.fwd_pass;  // inter-pass twiddles from a full table
     a.has_post = post_scale != nullptr;
     a.post = post_scale ? *post_scale : fe_zero();
     if (inverse && post_scale && T.log_n > 12 && T.inv_pass_n && fe_eq(*post_scale, T.inv_n)) {
@@ -870,42 +863,15 @@ void commit_fri_layer(hipStream_t st, const fe *layer, size_t L, int fold, uint8
     merkle_tree(st, leaves, rows, nodes);
 }
 
-// Three Merkle levels per launch: thread t merges the 8 child digests src[8t .. 8t+8) into
-// nodes[cnt + 4t .. +4), their pairs into nodes[cnt/2 + 2t .. +2) and those into nodes[cnt/4 + t].
-// One compression per thread per level-launch left every wave with a single dependent compression
-// behind its loads (and 14 launches per tree); seven per thread keep the VALU busy.
-__global__ void __launch_bounds__(256) k_merge_level3(const uint8_t *src, uint8_t *nodes, size_t cnt) {
-    const size_t q = cnt / 4;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < q; t += (size_t)gridDim.x * blockDim.x) {
-        uint32_t l[8], r[8], h0[8], h1[8], g0[8];
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const size_t c0 = 4 * t + 2 * half;
-            load_digest(src + 64 * c0, l);
-            load_digest(src + 64 * c0 + 32, r);
-            b3::merge(l, r, h0);
-            store_digest(nodes + 32 * (cnt + c0), h0);
-            load_digest(src + 64 * (c0 + 1), l);
-            load_digest(src + 64 * (c0 + 1) + 32, r);
-            b3::merge(l, r, h1);
-            store_digest(nodes + 32 * (cnt + c0 + 1), h1);
-            b3::merge(h0, h1, half ? r : g0);
-            store_digest(nodes + 32 * (cnt / 2 + 2 * t + half), half ? r : g0);
-        }
-        b3::merge(g0, r, h0);
-        store_digest(nodes + 32 * (cnt / 4 + t), h0);
-    }
-}
-
-// The same three levels with the child loads software-pipelined: a grid of a few waves per SIMD walks the
-// groups, each thread loading its next group's 8 children (into registers) before merging the current one.
-// With one group per thread every wave of a launch loads at the same moment and then merges at the same
-// moment, so the child fetch (the launch reads all 2^k leaf digests) is never hidden behind compute.
-// ZK_MERKLE_PF: grid cap of the pipelined kernel (0: the one-group-per-thread kernel above).  A/B on one box:
-// merkle 0.64 -> 0.55 ms per 2^20 proof for caps 1024 / 2048 / 4096 (two rounds of four waves per SIMD kept)
-#ifndef ZK_MERKLE_PF
-#define ZK_MERKLE_PF 2048
-#endif
+// Three Merkle levels per launch: thread t merges the 8 child digests src[8t .. 8t+8) into nodes[cnt + 4t .. +4),
+// their pairs into nodes[cnt/2 + 2t .. +2) and those into nodes[cnt/4 + t] (seven compressions per thread: one per
+// thread and level-launch left every wave a single dependent compression behind its loads).  The child loads are
+// software-pipelined: a grid of a few waves per SIMD walks the groups, each thread loading its next group's 8
+// children (into registers) before merging the current one.  With one group per thread every wave of a launch
+// loaded at the same moment and then merged at the same moment, so the child fetch (the launch reads all 2^k leaf
+// digests) was never hidden behind compute (A/B on one box: merkle 0.64 -> 0.55 ms per 2^20 proof with a grid cap
+// of 1024 / 2048 / 4096 blocks).
+constexpr unsigned MERKLE_PF_BLOCKS = 2048;  // grid cap: two rounds of four waves per SIMD on 256 CUs
 // half `half` of group t: children 8t + 4 half .. + 4 (c: 8 uint4) -> two parents and their parent g
 __device__ __forceinline__ void merge_half3(const uint4 c[8], uint8_t *nodes, size_t cnt, size_t t, int half,
                                             uint32_t g[8]) {
@@ -1006,17 +972,9 @@ void merkle_tree(hipStream_t st, const uint8_t *leaves, size_t nl, uint8_t *node
     const uint8_t *src = leaves;
     // wide levels: three per launch, seven compressions per thread (throughput)
     while (cnt >= ((size_t)1 << ZK_MERKLE_L3_MIN)) {
-        unsigned blocks = cdiv(cnt / 4, 256);
-        if (blocks > 65536) blocks = 65536;
-        if (ZK_MERKLE_PF) {
-            // at most ZK_MERKLE_PF blocks (1024: one round of four waves per SIMD on 256 CUs)
-            blocks = std::min<unsigned>(blocks, ZK_MERKLE_PF);
-            ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
-                    hipLaunchKernelGGL(k_merge_level3_pf, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
-        } else {
-            ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
-                    hipLaunchKernelGGL(k_merge_level3, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
-        }
+        const unsigned blocks = std::min<unsigned>(cdiv(cnt / 4, 256), MERKLE_PF_BLOCKS);
+        ZK_PROF(st, "merkle_level", 64.0 * cnt + 32.0 * (cnt + cnt / 2 + cnt / 4),
+                hipLaunchKernelGGL(k_merge_level3_pf, dim3(blocks), dim3(256), 0, st, src, nodes, cnt));
         src = nodes + 32 * (cnt / 4);
         cnt /= 8;
     }
@@ -1141,7 +1099,6 @@ void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_c
 // two boundary groups, one thread per CE-domain step.
 
 __constant__ fe c_mds[16];
-__constant__ fe c_inv_mds[16];
 
 // Sequence the row loads of one section after the arithmetic of the previous one: the row pointer
 // is laundered through an empty asm that consumes `dep`, so the scheduler cannot hoist ~45 independent
@@ -1166,9 +1123,6 @@ __device__ __forceinline__ fe mds_row(int r, const fe x[4]) {
 // det = 3^24 and |adj| < 2^39 (every row signed + - + -; tests/test_oracle_core.py checks adj, det and the
 // reference INV_MDS).  adj_row(r, y) = 3^24 (INV_MDS y)_r: four 128 x 39-bit products (8 MADs each) into a
 // 192-bit accumulator and one reduction, instead of four full 128 x 128-bit products.
-#ifndef ZK_EVAL_ADJ
-#define ZK_EVAL_ADJ 1
-#endif
 // s[0..6) += x * c, c < 2^40 (s stays below 2^192)
 __device__ __forceinline__ void acc192_madd(uint32_t s[6], fe x, uint64_t c) {
     const uint32_t xs[4] = {lo32(x.lo), hi32(x.lo), lo32(x.hi), hi32(x.hi)};
@@ -1213,7 +1167,7 @@ static constexpr fe ZK_INV3_72 = fe{0x8092deb1ab776293ull, 0xf0185d00eca40a3bull
 // Block-shared constants of one evaluation (read through LDS so that none of them is pinned in
 // SGPRs across the whole kernel -- the cause of SGPR spills and 1-wave occupancy before).
 struct EvalShared {
-    fe ct[20], cb[22], ct2[20], cb2[22], inv_mds[16];
+    fe ct[20], cb[22], ct2[20], cb2[22];
     fe ct3[4], nct[4], ct3b[4], nctb[4];  // constraints 12..15: ct 3^-72 and -ct (planes a, b)
     fe delta, bnd1, bnd1b;
 };
@@ -1245,7 +1199,6 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         else if (t == 42) S.bnd1 = K->bnd1;
         else if (t == 43) S.bnd1b = KE == 2 ? K2->bnd1 : fe_zero();
         else if (t == 44) S.delta = K->delta;
-        else if (t >= 64 && t < 80) S.inv_mds[t - 64] = c_inv_mds[t - 64];
         else if (t >= 80 && t < 84) {
             S.ct3[t - 80] = fe_mul(K->coeff_t[12 + t - 80], ZK_INV3_72);
             S.nct[t - 80] = fe_neg(K->coeff_t[12 + t - 80]);
@@ -1319,7 +1272,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         // 12..15 share the factor fh and 16..19 the factor nfh: sum the coefficient-weighted values first,
         // multiply by the flag once (ct_k (v_k f) summed = f (sum ct_k v_k): 6 multiplies fewer per row)
         fe sR = fe_zero(), sR2 = fe_zero();
-        if (ZK_EVAL_ADJ) {
+        {
             // ct_r ((INV_MDS y)_r^3 - m0_r) = ct3_r (adj_r y)^3 + (-ct_r) m0_r, summed lazily
             acc288 aR = acc288_zero(), aR2 = acc288_zero();
 #pragma unroll
@@ -1334,20 +1287,6 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             }
             sR = acc288_reduce(aR);
             if (KE == 2) sR2 = acc288_reduce(aR2);
-        } else {
-#pragma unroll
-            for (int r2 = 0; r2 < 4; r2++) {
-                acc288 am = acc288_zero();
-#pragma unroll
-                for (int c = 0; c < 4; c++) acc288_madd(am, S.inv_mds[4 * r2 + c], y[c]);
-                const fe acc = acc288_reduce(am);
-                const fe v = fe_sub(cube(acc), m0[r2]);
-                sR = fe_add(sR, fe_mul(S.ct[12 + r2], v));
-                if (KE == 2) {
-                    sR2 = fe_add(sR2, fe_mul(S.ct2[12 + r2], v));
-                    asm volatile("" : "+v"(sR2.lo), "+v"(sR2.hi));
-                }
-            }
         }
         t = fe_add(t, fe_mul(sR, fh));
         if (KE == 2) t2 = fe_add(t2, fe_mul(sR2, fh));
@@ -1545,13 +1484,9 @@ hipError_t upload_rescue_consts(hipStream_t st) {
     if (dev < 0 || dev >= 256) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lk(g_consts_mu);
     if (g_consts_done.test((size_t)dev)) return hipSuccess;
-    fe m[16], im[16];
-    for (int i = 0; i < 16; i++) {
-        m[i] = fe_make(ZK_MDS[i][0], ZK_MDS[i][1]);
-        im[i] = fe_make(ZK_INV_MDS[i][0], ZK_INV_MDS[i][1]);
-    }
+    fe m[16];
+    for (int i = 0; i < 16; i++) m[i] = fe_make(ZK_MDS[i][0], ZK_MDS[i][1]);
     e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mds), m, sizeof m, 0, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_inv_mds), im, sizeof im, 0, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess) g_consts_done.set((size_t)dev);
     return e;

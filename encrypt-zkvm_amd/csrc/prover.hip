@@ -963,9 +963,6 @@ struct TraceSrc {
 #ifndef ZK_UPLOAD_GROUPS
 #define ZK_UPLOAD_GROUPS 7
 #endif
-#ifndef ZK_UPLOAD_LDE_EVERY
-#define ZK_UPLOAD_LDE_EVERY 1  // coset-LDE launch after every this many interpolated groups
-#endif
 static_assert(W % ZK_UPLOAD_GROUPS == 0 && ZK_UPLOAD_GROUPS <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
 
 // hipMemcpyAsync from page-locked memory (zk_host_alloc, zk_host_register, any hipHostMalloc'd or
@@ -1003,19 +1000,13 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
     // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
     constexpr int per = W / ZK_UPLOAD_GROUPS;
-    size_t lde0 = 0;  // first column not yet extended
     for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
         ZK_TRY(upload_trace_group(p, src, n, g * per, per));
         ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->st2));
         const size_t c0 = (size_t)g * per;
         ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[g], 0));
         ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
-        if ((g + 1) % ZK_UPLOAD_LDE_EVERY == 0 || g + 1 == ZK_UPLOAD_GROUPS) {
-            const size_t c1 = c0 + per;
-            ntt_lde(p->st, pl->Tn, pl->ct, p->polys + lde0 * n, n, (int)(c1 - lde0), 0, 1, (int)B, p->lde + lde0 * B * n, B * n,
-                    n, p->tmp);
-            lde0 = c1;
-        }
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
     }
     hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);

@@ -202,9 +202,6 @@ inline int h2d_small(zk_prover *p, void *dst_dev, const void *src, size_t len) {
     ZK_CHECK_HIP(hipMemcpyAsync(dst_dev, s, len, hipMemcpyHostToDevice, p->st));
     return ZK_OK;
 }
-#ifndef ZK_COPY_KERNEL
-#define ZK_COPY_KERNEL 1  // A/B switch: 0 = one runtime hipMemcpyAsync (blit kernel) per read
-#endif
 // queue a device -> host read of len bytes (len % 4 == 0, src 4-byte aligned); dst is written by the
 // next d2h_flush.  Nothing is enqueued yet: the flush copies every pending read in one kernel, so src_dev must
 // hold the value to read until that flush (no later kernel in the stream may overwrite it before then).
@@ -213,7 +210,6 @@ inline int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
     if (p->io_pending.size() >= ZK_COPY_LIST_MAX) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "too many pending reads");
     uint8_t *s = io_take(p, len);
     if (!s) ZK_FAIL(ZK_ERR_OUT_OF_MEMORY, "pinned staging area exhausted");
-    if (!ZK_COPY_KERNEL) ZK_CHECK_HIP(hipMemcpyAsync(s, src_dev, len, hipMemcpyDeviceToHost, p->st));
     p->io_pending.push_back({dst, s, (const uint8_t *)src_dev, len});
     return ZK_OK;
 }
@@ -221,7 +217,7 @@ inline int d2h_small(zk_prover *p, void *dst, const void *src_dev, size_t len) {
 // hipMemcpyAsync issued one blit kernel of ~4.5 us per read), one stream sync, then the host copies.
 // The staging area starts over.
 inline int d2h_flush(zk_prover *p) {
-    if (ZK_COPY_KERNEL && !p->io_pending.empty()) {
+    if (!p->io_pending.empty()) {
         CopyList L;
         L.n = (int)p->io_pending.size();
         size_t words = 0;
