@@ -67,7 +67,7 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 //   lanes vary in the load and pass-2 store phases.  sw is linear over XOR, so an element at pos + d
 //   (d's bits zero in pos) is idx ^ sw(d).
 //   padded (small M): line*(M + 1) + pos.
-//   The 1024-point / 4-line and 4096-point / 1-line tiles (UNI below: the 2^20 and 2^22 four-step passes)
+//   The 1024-point / 4-line, 2048-point / 2-line and 4096-point / 1-line tiles (UNI below: the four-step passes)
 //   fold bits 4-7, 8-9 and 10-11 into bits 0-3 instead: their rounds with h <= 16 give every wave one
 //   butterfly index j (lanes spread over lines and groups, stride 4h), which the bits-4-5 fold leaves 4- and
 //   16-way conflicted; this one is conflict-free for those, the other rounds, the load orders and the
@@ -77,7 +77,9 @@ template <int LOGM, int TILE>
 struct Lds {
     static constexpr int M = 1 << LOGM, LPB = TILE >> LOGM;
     static constexpr bool SWZ = ZK_NTT_SWZ && LOGM >= 6;
-    static constexpr bool UNI = (LOGM == 10 || LOGM == 12) && TILE == 4096 && NTT_THREADS == 1024;
+    // 2048-point lines (the odd splits, 2^21 and 2^23) too: A/B pass 1 at 2^21 13.2 -> 12.3 ms, pass 2 at 2^23 51.8 ->
+    // 49.1 ms per proof; their trailing radix-2 stage stays generic
+    static constexpr bool UNI = (LOGM >= 10 && LOGM <= 12) && TILE == 4096 && NTT_THREADS == 1024;
     static constexpr int LLPB = LPB >= 16 ? 4 : LPB >= 8 ? 3 : LPB >= 4 ? 2 : LPB >= 2 ? 1 : 0;
     static constexpr int R = 4 - LLPB;
     static constexpr int LMASK = (1 << LLPB) - 1;
