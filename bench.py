@@ -589,7 +589,10 @@ def run_sharded(args):
                        "padded_ops": padded_length(src),
                        "options": ("ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5
                                    else "ProofOptions(32, 8, 0, None, 8, 127)"),
-                       "parallelism": f"coset-sharded x{world} (RCCL all-to-all / all-gather)"},
+                       "parallelism": f"coset-sharded x{world} (RCCL all-to-all / all-gather)",
+                       "timed_region": rec["timed_region"]},
+            "device_resident_ms": rec["device_resident_ms_per_proof"],
+            "device_resident_same_proof": rec["device_resident_same_proof"],
             "roofline": None, "cpu_baseline": None, "stage_ms": rec["stage_ms"],
             "proof_bytes": rec["proof_bytes"], "proof_verified_by_oracle": verified,
         }
