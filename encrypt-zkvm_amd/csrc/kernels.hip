@@ -1748,6 +1748,7 @@ void sum_partials(hipStream_t st, const fe *partials, int npolys, int nblk, fe *
 // B-coset LDE of D gives the DEEP values: the same field values as the point-wise quotient of the 35
 // LDE columns, without reading those columns (3.7 GB at 2^20) or inverting 8n denominators.
 constexpr int DIV_T = 256, DIV_E = 8, DIV_CH = DIV_T * DIV_E;
+static_assert(DIV_CH == ZK_DEEP_RANGE_QUANTUM, "a sharded DEEP range is whole phase-3 chunks");
 
 // base^e for e < 2048 (lo) and base^(2048 u) for u < H (hi), 4 bases: z, zg, 1/z, 1/zg
 struct DeepPowBases {
@@ -1774,14 +1775,15 @@ __device__ __forceinline__ fe block_sum256(fe v, fe *red) {
 }
 
 // phase 1: g1, g2 and per-256 totals (one coefficient per thread)
+// [kbase, kend): the coefficient range of this launch (a sharded rank's share; 0, n otherwise); n is the column stride
 __global__ void __launch_bounds__(DIV_T) k_deep_div_g(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
                                                      const DeepConsts *D, const fe *pw, size_t H, fe *g1, fe *g2,
-                                                     fe *bs) {
+                                                     fe *bs, size_t kbase, size_t kend) {
     __shared__ fe red[DIV_T / 64];
     const size_t per = 2048 + H;
-    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    const size_t k = kbase + blockIdx.x * (size_t)DIV_T + threadIdx.x;
     fe v1 = fe_zero(), v2 = fe_zero();
-    if (k < n) {
+    if (k < kend) {
         acc288 aA = acc288_zero(), aH = acc288_zero();
 #pragma unroll 4
         for (int c = 0; c < 28; c++) acc288_madd(aA, D->alpha_t[c], ld_fe(tpolys + (size_t)c * n + k));
@@ -1803,8 +1805,9 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_g(const fe *tpolys, const fe
 
 // phase 2 (one block): carry[j] = sum of the totals of blocks after j (exclusive suffix), NC components
 // per block entry (2: the two sums over F; 4: the two sums over E)
+// total (optional): the NC sums over all nb entries (a sharded rank's range totals, exchanged between ranks)
 template <int NC>
-__global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
+__global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb, fe *total) {
     __shared__ fe t[NC][1024];
     const int per = (nb + 1023) / 1024, lo = threadIdx.x * per, hi = min(lo + per, nb);
     fe a[NC];
@@ -1829,6 +1832,9 @@ __global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
         for (int c = 0; c < NC; c++) t[c][threadIdx.x] = x[c];
         __syncthreads();
     }
+    if (total && threadIdx.x == 0)
+#pragma unroll
+        for (int c = 0; c < NC; c++) total[c] = t[c][0];
 #pragma unroll
     for (int c = 0; c < NC; c++) a[c] = threadIdx.x + 1 < 1024 ? t[c][threadIdx.x + 1] : fe_zero();
     for (int j = hi - 1; j >= lo; j--)  // exclusive suffix within this thread's entries
@@ -1843,13 +1849,16 @@ __global__ void __launch_bounds__(1024) k_deep_div_scan(fe *bs, int nb) {
 // phase 3: thread owns 8 consecutive coefficients; D_k = z^-(k+1) suf1_k + zg^-(k+1) suf2_k.
 // ADD: D_k is added into Dk[k] (the boundary quotient into composition column 0).  rem_flag (optional):
 // set when sum_m g1_m or sum_m g2_m -- the remainders F1(z), F2(zg) of the divisions -- is nonzero.
+// [kbase, n): the coefficient range (a sharded rank's share ends at n = its range end); ext (optional): the sums
+// of g1, g2 over every coefficient past the range (the later ranks' totals)
 template <bool ADD>
 __global__ void __launch_bounds__(DIV_T) k_deep_div_q(const fe *g1, const fe *g2, const fe *carry, int nb1, size_t n,
-                                                     fe z, fe zg, const fe *pw, size_t H, fe *Dk, unsigned *rem_flag) {
+                                                     fe z, fe zg, const fe *pw, size_t H, fe *Dk, unsigned *rem_flag,
+                                                     size_t kbase, const fe *ext) {
     __shared__ fe t1[DIV_T], t2[DIV_T];
     const size_t per = 2048 + H;
     const fe *ilo = pw + 2 * per, *ihi = ilo + 2048, *jlo = pw + 3 * per, *jhi = jlo + 2048;
-    const size_t k0 = blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
+    const size_t k0 = kbase + blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
     fe a[DIV_E], b[DIV_E];
     fe s1 = fe_zero(), s2 = fe_zero();
 #pragma unroll
@@ -1878,6 +1887,10 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_q(const fe *g1, const fe *g2
     const int cb = min((int)blockIdx.x * (DIV_CH / DIV_T) + DIV_CH / DIV_T - 1, nb1 - 1);
     fe r1 = fe_add(carry[2 * cb], threadIdx.x + 1 < DIV_T ? t1[threadIdx.x + 1] : fe_zero());
     fe r2 = fe_add(carry[2 * cb + 1], threadIdx.x + 1 < DIV_T ? t2[threadIdx.x + 1] : fe_zero());
+    if (ext) {
+        r1 = fe_add(r1, ext[0]);
+        r2 = fe_add(r2, ext[1]);
+    }
     fe pz = pow_split(ilo, ihi, k0 + DIV_E), pg = pow_split(jlo, jhi, k0 + DIV_E);  // z^-(k+1) at k = k0 + 7
 #pragma unroll
     for (int e = DIV_E - 1; e >= 0; e--) {
@@ -1907,27 +1920,58 @@ void lde_cosets(hipStream_t st, const NttTables &Tn, const CosetTables &CT, cons
     ntt_lde(st, Tn, CT, coeffs, 0, 1, (int)r0, (int)stride, count, out, 0, n, ntt_tmp);
 }
 
-const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                    const void *deep_consts_dev, fe z, fe zg, fe *scratch) {
-    const size_t n = (size_t)1 << log_n;
-    const DeepConsts *D = (const DeepConsts *)deep_consts_dev;
-    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH;  // hi[] covers every t < nb * 2048 + 8
-    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *Dk = g2 + n, *bs = Dk + n;
+// Scratch layout (deep_poly_scratch): pw (4 power tables) | g1 (n) | g2 (n) | Dk (n) | block sums.
+// A range [k0, k0 + kn) of a sharded rank (deep_range_*): the same buffers indexed by global coefficient; the range
+// totals go to the block-sum area's tail (deep_range_total).
+static void deep_tables(hipStream_t st, size_t n, fe z, fe zg, fe *pw) {
+    const size_t H = n / 2048 + 2;  // hi[] covers every t < nb * 2048 + 8
     DeepPowBases pb;
     pb.b[0] = z;
     pb.b[1] = zg;
     pb.b[2] = fe_inv(z);
     pb.b[3] = fe_inv(zg);
     hipLaunchKernelGGL(k_deep_pow_tables, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, pw);
-    const size_t nb1 = (n + DIV_T - 1) / DIV_T;
-    ZK_PROF(st, "deep_combine", (16.0 * (28 + ccols) + 32.0) * n,
+}
+static void deep_phase1(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, size_t n, const DeepConsts *D,
+                        fe *scratch, size_t k0, size_t kn, fe *total) {
+    const size_t H = n / 2048 + 2, nb1 = (kn + DIV_T - 1) / DIV_T;
+    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *bs = g2 + 2 * n;
+    ZK_PROF(st, "deep_combine", (16.0 * (28 + ccols) + 32.0) * kn,
             hipLaunchKernelGGL(k_deep_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, cpolys, ccols, n, D, pw, H,
-                               g1, g2, bs));
-    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
-    ZK_PROF(st, "deep_divide", 48.0 * n,
-            hipLaunchKernelGGL(k_deep_div_q<false>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg, pw,
-                               H, Dk, nullptr));
-    return Dk;
+                               g1, g2, bs, k0, k0 + kn));
+    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1, total);
+}
+static void deep_phase3(hipStream_t st, size_t n, fe z, fe zg, fe *scratch, size_t k0, size_t kn, const fe *ext) {
+    const size_t H = n / 2048 + 2, nb = (kn + DIV_CH - 1) / DIV_CH, nb1 = (kn + DIV_T - 1) / DIV_T;
+    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *Dk = g2 + n, *bs = Dk + n;
+    ZK_PROF(st, "deep_divide", 48.0 * kn,
+            hipLaunchKernelGGL(k_deep_div_q<false>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, k0 + kn, z,
+                               zg, pw, H, Dk, nullptr, k0, ext));
+}
+const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                    const void *deep_consts_dev, fe z, fe zg, fe *scratch) {
+    const size_t n = (size_t)1 << log_n, H = n / 2048 + 2;
+    deep_tables(st, n, z, zg, scratch);
+    deep_phase1(st, tpolys, cpolys, ccols, n, (const DeepConsts *)deep_consts_dev, scratch, 0, n, nullptr);
+    deep_phase3(st, n, z, zg, scratch, 0, n, nullptr);
+    return scratch + 4 * (2048 + H) + 2 * n;
+}
+static fe *deep_range_total(fe *scratch, size_t n, int nc) {
+    const size_t H = n / 2048 + 2;
+    return scratch + 4 * (2048 + H) + 3 * n + (size_t)nc * ((n + DIV_T - 1) / DIV_T);
+}
+const fe *deep_range_begin(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                           const void *deep_consts_dev, fe z, fe zg, fe *scratch, size_t k0, size_t kn) {
+    const size_t n = (size_t)1 << log_n;
+    deep_tables(st, n, z, zg, scratch);
+    fe *total = deep_range_total(scratch, n, 2);
+    deep_phase1(st, tpolys, cpolys, ccols, n, (const DeepConsts *)deep_consts_dev, scratch, k0, kn, total);
+    return total;
+}
+const fe *deep_range_end(hipStream_t st, int log_n, fe z, fe zg, fe *scratch, size_t k0, size_t kn, const fe *ext) {
+    const size_t n = (size_t)1 << log_n, H = n / 2048 + 2;
+    deep_phase3(st, n, z, zg, scratch, k0, kn, ext);
+    return scratch + 4 * (2048 + H) + 2 * n;
 }
 
 // ---- boundary terms in coefficient form.  The assertion part of the composition,
@@ -1994,10 +2038,10 @@ void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirCon
     bp.bnd1 = K.bnd1;
     ZK_PROF(st, "boundary_poly", (16.0 * 12 + 32.0) * n,
             hipLaunchKernelGGL(k_bnd_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, n, bp, pw, H, g1, g2, bs));
-    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
+    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1, nullptr);
     ZK_PROF(st, "boundary_poly", 64.0 * n,
             hipLaunchKernelGGL(k_deep_div_q<true>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, fe_one(),
-                               c, pw, H, col0, flag));
+                               c, pw, H, col0, flag, (size_t)0, nullptr));
 }
 
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
@@ -2031,12 +2075,12 @@ __device__ __forceinline__ fe2 pow_split2(const fe2 *lo, const fe2 *hi, size_t t
 
 __global__ void __launch_bounds__(DIV_T) k_deep_div_g_ext(const fe *tpolys, const fe *cpolys, int ccols, size_t n,
                                                          const DeepConstsE *D, const fe2 *pw, size_t H, fe2 *g1,
-                                                         fe2 *g2, fe *bs) {
+                                                         fe2 *g2, fe *bs, size_t kbase, size_t kend) {
     __shared__ fe red[DIV_T / 64];
     const size_t per = 2048 + H;
-    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    const size_t k = kbase + blockIdx.x * (size_t)DIV_T + threadIdx.x;
     fe2 v1 = fe2_zero(), v2 = fe2_zero();
-    if (k < n) {
+    if (k < kend) {
         acc288 aA = acc288_zero(), aB = acc288_zero();
 #pragma unroll 4
         for (int c = 0; c < 28; c++) {
@@ -2072,11 +2116,11 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_g_ext(const fe *tpolys, cons
 
 __global__ void __launch_bounds__(DIV_T) k_deep_div_q_ext(const fe2 *g1, const fe2 *g2, const fe *carry, int nb1,
                                                          size_t n, fe2 z, fe2 zg, const fe2 *pw, size_t H, fe *Da,
-                                                         fe *Db) {
+                                                         fe *Db, size_t kbase, const fe *ext) {
     __shared__ fe2 t1[DIV_T], t2[DIV_T];
     const size_t per = 2048 + H;
     const fe2 *ilo = pw + 2 * per, *ihi = ilo + 2048, *jlo = pw + 3 * per, *jhi = jlo + 2048;
-    const size_t k0 = blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
+    const size_t k0 = kbase + blockIdx.x * (size_t)DIV_CH + (size_t)threadIdx.x * DIV_E;
     fe2 s1 = fe2_zero(), s2 = fe2_zero();
     for (int e = 0; e < DIV_E; e++) {
         const size_t k = k0 + e;
@@ -2102,6 +2146,10 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_q_ext(const fe2 *g1, const f
     const int cb = min((int)blockIdx.x * (DIV_CH / DIV_T) + DIV_CH / DIV_T - 1, nb1 - 1);
     fe2 r1 = fe2_add(fe2{carry[4 * cb], carry[4 * cb + 1]}, threadIdx.x + 1 < DIV_T ? t1[threadIdx.x + 1] : fe2_zero());
     fe2 r2 = fe2_add(fe2{carry[4 * cb + 2], carry[4 * cb + 3]}, threadIdx.x + 1 < DIV_T ? t2[threadIdx.x + 1] : fe2_zero());
+    if (ext) {
+        r1 = fe2_add(r1, fe2{ext[0], ext[1]});
+        r2 = fe2_add(r2, fe2{ext[2], ext[3]});
+    }
     fe2 pz = pow_split2(ilo, ihi, k0 + DIV_E), pg = pow_split2(jlo, jhi, k0 + DIV_E);
     for (int e = DIV_E - 1; e >= 0; e--) {
         const size_t k = k0 + e;
@@ -2117,27 +2165,59 @@ __global__ void __launch_bounds__(DIV_T) k_deep_div_q_ext(const fe2 *g1, const f
     }
 }
 
-const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
-                        const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch) {
-    const size_t n = (size_t)1 << log_n;
-    const DeepConstsE *D = (const DeepConstsE *)deep_consts_dev;
-    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH, nb1 = (n + DIV_T - 1) / DIV_T;
-    fe2 *pw = (fe2 *)scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n;
-    fe *Da = (fe *)(g2 + n), *Db = Da + n, *bs = Db + n;
+// scratch layout (E): pw (4 E power tables) | g1 (n E) | g2 (n E) | Da (n) | Db (n) | block sums (4 per block)
+static void deep_tables_ext(hipStream_t st, size_t n, fe2 z, fe2 zg, fe *scratch) {
+    const size_t H = n / 2048 + 2;
     DeepPowBasesE pb;
     pb.b[0] = z;
     pb.b[1] = zg;
     pb.b[2] = fe2_inv(z);
     pb.b[3] = fe2_inv(zg);
-    hipLaunchKernelGGL(k_deep_pow_tables_ext, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, pw);
-    ZK_PROF(st, "deep_combine", (16.0 * (28 + 2 * ccols) + 64.0) * n,
+    hipLaunchKernelGGL(k_deep_pow_tables_ext, dim3(cdiv(4 * (2048 + H), 256)), dim3(256), 0, st, pb, H, (fe2 *)scratch);
+}
+static void deep_phase1_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, size_t n,
+                            const DeepConstsE *D, fe *scratch, size_t k0, size_t kn, fe *total) {
+    const size_t H = n / 2048 + 2, nb1 = (kn + DIV_T - 1) / DIV_T;
+    fe2 *pw = (fe2 *)scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n;
+    fe *bs = (fe *)(g2 + n) + 2 * n;
+    ZK_PROF(st, "deep_combine", (16.0 * (28 + 2 * ccols) + 64.0) * kn,
             hipLaunchKernelGGL(k_deep_div_g_ext, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, cpolys, ccols, n, D, pw,
-                               H, g1, g2, bs));
-    hipLaunchKernelGGL(k_deep_div_scan<4>, dim3(1), dim3(1024), 0, st, bs, (int)nb1);
-    ZK_PROF(st, "deep_divide", 96.0 * n,
-            hipLaunchKernelGGL(k_deep_div_q_ext, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, z, zg,
-                               pw, H, Da, Db));
-    return Da;  // planes Da, Da + n
+                               H, g1, g2, bs, k0, k0 + kn));
+    hipLaunchKernelGGL(k_deep_div_scan<4>, dim3(1), dim3(1024), 0, st, bs, (int)nb1, total);
+}
+static void deep_phase3_ext(hipStream_t st, size_t n, fe2 z, fe2 zg, fe *scratch, size_t k0, size_t kn, const fe *ext) {
+    const size_t H = n / 2048 + 2, nb = (kn + DIV_CH - 1) / DIV_CH, nb1 = (kn + DIV_T - 1) / DIV_T;
+    fe2 *pw = (fe2 *)scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n;
+    fe *Da = (fe *)(g2 + n), *Db = Da + n, *bs = Db + n;
+    ZK_PROF(st, "deep_divide", 96.0 * kn,
+            hipLaunchKernelGGL(k_deep_div_q_ext, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, k0 + kn, z, zg,
+                               pw, H, Da, Db, k0, ext));
+}
+const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                        const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch) {
+    const size_t n = (size_t)1 << log_n, H = n / 2048 + 2;
+    deep_tables_ext(st, n, z, zg, scratch);
+    deep_phase1_ext(st, tpolys, cpolys, ccols, n, (const DeepConstsE *)deep_consts_dev, scratch, 0, n, nullptr);
+    deep_phase3_ext(st, n, z, zg, scratch, 0, n, nullptr);
+    return (fe *)((fe2 *)scratch + 4 * (2048 + H) + 2 * n);  // planes Da, Da + n
+}
+static fe *deep_range_total_ext(fe *scratch, size_t n) {
+    const size_t H = n / 2048 + 2;
+    return (fe *)((fe2 *)scratch + 4 * (2048 + H) + 2 * n) + 2 * n + 4 * ((n + DIV_T - 1) / DIV_T);
+}
+const fe *deep_range_begin_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                               const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch, size_t k0, size_t kn) {
+    const size_t n = (size_t)1 << log_n;
+    deep_tables_ext(st, n, z, zg, scratch);
+    fe *total = deep_range_total_ext(scratch, n);
+    deep_phase1_ext(st, tpolys, cpolys, ccols, n, (const DeepConstsE *)deep_consts_dev, scratch, k0, kn, total);
+    return total;
+}
+const fe *deep_range_end_ext(hipStream_t st, int log_n, fe2 z, fe2 zg, fe *scratch, size_t k0, size_t kn,
+                             const fe *ext) {
+    const size_t n = (size_t)1 << log_n, H = n / 2048 + 2;
+    deep_phase3_ext(st, n, z, zg, scratch, k0, kn, ext);
+    return (fe *)((fe2 *)scratch + 4 * (2048 + H) + 2 * n);
 }
 
 void deep_coeff_ext_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols,

@@ -4,7 +4,9 @@
 //   trace interpolation          host trace: split by column (a rank uploads and interpolates W/G columns,
 //                                round robin), in-place all-gathers of the coefficients; device trace: replicated
 //   trace LDE, constraint eval,  local: a coset's LDE is an independent size-n NTT, and constraint
-//   DEEP, first FRI fold         row i+8 / a fold row {e[r' + k N/fold]} stay inside one coset
+//   DEEP LDE, first FRI fold     row i+8 / a fold row {e[r' + k N/fold]} stay inside one coset
+//   OOD values, DEEP coefficients  split by coefficient range; all-gathers of partial sums / range totals and of
+//                                the quotient slices
 //   Merkle trees                 all-to-all of leaf digests into contiguous leaf ranges, a local
 //   (trace, composition, FRI 0)  subtree per rank, all-gather of the G subtree roots
 //   composition interpolation    per-coset inverse NTT local; all-to-all of coefficient slices for the
@@ -214,6 +216,15 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int lo
     acc = fe2_mulb(acc, F->inv_fold);
     out[t] = acc.a;
     out[om + t] = acc.b;
+}
+
+// the suffix carried into rank `rank`'s DEEP range: out[c] = sum over later ranks h of all[h * nc + c]
+__global__ void k_sh_suffix_carry(const fe *all, int G, int rank, int nc, fe *out) {
+    const int c = threadIdx.x;
+    if (c >= nc) return;
+    fe s = fe_zero();
+    for (int h = rank + 1; h < G; h++) s = fe_add(s, all[(size_t)h * nc + c]);
+    out[c] = s;
 }
 
 // ---------------------------------------------------------------- a Merkle tree split over G ranks
@@ -515,6 +526,38 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     coin.reseed(R.constraint_root);
 
+    // DEEP split by coefficient range (n / G per rank, whole phase-3 chunks): begin(p, k0) -> device totals (2 KX
+    // elements), end(p, k0, ext) -> the coefficient buffer (KX planes of n); `upload` stages the DEEP constants
+    const size_t nr = n / G;
+    const bool deep_split = nr % ZK_DEEP_RANGE_QUANTUM == 0;
+    auto deep_split_ranges = [&](int kx, auto begin, auto end, auto upload, std::vector<const fe *> &Dk) -> int {
+        const int nc = 2 * kx;
+        std::vector<const void *> snd(nlp);
+        std::vector<void *> rcv(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_TRY(upload(p));
+            snd[l] = begin(p, (size_t)X.rank[l] * nr);
+            rcv[l] = p->sh_buf;
+        }
+        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)nc * sizeof(fe)));
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            hipLaunchKernelGGL(k_sh_suffix_carry, dim3(1), dim3(64), 0, p->st, p->sh_buf, G, X.rank[l], nc, p->ood);
+            Dk[l] = end(p, (size_t)X.rank[l] * nr, p->ood);
+        }
+        for (int plane = 0; plane < kx; plane++) {
+            for (int l = 0; l < nlp; l++) {
+                snd[l] = Dk[l] + (size_t)plane * n + (size_t)X.rank[l] * nr;
+                rcv[l] = (void *)(Dk[l] + (size_t)plane * n);
+            }
+            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, nr * sizeof(fe)));
+        }
+        return ZK_OK;
+    };
+
     // S5: OOD frame -- every rank evaluates its 1/G of the coefficient range of the (replicated) polynomials, the
     // partial sums are all-gathered and added on the host -- then DEEP over the local cosets
     std::vector<fe> h;  // the OOD frame, flattened (k base elements per E value)
@@ -548,14 +591,29 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         ood_reseed(coin, h.data(), C, R);
         stage_mark(P0, "ood");
         const DeepConsts D = draw_deep_consts(coin, h.data(), C, z, zg, R);
+        std::vector<const fe *> Dk(nlp);
+        if (deep_split) {
+            // DEEP as an exact polynomial (kernels.hip), split by coefficient range: each rank combines and divides
+            // its n / G coefficients, the ranges' totals are all-gathered for the suffix carries, and the quotient
+            // slices are all-gathered (in place) before every rank extends it over its cosets
+            ZK_TRY(deep_split_ranges(1, [&](zk_prover *p, size_t k0) {
+                return deep_range_begin(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch, k0, nr);
+            }, [&](zk_prover *p, size_t k0, const fe *ext) {
+                return deep_range_end(p->st, log_n, z, zg, p->dscratch, k0, nr, ext);
+            }, [&](zk_prover *p) { return h2d_small(p, p->deep_consts, &D, sizeof D); }, Dk));
+        } else {
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ZK_TRY(h2d_small(p, p->deep_consts, &D, sizeof D));
+                Dk[l] = deep_poly(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch);
+            }
+        }
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ZK_TRY(h2d_small(p, p->deep_consts, &D, sizeof D));
-            // DEEP as an exact polynomial (kernels.hip): replicated coefficients, local cosets g + G j
-            const fe *Dk = deep_poly(p->st, p->polys, p->cpolys, C, log_n, p->deep_consts, z, zg, p->dscratch);
-            lde_cosets(p->st, pl->Tn, pl->ct, Dk, n, X.rank[l], G, Bl, p->deep, p->tmp);
+            lde_cosets(p->st, pl->Tn, pl->ct, Dk[l], n, X.rank[l], G, Bl, p->deep, p->tmp);  // local cosets g + G j
         }
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
@@ -569,14 +627,28 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         ood_reseed_ext(coin, hv, C, R, e, h);
         stage_mark(P0, "ood");
         const DeepConstsE D = draw_deep_consts_ext(coin, e, C, z, zg, R);
+        std::vector<const fe *> Dk(nlp);
+        if (deep_split) {
+            ZK_TRY(deep_split_ranges(2, [&](zk_prover *p, size_t k0) {
+                return deep_range_begin_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch,
+                                            k0, nr);
+            }, [&](zk_prover *p, size_t k0, const fe *ext) {
+                return deep_range_end_ext(p->st, log_n, z, zg, p->x_dscratch, k0, nr, ext);
+            }, [&](zk_prover *p) { return h2d_small(p, p->x_deep_consts, &D, sizeof D); }, Dk));
+        } else {
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
+                Dk[l] = deep_poly_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch);
+            }
+        }
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ZK_TRY(h2d_small(p, p->x_deep_consts, &D, sizeof D));
-            const fe *Dk = deep_poly_ext(p->st, p->polys, p->cpolys, C, log_n, p->x_deep_consts, z, zg, p->x_dscratch);
             for (int plane = 0; plane < 2; plane++)  // planar per rank: plane stride Bl * n
-                lde_cosets(p->st, pl->Tn, pl->ct, Dk + plane * n, n, X.rank[l], G, Bl,
+                lde_cosets(p->st, pl->Tn, pl->ct, Dk[l] + plane * n, n, X.rank[l], G, Bl,
                            p->x_deep + (size_t)plane * Bl * n, p->tmp);
         }
     }

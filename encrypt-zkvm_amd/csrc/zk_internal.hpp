@@ -254,6 +254,19 @@ const fe *deep_poly(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccol
                     const void *deep_consts_dev, fe z, fe zg, fe *scratch);
 const fe *deep_poly_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
                         const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch);
+// The same split by coefficient range over the ranks of a sharded proof: rank g computes the range [k0, k0 + kn)
+// (kn a multiple of ZK_DEEP_RANGE_QUANTUM) in two steps around one exchange.  deep_range_begin returns a device
+// pointer to the range's totals (2 base elements; over E 4); deep_range_end takes `ext`, the sum of the totals of
+// every later range (the suffix carried into this one), and returns the coefficient buffer (n; over E two planes of
+// n) with this range filled in.  The scratch is deep_poly's.
+constexpr size_t ZK_DEEP_RANGE_QUANTUM = 2048;
+const fe *deep_range_begin(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                           const void *deep_consts_dev, fe z, fe zg, fe *scratch, size_t k0, size_t kn);
+const fe *deep_range_end(hipStream_t st, int log_n, fe z, fe zg, fe *scratch, size_t k0, size_t kn, const fe *ext);
+const fe *deep_range_begin_ext(hipStream_t st, const fe *tpolys, const fe *cpolys, int ccols, int log_n,
+                               const void *deep_consts_dev, fe2 z, fe2 zg, fe *scratch, size_t k0, size_t kn);
+const fe *deep_range_end_ext(hipStream_t st, int log_n, fe2 z, fe2 zg, fe *scratch, size_t k0, size_t kn,
+                             const fe *ext);
 // DEEP through coefficient form (kernels.hip): the DEEP polynomial (S - S(z))/(x - z) + (A - A(zg))/(x - zg)
 // by suffix sums over the combined coefficients, one LDE over the B cosets (CosetTables) into ulde
 // (coset-major), and (out != nullptr) a natural-order copy in out.  scratch: 4 (2048 + n/2048 + 2) + 3n + 2 ceil(n/256)
