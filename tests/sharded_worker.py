@@ -6,7 +6,7 @@ RCCL rank runs (one local rank per process, rank-dependent ownership of cosets, 
 transport swapped.  Each job's proof sha256 goes to <out>/rank<r>.json; the test compares them with the golden
 proofs and, for the generated traces, with the single-GPU prover's proof (computed on rank 0).
 
-usage: python tests/sharded_worker.py RANK WORLD PORT OUTDIR
+usage: python tests/sharded_worker.py RANK WORLD PORT OUTDIR [selftest | large:<pinned case>]
 """
 import hashlib
 import json
@@ -91,6 +91,24 @@ def main():
     fn = torch_exchange()
     if mode == "selftest":
         (out / f"rank{rank}.json").write_text(json.dumps(selftest(rank, world, fn)))
+        dist.destroy_process_group()
+        return
+    if mode.startswith("large:"):  # one full-size pinned case (tests/golden/large), checked here on every rank
+        sys.path.insert(0, str(ROOT / "tests"))
+        from golden_large import LARGE_CASES, check_large_proof, large_inputs
+        from oracle import oracle
+        c = next(c for c in LARGE_CASES if c["name"] == mode[len("large:"):])
+        ht, trace, pub, opts = large_inputs(c)
+        sp = ShardedProver.host(rank, world, fn, 0, trace.shape[1])
+        try:
+            proof, rec = sp.prove(trace, pub, opts, record=True)
+        finally:
+            sp.close()
+            ht.close()
+        oracle.build()
+        check_large_proof(c, proof, rec, pub, oracle)
+        (out / f"rank{rank}.json").write_text(json.dumps({c["name"]: {"sha256": hashlib.sha256(proof).hexdigest(),
+                                                                       "want": c["proof_sha256"]}}))
         dist.destroy_process_group()
         return
     jobs = golden_jobs(world) + generated_jobs(rank)

@@ -26,10 +26,11 @@ def free_port():
         return str(s.getsockname()[1])
 
 
-def run_ranks(world, out, mode="prove", timeout=240):
+def run_ranks(world, out, mode="prove", timeout=240, env=None):
     port = free_port()
     procs = [subprocess.Popen([sys.executable, "-u", str(WORKER), str(r), str(world), port, str(out), mode],
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+             for r in range(world)]
     logs = []
     try:
         for p in procs:
@@ -76,3 +77,18 @@ def test_sharded_one_rank_per_process(tmp_path, world):
         assert want, name
         for r, x in enumerate(res):
             assert x[name]["sha256"] == want, (name, r)
+
+
+# full-size pinned configs with every rank in its own process: configs[2] (2^20) over 8 ranks, configs[4] (2^20, quadratic
+# extension, 128 bits) over 4, configs[3] (2^22) over 8 -- the north_star's sharded proof, with gloo in place of RCCL;
+# each rank regenerates the trace with the product VM (2 threads: the box's CPU share is split between the processes)
+# and checks the proof against the oracle's pin and both verifiers
+FULL_SIZE_MP = [("c2_cipher_2p20", 8), ("c4_cipher_2p20_quad", 4), ("c3_cipher_2p22", 8)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", FULL_SIZE_MP, ids=[f"{n}-w{w}" for n, w in FULL_SIZE_MP])
+def test_sharded_one_rank_per_process_full_size(tmp_path, name, world):
+    import os
+    res = run_ranks(world, tmp_path, f"large:{name}", timeout=280, env={**os.environ, "ZK_VM_THREADS": "2"})
+    assert all(x[name]["sha256"] == x[name]["want"] for x in res)
