@@ -59,6 +59,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ZK_BENCH_REHEARSE=1: rehearse the multi-GPU flow on fewer GPUs than ranks (several ranks per GPU): the process group
+# is gloo instead of RCCL, ranks share GPUs round robin and the sharded leg exchanges through zk_comm_create_host over
+# that group.  Same code path otherwise (barriers, max over ranks, rank 0's line, the sharded sub-record).
+REHEARSE = os.environ.get("ZK_BENCH_REHEARSE", "0") == "1"
+
+
 def setup_dist(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -68,8 +74,10 @@ def setup_dist(n_gpus):
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        if REHEARSE:
+            local %= max(1, torch.cuda.device_count())
+        backend = "nccl" if torch.cuda.is_available() and not REHEARSE else "gloo"
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
             if os.environ.get("ZK_NUMA_BIND", "1") != "0":
                 HOST["numa_node"] = bind_to_gpu_numa_node(local)
@@ -131,7 +139,7 @@ def max_over_ranks(pg, value, local):
     if pg is None:
         return value
     import torch
-    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    dev = f"cuda:{local}" if torch.cuda.is_available() and not REHEARSE else "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
@@ -525,12 +533,16 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
     log(f"[rank {rank}] sharded VM trace: n={n} ({time.perf_counter() - t0:.1f} s)")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
     opts = ProofOptions(43, 8, 0, 2, 8, 127) if config5 else ProofOptions()
-    uid = ShardedProver.unique_id() if rank == 0 else None
-    if pg is not None:
-        box = [uid]
-        pg.broadcast_object_list(box, src=0)
-        uid = box[0]
-    sp = ShardedProver.rccl(rank, world, uid, local, n)
+    if REHEARSE and world > 1:
+        from zkvm_amd.sharded import torch_exchange
+        sp = ShardedProver.host(rank, world, torch_exchange(), local, n)
+    else:
+        uid = ShardedProver.unique_id() if rank == 0 else None
+        if pg is not None:
+            box = [uid]
+            pg.broadcast_object_list(box, src=0)
+            uid = box[0]
+        sp = ShardedProver.rccl(rank, world, uid, local, n)
     last = {}
 
     def step_host():
