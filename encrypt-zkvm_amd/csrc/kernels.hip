@@ -280,7 +280,12 @@ __device__ __forceinline__ void lds_dft(fe *s, const fe *tw4096, const fe_ws *ws
 #endif
 template <int LOGM, int TILE>
 struct Fuse {
-    static constexpr bool OK = ZK_NTT_FUSE && Lds<LOGM, TILE>::UNI && (LOGM % 2 == 0) && TILE / 4 == NTT_THREADS;
+    static constexpr bool OK = ZK_NTT_FUSE && Lds<LOGM, TILE>::UNI && TILE / 4 == NTT_THREADS;
+    // odd LOGM (2048-point lines): the radix-4 rounds end one stage short, and the trailing radix-2 stage is the one
+    // fused with the store (last_r2_to); every value stays canonical (no lazy sums)
+    static constexpr bool ODD = LOGM % 2 == 1;
+    static constexpr int STOP = ODD ? LOGM - 1 : LOGM - 2;  // r4_rounds bound before the fused last stage
+    static constexpr bool LAZY = ZK_NTT_LAZY && !ODD;
 };
 // First round: thread q takes line q % LPB and the butterfly at bit-reversed positions 4g .. 4g+3 (g = q / LPB),
 // i.e. DFT inputs k0 + {0, M/2, M/4, 3M/4} with k0 = brev(4g), fetched by load(line, k).  Plain: one multiply by
@@ -342,6 +347,22 @@ __device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Sto
     store(line, j + h, o1);
     store(line, j + 2 * h, o2);
     store(line, j + 3 * h, o3);
+}
+
+// Last stage of an odd LOGM (radix 2, h = M/2): thread q takes line q % LPB and butterflies j = q / LPB + k TILE/(2 LPB)
+// ... over the TILE/2 butterflies; outputs j and j + h go to store(line, pos, value).  Per-lane two-part twiddles.
+template <int LOGM, int TILE, bool CT, typename Store>
+__device__ __forceinline__ void last_r2_to(const fe *s, const fe_w2 *w2t, Store store) {
+    using L = Lds<LOGM, TILE>;
+    constexpr int M = 1 << LOGM, LPB = TILE / M, h = M / 2;
+#pragma unroll
+    for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
+        const int line = bf % LPB, j = bf / LPB;
+        const int i0 = L::idx(line, j), i1 = L::at(i0, h);
+        const fe u = s[i0], v = fe_mul_w2(s[i1], w2t[CT ? h + j : j << (12 - LOGM)]);
+        store(line, j, fe_add(u, v));
+        store(line, j + h, fe_sub(u, v));
+    }
 }
 
 // XCD-aware block order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs
@@ -456,14 +477,17 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         const fe *stage = CT ? a.cos_stage + (size_t)r * 4096 : a.tw4096;
         const fe_ws *stage_ws = CT ? a.cos_stage_ws + (size_t)r * 4096 : a.tw_ws;
         const fe_w2 *stage_w2 = CT ? a.cos_stage_w2 + (size_t)r * 4096 : a.tw_w2;
-        first_round_from<LOGM, TILE, CT, ZK_NTT_LAZY>(
+        using F = Fuse<LOGM, TILE>;
+        first_round_from<LOGM, TILE, CT, F::LAZY>(
             s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); }, stage_ws);
-        r4_rounds<LOGM, TILE, 3, CT, LOGM - 2, ZK_NTT_LAZY>(s, stage, stage_ws, stage_w2);
+        r4_rounds<LOGM, TILE, 3, CT, F::STOP, F::LAZY>(s, stage, stage_ws, stage_w2);
         const fe *ptw = CT ? a.cos_pass + (size_t)r * n : a.pass_tw;
-        last_round_to<LOGM, TILE, CT, ZK_NTT_LAZY>(s, stage_w2, [&](int line, int j2, fe v) {
+        auto store = [&](int line, int j2, fe v) {
             const size_t o = (k1_0 + line) * M + j2;
             out[o] = fe_mul(v, ptw[o]);  // inter-pass twiddle w^(j2 k1) (CT: (s_r w_n^j2)^k1), contiguous over the block
-        });
+        };
+        if constexpr (F::ODD) last_r2_to<LOGM, TILE, CT>(s, stage_w2, store);
+        else last_round_to<LOGM, TILE, CT, F::LAZY>(s, stage_w2, store);
         return;
       }
     }
@@ -511,13 +535,16 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const fe *in = a.in + b * a.in_stride;
     if constexpr (Fuse<LOGM, TILE>::OK) {
         fe *out = a.out_of(b);
+        using F = Fuse<LOGM, TILE>;
         first_round_from<LOGM, TILE, false, false>(
             s, [&](int line, int k1) { return in[(size_t)k1 * n2 + j2_0 + line]; }, a.tw_ws);
-        r4_rounds<LOGM, TILE, 3, false, LOGM - 2, false>(s, a.tw4096, a.tw_ws, a.tw_w2);
-        last_round_to<LOGM, TILE, false, false>(s, a.tw_w2, [&](int line, int j1, fe v) {
+        r4_rounds<LOGM, TILE, 3, false, F::STOP, false>(s, a.tw4096, a.tw_ws, a.tw_w2);
+        auto store = [&](int line, int j1, fe v) {
             if (a.has_post) v = fe_mul(v, a.post);
             out[n2 * (size_t)j1 + j2_0 + line] = v;
-        });
+        };
+        if constexpr (F::ODD) last_r2_to<LOGM, TILE, false>(s, a.tw_w2, store);
+        else last_round_to<LOGM, TILE, false, false>(s, a.tw_w2, store);
         return;
     }
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
