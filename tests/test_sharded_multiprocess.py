@@ -88,7 +88,7 @@ FULL_SIZE_MP = [("c2_cipher_2p20", 8), ("c4_cipher_2p20_quad", 4), ("c3_cipher_2
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,world", FULL_SIZE_MP, ids=[f"{n}-w{w}" for n, w in FULL_SIZE_MP])
-def test_sharded_one_rank_per_process_full_size(tmp_path, name, world):
-    import os
+def test_sharded_one_rank_per_process_full_size(oracle, tmp_path, name, world):
+    import os  # (the oracle fixture builds the checker library once, before the ranks start)
     res = run_ranks(world, tmp_path, f"large:{name}", timeout=280, env={**os.environ, "ZK_VM_THREADS": "2"})
     assert all(x[name]["sha256"] == x[name]["want"] for x in res)
