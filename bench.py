@@ -9,12 +9,17 @@ is one zk_prove call from that host-resident trace to proof bytes (the reference
 builds a TraceTable in host memory and hands it to Prover::prove).  The library uploads it in column groups
 on a copy stream, overlapped with the interpolation and, with two provers in flight, with the other proof's
 kernels.  Beside `value` the line reports device_resident_ms (the trace already in HBM), pageable_host_ms
-(the trace in ordinary pageable memory) and latency_ms (one prove() call alone on the GPU).
+(the trace in ordinary pageable memory), latency_ms (one prove() call alone on the GPU) and steady_state_ms (the
+host-resident proofs over a 100-proof window: a 20-proof window pays the run's two ends -- nothing to compute
+before the first column group is up, fewer co-runners for the last proofs -- about 4 %,
+tools/inflight_timeline.py).
 
 Proofs in flight (--inflight P, default 4): each GPU holds P independent provers (own HBM buffers and
 streams, zk_prover objects) driven by P host threads, so one prover's trace upload, host-side transcript round
 trips and proof tail overlap the others' kernels (host-resident trace, one box: 13.6-13.8 ms per proof at P = 3,
-13.2-13.4 at P = 4, device-resident 12.7-12.9; 16.1 ms at P = 2 with HIP's default 4 hardware queues).  The K timed
+13.2-13.4 at P = 4, device-resident 12.7-12.9; 16.1 ms at P = 2 with HIP's default 4 hardware queues).  The
+provers' streams are independent; the copy engines already serve their uploads near-FIFO (a cross-prover upload
+order measured neutral, DESIGN.md section 4 dead ends).  The K timed
 steps are K complete proofs, dealt round-robin to the provers; per-proof latency is stage_ms.
 
 Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
@@ -52,6 +57,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICRO
 FE_MUL_PEAK = 536.78e9
 FE_ADD_PEAK = 2922.68e9
 FE_SUB_PEAK = 3251.22e9
+STEADY_PROOFS = 100  # steady_state_ms window (host-resident, same provers; outside the headline)
 METRIC = "STARK prove: trace-steps/sec at 2^20 steps; achieved HBM GB/s vs 8 TB/s peak"
 
 
@@ -367,8 +373,10 @@ def main():
     # ---- comparison legs (same provers, same count, outside the headline): the trace already in HBM
     # (zk_prove_device), and the host trace in pageable memory (runtime-staged copies)
     cmp_steps = max(2 * P, min(args.steps, 10))
-    dev_s = pag_s = latency_ms = None
+    dev_s = pag_s = latency_ms = steady_s = None
     if not args.no_compare:
+        steady_s = run_proofs_timed(fns, STEADY_PROOFS, pg, local)
+        assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
         d_traces = [g.upload_trace(trace)[0] for g in provers]
 
         def dev_step(k):
@@ -422,7 +430,7 @@ def main():
     host.close()
 
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
-                     latency_ms, dev_s, pag_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
+                     latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
                      zk_verified) if rank == 0 else None
 
     # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A
@@ -461,7 +469,7 @@ SHARDED_TIMEOUT_S = 240
 
 
 def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops, latency_ms,
-               dev_s, pag_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified):
+               dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified):
     """rank 0's JSON line (the driver's contract) from the measurements of main()."""
     dom = max(kstats.items(), key=lambda kv: kv[1][0])
     name, (tot_ms, launches, tot_bytes) = dom
@@ -504,6 +512,7 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
         "latency_ms": round(latency_ms, 3) if latency_ms is not None else None,
         "device_resident_ms": round(1e3 * dev_s / cmp_steps, 3) if dev_s is not None else None,
         "pageable_host_ms": round(1e3 * pag_s / cmp_steps, 3) if pag_s is not None else None,
+        "steady_state_ms": round(1e3 * steady_s / STEADY_PROOFS, 3) if steady_s is not None else None,
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
