@@ -342,8 +342,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // S2: the trace polynomials on every rank, then the local coset LDE and the distributed commitment.
     //  * host trace: split by column, round robin -- in round k rank g uploads (copy stream) and interpolates column
     //    c = g + G k, and an in-place all-gather fills columns [G k, G k + G) on every rank (p->polys holds
-    //    8 ceil(W / 8) columns; a column past W is padding).  Each rank moves 1/G of the trace over its PCIe link
-    //    instead of all of it, and round k + 1's upload overlaps round k's interpolation and all-gather;
+    //    8 ceil(W / 8) columns; a column past W is padding), after which every rank extends those columns over its
+    //    cosets.  Each rank moves 1/G of the trace over its PCIe link instead of all of it, and round k + 1's upload
+    //    overlaps round k's interpolation, all-gather and coset LDE;
     //  * trace already in every rank's HBM (trace = NULL): each rank interpolates all W columns itself, which costs
     //    less than receiving (G-1)/G of the coefficients over xGMI.
     const fe inv_n = h_inv(fe_make(n));
@@ -391,18 +392,23 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 rcv[l] = p->polys + (size_t)G * k * n;
             }
             ZK_TRY(X.comm->all_gather(X.P, snd, rcv, col));
+            // this round's G columns are complete on every rank: extend them over the local cosets now, so the
+            // LDE runs under the next round's upload instead of after the last one
+            const int c0 = G * k, nc = std::min(G, W - c0);
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, nc, X.rank[l], G, Bl,
+                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+            }
         }
     } else {
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             ntt(p->st, X.pl[l]->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
+            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
         }
-    }
-    for (int l = 0; l < nlp; l++) {
-        zk_prover *p = X.P[l];
-        ZK_CHECK_HIP(hipSetDevice(p->device));
-        ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
     }
     stage_mark(P0, "trace_lde");
     std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);
