@@ -350,6 +350,47 @@ __device__ __forceinline__ fe fe_mul_uniform(fe A, const fe_ws &W) {
     return ws_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
 }
 
+// the same product with the W words in VGPRs: a W set shared by a group of lanes (vector loads), e.g. the NTT's
+// group-uniform rounds (kernels.hip r4_round), where 16 lanes of a quarter-wave multiply by one twiddle
+__device__ __forceinline__ void col3v(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2) {
+    uint64_t k0, k1, k2, kd;
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %8, %9, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %10, %11, %0\n\t"
+        "v_addc_co_u32 %1, %5, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %5, %1, 0, %4"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(kd)
+        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2));
+}
+__device__ __forceinline__ void col4v(uint64_t &a, uint32_t &h, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                                      uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+    uint64_t k0, k1, k2, k3, kd;
+    asm("v_mad_u64_u32 %0, %2, %7, %8, %0\n\t"
+        "v_mad_u64_u32 %0, %3, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %0, %4, %11, %12, %0\n\t"
+        "v_mad_u64_u32 %0, %5, %13, %14, %0\n\t"
+        "v_addc_co_u32 %1, %6, 0, 0, %2\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %3\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %4\n\t"
+        "v_addc_co_u32 %1, %6, %1, 0, %5"
+        : "+v"(a), "=&v"(h), "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(kd)
+        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2), "v"(x3), "v"(y3));
+}
+__device__ __forceinline__ fe fe_mul_wsv(fe A, const fe_ws &W) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint32_t r0, r1, r2, r3, h = 0;
+    uint64_t a = (uint64_t)x0 * W.w[0];
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col3v(a, h, x1, W.w[1], x2, W.w[2], x3, W.w[3]);                 ZK_WSHIFT(r0);
+    col4v(a, h, x0, W.w[4], x1, W.w[5], x2, W.w[6], x3, W.w[7]);     ZK_WSHIFT(r1);
+    col4v(a, h, x0, W.w[8], x1, W.w[9], x2, W.w[10], x3, W.w[11]);   ZK_WSHIFT(r2);
+    col4v(a, h, x0, W.w[12], x1, W.w[13], x2, W.w[14], x3, W.w[15]); ZK_WSHIFT(r3);
+#undef ZK_WSHIFT
+    return ws_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
+}
+
 // ---- per-lane constant in two parts (32 B): a w = (a mod 2^64) w + (a >> 64) (w 2^64 mod p), a 193-bit sum
 // of two 64 x 128-bit products (five columns), one K-fold of its top 65 bits (H C = H K 2^32 - H), then
 // ws_fold's final step.  99 issue slots against fe_mul's 113 (tools/ubench/fmul_lab.hip v5): for per-lane

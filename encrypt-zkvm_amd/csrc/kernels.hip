@@ -55,6 +55,12 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 #ifndef ZK_NTT_J0
 #define ZK_NTT_J0 1  // plain-DFT wave-uniform rounds: the waves with j = 0 skip their three unit-twiddle multiplies
 #endif
+#ifndef ZK_NTT_GRP
+#define ZK_NTT_GRP 1  // group-uniform (16 lanes per twiddle) W-set multiplies in the h = 64 round of 1024-point lines
+#endif
+#ifndef ZK_NTT_GRP_LAST
+#define ZK_NTT_GRP_LAST 0  // the same W-set multiplies in the fused last round (4 lanes per twiddle)
+#endif
 #ifndef ZK_NTT_SWZ
 #define ZK_NTT_SWZ 1  // XOR-swizzled LDS tiles (0: one pad element per line)
 #endif
@@ -143,6 +149,34 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         if (!triv) u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
         else if (LZ) u2 = fe_canon(a2);
         const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
+        fe o0, o1, o2, o3;
+        addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
+        s[p] = o0;
+        s[p2h] = o2;
+        s[ph] = o1;
+        s[p3h] = o3;
+        __syncthreads();
+        return;
+    }
+    if constexpr (L::UNI && ZK_NTT_GRP && LOGM == 10 && h == 64) {
+        // group-uniform twiddles (h = 64 of a 1024-point line): wave w takes the 4 butterfly classes j = 4w .. 4w+3,
+        // one per quarter-wave, each of the 16 (line, group) pairs a 4-line tile holds, so the 16 lanes of a
+        // quarter-wave share one twiddle and its W set (vector loads of one 64-B entry; fe_mul_wsv, 80 issue slots
+        // against fe_mul_w2's 99).  The lanes of a quarter-wave differ in line and group: the UNI swizzle folds
+        // both into the low 4 bits, so the LDS phases stay conflict-free.
+        constexpr int LH = LG - 1;
+        const int w = (int)threadIdx.x >> 6, l = threadIdx.x & 63;
+        const int j = (w << 2) | (l >> 4);
+        const int pidx = l & 15;
+        const int line = pidx >> (LOGM - 2 - LH), grp = pidx & ((M >> (2 + LH)) - 1);
+        const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
+        const fe_ws W1 = ws[CT ? h + j : j << (12 - LG)];
+        const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
+        const fe t1 = fe_mul_wsv(x1, W1), t3 = fe_mul_wsv(x3, W1);
+        fe a0, a1, a2, a3;
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
+        const fe u2 = fe_mul_wsv(a2, ws[CT ? 2 * h + j : j << (11 - LG)]);
+        const fe u3 = fe_mul_wsv(a3, ws[CT ? 3 * h + j : (j + h) << (11 - LG)]);
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
@@ -329,18 +363,29 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
 // Last round (h = M/4): thread q takes line q % LPB and butterfly index j = q / LPB; its outputs at positions
 // j + {0, h, 2h, 3h} go to store(line, pos, value).  Per-lane two-part twiddles as in r4_round's UNI branch.
 template <int LOGM, int TILE, bool CT, bool LZ, typename Store>
-__device__ __forceinline__ void last_round_to(const fe *s, const fe_w2 *w2t, Store store) {
+__device__ __forceinline__ void last_round_to(const fe *s, const fe_ws *ws, const fe_w2 *w2t, Store store) {
     using L = Lds<LOGM, TILE>;
     constexpr int M = 1 << LOGM, LPB = TILE / M, LG = LOGM - 1, h = M / 4;
     const int q = threadIdx.x, line = q % LPB, j = q / LPB;
     const int p = L::idx(line, j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
-    const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
     const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-    const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
-    fe a0, a1, a2, a3;
-    addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-    const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
-    const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+    fe t1, t3, u2, u3, a0, a1, a2, a3;
+    if constexpr (ZK_NTT_GRP_LAST && LPB == 4) {
+        // the LPB lanes of one j (its lines) share the twiddle: W sets through vector loads (fe_mul_wsv)
+        const fe_ws W1 = ws[CT ? h + j : j << (12 - LG)];
+        t1 = fe_mul_wsv(x1, W1);
+        t3 = fe_mul_wsv(x3, W1);
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
+        u2 = fe_mul_wsv(a2, ws[CT ? 2 * h + j : j << (11 - LG)]);
+        u3 = fe_mul_wsv(a3, ws[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+    } else {
+        const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
+        t1 = fe_mul_w2(x1, w1);
+        t3 = fe_mul_w2(x3, w1);
+        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
+        u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
+        u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+    }
     fe o0, o1, o2, o3;
     addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);  // LZ: the store canonicalises (a multiply or fe_canon)
     store(line, j, o0);
@@ -487,7 +532,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
             out[o] = fe_mul(v, ptw[o]);  // inter-pass twiddle w^(j2 k1) (CT: (s_r w_n^j2)^k1), contiguous over the block
         };
         if constexpr (F::ODD) last_r2_to<LOGM, TILE, CT>(s, stage_w2, store);
-        else last_round_to<LOGM, TILE, CT, F::LAZY>(s, stage_w2, store);
+        else last_round_to<LOGM, TILE, CT, F::LAZY>(s, stage_ws, stage_w2, store);
         return;
       }
     }
@@ -544,7 +589,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
             out[n2 * (size_t)j1 + j2_0 + line] = v;
         };
         if constexpr (F::ODD) last_r2_to<LOGM, TILE, false>(s, a.tw_w2, store);
-        else last_round_to<LOGM, TILE, false, false>(s, a.tw_w2, store);
+        else last_round_to<LOGM, TILE, false, false>(s, a.tw_ws, a.tw_w2, store);
         return;
     }
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
