@@ -56,7 +56,7 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 #define ZK_NTT_J0 1  // plain-DFT wave-uniform rounds: the waves with j = 0 skip their three unit-twiddle multiplies
 #endif
 #ifndef ZK_NTT_GRP
-#define ZK_NTT_GRP 1  // group-uniform (16 lanes per twiddle) W-set multiplies in the h = 64 round of 1024-point lines
+#define ZK_NTT_GRP 1  // group-uniform (16 lanes per twiddle) W-set multiplies in the h = 64 round: 1 for 1024-point lines, 2 for every UNI tile
 #endif
 #ifndef ZK_NTT_GRP_LAST
 #define ZK_NTT_GRP_LAST 0  // the same W-set multiplies in the fused last round (4 lanes per twiddle)
@@ -158,9 +158,9 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         __syncthreads();
         return;
     }
-    if constexpr (L::UNI && ZK_NTT_GRP && LOGM == 10 && h == 64) {
-        // group-uniform twiddles (h = 64 of a 1024-point line): wave w takes the 4 butterfly classes j = 4w .. 4w+3,
-        // one per quarter-wave, each of the 16 (line, group) pairs a 4-line tile holds, so the 16 lanes of a
+    if constexpr (L::UNI && ZK_NTT_GRP && (ZK_NTT_GRP == 2 || LOGM == 10) && h == 64) {
+        // group-uniform twiddles (h = 64): wave w takes the 4 butterfly classes j = 4w .. 4w+3, one per quarter-wave,
+        // each of the 16 (line, group) pairs a 4096-element tile holds (any M of a UNI tile), so the 16 lanes of a
         // quarter-wave share one twiddle and its W set (vector loads of one 64-B entry; fe_mul_wsv, 80 issue slots
         // against fe_mul_w2's 99).  The lanes of a quarter-wave differ in line and group: the UNI swizzle folds
         // both into the low 4 bits, so the LDS phases stay conflict-free.
