@@ -191,7 +191,7 @@ def run_proofs(fns, count: int):
         raise errs[0]
 
 
-def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0):
+def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0, repeats: int = 3):
     """The oracle's single-threaded CPU prove (the build's restatement of the reference path; the
     reference Rust prover cannot be built here) on a bounded sample of the same generator."""
     from oracle import oracle as orc
@@ -203,13 +203,20 @@ def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0):
     trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
     pub = orc.make_pub(h, outputs)
     opts = orc.default_options(num_queries=43, field_extension=2) if config5 else orc.default_options()
-    t0 = time.perf_counter()
-    orc.prove(trace, pub, opts)
-    dt = time.perf_counter() - t0
+    runs = []
+    for _ in range(max(1, repeats)):  # each CPU config timed 3x in the same invocation, median
+        t0 = time.perf_counter()
+        orc.prove(trace, pub, opts)
+        runs.append(time.perf_counter() - t0)
+    dt = sorted(runs)[len(runs) // 2]
     n = trace.shape[1]
     out = {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port",
-           "sample": f"oracle or_prove (C, 1 thread) on one 2^{log_n}-step trace of the same cipher-mix "
-                     f"generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s"}
+           "runs_s": [round(r, 2) for r in runs],
+           "sample": f"oracle or_prove (C, 1 thread), median of {len(runs)} proofs of one 2^{log_n}-step trace of the "
+                     f"same cipher-mix generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s; a "
+                     f"2^{log_n} sample of the 2^20 config (the CPU prover's time per step grows with log n: the "
+                     f"2^20 pin took 246.9 s in the build container, tests/golden/large/cases.json), so this figure "
+                     f"flatters the CPU"}
     if all_cores > 1:
         # the reference prover is single-threaded (no rayon), so its whole-host throughput is one proof per
         # core: all_cores threads each prove the same trace at once (ctypes releases the GIL; the oracle
@@ -247,6 +254,38 @@ def host_cores(req: int) -> int:
     if omp.isdigit() and int(omp) > 0:
         n = min(n, int(omp))
     return max(1, min(n, 16))
+
+
+PINS = ROOT / "tests" / "golden" / "large" / "cases.json"
+
+
+def find_pin(log_n: int, seed: int, opts, generator: str = "cipher"):
+    """The committed full-size oracle pin (tests/golden/large, tools/gen_golden_large.py) of exactly this workload --
+    trace length, generator, seed and proof options -- or None.  The bench's rank-0 replica workload (seed 1000,
+    2^20) is configs[2]'s pin c2_cipher_2p20 (c4_cipher_2p20_quad with --config5), the sharded leg's is c3_cipher_2p22."""
+    if not PINS.exists():
+        return None
+    want = {"num_queries": opts.num_queries, "blowup": opts.blowup_factor, "grinding": opts.grinding_factor,
+            "field_extension": opts.field_extension, "fri_folding": opts.fri_folding_factor,
+            "fri_rem_max_deg": opts.fri_remainder_max_degree}
+    for c in json.loads(PINS.read_text())["cases"]:
+        if c["log_n"] == log_n and c["seed"] == seed and c["generator"] == generator and c["options"] == want:
+            return c
+    return None
+
+
+def pin_check(proof: bytes, pin):
+    """{"pin": name, "proof_matches_pin": bool} (None without a pin)."""
+    import hashlib
+    if pin is None:
+        return None
+    return {"pin": pin["name"], "proof_matches_pin": len(proof) == pin["proof_len"] and
+            hashlib.sha256(proof).hexdigest() == pin["proof_sha256"]}
+
+
+def all_ranks_true(pg, ok: bool, local: int) -> bool:
+    """True iff ok holds on every rank (a MAX over ranks of the failure flag)."""
+    return max_over_ranks(pg, 0.0 if ok else 1.0, local) == 0.0
 
 
 def pmc_traffic(kernel: str, config5: bool = False):
@@ -293,7 +332,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed proofs before the timed region (default 3 per prover in flight; the first proof of "
+                         "each prover builds its per-size tables)")
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--cpu-log-n", type=int, default=18)  # ~20 s of single-core oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -360,12 +401,11 @@ def main():
 
     # ---- value: zk_prove from the host-resident (page-locked) trace to proof bytes, P proofs in flight
     fns = [host_step(k, trace) for k in range(P)]
-    for f in fns:  # every prover's first proof builds its per-size tables
-        f()
-    # warm-up: at least three proofs per prover (the first proofs after the tables pay page faults and
-    # clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms, tools/proof_times.py)
-    warm = max(args.warmup, 3 * P)
-    run_proofs(fns, warm - P)
+    # warm-up: exactly --warmup untimed proofs, dealt round-robin (each prover's first proof builds its per-size
+    # tables; the next ones pay page faults and clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms,
+    # tools/proof_times.py); the default is three per prover
+    warm = args.warmup if args.warmup is not None else 3 * P
+    run_proofs(fns, warm)
     elapsed = run_proofs_timed(fns, args.steps, pg, local)
     proof = last[0]
     assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
@@ -425,13 +465,17 @@ def main():
         verified = orc.verify(proof, opub, min_sec)[0] == 0
     from zkvm_amd.prover import verify as zk_verify
     zk_verified = zk_verify(proof, pub, min_sec)[0] == 0
+    # every rank: its proof accepted by zk_verify; rank 0's workload (seed 1000) is a committed oracle pin, so its
+    # proof must also equal the pin byte for byte (the other ranks' seeds have no pin)
+    pin = pin_check(proof, find_pin(args.log_n, 1000 + rank, opts))
+    all_verified = all_ranks_true(pg, zk_verified, local)
     gpu.close()
     trace = None
     host.close()
 
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
-                     zk_verified) if rank == 0 else None
+                     zk_verified, pin, all_verified) if rank == 0 else None
 
     # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A
     # watchdog bounds it: should a collective never complete, rank 0 still prints the line (with the error) and
@@ -442,11 +486,14 @@ def main():
             done = threading.Event()
 
             def watchdog():
+                # a hung collective: rank 0 still prints the line (the replica value stands, the sharded error is
+                # in it), then every rank exits NON-zero so a stuck sharded proof is never mistaken for a clean run
                 if not done.wait(SHARDED_TIMEOUT_S):
                     if out is not None:
-                        out["sharded"] = {"error": f"the sharded proof did not finish within {SHARDED_TIMEOUT_S} s"}
+                        out["sharded"] = {"error": f"the sharded proof did not finish within {SHARDED_TIMEOUT_S} s",
+                                          "timed_out": True}
                         print(json.dumps(out), flush=True)
-                    os._exit(0)
+                    os._exit(3)
 
             threading.Thread(target=watchdog, daemon=True).start()
             try:
@@ -469,7 +516,8 @@ SHARDED_TIMEOUT_S = 240
 
 
 def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops, latency_ms,
-               dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified):
+               dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified, pin,
+               all_verified):
     """rank 0's JSON line (the driver's contract) from the measurements of main()."""
     dom = max(kstats.items(), key=lambda kv: kv[1][0])
     name, (tot_ms, launches, tot_bytes) = dom
@@ -518,6 +566,8 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
         "vm": vm_rec,
         "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
+        "proof_matches_pin": pin["proof_matches_pin"] if pin else None, "pin": pin["pin"] if pin else None,
+        "all_ranks_verified_by_zk_verify": all_verified,
     }
     return out
 
@@ -559,14 +609,24 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
 
     elapsed = timed_loop(step_host, steps, warmup, pg, local)
     stages = sp.stage_times()
+    xchg_host = sp.exchange_stats()
     sp.upload_trace(trace)
 
     def step_dev():
         last["proof_dev"] = sp.prove(None, pub, opts, n=n)[0]
 
     elapsed_dev = timed_loop(step_dev, steps, 1, pg, local)
+    xchg_dev = sp.exchange_stats()
     proof = last["proof"]
     same = last["proof_dev"] == proof
+    # self-check on every rank: the RCCL proof equals the committed oracle pin of this exact workload (configs[3]:
+    # c3_cipher_2p22, seed 1000) and zk_verify accepts it; all ranks must agree
+    from zkvm_amd.prover import verify as zk_verify
+    pin = pin_check(proof, find_pin(log_n, 1000, opts))
+    ok_verify = zk_verify(proof, pub, 128 if config5 else 95)[0] == 0
+    ok_pin = pin["proof_matches_pin"] if pin else True
+    all_verify = all_ranks_true(pg, ok_verify and same, local)
+    all_pin = all_ranks_true(pg, ok_pin, local) if pin else None
     sp.close()
     del trace
     host.close()
@@ -577,7 +637,24 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
             "device_resident_ms_per_proof": round(1e3 * elapsed_dev / steps, 3),
             "device_resident_same_proof": same,
             "stage_ms": {k: round(v, 3) for k, v in stages.items()}, "proof_bytes": len(proof),
+            "pin": pin["pin"] if pin else None, "proof_matches_pin": all_pin,
+            "all_ranks_verified_by_zk_verify": all_verify,
+            "exchange": exchange_record(xchg_host), "exchange_device_resident": exchange_record(xchg_dev),
             "pub": pub, "proof": proof, "n": n, "min_sec": 128 if config5 else 95}
+
+
+def exchange_record(stats):
+    """Per collective of the last sharded proof on rank 0: ms (HIP events around it on the prover's stream, waiting
+    for peers included), MB received from the other ranks, calls, and the effective receive rate."""
+    out = {}
+    for name, (ms, by, calls) in stats.items():
+        out[name] = {"ms": round(ms, 3), "mb_received": round(by / 1e6, 3), "calls": calls,
+                     "gb_per_s": round(by / 1e6 / ms, 2) if ms > 0 else None}
+    tot_ms = sum(v[0] for v in stats.values())
+    tot_b = sum(v[1] for v in stats.values())
+    out["total"] = {"ms": round(tot_ms, 3), "mb_received": round(tot_b / 1e6, 3),
+                    "gb_per_s": round(tot_b / 1e6 / tot_ms, 2) if tot_ms > 0 else None}
+    return out
 
 
 def run_sharded(args):
@@ -585,7 +662,8 @@ def run_sharded(args):
     from zkvm_amd import native
     from zkvm_amd.workloads import ops_for_trace_len, padded_length
     native.lib()
-    rec = sharded_leg(args, args.log_n, world, rank, local, pg, args.steps, args.warmup, args.config5)
+    warm = args.warmup if args.warmup is not None else 3
+    rec = sharded_leg(args, args.log_n, world, rank, local, pg, args.steps, warm, args.config5)
     verified = None
     if rank == 0 and not args.no_verify:
         import ctypes as C
@@ -602,7 +680,7 @@ def run_sharded(args):
         n = rec["n"]
         out = {
             "metric": METRIC, "value": rec["trace_steps_per_s"], "unit": "trace-steps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_proof"],
+            "steps": args.steps, "warmup": warm, "ms_per_step": rec["ms_per_proof"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f128",
             "data": "synthetic (seeded VM trace)",
             "config": {"workload": rec["workload"], "trace_len": n, "trace_width": 28, "lde_len": 8 * n,
@@ -616,6 +694,9 @@ def run_sharded(args):
             "device_resident_same_proof": rec["device_resident_same_proof"],
             "roofline": None, "cpu_baseline": None, "stage_ms": rec["stage_ms"],
             "proof_bytes": rec["proof_bytes"], "proof_verified_by_oracle": verified,
+            "pin": rec["pin"], "proof_matches_pin": rec["proof_matches_pin"],
+            "all_ranks_verified_by_zk_verify": rec["all_ranks_verified_by_zk_verify"],
+            "exchange": rec["exchange"], "exchange_device_resident": rec["exchange_device_resident"],
         }
         print(json.dumps(out), flush=True)
     if pg is not None:

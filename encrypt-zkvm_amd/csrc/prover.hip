@@ -353,6 +353,7 @@ void zk_prover_destroy(zk_prover *p) {
     (void)hipStreamSynchronize(p->st);
     if (p->st2) (void)hipStreamSynchronize(p->st2);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
+    for (auto &e : p->xchg_pool) (void)hipEventDestroy(e);
     for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
     if (p->st2) (void)hipStreamDestroy(p->st2);
@@ -374,6 +375,7 @@ int zk_prover_trace_buffer(zk_prover *p, void **d_trace) {
 void zk::stage_begin(zk_prover *p) {
     p->stage_names.clear();
     p->stage_done = false;
+    p->xchg.clear();
 }
 void zk::stage_mark(zk_prover *p, const char *name) {
     const size_t i = p->stage_names.size();
@@ -401,6 +403,40 @@ int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, 
     for (int i = 0; i < k && i < cap; i++) {
         if (names) names[i] = p->stage_ms[i].first;
         if (ms) ms[i] = p->stage_ms[i].second;
+    }
+    if (count) *count = k;
+    return ZK_OK;
+}
+
+int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
+                             int *count) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    std::vector<const char *> nm;
+    std::vector<float> t;
+    std::vector<double> b;
+    std::vector<int> c;
+    if (p->stage_done)
+        for (const auto &r : p->xchg) {
+            float x = 0;
+            (void)hipEventElapsedTime(&x, p->xchg_pool[r.ev], p->xchg_pool[r.ev + 1]);
+            size_t i = 0;
+            while (i < nm.size() && strcmp(nm[i], r.name)) i++;
+            if (i == nm.size()) {
+                nm.push_back(r.name);
+                t.push_back(0);
+                b.push_back(0);
+                c.push_back(0);
+            }
+            t[i] += x;
+            b[i] += r.bytes;
+            c[i] += 1;
+        }
+    const int k = (int)nm.size();
+    for (int i = 0; i < k && i < cap; i++) {
+        if (names) names[i] = nm[i];
+        if (ms) ms[i] = t[i];
+        if (bytes) bytes[i] = b[i];
+        if (calls) calls[i] = c[i];
     }
     if (count) *count = k;
     return ZK_OK;
@@ -1108,14 +1144,16 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     ZK_REQUIRE_FULL_PROVER(p);
     ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
     // copies from the caller's host columns may still be in flight on an early error return: the caller
-    // may free those columns as soon as this returns (a completed proof has long finished them)
+    // may free those columns as soon as this returns (a completed proof has long finished them).  Kernels of
+    // a failed proof may also still be queued on st: the next proof's uploads into d_trace (on st2, ordered
+    // only by the previous proof having drained st) must not race them, so both streams drain here.
     struct CopyGuard {
         zk_prover *p;
-        bool on;
         ~CopyGuard() {
-            if (on) (void)hipStreamSynchronize(p->st2);
+            (void)hipStreamSynchronize(p->st2);
+            (void)hipStreamSynchronize(p->st);
         }
-    } copy_guard{p, src.cols != nullptr};
+    } copy_guard{p};
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));

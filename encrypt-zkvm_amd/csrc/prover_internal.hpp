@@ -169,6 +169,15 @@ struct zk_prover {
     std::vector<const char *> stage_names;  // stage_names[i] ends at event stage_pool[i]
     bool stage_done = false;                // the last proof completed: its events may be read
     std::vector<std::pair<const char *, float>> stage_ms;
+    // exchanges of the last sharded proof (shard.hip xchg): name, bytes this rank received from the other ranks,
+    // and the events bracketing the collective on the stream it ran on (pooled like the stage events)
+    struct XchgRec {
+        const char *name;
+        double bytes;
+        size_t ev;  // xchg_pool[ev] before, xchg_pool[ev + 1] after
+    };
+    std::vector<hipEvent_t> xchg_pool;
+    std::vector<XchgRec> xchg;
     // kernel stats (names / totals of the last profile)
     std::vector<std::string> kstat_names;
     std::vector<float> kstat_ms;

@@ -264,10 +264,34 @@ struct Ctx {
     size_t n;
 };
 
+
+// One collective of the proof, timed: events on local rank 0's stream before and after it (the time includes any
+// wait for slower ranks), and the bytes this rank receives from the others -- zk_prover_exchange_stats reports them
+// per name, so a multi-GPU run measures its own link rate.
+enum XOp { A2A, AG };
+int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd, const std::vector<void *> &rcv,
+         size_t bytes) {
+    zk_prover *p = X.P[0];
+    const size_t e = p->xchg.size() * 2;
+    while (p->xchg_pool.size() < e + 2) {
+        hipEvent_t ev;
+        ZK_CHECK_HIP(hipEventCreate(&ev));
+        p->xchg_pool.push_back(ev);
+    }
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e], p->st));
+    ZK_TRY(op == A2A ? X.comm->all_to_all(X.P, snd, rcv, bytes) : X.comm->all_gather(X.P, snd, rcv, bytes));
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e + 1], p->st));
+    p->xchg.push_back({name, (double)bytes * (X.G - 1), e});
+    return ZK_OK;
+}
+
 // leaves (hash kernel writes all-to-all order into a2a_send), all-to-all, permute, subtree, roots
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
-                const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes) {
+                const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes, const char *digests_name,
+                const char *roots_name) {
     const int nl = (int)X.P.size();
     T.M = M;
     T.G = X.G;
@@ -284,7 +308,7 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
         snd[l] = scratch[l];
         rcv[l] = scratch[l] + 32 * T.Mr;
     }
-    ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, 32 * (size_t)X.Bl * mg));
+    ZK_TRY(xchg(X, digests_name, A2A, snd, rcv, 32 * (size_t)X.Bl * mg));
     std::vector<const void *> rs(nl);
     std::vector<void *> rr(nl);
     for (int l = 0; l < nl; l++) {
@@ -296,7 +320,7 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
         rs[l] = T.Mr >= 2 ? nodes[l] + 32 : leaves[l];
         rr[l] = p->sh_roots;
     }
-    ZK_TRY(X.comm->all_gather(X.P, rs, rr, 32));
+    ZK_TRY(xchg(X, roots_name, AG, rs, rr, 32));
     std::vector<uint8_t> roots(32 * X.G);
     ZK_TRY(d2h_small(X.P[0], roots.data(), X.P[0]->sh_roots, roots.size()));
     ZK_TRY(d2h_flush(X.P[0]));
@@ -391,7 +415,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 snd[l] = p->polys + c * n;
                 rcv[l] = p->polys + (size_t)G * k * n;
             }
-            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, col));
+            ZK_TRY(xchg(X, "trace_coeffs", AG, snd, rcv, col));
             // this round's G columns are complete on every rank: extend them over the local cosets now, so the
             // LDE runs under the next round's upload instead of after the last one
             const int c0 = G * k, nc = std::min(G, W - c0);
@@ -422,7 +446,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         zk_prover *p = X.P[l];
         hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, W, log_n, Bl,
                            log_mg, send);
-    }, scratch, lv, nd));
+    }, scratch, lv, nd, "trace_digests", "trace_roots"));
     memcpy(R.trace_root, Ttrace.root, 32);
     stage_mark(P0, "trace_commit");
     coin.reseed(R.trace_root);
@@ -475,7 +499,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = p->tmp;
             rcv[l] = COMP(p);
         }
-        ZK_TRY(X.comm->all_to_all(X.P, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe)));
+        ZK_TRY(xchg(X, "comp_slices", A2A, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe)));
         const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
         std::vector<const void *> fs(nlp);
         std::vector<void *> fr(nlp);
@@ -502,9 +526,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 s2[l] = CTMP(X.P[l]) + c * kg;
                 r2[l] = X.P[l]->cpolys + (size_t)c * n;
             }
-            ZK_TRY(X.comm->all_gather(X.P, s2, r2, kg * sizeof(fe)));
+            ZK_TRY(xchg(X, "comp_columns", AG, s2, r2, kg * sizeof(fe)));
         }
-        ZK_TRY(X.comm->all_gather(X.P, fs, fr, sizeof(unsigned)));
+        ZK_TRY(xchg(X, "degree_flags", AG, fs, fr, sizeof(unsigned)));
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
@@ -520,7 +544,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         zk_prover *p = X.P[l];
         hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, CLDE(p), CK, log_n, Bl,
                            log_mg, send);
-    }, scratch, lv, nd));
+    }, scratch, lv, nd, "comp_digests", "comp_roots"));
     memcpy(R.constraint_root, Tcomp.root, 32);
     stage_mark(P0, "composition");
     unsigned degree_flag = 0;
@@ -547,7 +571,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = begin(p, (size_t)X.rank[l] * nr);
             rcv[l] = p->sh_buf;
         }
-        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)nc * sizeof(fe)));
+        ZK_TRY(xchg(X, "deep_totals", AG, snd, rcv, (size_t)nc * sizeof(fe)));
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
@@ -559,7 +583,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 snd[l] = Dk[l] + (size_t)plane * n + (size_t)X.rank[l] * nr;
                 rcv[l] = (void *)(Dk[l] + (size_t)plane * n);
             }
-            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, nr * sizeof(fe)));
+            ZK_TRY(xchg(X, "deep_slices", AG, snd, rcv, nr * sizeof(fe)));
         }
         return ZK_OK;
     };
@@ -578,7 +602,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = p->ood;
             rcv[l] = p->sh_buf;
         }
-        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)nv * sizeof(fe)));
+        ZK_TRY(xchg(X, "ood_parts", AG, snd, rcv, (size_t)nv * sizeof(fe)));
         std::vector<fe> parts((size_t)G * nv);
         ZK_CHECK_HIP(hipSetDevice(P0->device));
         ZK_TRY(d2h_small(P0, parts.data(), P0->sh_buf, parts.size() * sizeof(fe)));
@@ -685,7 +709,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = DEEP(X.P[l]);
             rcv[l] = COMP(X.P[l]);
         }
-        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)KX * Bl * n * sizeof(fe)));
+        ZK_TRY(xchg(X, "remainder_layer", AG, snd, rcv, (size_t)KX * Bl * n * sizeof(fe)));
         ZK_CHECK_HIP(hipSetDevice(P0->device));
         for (int pln = 0; pln < KX; pln++)
             hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(N, 256)), dim3(256), 0, P0->st,
@@ -708,7 +732,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             else
                 hipLaunchKernelGGL(k_sh_hash_fri0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->x_deep,
                                    log_n, Bl, (int)fold, log_m, log_mg, send);
-        }, scratch, f0l, f0n));
+        }, scratch, f0l, f0n, "fri0_digests", "fri0_roots"));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
         {
@@ -743,7 +767,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 snd[l] = CTMP(p);
                 rcv[l] = COMP(p);
             }
-            ZK_TRY(X.comm->all_gather(X.P, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
+            ZK_TRY(xchg(X, "fri_layer1", AG, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
             ZK_CHECK_HIP(hipSetDevice(P0->device));
             for (int pln = 0; pln < KX; pln++)
                 hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st,
@@ -887,7 +911,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = p->gather_out;
             rcv[l] = p->sh_buf;
         }
-        ZK_TRY(X.comm->all_gather(X.P, snd, rcv, NK * sizeof(fe)));
+        ZK_TRY(xchg(X, "openings", AG, snd, rcv, NK * sizeof(fe)));
     }
     std::vector<fe> all((size_t)G * NK), got(NK);
     ZK_CHECK_HIP(hipMemcpyAsync(all.data(), P0->sh_buf, all.size() * sizeof(fe), hipMemcpyDeviceToHost, P0->st));

@@ -426,9 +426,19 @@ int run_program(const CompiledProgram &P, const Machine &M, fe *t, size_t n, con
     if (!t) return ZK_OK;
     // chunk c starts at row bnd[c] with the state of row bnd[c] - 1 (write_rows steps once before writing
     // a row in [1, len]); chunk 0 starts from the zero state at row 0
+    // a thread that cannot be started (resource limits) leaves its chunk to the calling thread: no exception may
+    // cross the C ABI
     std::vector<std::thread> th;
-    for (int k = 1; k < T; k++) th.emplace_back(write_rows, std::cref(P), std::cref(M), start[k], bnd[k], bnd[k + 1], t, n, last);
+    std::vector<int> mine;
+    for (int k = 1; k < T; k++) {
+        try {
+            th.emplace_back(write_rows, std::cref(P), std::cref(M), start[k], bnd[k], bnd[k + 1], t, n, last);
+        } catch (...) {
+            mine.push_back(k);
+        }
+    }
     write_rows(P, M, StackState(), 0, bnd[1], t, n, last);
+    for (int k : mine) write_rows(P, M, start[k], bnd[k], bnd[k + 1], t, n, last);
     for (auto &x : th) x.join();
     return ZK_OK;
 }

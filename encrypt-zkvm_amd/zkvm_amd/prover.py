@@ -188,24 +188,40 @@ class GpuProver:
         return {names[i].decode(): (mu[i], ad[i]) for i in range(min(cnt.value, 64)) if mu[i] or ad[i]}
 
 
+class _PinnedBlock:
+    """Owner of one zk_host_alloc block.  numpy arrays over it keep it as their base (__array_interface__), so
+    the block is freed only when the last array that views it is gone."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib().zk_host_alloc(nbytes, C.byref(p)), "zk_host_alloc")
+        self.ptr = p.value
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().zk_host_free(C.c_void_p(self.ptr))
+                self.ptr = None
+        except Exception:
+            pass
+
+
 class HostTrace:
     """A (28, n, 2) uint64 trace array in page-locked host memory (zk_host_alloc): the VM writes into it
-    (vm_trace(..., out=...)) and zk_prove DMAs it at the link rate.  Free with close() (or a with-block)."""
+    (vm_trace(..., out=...)) and zk_prove DMAs it at the link rate.  close() (or a with-block) drops this
+    object's reference; the memory goes back once no array returned from it (trace(..., out=...)) is alive."""
 
     def __init__(self, n: int):
-        p = C.c_void_p()
-        nbytes = 28 * n * 16
-        check(lib().zk_host_alloc(nbytes, C.byref(p)), "zk_host_alloc")
-        self.ptr = p
         self.n = n
-        buf = (C.c_uint8 * nbytes).from_address(p.value)
-        self.array = np.frombuffer(buf, dtype=np.uint64).reshape(28, n, 2)
+        self.array = np.asarray(_PinnedBlock(28 * n * 16)).view(np.uint64).reshape(28, n, 2)
+
+    @property
+    def ptr(self):
+        return None if self.array is None else self.array.ctypes.data
 
     def close(self):
-        if self.ptr:
-            self.array = None
-            lib().zk_host_free(self.ptr)
-            self.ptr = None
+        self.array = None
 
     def __enter__(self):
         return self

@@ -133,6 +133,17 @@ class ShardedProver:
         lib().zk_prover_stage_times(self.provers[0], names, ms, 32, C.byref(cnt))
         return {names[i].decode(): ms[i] for i in range(cnt.value)}
 
+    def exchange_stats(self) -> dict:
+        """{collective: (ms, bytes received from the other ranks, calls)} of the last proof on local rank 0's
+        stream (zk_prover_exchange_stats): events around each collective, so the time includes waiting for peers."""
+        names = (C.c_char_p * 32)()
+        ms = (C.c_float * 32)()
+        by = (C.c_double * 32)()
+        calls = (C.c_int * 32)()
+        cnt = C.c_int(0)
+        check(lib().zk_prover_exchange_stats(self.provers[0], names, ms, by, calls, 32, C.byref(cnt)))
+        return {names[i].decode(): (ms[i], by[i], calls[i]) for i in range(min(cnt.value, 32))}
+
     def close(self):
         for p in self.provers:
             lib().zk_prover_destroy(p)

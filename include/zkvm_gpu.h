@@ -219,6 +219,13 @@ void zk_comm_destroy(zk_comm *comm);
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec);
+/* The collectives of the last sharded proof on this (local rank 0) prover, aggregated by name (trace_coeffs,
+ * trace_digests, trace_roots, comp_slices, comp_columns, degree_flags, comp_digests, comp_roots, ood_parts,
+ * deep_totals, deep_slices, fri0_digests, fri0_roots, fri_layer1, openings): ms between HIP events recorded on the
+ * prover's stream around each call (waiting for slower ranks included), bytes this rank received from the other
+ * ranks, and the number of calls.  Valid once the proof has returned, until the next proof. */
+int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
+                             int *count);
 
 /* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
  * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required

@@ -513,3 +513,30 @@ def test_largest_single_gpu_trace_2p23(oracle):
         ht.close()
     assert verify(proof, pub, 95) == (0, "")
     assert oracle.verify(proof, oracle_pub(oracle, pub), 95) == (0, "")
+
+
+def test_host_trace_memory_outlives_its_owner(gpu, oracle):
+    """A trace written into a HostTrace that is dropped at once (`trace, o = prog.trace(..., out=HostTrace(n))`)
+    keeps its page-locked block alive: the array's base chain owns the allocation, so proving from it reads live
+    memory and gives the oracle's proof."""
+    import gc
+
+    from golden_large import oracle_pub
+    from zkvm_amd.prover import HostTrace, Program, _PinnedBlock
+    w = make_workload(LR_PROGRAM, seed=21)
+    prog = Program(LR_PROGRAM)
+    trace, outputs = prog.trace(w.public, w.secret, w.server_key, w.last_row, out=HostTrace(prog.trace_len))
+    h = prog.hash
+    prog.close()
+    gc.collect()
+    base = trace
+    while base is not None and not isinstance(base, _PinnedBlock):
+        base = getattr(base, "base", None)
+    assert isinstance(base, _PinnedBlock) and base.ptr
+    scratch = [np.full((28, trace.shape[1], 2), 0xAB, dtype=np.uint64) for _ in range(8)]  # reuse freed pages, if any
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    proof, _, _, rc = gpu.prove(trace, pub, ProofOptions())
+    del scratch
+    assert rc == 0
+    ref, _, _ = oracle.prove(np.array(trace), oracle_pub(oracle, pub))
+    assert proof == ref
