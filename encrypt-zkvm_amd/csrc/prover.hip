@@ -257,6 +257,42 @@ int zk_device_count(int *count) {
     return ZK_OK;
 }
 
+// One upload stream per device for the process (created on first use, kept for the process's lifetime), shared by
+// every prover on that device, with the mutex that keeps one prover's copy and its event record adjacent.
+static int shared_upload_stream(int device, hipStream_t *st, std::mutex **mu) {
+    struct Up {
+        hipStream_t st = nullptr;
+        std::mutex mu;
+    };
+    static std::mutex reg_mu;
+    static std::map<int, Up *> reg;  // process lifetime: never freed
+    std::lock_guard<std::mutex> lk(reg_mu);
+    Up *&u = reg[device];
+    if (!u) {
+        auto fresh = std::make_unique<Up>();
+        ZK_CHECK_HIP(hipStreamCreateWithFlags(&fresh->st, hipStreamNonBlocking));
+        u = fresh.release();
+    }
+    *st = u->st;
+    *mu = &u->mu;
+    return ZK_OK;
+}
+
+int zk::upload_gate(zk_prover *p, hipEvent_t ev) {
+    static const bool host_gate = [] {
+        const char *e = getenv("ZK_UPLOAD_GATE");
+        return e && !strcmp(e, "host");
+    }();
+    if (host_gate) ZK_CHECK_HIP(hipEventSynchronize(ev));
+    else ZK_CHECK_HIP(hipStreamWaitEvent(p->st, ev, 0));
+    return ZK_OK;
+}
+
+void zk::upload_drain(zk_prover *p) {
+    for (auto &e : p->ev_up)
+        if (e) (void)hipEventSynchronize(e);
+}
+
 // world = 0: a full prover; world = G: one rank of a G-way coset-sharded proof (blowup 8), whose LDE-domain
 // buffers (trace / composition LDE, DEEP, NTT scratch, Merkle subtrees) hold N / G points instead of N
 static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk_prover **out) {
@@ -281,7 +317,16 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     p->max_n = max_n;
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
-    ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+    {
+        const char *e = getenv("ZK_UPLOAD_STREAM");
+        if (e && !strcmp(e, "own")) {
+            ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->up, hipStreamNonBlocking));
+            p->up_owned = true;
+            p->up_mu = new std::mutex();
+        } else {
+            ZK_TRY(shared_upload_stream(device, &p->up, &p->up_mu));
+        }
+    }
     for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
@@ -351,16 +396,20 @@ void zk_prover_destroy(zk_prover *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     (void)hipStreamSynchronize(p->st);
-    if (p->st2) (void)hipStreamSynchronize(p->st2);
+    upload_drain(p);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
     for (auto &e : p->xchg_pool) (void)hipEventDestroy(e);
     for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
-    if (p->st2) (void)hipStreamDestroy(p->st2);
+    if (p->up_owned) {
+        (void)hipStreamDestroy(p->up);
+        delete p->up_mu;
+    }
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
     if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
+    if (p->h_vm) (void)hipHostFree(p->h_vm);
     delete p->open;
     delete p;
 }
@@ -1012,7 +1061,7 @@ static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c
         int e = c + 1;
         while (e < c0 + nc && src.cols[e] == src.cols[e - 1] + col) e++;
         ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, src.cols[c], (size_t)(e - c) * col, hipMemcpyHostToDevice,
-                                    p->st2));
+                                    p->up));
         c = e;
     }
     return ZK_OK;
@@ -1037,10 +1086,13 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
     constexpr int per = W / ZK_UPLOAD_GROUPS;
     for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
-        ZK_TRY(upload_trace_group(p, src, n, g * per, per));
-        ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->st2));
+        {
+            std::lock_guard<std::mutex> lk(*p->up_mu);
+            ZK_TRY(upload_trace_group(p, src, n, g * per, per));
+            ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
+        }
         const size_t c0 = (size_t)g * per;
-        ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[g], 0));
+        ZK_TRY(upload_gate(p, p->ev_up[g]));
         ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
     }
@@ -1145,12 +1197,12 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     ZK_TRY(check_prove_args(n, p->max_n, p->max_b, opt, pub));
     // copies from the caller's host columns may still be in flight on an early error return: the caller
     // may free those columns as soon as this returns (a completed proof has long finished them).  Kernels of
-    // a failed proof may also still be queued on st: the next proof's uploads into d_trace (on st2, ordered
-    // only by the previous proof having drained st) must not race them, so both streams drain here.
+    // a failed proof may also still be queued on st: the next proof's uploads into d_trace (on the upload stream,
+    // ordered only by the previous proof having drained st) must not race them, so both drain here.
     struct CopyGuard {
         zk_prover *p;
         ~CopyGuard() {
-            (void)hipStreamSynchronize(p->st2);
+            upload_drain(p);
             (void)hipStreamSynchronize(p->st);
         }
     } copy_guard{p};
@@ -1540,7 +1592,7 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     uint8_t r[32];
     rc = trace_lde_commit(p, pl, src, n, r);
     if (!rc) rc = d2h_flush(p);
-    (void)hipStreamSynchronize(p->st2);  // the caller's trace is no longer read once this returns
+    upload_drain(p);  // the caller's trace is no longer read once this returns
     if (rc) return rc;
     if (root) memcpy(root, r, 32);
     *out = new zk_trace_lde{p, n, blowup, W};

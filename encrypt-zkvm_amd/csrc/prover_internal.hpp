@@ -6,6 +6,7 @@
 
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -102,9 +103,14 @@ struct Openings;
 struct zk_prover {
     int device = 0;
     hipStream_t st = nullptr;
-    // copy stream: a host-resident trace is uploaded here in column groups, each group's event gating its
-    // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it
-    hipStream_t st2 = nullptr;
+    // upload stream: a host-resident trace goes up here in column groups, each group's event gating its
+    // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it.  By default one
+    // stream per device shared by all its provers (upload_stream: the link is one resource, and the process then
+    // needs P + 1 hardware queues for P provers instead of 2P; ZK_UPLOAD_STREAM=own gives each prover its own).
+    // up_mu orders one prover's (copy, event) pairs against the other provers' on a shared stream.
+    hipStream_t up = nullptr;
+    bool up_owned = false;
+    std::mutex *up_mu = nullptr;
     // ... each group's event gating its kernels on st.  Measured (tools/ubench/upload_probe.hip): an event recorded
     // between the 16 MiB column copies of one stream halves their rate (29.7 vs 55 GB/s), but not between 112 MiB
     // copies (56.8 GB/s), so contiguous columns go up as one copy per group.  (Stream write / wait-value packets
@@ -143,6 +149,10 @@ struct zk_prover {
     std::vector<PendingRead> io_pending;
     uint64_t *h_gather_idx = nullptr;  // pinned host staging of the opening addresses / values
     fe *h_gather_out = nullptr;
+    // pinned staging of the device trace generator's upload (vm_gpu.hip: chunk states, inputs, last row), grown
+    // on demand
+    uint8_t *h_vm = nullptr;
+    size_t h_vm_cap = 0;
     zk::Openings *open = nullptr;      // per-proof openings, storage kept across proofs
     std::vector<uint8_t> proof_bytes;  // the serialized proof, storage kept across proofs
     unsigned *flag = nullptr;
@@ -189,6 +199,14 @@ struct zk_prover {
 };
 
 namespace zk {
+
+// Upload gating (trace_lde_commit, shard.hip S2): make the compute stream's next kernels wait for upload event ev.
+// ZK_UPLOAD_GATE=host blocks the host thread on the event before it enqueues them (the compute stream never parks on
+// a cross-stream wait, which with fewer hardware queues than streams holds up the kernels of whatever stream shares
+// its queue); the default is a device-side stream wait.
+int upload_gate(zk_prover *p, hipEvent_t ev);
+// wait until every upload this prover has enqueued has completed (the caller's host buffers are free again)
+void upload_drain(zk_prover *p);
 
 // the single-GPU prove path (prover.hip) for a sharded proof over one rank: trace = host column-major trace, or
 // NULL when it already sits in p->d_trace

@@ -381,7 +381,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             if (!on) return;
             for (zk_prover *p : P) {
                 (void)hipSetDevice(p->device);
-                (void)hipStreamSynchronize(p->st2);
+                upload_drain(p);
             }
         }
     } copy_guard{X.P, trace != nullptr};
@@ -394,10 +394,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 zk_prover *p = X.P[l];
                 const int c = X.rank[l] + G * k;
                 ZK_CHECK_HIP(hipSetDevice(p->device));
+                std::lock_guard<std::mutex> lk(*p->up_mu);
                 if (c < W)
                     ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, trace + (size_t)c * col, col,
-                                                hipMemcpyHostToDevice, p->st2));
-                ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->st2));
+                                                hipMemcpyHostToDevice, p->up));
+                ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->up));
             }
             return ZK_OK;
         };
@@ -410,7 +411,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 zk_prover *p = X.P[l];
                 const size_t c = (size_t)X.rank[l] + (size_t)G * k;
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[k], 0));
+                ZK_TRY(upload_gate(p, p->ev_up[k]));
                 if (c < (size_t)W) ntt(p->st, X.pl[l]->Tn, p->d_trace + c * n, n, p->polys + c * n, n, 1, true, nullptr, &inv_n, p->tmp);
                 snd[l] = p->polys + c * n;
                 rcv[l] = p->polys + (size_t)G * k * n;

@@ -22,20 +22,18 @@
 #include "../../include/zkvm_gpu.h"
 #include "host_field.hpp"
 #include "rescue_consts.hpp"
+#include "vm_internal.hpp"
 
 using namespace zk;
+using namespace zk::vm;
+
+namespace zk {
+namespace vm {
+thread_local std::string vm_err;
+}
+}  // namespace zk
 
 namespace {
-
-thread_local std::string vm_err;
-
-enum : uint8_t { NOOP = 0x00, PUSH = 0x10, READ = 0x11, READ2 = 0x12, ADD = 0x08, MUL = 0x09, SADD = 0x0a,
-                 SMUL = 0x0c, ADD2 = 0x0b };
-constexpr int CYCLE = 16, NUM_ROUNDS = 14, MAX_STACK = 16, MIN_TRACE = 16;
-
-struct Op {
-    uint8_t code, value;
-};
 
 std::string op_str(Op o) {
     switch (o.code) {
@@ -251,15 +249,8 @@ int compile(const std::string &src, std::vector<Op> &code) {
 // (vm/src/processor/chiplets.rs; crypto/src/rescue.rs:102-118): it is a function of the compiled code alone, and
 // its final state is Program::compile's hash (vm/src/program/mod.rs:88-95).  The reference hashes the code at
 // compile time and runs the same sponge again inside every Processor::run; here the compiled program keeps the
-// per-step states it computed for the hash, so a run of the program on new inputs (the per-proof step) is the
-// stack machine and the column writes only, split over threads.
-struct CompiledProgram {
-    std::vector<Op> code;
-    std::vector<fe> sponge[4];  // state after step k (k = 0..len; k = 0 is the zero state), per lane
-    fe hash[2];
-    size_t chiplet_err = 0;     // 1-based step of a non-noop op on a non-round step (0: none)
-    size_t trace_len = 0;       // Processor::trace length (power of two)
-};
+// per-step states it computed for the hash (CompiledProgram, vm_internal.hpp), so a run of the program on new
+// inputs (the per-proof step) is the stack machine and the column writes only, split over threads.
 
 int build_program(const char *source, CompiledProgram &P) {
     int rc = compile(source, P.code);
@@ -395,18 +386,12 @@ void write_rows(const CompiledProgram &P, const Machine &M, StackState st, size_
     }
 }
 
-int run_program(const CompiledProgram &P, const Machine &M, fe *t, size_t n, const fe *last, fe *outputs) {
+// Pass 1 the reference's way (Machine::step, a full register copy per op): only to report the first error with the
+// reference's status and text once the fast pass (stack_pass_impl) has found that the run fails.
+int slow_pass_error(const CompiledProgram &P, const Machine &M) {
     const size_t len = P.code.size();
-    const int T = (int)std::min<size_t>((size_t)vm_threads(), std::max<size_t>(1, n / 4096));
-    // chunk c covers rows [bnd[c], bnd[c + 1]); pass 1 records the state after step bnd[c] - 1 ... i.e. the
-    // state row bnd[c] - 1 shows, from which write_rows steps forward
-    std::vector<size_t> bnd(T + 1);
-    for (int c = 0; c <= T; c++) bnd[c] = n * (size_t)c / (size_t)T;
-    std::vector<StackState> start(T);
     StackState st, nx;
-    int c = 1;
-    for (size_t k = 1; k <= len; k++) {  // state after step k (row k)
-        while (c < T && bnd[c] - 1 < k) start[c++] = st;
+    for (size_t k = 1; k <= len; k++) {
         int rc = M.step(st, nx, P.code[k - 1], k);
         if (rc) return rc;
         st = nx;
@@ -415,17 +400,120 @@ int run_program(const CompiledProgram &P, const Machine &M, fe *t, size_t n, con
             return ZK_ERR_CHIPLETS;
         }
     }
-    while (c < T) start[c++] = st;
     if (len % CYCLE) {
         vm_err = "chiplets error at " + std::to_string(len) + ": trace length should be a multiple of 16, but was " +
                  std::to_string(len);
         return ZK_ERR_CHIPLETS;
     }
+    vm_err = "internal error: the VM's two stack passes disagree";
+    return ZK_ERR_INVALID_ARG;
+}
+
+// The stack pass (vm_internal.hpp stack_pass): states[c] = the state row row_of(c) - 1 shows.  The stack is kept
+// bottom first (b[0..d)), so a push is one store, a pop a decrement and the ciphertext ops touch their L slots only.
+template <class RowOf>
+int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, RowOf row_of, VmState *states,
+                    fe *outputs) {
+    const size_t len = P.code.size(), L = in.L;
+    const fe delta = fe_make(in.delta);
+    fe b[MAX_STACK];
+    size_t d = 0, ta = 0, tb = 0, c = 0;
+    auto snap = [&](VmState &s) {
+        for (size_t i = 0; i < (size_t)MAX_STACK; i++) s.reg[i] = i < d ? b[d - 1 - i] : fe_zero();
+        s.depth = (uint32_t)d;
+        s.ta = (uint32_t)ta;
+        s.tb = (uint32_t)tb;
+        s.pad = 0;
+    };
+    auto sec = [&](size_t i) { return fe_from_bytes(in.sec + 16 * i); };
+    while (c < nstates && row_of(c) <= 1) snap(states[c++]);  // rows -1 and 0 show the zero state
+    bool err = false;
+    for (size_t k = 1; k <= len && !err; k++) {
+        const Op o = P.code[k - 1];
+        switch (o.code) {
+        case NOOP:
+            break;
+        case PUSH:
+            if (d + 1 > (size_t)MAX_STACK) err = true;
+            else b[d++] = fe_make(o.value);
+            break;
+        case READ:
+            if (d + 1 > (size_t)MAX_STACK || ta >= in.npub) err = true;
+            else b[d++] = fe_make(in.pub[ta++]);
+            break;
+        case READ2:
+            if (tb >= in.nsec || d + L > (size_t)MAX_STACK) err = true;
+            else {
+                for (size_t i = 0; i < L; i++) b[d + L - 1 - i] = sec(tb * L + i);
+                d += L;
+                tb++;
+            }
+            break;
+        case ADD:
+        case MUL:
+            if (d < 2) err = true;
+            else {
+                b[d - 2] = o.code == ADD ? fe_add(b[d - 1], b[d - 2]) : fe_mul(b[d - 1], b[d - 2]);
+                d--;
+            }
+            break;
+        case SADD:  // ServerKey::scalar_add (fhe/src/server_key.rs:104-114): s'[L-1] = s[L] + delta s0
+            if (d < L + 1) err = true;
+            else {
+                const fe s0 = b[--d];
+                b[d - L] = fe_add(b[d - L], fe_mul(delta, s0));
+            }
+            break;
+        case SMUL:  // ServerKey::scalar_mul (server_key.rs:116-124): s'[i] = s[i + 1] s0
+            if (d < L + 1) err = true;
+            else {
+                const fe s0 = b[--d];
+                for (size_t i = 0; i < L; i++) b[d - 1 - i] = fe_mul(b[d - 1 - i], s0);
+            }
+            break;
+        case ADD2:  // ServerKey::add (server_key.rs:89-102): s'[i] = s[i] + s[i + L]
+            if (d < 2 * L) err = true;
+            else {
+                for (size_t i = 0; i < L; i++) b[d - L - 1 - i] = fe_add(b[d - 1 - i], b[d - L - 1 - i]);
+                d -= L;
+            }
+            break;
+        default:
+            err = true;
+        }
+        if (P.chiplet_err == k) err = true;
+        while (!err && c < nstates && row_of(c) == k + 1) snap(states[c++]);
+    }
+    if (err || len % CYCLE) {
+        std::vector<fe> sv(in.nsec * L);
+        for (size_t i = 0; i < sv.size(); i++) sv[i] = sec(i);
+        return slow_pass_error(P, Machine{in.pub, in.npub, sv.data(), in.nsec, in.L, in.delta});
+    }
+    while (c < nstates) snap(states[c++]);
     if (outputs)
-        for (int i = 0; i < MAX_STACK; i++) outputs[i] = st.reg[i];
-    if (!t) return ZK_OK;
-    // chunk c starts at row bnd[c] with the state of row bnd[c] - 1 (write_rows steps once before writing
-    // a row in [1, len]); chunk 0 starts from the zero state at row 0
+        for (size_t i = 0; i < (size_t)MAX_STACK; i++) outputs[i] = i < d ? b[d - 1 - i] : fe_zero();
+    return ZK_OK;
+}
+
+int run_program(const CompiledProgram &P, const Inputs &in, fe *t, size_t n, const fe *last, fe *outputs) {
+    const int T = (int)std::min<size_t>((size_t)vm_threads(), std::max<size_t>(1, n / 4096));
+    // chunk c covers rows [bnd[c], bnd[c + 1]) and starts from the state row bnd[c] - 1 shows (write_rows steps
+    // once before writing a row in [1, len]; chunk 0 starts from the zero state at row 0)
+    std::vector<size_t> bnd(T + 1);
+    for (int c = 0; c <= T; c++) bnd[c] = n * (size_t)c / (size_t)T;
+    std::vector<VmState> vs(T);
+    int rc = stack_pass_impl(P, in, (size_t)T, [&](size_t c) { return bnd[c]; }, vs.data(), outputs);
+    if (rc || !t) return rc;
+    std::vector<fe> sec(in.nsec * in.L);
+    for (size_t i = 0; i < sec.size(); i++) sec[i] = fe_from_bytes(in.sec + 16 * i);
+    const Machine M{in.pub, in.npub, sec.data(), in.nsec, in.L, in.delta};
+    std::vector<StackState> start(T);
+    for (int c = 0; c < T; c++) {
+        memcpy(start[c].reg, vs[c].reg, sizeof start[c].reg);
+        start[c].depth = vs[c].depth;
+        start[c].ta = vs[c].ta;
+        start[c].tb = vs[c].tb;
+    }
     // a thread that cannot be started (resource limits) leaves its chunk to the calling thread: no exception may
     // cross the C ABI
     std::vector<std::thread> th;
@@ -443,17 +531,12 @@ int run_program(const CompiledProgram &P, const Machine &M, fe *t, size_t n, con
     return ZK_OK;
 }
 
-int parse_inputs(const uint8_t *secret, size_t num_secret, uint32_t lwe_size, std::vector<fe> &sec) {
-    sec.resize(num_secret * lwe_size);
-    for (size_t i = 0; i < sec.size(); i++) sec[i] = fe_from_bytes(secret + 16 * i);
-    return ZK_OK;
-}
-
 }  // namespace
 
-struct zk_program {
-    CompiledProgram P;
-};
+int zk::vm::stack_pass(const CompiledProgram &P, const Inputs &in, size_t stride, size_t nstates, VmState *states,
+                       fe *outputs) {
+    return stack_pass_impl(P, in, nstates, [stride](size_t c) { return c * stride; }, states, outputs);
+}
 
 extern "C" int zk_program_compile(const char *source, zk_program **out, uint8_t *program_hash, size_t *trace_len) {
     if (!source || !out) return ZK_ERR_INVALID_ARG;
@@ -483,12 +566,10 @@ extern "C" int zk_program_trace(const zk_program *prog, const uint8_t *public_in
     const size_t n = P.trace_len;
     *n_out = n;
     if (trace_out && n > cap_rows) return ZK_ERR_BUFFER_TOO_SMALL;
-    std::vector<fe> sec;
-    parse_inputs(secret, num_secret, lwe_size, sec);
-    const Machine M{public_in, num_public, sec.data(), num_secret, lwe_size, delta};
+    const Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
     fe last[28], outs[MAX_STACK];
     for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
-    const int rc = run_program(P, M, reinterpret_cast<fe *>(trace_out), n, last, outs);
+    const int rc = run_program(P, in, reinterpret_cast<fe *>(trace_out), n, last, outs);
     if (rc) return rc;
     if (outputs)
         for (int i = 0; i < MAX_STACK; i++) fe_to_bytes(outs[i], outputs + 16 * i);

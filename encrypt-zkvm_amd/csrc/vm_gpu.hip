@@ -1,0 +1,378 @@
+// vm_gpu.hip -- the VM's trace written on the GPU, straight into the prover's trace buffer, and vm::prove as one call.
+//
+// The reference builds the 28-column trace on the host (Processor::run + trace, vm/src/processor/mod.rs:61-95)
+// and hands it to Prover::prove (vm/src/lib.rs:13-29); moving it to the device costs 448 MiB over PCIe per
+// 2^20-step proof.  Here the host keeps only the sequential part -- one pass of the stack machine, which checks every
+// error the reference raises and produces the outputs (vm.cpp stack_pass) -- and ships the machine state every S rows
+// plus the inputs (~6 MB at 2^20).  The GPU then:
+//   k_vm_fixed   the 11 columns that do not depend on the inputs: clk, the 5 opcode bits, the hash flag, the sponge
+//                state (from the program's device copy, uploaded once per device) and the last (random) row;
+//   k_vm_states  one thread per S-row segment replays the stack machine from its coarse state and stores the state
+//                every K rows (SoA, so the next kernel loads it coalesced);
+//   k_vm_rows    one thread per K-row chunk replays K steps and writes the depth and the 16 stack registers of each
+//                row (a lane's K consecutive rows fill whole 128-byte lines of each column).
+// The device step is the reference's stack.rs semantics on a register file, top first, with static shifts: the
+// ciphertext width L = lwe_size is a template parameter (1..5: the AIR's range, zk_prove's lwe_size check), so every
+// shift is a fixed register move under the op's exec mask.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "prover_internal.hpp"
+#include "vm_internal.hpp"
+
+using namespace zk;
+using zk::vm::Op;
+using zk::vm::VmState;
+
+namespace {
+
+constexpr int VM_S = 64;  // rows per host state (k_vm_states segment; ZK_VM_SEG overrides, a multiple of VM_K)
+constexpr int VM_K = 8;   // rows per device state (k_vm_rows chunk)
+constexpr int NREG = zk::vm::MAX_STACK;
+
+struct DevState {
+    fe t[NREG];
+    uint32_t d, ta, tb;
+};
+
+template <int S>
+__device__ __forceinline__ void shift_up(fe (&t)[NREG]) {  // t[i] = t[i - S]; t[0..S) are overwritten by the caller
+#pragma unroll
+    for (int i = NREG - 1; i >= S; i--) t[i] = t[i - S];
+}
+template <int S>
+__device__ __forceinline__ void shift_down(fe (&t)[NREG]) {  // t[i] = t[i + S], zeros enter at the bottom
+#pragma unroll
+    for (int i = 0; i < NREG - S; i++) t[i] = t[i + S];
+#pragma unroll
+    for (int i = NREG - S; i < NREG; i++) t[i] = fe_zero();
+}
+
+// One op (vm/src/processor/stack.rs; the ciphertext ops of fhe/src/server_key.rs:89-124).  The host pass has run
+// the program without error, so no check is repeated here; entries at or beyond the depth stay zero.
+template <int L>
+__device__ __forceinline__ void vm_step(DevState &s, Op o, const uint8_t *pub, const fe *sec, fe delta) {
+    switch (o.code) {
+    case zk::vm::PUSH:
+    case zk::vm::READ: {
+        const fe v = fe_make(o.code == zk::vm::PUSH ? o.value : pub[s.ta]);
+        s.ta += o.code == zk::vm::READ;
+        shift_up<1>(s.t);
+        s.t[0] = v;
+        s.d += 1;
+        break;
+    }
+    case zk::vm::READ2: {
+        shift_up<L>(s.t);
+        const fe *c = sec + (size_t)s.tb * L;
+#pragma unroll
+        for (int i = 0; i < L; i++) s.t[i] = c[i];
+        s.tb += 1;
+        s.d += L;
+        break;
+    }
+    case zk::vm::ADD:
+    case zk::vm::MUL: {
+        const fe v = o.code == zk::vm::ADD ? fe_add(s.t[0], s.t[1]) : fe_mul(s.t[0], s.t[1]);
+        shift_down<1>(s.t);
+        s.t[0] = v;
+        s.d -= 1;
+        break;
+    }
+    case zk::vm::SADD: {  // s'[i] = s[i + 1], s'[L - 1] += delta s0
+        const fe s0 = s.t[0];
+        shift_down<1>(s.t);
+        s.t[L - 1] = fe_add(s.t[L - 1], fe_mul(delta, s0));
+        s.d -= 1;
+        break;
+    }
+    case zk::vm::SMUL: {  // s'[i] = s[i + 1] s0, i < L
+        const fe s0 = s.t[0];
+        shift_down<1>(s.t);
+#pragma unroll
+        for (int i = 0; i < L; i++) s.t[i] = fe_mul(s.t[i], s0);
+        s.d -= 1;
+        break;
+    }
+    case zk::vm::ADD2: {  // s'[i] = s[i] + s[i + L], i < L
+#pragma unroll
+        for (int i = 0; i < L; i++) s.t[i + L] = fe_add(s.t[i], s.t[i + L]);
+        shift_down<L>(s.t);
+        s.d -= L;
+        break;
+    }
+    default:  // NOOP
+        break;
+    }
+}
+
+// SoA state planes: register i of state c at F[i * nf + c], {d, ta, tb} at F[NREG * nf + c]
+__device__ __forceinline__ void store_state(fe *F, size_t nf, size_t c, const DevState &s) {
+#pragma unroll
+    for (int i = 0; i < NREG; i++) F[(size_t)i * nf + c] = s.t[i];
+    reinterpret_cast<uint4 *>(F + (size_t)NREG * nf)[c] = make_uint4(s.d, s.ta, s.tb, 0);
+}
+__device__ __forceinline__ void load_state(const fe *F, size_t nf, size_t c, DevState &s) {
+#pragma unroll
+    for (int i = 0; i < NREG; i++) s.t[i] = F[(size_t)i * nf + c];
+    const uint4 m = reinterpret_cast<const uint4 *>(F + (size_t)NREG * nf)[c];
+    s.d = m.x;
+    s.ta = m.y;
+    s.tb = m.z;
+}
+
+// rows [t S, (t + 1) S): from the host's state of row t S - 1, the state of row c K - 1 for every chunk c inside
+template <int L>
+__global__ void __launch_bounds__(64) k_vm_states(const VmState *H, size_t nseg, int seg, const Op *code, size_t len,
+                                                  const uint8_t *pub, const fe *sec, fe delta, fe *F, size_t nf) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= nseg) return;
+    DevState s;
+    const VmState &h = H[t];
+#pragma unroll
+    for (int i = 0; i < NREG; i++) s.t[i] = h.reg[i];
+    s.d = h.depth;
+    s.ta = h.ta;
+    s.tb = h.tb;
+    const size_t r0 = t * (size_t)seg;
+    for (int k = 0;; k++) {
+        const size_t r = r0 + k;
+        if (k % VM_K == 0) {
+            store_state(F, nf, r / VM_K, s);  // the state row r - 1 shows
+            if (k == seg - VM_K) break;        // the next segment starts from the host's state
+        }
+        if (r >= 1 && r <= len) vm_step<L>(s, code[r - 1], pub, sec, delta);
+    }
+}
+
+// rows [c K, (c + 1) K) of columns 11 (depth) and 12..27 (stack): the state after step min(r, len) of each row r
+template <int L>
+__global__ void __launch_bounds__(256) k_vm_rows(const fe *F, size_t nf, const Op *code, size_t len,
+                                                 const uint8_t *pub, const fe *sec, fe delta, fe *trace, size_t n) {
+    const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (c >= nf) return;
+    DevState s;
+    load_state(F, nf, c, s);
+    for (int k = 0; k < VM_K; k++) {
+        const size_t r = c * VM_K + k;
+        if (r >= 1 && r <= len) vm_step<L>(s, code[r - 1], pub, sec, delta);
+        if (r == n - 1) break;  // the last row is the caller's random row (k_vm_fixed)
+        trace[11 * n + r] = fe_make(s.d);
+#pragma unroll
+        for (int i = 0; i < NREG; i++) trace[(size_t)(12 + i) * n + r] = s.t[i];
+    }
+}
+
+// the input-independent columns: clk, opcode bits (col 5 = MSB), hash flag, sponge after step min(r, len); row n - 1
+// is the caller's random row in every column (vm/src/processor/mod.rs:86-92)
+__global__ void __launch_bounds__(256) k_vm_fixed(const Op *code, size_t len, const fe *sponge, const fe *last,
+                                                  fe *trace, size_t n) {
+    const size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    if (r == n - 1) {
+        for (int col = 0; col < 28; col++) trace[(size_t)col * n + r] = last[col];
+        return;
+    }
+    const uint32_t op = r < len ? code[r].code : 0u;
+    trace[r] = fe_make(r);
+#pragma unroll
+    for (int i = 0; i < 5; i++) trace[(size_t)(1 + i) * n + r] = fe_make((op >> i) & 1u);
+    trace[6 * n + r] = fe_make(r < len ? 1u : 0u);
+    const size_t rr = r <= len ? r : len;
+#pragma unroll
+    for (int i = 0; i < 4; i++) trace[(size_t)(7 + i) * n + r] = sponge[(size_t)i * (len + 1) + rr];
+}
+
+template <int L>
+void launch_machine(hipStream_t st, const VmState *H, size_t nseg, int seg, const Op *code, size_t len,
+                    const uint8_t *pub, const fe *sec, fe delta, fe *F, size_t nf, fe *trace, size_t n) {
+    ZK_PROF(st, "vm_states", (double)nseg * sizeof(VmState) + (double)nf * (NREG + 1) * 16,
+            hipLaunchKernelGGL(k_vm_states<L>, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, st, H, nseg, seg, code,
+                               len, pub, sec, delta, F, nf));
+    ZK_PROF(st, "vm_rows", (double)nf * (NREG + 1) * 16 + (double)n * 17 * 16,
+            hipLaunchKernelGGL(k_vm_rows<L>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, F, nf, code, len,
+                               pub, sec, delta, trace, n));
+}
+
+// the program's code and sponge columns on p's device (uploaded once, kept until zk_program_free)
+int device_program(zk_program *prog, int device, const zk_program::Device **out) {
+    std::lock_guard<std::mutex> lk(prog->mu);
+    for (const auto &d : prog->dev)
+        if (d.device == device) {
+            *out = &d;
+            return ZK_OK;
+        }
+    const auto &P = prog->P;
+    const size_t len = P.code.size();
+    zk_program::Device d{device, nullptr, nullptr};
+    ZK_CHECK_HIP(hipMalloc(&d.code, len * sizeof(Op) + 16));
+    hipError_t e = hipMalloc(&d.sponge, 4 * (len + 1) * sizeof(fe));
+    if (e != hipSuccess) {
+        (void)hipFree(d.code);
+        ZK_CHECK_HIP(e);
+    }
+    prog->dev.push_back(d);  // freed by ~zk_program even if a copy below fails
+    ZK_CHECK_HIP(hipMemcpy(d.code, P.code.data(), len * sizeof(Op), hipMemcpyHostToDevice));
+    for (int i = 0; i < 4; i++)
+        ZK_CHECK_HIP(hipMemcpy(d.sponge + (size_t)i * (len + 1), P.sponge[i].data(), (len + 1) * sizeof(fe),
+                               hipMemcpyHostToDevice));
+    *out = &prog->dev.back();
+    return ZK_OK;
+}
+
+// Processor::trace's random last row (vm/src/processor/mod.rs:86-92: a nonzero u128 that is a field element)
+void random_last_row(fe last[28]) {
+    std::random_device rd;
+    for (int c = 0; c < 28; c++) {
+        for (;;) {
+            const uint64_t lo = ((uint64_t)rd() << 32) | rd(), hi = ((uint64_t)rd() << 32) | rd();
+            const bool below_p = hi < ZK_P_HI || (hi == ZK_P_HI && lo < ZK_P_LO);
+            if (below_p && (lo | hi)) {
+                last[c] = fe_make(lo, hi);
+                break;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+zk_program::~zk_program() {
+    for (auto &d : dev) {
+        (void)hipSetDevice(d.device);
+        (void)hipFree(d.code);
+        (void)hipFree(d.sponge);
+    }
+}
+
+namespace zk {
+// The trace of `prog` on these inputs into p->d_trace (28 x n column-major), stream-ordered on p->st; *n_out and
+// outputs (16 elements) on success.  Nothing waits for the kernels: the caller's next work on p->st follows them.
+int vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
+                    size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, size_t *n_out,
+                    fe *outputs) {
+    if (!p || !prog || !n_out || (num_secret && !secret) || (num_public && !public_in))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (lwe_size < 1 || lwe_size > 5)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (the AIR's ciphertext width, as zk_prove requires)");
+    const auto &P = prog->P;
+    const size_t n = P.trace_len, len = P.code.size();
+    *n_out = n;
+    if (n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "the program's trace is longer than the prover's max_trace_len");
+    ZK_CHECK_HIP(hipSetDevice(p->device));
+    static const size_t seg_env = [] {
+        const char *e = getenv("ZK_VM_SEG");
+        const long v = e ? atol(e) : 0;
+        return (v >= VM_K && v % VM_K == 0 && v <= 4096) ? (size_t)v : (size_t)VM_S;
+    }();
+    const size_t S = std::min<size_t>(seg_env, n), nseg = n / S, nf = n / VM_K;
+    // the staging area is reused: the previous upload from it must have completed
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    const size_t b_states = nseg * sizeof(VmState), b_sec = num_secret * lwe_size * sizeof(fe), b_last = 28 * sizeof(fe);
+    const size_t need = b_states + b_sec + b_last + num_public + 64;
+    if (need > p->h_vm_cap) {
+        if (p->h_vm) (void)hipHostFree(p->h_vm);
+        p->h_vm = nullptr;
+        p->h_vm_cap = 0;
+        ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_vm, need, hipHostMallocDefault));
+        p->h_vm_cap = need;
+    }
+    uint8_t *h = p->h_vm;
+    VmState *H = reinterpret_cast<VmState *>(h);
+    // the sequential part on the host: every error the reference raises, the outputs, the state every S rows
+    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
+    const int rc = zk::vm::stack_pass(P, in, S, nseg, H, outputs);
+    if (rc) {
+        g_err = zk::vm::vm_err;
+        return rc;
+    }
+    if (b_sec) memcpy(h + b_states, secret, b_sec);
+    fe last[28];
+    if (last_row)
+        for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
+    else
+        random_last_row(last);
+    memcpy(h + b_states + b_sec, last, b_last);
+    if (num_public) memcpy(h + b_states + b_sec + b_last, public_in, num_public);
+    const zk_program::Device *dp = nullptr;
+    ZK_TRY(device_program(prog, p->device, &dp));
+    // device staging: the LDE buffer (written by the proof's LDE before anything reads it) holds the upload, the
+    // NTT scratch the device states; both are free between proofs
+    uint8_t *dv = reinterpret_cast<uint8_t *>(p->lde);
+    ZK_CHECK_HIP(hipMemcpyAsync(dv, h, need - 64, hipMemcpyHostToDevice, p->st));
+    const VmState *dH = reinterpret_cast<const VmState *>(dv);
+    const fe *dsec = reinterpret_cast<const fe *>(dv + b_states);
+    const fe *dlast = reinterpret_cast<const fe *>(dv + b_states + b_sec);
+    const uint8_t *dpub = dv + b_states + b_sec + b_last;
+    fe *F = p->tmp;
+    const fe dl = fe_make(delta);
+    ZK_PROF(p->st, "vm_fixed", (double)n * 11 * 16,
+            hipLaunchKernelGGL(k_vm_fixed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, p->st, dp->code, len,
+                               dp->sponge, dlast, p->d_trace, n));
+    switch (lwe_size) {
+    case 1: launch_machine<1>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    case 2: launch_machine<2>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    case 3: launch_machine<3>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    case 4: launch_machine<4>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    default: launch_machine<5>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    }
+    ZK_CHECK_HIP(hipGetLastError());
+    return ZK_OK;
+}
+}  // namespace zk
+
+int zk_vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public,
+                       const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                       const uint8_t *last_row, size_t *n_out, uint8_t *outputs) {
+    fe outs[NREG];
+    int rc = zk::vm_trace_device(p, prog, public_in, num_public, secret, num_secret, lwe_size, delta, last_row, n_out,
+                                 outs);
+    if (rc) return rc;
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    if (outputs)
+        for (int i = 0; i < NREG; i++) fe_to_bytes(outs[i], outputs + 16 * i);
+    return ZK_OK;
+}
+
+int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
+                size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, const zk_options *opt,
+                uint8_t *proof_out, size_t *proof_len, uint8_t *outputs, uint8_t *program_hash) {
+    if (!p || !prog || !opt || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    ZK_REQUIRE_FULL_PROVER(p);
+    // Processor::run + output + trace (vm/src/lib.rs:14-18), on the device
+    fe outs[NREG];
+    size_t n = 0;
+    ZK_TRY(zk::vm_trace_device(p, prog, public_in, num_public, secret, num_secret, lwe_size, delta, last_row, &n,
+                               outs));
+    // ExecutionProver::new(options, hash, output, server_key) + prove(trace) (:20-26) on the trace in HBM
+    zk_pub_inputs pub;
+    memset(&pub, 0, sizeof pub);
+    fe_to_bytes(prog->P.hash[0], pub.program_hash[0]);
+    fe_to_bytes(prog->P.hash[1], pub.program_hash[1]);
+    for (int i = 0; i < NREG; i++) fe_to_bytes(outs[i], pub.stack_outputs[i]);
+    pub.lwe_size = lwe_size;
+    pub.delta = delta;
+    if (outputs) memcpy(outputs, pub.stack_outputs, sizeof pub.stack_outputs);
+    if (program_hash) memcpy(program_hash, pub.program_hash, sizeof pub.program_hash);
+    return zk_prove_device(p, p->d_trace, n, opt, &pub, proof_out, proof_len, nullptr, nullptr);
+}
+
+// diagnostics: the host stack pass's states every `stride` rows (CPU tests check them against host-written traces)
+extern "C" int zk_diag_vm_states(const zk_program *prog, const uint8_t *public_in, size_t num_public,
+                                 const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                                 size_t stride, size_t nstates, uint8_t *states_out, uint8_t *outputs) {
+    if (!prog || !states_out || !stride) return ZK_ERR_INVALID_ARG;
+    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
+    std::vector<VmState> st(nstates);
+    fe outs[NREG];
+    const int rc = zk::vm::stack_pass(prog->P, in, stride, nstates, st.data(), outs);
+    if (rc) return rc;
+    memcpy(states_out, st.data(), nstates * sizeof(VmState));
+    if (outputs)
+        for (int i = 0; i < NREG; i++) fe_to_bytes(outs[i], outputs + 16 * i);
+    return ZK_OK;
+}

@@ -33,7 +33,8 @@ EXPORTED = (
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_prover_exchange_stats", "zk_vm_trace",
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_prove_sharded",
-    "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error",
+    "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error", "zk_vm_trace_device",
+    "zk_vm_prove",
 )
 
 
@@ -139,6 +140,9 @@ def lib():
         L.zk_vm_last_error.restype = C.c_char_p
         L.zk_program_compile.argtypes = [C.c_char_p, C.POINTER(vp), vp, C.POINTER(sz)]
         L.zk_program_trace.argtypes = [vp, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp]
+        L.zk_vm_trace_device.argtypes = [vp, vp, vp, sz, vp, sz, u32, u32, vp, C.POINTER(sz), vp]
+        L.zk_vm_prove.argtypes = [vp, vp, vp, sz, vp, sz, u32, u32, vp, C.POINTER(Options), vp, C.POINTER(sz), vp, vp]
+        L.zk_diag_vm_states.argtypes = [vp, vp, sz, vp, sz, u32, u32, sz, sz, vp, vp]
         L.zk_program_free.argtypes = [vp]
         L.zk_program_free.restype = None
         L.zk_diag_mul_limbs_host.argtypes = [vp, vp, vp, sz]

@@ -346,6 +346,54 @@ class Program:
             raise ZkError(rc, lib().zk_vm_last_error().decode())
         return trace, bytes_elems(outputs.raw)
 
+    @staticmethod
+    def encode_inputs(public, secret, server_key):
+        """ProgramInputs in the C ABI's form (public u8 bytes, secret ciphertexts as 16-byte elements, lwe_size,
+        delta): encode once, run many times."""
+        sec = elems_bytes([v for ct in secret for v in ct])
+        return (bytes(public), len(public), sec, len(secret), server_key.lwe_size(), server_key.parameters.delta)
+
+    def trace_device(self, gpu: "GpuProver", inputs, last_row=None):
+        """Processor::run + trace written by the GPU into gpu's trace buffer (zk_vm_trace_device); inputs from
+        encode_inputs.  Returns (device pointer, n, outputs[16]).  last_row None: drawn at random, as
+        Processor::trace does."""
+        n = C.c_size_t(0)
+        outputs = C.create_string_buffer(256)
+        rc = lib().zk_vm_trace_device(gpu.handle, self.handle, *inputs,
+                                      elems_bytes(last_row) if last_row is not None else None, C.byref(n), outputs)
+        if rc:
+            check(rc, "zk_vm_trace_device")
+        return gpu.trace_buffer(), n.value, bytes_elems(outputs.raw)
+
+    def prove_device(self, gpu: "GpuProver", inputs, last_row=None, options: ProofOptions = None):
+        """vm::prove (vm/src/lib.rs:13-29) with the trace generated on the GPU (zk_vm_prove); inputs from
+        encode_inputs.  Returns (hash, outputs, proof)."""
+        opt = (options or REFERENCE_OPTIONS).to_c()
+        if getattr(gpu, "_proof_buf", None) is None:
+            gpu._proof_buf = C.create_string_buffer(4 << 20)
+        buf = gpu._proof_buf
+        plen = C.c_size_t(len(buf))
+        outputs = C.create_string_buffer(256)
+        h = C.create_string_buffer(32)
+        rc = lib().zk_vm_prove(gpu.handle, self.handle, *inputs,
+                               elems_bytes(last_row) if last_row is not None else None, C.byref(opt), buf,
+                               C.byref(plen), outputs, h)
+        if rc:
+            check(rc, "zk_vm_prove")
+        return bytes_elems(h.raw), bytes_elems(outputs.raw), C.string_at(buf, plen.value)
+
+    def stack_states(self, public, secret, server_key, stride: int, count: int):
+        """The host stack pass behind the device generator (diagnostics): (states as a (count, 17, 2) uint64 array --
+        16 registers top first, then [depth | ta << 32, tb] -- and outputs[16]); state c is what row c*stride - 1
+        shows."""
+        out = np.zeros((count, 17, 2), dtype=np.uint64)
+        outputs = C.create_string_buffer(256)
+        rc = lib().zk_diag_vm_states(self.handle, *self.encode_inputs(public, secret, server_key), stride, count,
+                                     out.ctypes.data, outputs)
+        if rc:
+            raise ZkError(rc, lib().zk_vm_last_error().decode())
+        return out, bytes_elems(outputs.raw)
+
     def close(self):
         if self.handle:
             lib().zk_program_free(self.handle)

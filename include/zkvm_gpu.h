@@ -268,6 +268,24 @@ int zk_program_trace(const zk_program *prog, const uint8_t *public_in, size_t nu
 void zk_program_free(zk_program *prog);
 const char *zk_vm_last_error(void);
 
+/* ---- vm::prove (vm/src/lib.rs:13-29) with the trace written on the GPU ----
+ * zk_vm_trace_device = Processor::run + output + trace (vm/src/processor/mod.rs:61-101) into the prover's own trace
+ * buffer (zk_prover_trace_buffer, 28 x n column-major): the host runs the stack machine once (every error the
+ * reference raises, with its status and text in zk_vm_last_error / zk_last_error; the 16 outputs) and uploads its
+ * state every 64 rows plus the inputs (~6 MB at 2^20 instead of the 448 MiB trace); kernels replay the machine and
+ * write the rows.  lwe_size must be in [1, 5] (the AIR's range).  last_row: the 28 values Processor::trace draws from
+ * thread_rng() (mod.rs:86-92), or NULL to draw them here (uniform nonzero field elements).  Returns once the trace is
+ * in HBM.  Works on every prover, a rank of a sharded proof included (then zk_prove_sharded with trace = NULL). */
+int zk_vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public,
+                       const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                       const uint8_t *last_row, size_t *n_out, uint8_t *outputs);
+/* The whole of vm::prove on one GPU: the device trace above, then ExecutionProver::new(options, program hash,
+ * outputs, server key) + prove (vm/src/lib.rs:20-26) on it -- the same proof bytes as zk_prove of the host VM's trace.
+ * outputs (16 x 16 B) and program_hash (2 x 16 B) are optional outputs (the reference returns (hash, output, proof)). */
+int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
+                size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, const zk_options *opt,
+                uint8_t *proof_out, size_t *proof_len, uint8_t *outputs, uint8_t *program_hash);
+
 #ifdef __cplusplus
 }
 #endif

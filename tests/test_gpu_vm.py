@@ -1,0 +1,146 @@
+"""The VM trace written on the GPU (zk_vm_trace_device, csrc/vm_gpu.hip) and vm::prove as one call (zk_vm_prove):
+the device trace must equal the host VM's trace byte for byte (which the CPU tests pin to the oracle VM and to the
+full-size pins' trace sha256), and zk_vm_prove's proof must equal the proof of the host trace."""
+import hashlib
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from zkvm_amd import native
+from zkvm_amd.prover import GpuProver, Program, ProofOptions, ZkError, _hip, make_pub_inputs
+from zkvm_amd.workloads import (LR_PROGRAM, LweParameters, cipher_mix_program, make_workload, ops_for_trace_len,
+                                push_add_program)
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from golden_large import LARGE_CASES  # noqa: E402
+from test_vm_parallel import random_program  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def device_trace(gpu, prog, w, last_row="given"):
+    inp = Program.encode_inputs(w.public, w.secret, w.server_key)
+    d, n, outs = prog.trace_device(gpu, inp, w.last_row if last_row == "given" else None)
+    host = np.zeros((28, n, 2), dtype=np.uint64)
+    import ctypes as C
+    assert _hip().hipMemcpy(host.ctypes.data_as(C.c_void_p), C.c_void_p(d), host.nbytes, 2) == 0
+    return host, outs
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    assert native.device_count() > 0, "no GPU visible"
+    g = GpuProver(0, max_trace_len=1 << 16)
+    yield g
+    g.close()
+
+
+@pytest.mark.parametrize("src", [LR_PROGRAM, push_add_program(100), cipher_mix_program(300)[0],
+                                 ops_for_trace_len(14, "cipher"), ops_for_trace_len(16, "pushadd")],
+                         ids=["lr", "pushadd100", "cipher300", "cipher_2p14", "pushadd_2p16"])
+def test_device_trace_matches_host_vm(gpu, src):
+    w = make_workload(src, seed=31)
+    prog = Program(src)
+    htrace, houts = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+    dtrace, douts = device_trace(gpu, prog, w)
+    prog.close()
+    assert douts == houts
+    assert np.array_equal(dtrace, htrace)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_device_trace_other_lwe_sizes(gpu, k):
+    """lwe_size 2..5 (the AIR's range; k = 4 is the default above): the templated device step per ciphertext
+    width."""
+    src = cipher_mix_program(40)[0]
+    w = make_workload(src, seed=40 + k, params=LweParameters(k=k))
+    prog = Program(src)
+    htrace, houts = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+    dtrace, douts = device_trace(gpu, prog, w)
+    prog.close()
+    assert douts == houts and np.array_equal(dtrace, htrace)
+
+
+def test_device_trace_random_programs(gpu):
+    """The differential programs of test_vm_parallel (mostly valid, some failing): the same status and text as the
+    host VM, and on success the same trace."""
+    rnd = random.Random(4242)
+    ok = 0
+    for i in range(120):
+        src = random_program(rnd)
+        short = rnd.random() < 0.3
+        w = make_workload(src or "push.1\n", seed=2000 + i, n_pub=rnd.randrange(0, 40) if short else None,
+                          n_sec=rnd.randrange(0, 12) if short else None)
+        try:
+            prog = Program(src)
+        except ZkError:
+            continue
+        try:
+            htrace, houts = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+            hres = ("ok",)
+        except ZkError as e:
+            hres = ("err", e.code, str(e).split("] ", 1)[1])
+        try:
+            dtrace, douts = device_trace(gpu, prog, w)
+            dres = ("ok",)
+        except ZkError as e:
+            dres = ("err", e.code, str(e).split(": ", 1)[1])
+        prog.close()
+        assert hres == dres, (src, hres, dres)
+        if hres[0] == "ok":
+            ok += 1
+            assert douts == houts and np.array_equal(dtrace, htrace), src
+    assert ok >= 15
+
+
+def test_vm_prove_equals_host_trace_proof(gpu):
+    """zk_vm_prove (vm::prove with the trace written on the GPU) gives the proof of the host VM's trace, and the
+    program hash / outputs of the reference's (hash, output, proof)."""
+    src = cipher_mix_program(200)[0]
+    w = make_workload(src, seed=9)
+    prog = Program(src)
+    trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+    pub = make_pub_inputs(prog.hash, outs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    ref, _, _, rc = gpu.prove(trace, pub, ProofOptions())
+    assert rc == 0
+    h, o, proof = prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
+    assert (h, o) == (prog.hash, outs) and proof == ref
+    # a random last row (Processor::trace's thread_rng draw): a different, still valid proof
+    from zkvm_amd.prover import verify
+    _, o2, proof2 = prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), None)
+    assert o2 == outs and proof2 != ref and verify(proof2, pub, 95) == (0, "")
+    prog.close()
+
+
+def test_vm_prove_reports_vm_errors(gpu):
+    prog = Program("read2\nadd\n")
+    w = make_workload("read2\nadd\n", seed=3)
+    with pytest.raises(ZkError) as e:
+        prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
+    assert e.value.code == native.ZK_ERR_STACK and "stack error at 2: add operation stack underflow" in str(e.value)
+    prog.close()
+
+
+@pytest.mark.parametrize("log_n", sorted({c["log_n"] for c in LARGE_CASES if c["options"]["field_extension"] == 1
+                                          and c["seed"] == 1000}))
+def test_device_trace_full_size_pins(log_n, oracle):
+    """configs[2] (2^20) and configs[3] (2^22): the device-written trace hashes to the pin's trace sha256 (the oracle
+    VM's trace), and zk_vm_prove's proof equals the pinned proof byte for byte."""
+    c = next(c for c in LARGE_CASES if c["log_n"] == log_n and c["seed"] == 1000
+             and c["options"]["field_extension"] == 1)
+    src = ops_for_trace_len(log_n, c["generator"])
+    w = make_workload(src, seed=c["seed"])
+    prog = Program(src)
+    g = GpuProver(0, max_trace_len=1 << log_n)
+    try:
+        dtrace, _ = device_trace(g, prog, w)
+        assert hashlib.sha256(dtrace.tobytes()).hexdigest() == c["trace_sha256"]
+        del dtrace
+        _, _, proof = prog.prove_device(g, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
+    finally:
+        g.close()
+        prog.close()
+    assert len(proof) == c["proof_len"] and hashlib.sha256(proof).hexdigest() == c["proof_sha256"]

@@ -118,3 +118,59 @@ def test_program_errors_surface():
     with pytest.raises(ZkError) as e:
         prog.trace([], [], ServerKey(seed=0), [1] * 28)
     assert e.value.code == native.ZK_ERR_STACK and "stack underflow" in str(e.value)
+
+
+def test_stack_pass_states_match_trace_rows():
+    """The host stack pass behind the device trace generator (vm.cpp stack_pass: bottom-first stack, one store per
+    push) against the rows the reference-shaped VM writes: state c equals row c*stride - 1 (registers, depth), the
+    outputs agree, and a failing run reports the same status and text."""
+    rnd = random.Random(77)
+    checked = 0
+    for i in range(160):
+        src = random_program(rnd)
+        short = rnd.random() < 0.3
+        w = make_workload(src or "push.1\n", seed=1000 + i, n_pub=rnd.randrange(0, 40) if short else None,
+                          n_sec=rnd.randrange(0, 12) if short else None)
+        try:
+            prog = Program(src)
+        except ZkError:
+            continue
+        try:
+            trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+        except ZkError as e:
+            with pytest.raises(ZkError) as e2:
+                prog.stack_states(w.public, w.secret, w.server_key, 8, 4)
+            assert e2.value.code == e.code and str(e2.value).split("] ", 1)[1] == str(e).split("] ", 1)[1]
+            prog.close()
+            continue
+        n = trace.shape[1]
+        for stride in (8, 16, 64):
+            if stride > n:
+                continue
+            count = n // stride
+            states, souts = prog.stack_states(w.public, w.secret, w.server_key, stride, count)
+            assert souts == outs
+            assert not states[0].any()
+            rows = np.arange(1, count) * stride - 1
+            assert np.array_equal(states[1:, :16, :], trace[12:28, rows, :].transpose(1, 0, 2))
+            assert np.array_equal(states[1:, 16, 0] & 0xFFFFFFFF, trace[11, rows, 0])
+        prog.close()
+        checked += 1
+    assert checked >= 20
+
+
+def test_stack_pass_full_size_pin():
+    """configs[2]'s 2^20 trace: the stack pass's states every 64 rows (what the device generator uploads) equal the
+    rows of the pinned trace."""
+    c = next(c for c in LARGE_CASES if c["log_n"] == 20)
+    src = ops_for_trace_len(20, c["generator"])
+    w = make_workload(src, seed=c["seed"])
+    prog = Program(src)
+    trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+    assert hashlib.sha256(trace.tobytes()).hexdigest() == c["trace_sha256"]
+    states, souts = prog.stack_states(w.public, w.secret, w.server_key, 64, (1 << 20) // 64)
+    rows = np.arange(1, (1 << 20) // 64) * 64 - 1
+    assert souts == outs
+    assert np.array_equal(states[1:, :16, :], trace[12:28, rows, :].transpose(1, 0, 2))
+    assert np.array_equal(states[1:, 16, 0] & 0xFFFFFFFF, trace[11, rows, 0])
+    prog.close()
