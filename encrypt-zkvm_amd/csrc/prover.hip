@@ -1039,6 +1039,7 @@ static int lde_commit(zk_prover *p, Plan *pl, const fe *polys, int ncols, fe *ld
 struct TraceSrc {
     const fe *dev = nullptr;
     const uint8_t *const *cols = nullptr;
+    const FixedCols *fixed = nullptr;  // with dev: only the dynamic columns are in dev (zk_vm_prove)
 };
 
 // Column groups of a host-resident trace upload: 7 groups of 4 columns.  The copy engine streams group g + 1 while
@@ -1073,6 +1074,24 @@ static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c
 // event gates that group's interpolation and coset LDE on the compute stream.
 static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
     const fe inv_n = h_inv(fe_make(n));
+    if (src.dev && src.fixed) {
+        // zk_vm_prove: interpolate and extend the dynamic stack columns only; the preprocessed ones by one pass
+        const FixedCols &fx = *src.fixed;
+        const size_t B = (size_t)1 << pl->log_b, c0 = 12;
+        if (fx.md > 0) {
+            ntt(p->st, pl->Tn, src.dev + c0 * n, n, p->polys + c0 * n, n, fx.md, true, nullptr, &inv_n, p->tmp);
+            ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, fx.md, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n,
+                    p->tmp);
+        }
+        if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
+        fe_ws ws[W];
+        for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
+        ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
+        fixed_axpy(p->st, fx, p->fix_ws, n, B, p->polys, p->lde);
+        hash_rows_cosets(p->st, p->lde, W, pl->log_n, pl->log_b, 0, pl->log_b, p->leaves);
+        merkle_tree(p->st, p->leaves, n * B, p->nodes);
+        return d2h_small(p, root, p->nodes + 32, 32);
+    }
     if (src.dev) {
         ntt(p->st, pl->Tn, src.dev, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
         return lde_commit(p, pl, p->polys, W, p->lde, p->leaves, p->nodes, root);
@@ -1505,6 +1524,14 @@ int zk_prove_device(zk_prover *p, const void *d_trace, size_t n, const zk_option
     TraceSrc src;
     src.dev = (const fe *)d_trace;
     return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+}
+
+int zk::prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inputs *pub, const FixedCols *fx,
+                    uint8_t *proof_out, size_t *proof_len) {
+    TraceSrc src;
+    src.dev = p->d_trace;
+    src.fixed = fx;
+    return prove_impl(p, src, n, opt, pub, proof_out, proof_len, nullptr, nullptr);
 }
 
 int zk::prove_single(zk_prover *p, const uint8_t *trace, size_t n, const zk_options *opt, const zk_pub_inputs *pub,

@@ -159,6 +159,7 @@ struct zk_prover {
     void *air_consts = nullptr, *deep_consts = nullptr, *fold_consts = nullptr;
     uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
     fe *fri_alphas = nullptr;     // the alphas the device coin drew (2 per layer)
+    fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
@@ -207,6 +208,26 @@ namespace zk {
 int upload_gate(zk_prover *p, hipEvent_t ev);
 // wait until every upload this prover has enqueued has completed (the caller's host buffers are free again)
 void upload_drain(zk_prover *p);
+
+// vm::prove's preprocessed trace columns (vm_gpu.hip, zk_vm_prove).  Columns 0..11 (clk, opcode bits, hash flag,
+// sponge, stack depth) depend on the program and lwe_size only, and a stack register column 12 + i with i >= the
+// program's maximum depth is zero: every such column c is f_c + last[c] e_(n-1), with f_c fixed per program (f_c = 0
+// for the zero registers) and last[c] the random last row.  Interpolation and coset LDE are linear, so its
+// coefficients and LDE are f_c's (computed once per program) plus last[c] times those of e_(n-1) (the Lagrange
+// basis polynomial of the last row): one streaming pass instead of 1 + B size-n NTTs per column.
+struct FixedCols {
+    int md;                  // trace columns 12 .. 12 + md - 1 are the dynamic ones (stack registers within depth)
+    const fe *fpolys;        // 12 x n coefficients of f_0 .. f_11 (column-major)
+    const fe *flde;          // 12 x B n, coset-major like the prover's LDE
+    const fe *lagr;          // n coefficients of e_(n-1)'s interpolant
+    const fe *lagr_lde;      // B n, coset-major
+    fe last[W];              // the last row
+};
+// zk_prove_device of p->d_trace (whose dynamic columns hold the trace) with the preprocessed columns of fx
+int prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inputs *pub, const FixedCols *fx,
+                uint8_t *proof_out, size_t *proof_len);
+// polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip)
+void fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t n, size_t B, fe *polys, fe *lde);
 
 // the single-GPU prove path (prover.hip) for a sharded proof over one rank: trace = host column-major trace, or
 // NULL when it already sits in p->d_trace

@@ -413,11 +413,11 @@ int slow_pass_error(const CompiledProgram &P, const Machine &M) {
 // bottom first (b[0..d)), so a push is one store, a pop a decrement and the ciphertext ops touch their L slots only.
 template <class RowOf>
 int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, RowOf row_of, VmState *states,
-                    fe *outputs) {
+                    fe *outputs, uint32_t *max_depth = nullptr) {
     const size_t len = P.code.size(), L = in.L;
     const fe delta = fe_make(in.delta);
     fe b[MAX_STACK];
-    size_t d = 0, ta = 0, tb = 0, c = 0;
+    size_t d = 0, ta = 0, tb = 0, c = 0, md = 0;
     auto snap = [&](VmState &s) {
         for (size_t i = 0; i < (size_t)MAX_STACK; i++) s.reg[i] = i < d ? b[d - 1 - i] : fe_zero();
         s.depth = (uint32_t)d;
@@ -482,6 +482,7 @@ int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, 
             err = true;
         }
         if (P.chiplet_err == k) err = true;
+        md = std::max(md, d);
         while (!err && c < nstates && row_of(c) == k + 1) snap(states[c++]);
     }
     if (err || len % CYCLE) {
@@ -490,6 +491,7 @@ int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, 
         return slow_pass_error(P, Machine{in.pub, in.npub, sv.data(), in.nsec, in.L, in.delta});
     }
     while (c < nstates) snap(states[c++]);
+    if (max_depth) *max_depth = (uint32_t)md;
     if (outputs)
         for (size_t i = 0; i < (size_t)MAX_STACK; i++) outputs[i] = i < d ? b[d - 1 - i] : fe_zero();
     return ZK_OK;
@@ -534,8 +536,8 @@ int run_program(const CompiledProgram &P, const Inputs &in, fe *t, size_t n, con
 }  // namespace
 
 int zk::vm::stack_pass(const CompiledProgram &P, const Inputs &in, size_t stride, size_t nstates, VmState *states,
-                       fe *outputs) {
-    return stack_pass_impl(P, in, nstates, [stride](size_t c) { return c * stride; }, states, outputs);
+                       fe *outputs, uint32_t *max_depth) {
+    return stack_pass_impl(P, in, nstates, [stride](size_t c) { return c * stride; }, states, outputs, max_depth);
 }
 
 extern "C" int zk_program_compile(const char *source, zk_program **out, uint8_t *program_hash, size_t *trace_len) {

@@ -149,21 +149,29 @@ __global__ void __launch_bounds__(64) k_vm_states(const VmState *H, size_t nseg,
     }
 }
 
-// rows [c K, (c + 1) K) of columns 11 (depth) and 12..27 (stack): the state after step min(r, len) of each row r
+// rows [c K, (c + 1) K) of the machine's columns: the state after step min(r, len) of each row r -- the depth (column
+// 11) when `depth`, the stack registers 0 .. nregs - 1 (columns 12 .. 12 + nregs - 1); row n - 1 holds the caller's
+// random row, written here when `last` is given (else by k_vm_fixed)
 template <int L>
 __global__ void __launch_bounds__(256) k_vm_rows(const fe *F, size_t nf, const Op *code, size_t len,
-                                                 const uint8_t *pub, const fe *sec, fe delta, fe *trace, size_t n) {
+                                                 const uint8_t *pub, const fe *sec, fe delta, int nregs, bool depth,
+                                                 const fe *last, fe *trace, size_t n) {
     const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (c >= nf) return;
     DevState s;
     load_state(F, nf, c, s);
     for (int k = 0; k < VM_K; k++) {
         const size_t r = c * VM_K + k;
+        if (r == n - 1) {
+            if (last)
+                for (int i = 0; i < nregs; i++) trace[(size_t)(12 + i) * n + r] = last[12 + i];
+            break;
+        }
         if (r >= 1 && r <= len) vm_step<L>(s, code[r - 1], pub, sec, delta);
-        if (r == n - 1) break;  // the last row is the caller's random row (k_vm_fixed)
-        trace[11 * n + r] = fe_make(s.d);
+        if (depth) trace[11 * n + r] = fe_make(s.d);
 #pragma unroll
-        for (int i = 0; i < NREG; i++) trace[(size_t)(12 + i) * n + r] = s.t[i];
+        for (int i = 0; i < NREG; i++)
+            if (i < nregs) trace[(size_t)(12 + i) * n + r] = s.t[i];
     }
 }
 
@@ -187,40 +195,76 @@ __global__ void __launch_bounds__(256) k_vm_fixed(const Op *code, size_t len, co
     for (int i = 0; i < 4; i++) trace[(size_t)(7 + i) * n + r] = sponge[(size_t)i * (len + 1) + rr];
 }
 
+// the preprocessed columns (FixedCols): out[c][i] = F[src][i] (0 when src < 0) + last[c] base[i] for the ncol
+// columns listed, over `count` points of planes of `stride` (coefficients: n; LDE: B n).  Streaming, HBM-bound: per
+// point the Lagrange value once, then per column one read (nonzero f_c) and one write.
+struct AxpyCols {
+    int ncol;
+    uint8_t col[W];
+    int8_t src[W];
+};
+__global__ void __launch_bounds__(256) k_fixed_axpy(const fe *F, const fe *base, size_t stride, AxpyCols A,
+                                                    const fe_ws *ws, fe *out) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= stride) return;
+    const fe b = base[i];
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+        if (k < A.ncol) {
+            const int c = A.col[k], s = A.src[k];
+            const fe t = fe_mul_uniform(b, load_fe_ws(ws, c));
+            out[(size_t)c * stride + i] = s >= 0 ? fe_add(F[(size_t)s * stride + i], t) : t;
+        }
+    }
+}
+
 template <int L>
 void launch_machine(hipStream_t st, const VmState *H, size_t nseg, int seg, const Op *code, size_t len,
-                    const uint8_t *pub, const fe *sec, fe delta, fe *F, size_t nf, fe *trace, size_t n) {
+                    const uint8_t *pub, const fe *sec, fe delta, fe *F, size_t nf, int nregs, bool depth,
+                    const fe *last, fe *trace, size_t n) {
     ZK_PROF(st, "vm_states", (double)nseg * sizeof(VmState) + (double)nf * (NREG + 1) * 16,
             hipLaunchKernelGGL(k_vm_states<L>, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, st, H, nseg, seg, code,
                                len, pub, sec, delta, F, nf));
-    ZK_PROF(st, "vm_rows", (double)nf * (NREG + 1) * 16 + (double)n * 17 * 16,
+    ZK_PROF(st, "vm_rows", (double)nf * (NREG + 1) * 16 + (double)n * (nregs + depth) * 16,
             hipLaunchKernelGGL(k_vm_rows<L>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, F, nf, code, len,
-                               pub, sec, delta, trace, n));
+                               pub, sec, delta, nregs, depth, last, trace, n));
 }
 
-// the program's code and sponge columns on p's device (uploaded once, kept until zk_program_free)
-int device_program(zk_program *prog, int device, const zk_program::Device **out) {
-    std::lock_guard<std::mutex> lk(prog->mu);
-    for (const auto &d : prog->dev)
-        if (d.device == device) {
-            *out = &d;
+struct DevProg {
+    const Op *code;
+    const fe *sponge;
+};
+
+// the program's code and sponge columns on `device` (uploaded once, kept until zk_program_free); prog->mu held
+int device_program_locked(zk_program *prog, int device, zk_program::Device **out) {
+    for (auto &d : prog->dev)
+        if (d->device == device) {
+            *out = d.get();
             return ZK_OK;
         }
     const auto &P = prog->P;
     const size_t len = P.code.size();
-    zk_program::Device d{device, nullptr, nullptr};
-    ZK_CHECK_HIP(hipMalloc(&d.code, len * sizeof(Op) + 16));
-    hipError_t e = hipMalloc(&d.sponge, 4 * (len + 1) * sizeof(fe));
-    if (e != hipSuccess) {
-        (void)hipFree(d.code);
-        ZK_CHECK_HIP(e);
-    }
-    prog->dev.push_back(d);  // freed by ~zk_program even if a copy below fails
-    ZK_CHECK_HIP(hipMemcpy(d.code, P.code.data(), len * sizeof(Op), hipMemcpyHostToDevice));
+    auto d = std::make_unique<zk_program::Device>();
+    d->device = device;
+    d->code = nullptr;
+    d->sponge = nullptr;
+    ZK_CHECK_HIP(hipMalloc(&d->code, len * sizeof(Op) + 16));
+    zk_program::Device *raw = d.get();
+    prog->dev.push_back(std::move(d));  // freed by ~zk_program even if a step below fails
+    ZK_CHECK_HIP(hipMalloc(&raw->sponge, 4 * (len + 1) * sizeof(fe)));
+    ZK_CHECK_HIP(hipMemcpy(raw->code, P.code.data(), len * sizeof(Op), hipMemcpyHostToDevice));
     for (int i = 0; i < 4; i++)
-        ZK_CHECK_HIP(hipMemcpy(d.sponge + (size_t)i * (len + 1), P.sponge[i].data(), (len + 1) * sizeof(fe),
+        ZK_CHECK_HIP(hipMemcpy(raw->sponge + (size_t)i * (len + 1), P.sponge[i].data(), (len + 1) * sizeof(fe),
                                hipMemcpyHostToDevice));
-    *out = &prog->dev.back();
+    *out = raw;
+    return ZK_OK;
+}
+
+int device_program(zk_program *prog, int device, DevProg *out) {
+    std::lock_guard<std::mutex> lk(prog->mu);
+    zk_program::Device *d = nullptr;
+    ZK_TRY(device_program_locked(prog, device, &d));
+    *out = DevProg{d->code, d->sponge};
     return ZK_OK;
 }
 
@@ -239,30 +283,23 @@ void random_last_row(fe last[28]) {
     }
 }
 
-}  // namespace
+// Which columns of the trace vm_generate writes
+struct GenMode {
+    bool fixed;  // the input-independent columns 0..10 and the depth (11)
+    int nregs;   // stack registers 0 .. nregs - 1 (columns 12 ..)
+};
 
-zk_program::~zk_program() {
-    for (auto &d : dev) {
-        (void)hipSetDevice(d.device);
-        (void)hipFree(d.code);
-        (void)hipFree(d.sponge);
-    }
-}
-
-namespace zk {
-// The trace of `prog` on these inputs into p->d_trace (28 x n column-major), stream-ordered on p->st; *n_out and
-// outputs (16 elements) on success.  Nothing waits for the kernels: the caller's next work on p->st follows them.
-int vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
-                    size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, size_t *n_out,
-                    fe *outputs) {
-    if (!p || !prog || !n_out || (num_secret && !secret) || (num_public && !public_in))
-        ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
-    if (lwe_size < 1 || lwe_size > 5)
-        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (the AIR's ciphertext width, as zk_prove requires)");
+// The trace of `prog` on `in` into p->d_trace (28 x n column-major; the columns `mode` selects), stream-ordered on
+// p->st: the host stack pass (errors, outputs, the state every S rows, the maximum depth), one upload of the states,
+// inputs and last row, then the kernels.  Nothing waits for them.
+int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const fe last[28], GenMode mode,
+                size_t *n_out, fe *outputs, uint32_t *max_depth) {
     const auto &P = prog->P;
     const size_t n = P.trace_len, len = P.code.size();
     *n_out = n;
     if (n > p->max_n) ZK_FAIL(ZK_ERR_INVALID_ARG, "the program's trace is longer than the prover's max_trace_len");
+    if (in.L < 1 || in.L > 5)
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "lwe_size must be in [1, 5] (the AIR's ciphertext width, as zk_prove requires)");
     ZK_CHECK_HIP(hipSetDevice(p->device));
     static const size_t seg_env = [] {
         const char *e = getenv("ZK_VM_SEG");
@@ -272,66 +309,150 @@ int vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, si
     const size_t S = std::min<size_t>(seg_env, n), nseg = n / S, nf = n / VM_K;
     // the staging area is reused: the previous upload from it must have completed
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-    const size_t b_states = nseg * sizeof(VmState), b_sec = num_secret * lwe_size * sizeof(fe), b_last = 28 * sizeof(fe);
-    const size_t need = b_states + b_sec + b_last + num_public + 64;
-    if (need > p->h_vm_cap) {
+    const size_t b_states = nseg * sizeof(VmState), b_sec = in.nsec * in.L * sizeof(fe), b_last = 28 * sizeof(fe);
+    const size_t bytes = b_states + b_sec + b_last + in.npub;
+    if (bytes + 64 > p->h_vm_cap) {
         if (p->h_vm) (void)hipHostFree(p->h_vm);
         p->h_vm = nullptr;
         p->h_vm_cap = 0;
-        ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_vm, need, hipHostMallocDefault));
-        p->h_vm_cap = need;
+        ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_vm, bytes + 64, hipHostMallocDefault));
+        p->h_vm_cap = bytes + 64;
     }
     uint8_t *h = p->h_vm;
-    VmState *H = reinterpret_cast<VmState *>(h);
     // the sequential part on the host: every error the reference raises, the outputs, the state every S rows
-    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
-    const int rc = zk::vm::stack_pass(P, in, S, nseg, H, outputs);
+    const int rc = zk::vm::stack_pass(P, in, S, nseg, reinterpret_cast<VmState *>(h), outputs, max_depth);
     if (rc) {
         g_err = zk::vm::vm_err;
         return rc;
     }
-    if (b_sec) memcpy(h + b_states, secret, b_sec);
-    fe last[28];
-    if (last_row)
-        for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
-    else
-        random_last_row(last);
+    if (b_sec) memcpy(h + b_states, in.sec, b_sec);
     memcpy(h + b_states + b_sec, last, b_last);
-    if (num_public) memcpy(h + b_states + b_sec + b_last, public_in, num_public);
-    const zk_program::Device *dp = nullptr;
+    if (in.npub) memcpy(h + b_states + b_sec + b_last, in.pub, in.npub);
+    DevProg dp;
     ZK_TRY(device_program(prog, p->device, &dp));
     // device staging: the LDE buffer (written by the proof's LDE before anything reads it) holds the upload, the
     // NTT scratch the device states; both are free between proofs
     uint8_t *dv = reinterpret_cast<uint8_t *>(p->lde);
-    ZK_CHECK_HIP(hipMemcpyAsync(dv, h, need - 64, hipMemcpyHostToDevice, p->st));
+    ZK_CHECK_HIP(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, p->st));
     const VmState *dH = reinterpret_cast<const VmState *>(dv);
     const fe *dsec = reinterpret_cast<const fe *>(dv + b_states);
     const fe *dlast = reinterpret_cast<const fe *>(dv + b_states + b_sec);
     const uint8_t *dpub = dv + b_states + b_sec + b_last;
     fe *F = p->tmp;
-    const fe dl = fe_make(delta);
-    ZK_PROF(p->st, "vm_fixed", (double)n * 11 * 16,
-            hipLaunchKernelGGL(k_vm_fixed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, p->st, dp->code, len,
-                               dp->sponge, dlast, p->d_trace, n));
-    switch (lwe_size) {
-    case 1: launch_machine<1>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
-    case 2: launch_machine<2>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
-    case 3: launch_machine<3>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
-    case 4: launch_machine<4>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
-    default: launch_machine<5>(p->st, dH, nseg, (int)S, dp->code, len, dpub, dsec, dl, F, nf, p->d_trace, n); break;
+    const fe dl = fe_make(in.delta);
+    if (mode.fixed)
+        ZK_PROF(p->st, "vm_fixed", (double)n * 11 * 16,
+                hipLaunchKernelGGL(k_vm_fixed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, p->st, dp.code, len,
+                                   dp.sponge, dlast, p->d_trace, n));
+    const fe *rlast = mode.fixed ? nullptr : dlast;
+#define ZK_VM_LAUNCH(LL)                                                                                              \
+    launch_machine<LL>(p->st, dH, nseg, (int)S, dp.code, len, dpub, dsec, dl, F, nf, mode.nregs, mode.fixed, rlast, \
+                       p->d_trace, n)
+    switch (in.L) {
+    case 1: ZK_VM_LAUNCH(1); break;
+    case 2: ZK_VM_LAUNCH(2); break;
+    case 3: ZK_VM_LAUNCH(3); break;
+    case 4: ZK_VM_LAUNCH(4); break;
+    default: ZK_VM_LAUNCH(5); break;
     }
+#undef ZK_VM_LAUNCH
     ZK_CHECK_HIP(hipGetLastError());
     return ZK_OK;
 }
-}  // namespace zk
+
+// The preprocessed columns of (prog, lwe_size, blowup) on p's device (zk_program::Fixed), built on first use with
+// this call's inputs: the full trace with a zero last row, its columns 0..11 interpolated and extended, and the
+// Lagrange polynomial of the last row.  Returned by value (the cache may grow while the caller proves).
+int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint32_t B, zk_program::Fixed *out) {
+    std::lock_guard<std::mutex> lk(prog->mu);
+    zk_program::Device *d = nullptr;
+    ZK_TRY(device_program_locked(prog, p->device, &d));
+    for (const auto &f : d->fixed)
+        if (f.L == in.L && f.B == B) {
+            *out = f;
+            return ZK_OK;
+        }
+    const size_t n = prog->P.trace_len;
+    Plan *pl = nullptr;
+    ZK_TRY(get_plan(p, n, B, &pl));
+    zk_program::Fixed f{in.L, B, 0, nullptr, nullptr, nullptr, nullptr};
+    ZK_CHECK_HIP(hipMalloc(&f.fpolys, 12 * n * sizeof(fe)));
+    d->fixed.push_back(f);  // freed by ~zk_program; completed below
+    zk_program::Fixed &g = d->fixed.back();
+    ZK_CHECK_HIP(hipMalloc(&g.flde, 12 * B * n * sizeof(fe)));
+    ZK_CHECK_HIP(hipMalloc(&g.lagr, n * sizeof(fe)));
+    ZK_CHECK_HIP(hipMalloc(&g.lagr_lde, B * n * sizeof(fe)));
+    // f_0 .. f_11: the program-only columns with the last row zeroed
+    fe zero[28], outs[NREG];
+    memset(zero, 0, sizeof zero);
+    uint32_t md = 0;
+    size_t nn = 0;
+    ZK_TRY(vm_generate(p, prog, in, zero, GenMode{true, NREG}, &nn, outs, &md));
+    const fe inv_n = h_inv(fe_make(n));
+    ntt(p->st, pl->Tn, p->d_trace, n, g.fpolys, n, 12, true, nullptr, &inv_n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, 0, 1, (int)B, g.flde, B * n, n, p->tmp);
+    // e_(n-1): zeros but a one in the last row
+    ZK_CHECK_HIP(hipMemsetAsync(p->polys, 0, n * sizeof(fe), p->st));
+    const fe one = fe_one();
+    ZK_TRY(h2d_small(p, p->polys + (n - 1), &one, sizeof one));
+    ntt(p->st, pl->Tn, p->polys, n, g.lagr, n, 1, true, nullptr, &inv_n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, 0, 1, (int)B, g.lagr_lde, B * n, n, p->tmp);
+    ZK_TRY(io_rewind(p));  // sync: the cache is complete, the staging area starts over
+    g.md = (int)md;
+    *out = g;
+    return ZK_OK;
+}
+
+}  // namespace
+
+void zk::fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t n, size_t B, fe *polys, fe *lde) {
+    AxpyCols A;
+    A.ncol = 0;
+    for (int c = 0; c < W; c++) {
+        if (c >= 12 && c < 12 + fx.md) continue;  // dynamic: interpolated and extended from the trace
+        A.col[A.ncol] = (uint8_t)c;
+        A.src[A.ncol] = (int8_t)(c < 12 ? c : -1);
+        A.ncol++;
+    }
+    const size_t nf = 12, nz = (size_t)A.ncol - nf;
+    ZK_PROF(st, "fixed_axpy", (double)n * 16 * (1 + 2 * nf + nz),
+            hipLaunchKernelGGL(k_fixed_axpy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, fx.fpolys, fx.lagr, n, A,
+                               ws_dev, polys));
+    ZK_PROF(st, "fixed_axpy", (double)B * n * 16 * (1 + 2 * nf + nz),
+            hipLaunchKernelGGL(k_fixed_axpy, dim3((unsigned)((B * n + 255) / 256)), dim3(256), 0, st, fx.flde,
+                               fx.lagr_lde, B * n, A, ws_dev, lde));
+}
+
+zk_program::~zk_program() {
+    for (auto &d : dev) {
+        (void)hipSetDevice(d->device);
+        (void)hipFree(d->code);
+        (void)hipFree(d->sponge);
+        for (auto &f : d->fixed) {
+            (void)hipFree(f.fpolys);
+            (void)hipFree(f.flde);
+            (void)hipFree(f.lagr);
+            (void)hipFree(f.lagr_lde);
+        }
+    }
+}
+
+static void read_last(const uint8_t *last_row, fe last[28]) {
+    if (last_row)
+        for (int c = 0; c < 28; c++) last[c] = fe_from_bytes(last_row + 16 * c);
+    else
+        random_last_row(last);
+}
 
 int zk_vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public,
                        const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
                        const uint8_t *last_row, size_t *n_out, uint8_t *outputs) {
-    fe outs[NREG];
-    int rc = zk::vm_trace_device(p, prog, public_in, num_public, secret, num_secret, lwe_size, delta, last_row, n_out,
-                                 outs);
-    if (rc) return rc;
+    if (!p || !prog || !n_out || (num_secret && !secret) || (num_public && !public_in))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    fe outs[NREG], last[28];
+    read_last(last_row, last);
+    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
+    ZK_TRY(vm_generate(p, prog, in, last, GenMode{true, NREG}, n_out, outs, nullptr));
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     if (outputs)
         for (int i = 0; i < NREG; i++) fe_to_bytes(outs[i], outputs + 16 * i);
@@ -341,13 +462,27 @@ int zk_vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in,
 int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
                 size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, const zk_options *opt,
                 uint8_t *proof_out, size_t *proof_len, uint8_t *outputs, uint8_t *program_hash) {
-    if (!p || !prog || !opt || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (!p || !prog || !opt || !proof_len || (num_secret && !secret) || (num_public && !public_in))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     ZK_REQUIRE_FULL_PROVER(p);
-    // Processor::run + output + trace (vm/src/lib.rs:14-18), on the device
-    fe outs[NREG];
+    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
+    fe outs[NREG], last[28];
+    read_last(last_row, last);
+    // ZK_VM_PREPROCESS=0: every column from the device trace (no per-program preprocessed columns)
+    const char *pe = getenv("ZK_VM_PREPROCESS");
+    const bool pre = !(pe && !strcmp(pe, "0")) && opt->blowup <= p->max_b && opt->blowup >= 8;
     size_t n = 0;
-    ZK_TRY(zk::vm_trace_device(p, prog, public_in, num_public, secret, num_secret, lwe_size, delta, last_row, &n,
-                               outs));
+    zk_program::Fixed f{};
+    uint32_t md = 0;
+    if (pre) {
+        // Processor::run + trace (vm/src/lib.rs:14-18): the program-only columns come from the program's preprocessed
+        // coefficients / LDE; only the stack registers the program ever uses are generated
+        ZK_TRY(fixed_columns(p, prog, in, opt->blowup, &f));
+        ZK_TRY(vm_generate(p, prog, in, last, GenMode{false, f.md}, &n, outs, &md));
+        if ((int)md != f.md) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the stack depth depends on the inputs");
+    } else {
+        ZK_TRY(vm_generate(p, prog, in, last, GenMode{true, NREG}, &n, outs, nullptr));
+    }
     // ExecutionProver::new(options, hash, output, server_key) + prove(trace) (:20-26) on the trace in HBM
     zk_pub_inputs pub;
     memset(&pub, 0, sizeof pub);
@@ -358,7 +493,15 @@ int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t
     pub.delta = delta;
     if (outputs) memcpy(outputs, pub.stack_outputs, sizeof pub.stack_outputs);
     if (program_hash) memcpy(program_hash, pub.program_hash, sizeof pub.program_hash);
-    return zk_prove_device(p, p->d_trace, n, opt, &pub, proof_out, proof_len, nullptr, nullptr);
+    if (!pre) return zk_prove_device(p, p->d_trace, n, opt, &pub, proof_out, proof_len, nullptr, nullptr);
+    FixedCols fx;
+    fx.md = f.md;
+    fx.fpolys = f.fpolys;
+    fx.flde = f.flde;
+    fx.lagr = f.lagr;
+    fx.lagr_lde = f.lagr_lde;
+    memcpy(fx.last, last, sizeof fx.last);
+    return prove_fixed(p, n, opt, &pub, &fx, proof_out, proof_len);
 }
 
 // diagnostics: the host stack pass's states every `stride` rows (CPU tests check them against host-written traces)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -54,9 +55,10 @@ struct VmState {
 // states[c] = the state shown at row c * stride - 1 (c = 0: the zero state; rows past the program show the final
 // state) for c < nstates, and the 16 outputs -- or, on any error, the reference's status and message (vm_err), as
 // zk_program_trace reports them.  The stack lives bottom first in a 16-slot array, so an op touches only the slots
-// it reads or writes (PUSH one store, SMUL L multiplies) instead of shifting all sixteen.
+// it reads or writes (PUSH one store, SMUL L multiplies) instead of shifting all sixteen.  max_depth (optional): the
+// largest stack depth of the run -- a function of the code and L alone, like the whole depth column.
 int stack_pass(const CompiledProgram &P, const Inputs &in, size_t stride, size_t nstates, VmState *states,
-               fe *outputs);
+               fe *outputs, uint32_t *max_depth = nullptr);
 
 }  // namespace vm
 }  // namespace zk
@@ -65,12 +67,20 @@ int stack_pass(const CompiledProgram &P, const Inputs &in, size_t stride, size_t
 // (vm_gpu.hip: the code and the sponge columns, uploaded once per device and kept until zk_program_free).
 struct zk_program {
     zk::vm::CompiledProgram P;
+    // zk_vm_prove's preprocessed columns of this program for one (lwe_size, blowup) on one device (prover.hip
+    // FixedCols): the program-only columns' coefficients and LDE, and the last row's Lagrange polynomial
+    struct Fixed {
+        uint32_t L, B;
+        int md;  // maximum stack depth
+        fe *fpolys, *flde, *lagr, *lagr_lde;
+    };
     struct Device {
         int device;
         zk::vm::Op *code;  // len ops
         fe *sponge;        // 4 lanes x (len + 1)
+        std::vector<Fixed> fixed;
     };
     std::mutex mu;
-    std::vector<Device> dev;
+    std::vector<std::unique_ptr<Device>> dev;  // stable addresses: a Device is used without the lock held
     ~zk_program();
 };

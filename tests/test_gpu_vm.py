@@ -96,9 +96,12 @@ def test_device_trace_random_programs(gpu):
     assert ok >= 15
 
 
-def test_vm_prove_equals_host_trace_proof(gpu):
+@pytest.mark.parametrize("preprocess", ["1", "0"])
+def test_vm_prove_equals_host_trace_proof(gpu, preprocess, monkeypatch):
     """zk_vm_prove (vm::prove with the trace written on the GPU) gives the proof of the host VM's trace, and the
-    program hash / outputs of the reference's (hash, output, proof)."""
+    program hash / outputs of the reference's (hash, output, proof) -- with the program's preprocessed columns
+    (default) and with every column generated and interpolated per proof (ZK_VM_PREPROCESS=0)."""
+    monkeypatch.setenv("ZK_VM_PREPROCESS", preprocess)
     src = cipher_mix_program(200)[0]
     w = make_workload(src, seed=9)
     prog = Program(src)
@@ -144,3 +147,25 @@ def test_device_trace_full_size_pins(log_n, oracle):
         g.close()
         prog.close()
     assert len(proof) == c["proof_len"] and hashlib.sha256(proof).hexdigest() == c["proof_sha256"]
+
+
+def test_vm_prove_preprocessed_columns_across_provers_and_inputs(gpu):
+    """The preprocessed columns are built once per (program, device, lwe_size, blowup) by whichever prover comes first
+    and reused: a second prover, other inputs and a blowup-16 proof all give the host-trace proofs."""
+    src = ops_for_trace_len(14, "cipher")
+    prog = Program(src)
+    g2 = GpuProver(0, max_trace_len=1 << 14, max_blowup=16)
+    try:
+        for seed, g, opts in [(1, gpu, ProofOptions()), (2, g2, ProofOptions()), (3, gpu, ProofOptions()),
+                              (4, g2, ProofOptions(28, 16, 0, 1, 4, 63))]:
+            w = make_workload(src, seed=seed)
+            trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+            pub = make_pub_inputs(prog.hash, outs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+            ref, _, _, rc = g.prove(trace, pub, opts)
+            assert rc == 0
+            _, _, proof = prog.prove_device(g, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row,
+                                            opts)
+            assert proof == ref, (seed, opts)
+    finally:
+        g2.close()
+        prog.close()
