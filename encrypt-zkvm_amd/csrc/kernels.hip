@@ -902,6 +902,41 @@ void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int 
             hipLaunchKernelGGL(k_hash_rows, dim3(cdiv(M, 256)), dim3(256), 0, st, base, ncols, log_n, log_b, r0, log_rc, leaves));
 }
 
+// One BLAKE3 block of every row: columns 4 blk .. 4 blk + 3 (64 bytes) compressed into the row's chaining value,
+// kept in its leaf slot between blocks (IV before block 0; after the last block the slot holds the digest).  The
+// trace rows (28 elements = 7 full blocks) are hashed this way block by block as their columns' LDEs complete, so
+// a host-resident proof hashes its rows under the rest of the upload instead of after it.
+__global__ void __launch_bounds__(256) k_hash_rows_block(const fe *base, int log_n, int log_b, int blk, int nblk,
+                                                         uint8_t *cv_leaves) {
+    const size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= N) return;
+    const size_t r = t & (B - 1), q = t >> log_b;
+    const fe *p = base + r * n + q + (size_t)(4 * blk) * B * n;
+    uint32_t h[8], m[16];
+    uint8_t *slot = cv_leaves + 32 * ((q << log_b) + r);
+    if (blk == 0) b3::iv(h);
+    else load_digest(slot, h);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const fe v = p[(size_t)e * B * n];
+        m[4 * e + 0] = (uint32_t)v.lo;
+        m[4 * e + 1] = (uint32_t)(v.lo >> 32);
+        m[4 * e + 2] = (uint32_t)v.hi;
+        m[4 * e + 3] = (uint32_t)(v.hi >> 32);
+    }
+    const uint32_t flags = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == nblk - 1 ? (b3::CHUNK_END | b3::ROOT) : 0u);
+    b3::compress(h, m, 0, 0, 64, flags);
+    store_digest(slot, h);
+}
+
+void hash_rows_block(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int blk, uint8_t *leaves) {
+    const size_t N = (size_t)1 << (log_n + log_b);
+    ZK_PROF(st, "hash_rows", (64.0 + (blk ? 64.0 : 32.0)) * N,
+            hipLaunchKernelGGL(k_hash_rows_block, dim3(cdiv(N, 256)), dim3(256), 0, st, base, log_n, log_b, blk,
+                               ncols / 4, leaves));
+}
+
 // Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).
 void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
                              uint8_t *nodes) {

@@ -1042,14 +1042,23 @@ struct TraceSrc {
     const FixedCols *fixed = nullptr;  // with dev: only the dynamic columns are in dev (zk_vm_prove)
 };
 
-// Column groups of a host-resident trace upload: 7 groups of 4 columns.  The copy engine streams group g + 1 while
-// the CUs interpolate and extend group g; more groups overlap more of the copy but add a launch drain per NTT pass
-// and group.  A/B on one box (3 provers in flight): 1 group 12.73-13.02 ms per proof at 22.7 ms latency, 2 groups
-// 13.15-13.24 / 18.7, 4 groups 13.16-13.32 / 16.8, 7 groups 13.02-13.04 / 15.9 (device-resident 12.15-12.32).
-#ifndef ZK_UPLOAD_GROUPS
-#define ZK_UPLOAD_GROUPS 7
-#endif
-static_assert(W % ZK_UPLOAD_GROUPS == 0 && ZK_UPLOAD_GROUPS <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
+// Column groups of a host-resident trace upload.  The copy engine streams group g + 1 while the CUs interpolate and
+// extend group g; more groups overlap more of the copy but add a launch drain per NTT pass and group.  A/B on one box
+// (3 provers in flight): 1 group 12.73-13.02 ms per proof at 22.7 ms latency, 2 groups 13.15-13.24 / 18.7, 4 groups
+// 13.16-13.32 / 16.8, 7 groups of 4 13.02-13.04 / 15.9 (device-resident 12.15-12.32).
+// Round 4 (ZK_UPLOAD_PLAN=incr, the default): the rows are hashed block by block as their columns' LDEs complete
+// (hash_rows_block: a 28-element row is 7 BLAKE3 blocks of 4 columns), and the last 4 columns go up as two groups of
+// 2, so after the last copy only 2 columns' NTTs, one compression per row and the Merkle tree remain.
+// ZK_UPLOAD_PLAN=legacy: 7 groups of 4, all rows hashed after the last group.
+static const int kPlanLegacy[] = {4, 4, 4, 4, 4, 4, 4};
+static const int kPlanIncr[] = {4, 4, 4, 4, 4, 4, 2, 2};
+static bool upload_plan_incr() {
+    static const bool incr = [] {
+        const char *e = getenv("ZK_UPLOAD_PLAN");
+        return !(e && !strcmp(e, "legacy"));
+    }();
+    return incr;
+}
 
 // hipMemcpyAsync from page-locked memory (zk_host_alloc, zk_host_register, any hipHostMalloc'd or
 // hipHostRegister'ed buffer) is a DMA in stream order; from pageable memory the runtime stages the copy
@@ -1070,7 +1079,7 @@ static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c
 
 // S2: interpolate the 28 trace columns (winter-math interpolate_poly over <w_n>), extend them over the B
 // cosets of the LDE domain (coset r: the coefficients scaled by (3 w_N^r)^k) and commit to the rows.
-// A host-resident trace goes up on the copy stream in ZK_UPLOAD_GROUPS column groups; each group's
+// A host-resident trace goes up on the upload stream in the column groups of the upload plan; each group's
 // event gates that group's interpolation and coset LDE on the compute stream.
 static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
     const fe inv_n = h_inv(fe_make(n));
@@ -1103,19 +1112,27 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // Group by group: its copies, then its kernels.  From page-locked memory every call returns at once (the
     // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
     // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
-    constexpr int per = W / ZK_UPLOAD_GROUPS;
-    for (int g = 0; g < ZK_UPLOAD_GROUPS; g++) {
+    const bool incr = upload_plan_incr();
+    const int *plan = incr ? kPlanIncr : kPlanLegacy;
+    const int ngroups = incr ? (int)(sizeof kPlanIncr / sizeof(int)) : (int)(sizeof kPlanLegacy / sizeof(int));
+    static_assert(sizeof kPlanIncr / sizeof(int) <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
+    int c0 = 0, hashed = 0;
+    for (int g = 0; g < ngroups; g++) {
+        const int nc = plan[g];
         {
             std::lock_guard<std::mutex> lk(*p->up_mu);
-            ZK_TRY(upload_trace_group(p, src, n, g * per, per));
+            ZK_TRY(upload_trace_group(p, src, n, c0, nc));
             ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
         }
-        const size_t c0 = (size_t)g * per;
         ZK_TRY(upload_gate(p, p->ev_up[g]));
-        ntt(p->st, pl->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, per, true, nullptr, &inv_n, p->tmp);
-        ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, per, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n, p->tmp);
+        ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
+                p->tmp);
+        c0 += nc;
+        if (incr)
+            for (; 4 * (hashed + 1) <= c0; hashed++) hash_rows_block(p->st, p->lde, W, log_n, log_b, hashed, p->leaves);
     }
-    hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
+    if (!incr) hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);
     return d2h_small(p, root, p->nodes + 32, 32);
 }

@@ -7,8 +7,8 @@
 set -o pipefail
 O=gpurun_out
 mkdir -p $O
-run() {  # name queues stream gate inflight
-  GPU_MAX_HW_QUEUES=$2 ZK_UPLOAD_STREAM=$3 ZK_UPLOAD_GATE=$4 timeout -k 10 400 python3 bench.py --no-cpu-baseline \
+run() {  # name queues stream gate inflight [upload plan]
+  GPU_MAX_HW_QUEUES=$2 ZK_UPLOAD_STREAM=$3 ZK_UPLOAD_GATE=$4 ZK_UPLOAD_PLAN=${6:-incr} timeout -k 10 400 python3 bench.py --no-cpu-baseline \
     --no-verify --inflight $5 ${BENCH_ARGS:-} > $O/abq_$1.json 2> $O/abq_$1.err || { echo "$1 FAILED"; tail -5 $O/abq_$1.err; exit 1; }
   python3 - "$1" "$O/abq_$1.json" <<'PY'
 import json, sys
@@ -19,6 +19,8 @@ print(f"{sys.argv[1]:>14} {b['ms_per_step']:7.3f} steady {b.get('steady_state_ms
 PY
 }
 for rep in 1 2; do
+  run q16_own_dev_p4_legacy 16 own device 4 legacy
+  run q4_own_dev_p4_legacy 4 own device 4 legacy
   run q4_own_dev_p4 4 own device 4
   run q4_sh_dev_p4 4 shared device 4
   run q4_sh_host_p4 4 shared host 4
