@@ -440,6 +440,16 @@ struct NttArgs {
     const fe_ws *cos_stage_ws;  // ... their W sets
     const fe_w2 *cos_stage_w2;  // ... and two-part forms
     const fe *cos_pass;   // ... and per-coset pass-1 twiddles (s_r w_n^j2)^k1, n apart (CosetTables::pass)
+    // Sparse columns (SparseCols): a column whose entries are zero but the last one transforms to last * fill
+    // (fill: the transform of the unit vector e_(n-1); coset r's at fill + r * fill_stride).  Pass 1 skips its
+    // blocks, pass 2 writes the product; nz[sp_col0 + column] == 0 marks such a column (four-step only)
+    const unsigned *nz;
+    const fe *sp_last, *sp_fill;
+    size_t sp_fill_stride;
+    int sp_col0;
+    __device__ __forceinline__ bool sparse(uint32_t b) const {
+        return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
+    }
     // (32-bit: batch entries and grid sizes are < 2^32; 64-bit division is a long VALU sequence)
     __device__ __forceinline__ int coset_of(uint32_t b) const { return cos_r0 + (int)(b % (uint32_t)ncos) * cos_rstride; }
     __device__ __forceinline__ fe *out_of(uint32_t b) const {
@@ -513,6 +523,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         k1_0 = (size_t)(lin32 / (uint32_t)batch) * LPB;
         b = lin32 % (uint32_t)batch;
     }
+    if (a.sparse(b)) return;  // pass 2 writes its output
     const fe *in = a.in + (size_t)(b / (uint32_t)a.ncos) * a.in_stride;
     const int r = a.coset_of(b);
     fe *out = a.out + b * a.out_stride;
@@ -577,6 +588,18 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     const size_t n2 = n >> LOGM;
     const size_t j2_0 = xcd_block(blockIdx.x, gridDim.x) * LPB;
     const size_t b = blockIdx.y;
+    if (a.sparse((uint32_t)b)) {
+        // last * (the transform of e_(n-1)) over this block's outputs
+        const int col = a.sp_col0 + (int)(b / (uint32_t)a.ncos);
+        const fe last = a.sp_last[col];
+        const fe *fill = a.sp_fill + (size_t)a.coset_of((uint32_t)b) * a.sp_fill_stride;
+        fe *out = a.out_of((uint32_t)b);
+        for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+            const size_t o = n2 * (size_t)(e / LPB) + j2_0 + (size_t)(e % LPB);
+            out[o] = fe_mul(last, fill[o]);
+        }
+        return;
+    }
     const fe *in = a.in + b * a.in_stride;
     if constexpr (Fuse<LOGM, TILE>::OK) {
         fe *out = a.out_of(b);
@@ -696,8 +719,9 @@ int ntt_log_n2(int L) {
 }
 
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride, int batch,
-         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp) {
+         bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, const SparseCols *sp) {
     NttArgs a;
+    memset(&a, 0, sizeof a);
     a.in = in;
     a.out = out;
     a.in_stride = in_stride;
@@ -726,6 +750,13 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.cos_stage = a.cos_pass = nullptr;
     a.cos_stage_ws = nullptr;
     a.cos_stage_w2 = nullptr;
+    if (sp && T.log_n > 12 && inverse && post_scale && fe_eq(*post_scale, T.inv_n)) {  // interpolation
+        a.nz = sp->nz;
+        a.sp_last = sp->last;
+        a.sp_fill = sp->lagr;
+        a.sp_fill_stride = 0;
+        a.sp_col0 = sp->col0;
+    }
     ntt_run(st, a, batch, tmp);
 }
 
@@ -755,7 +786,8 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
 }
 
 void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
-             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp) {
+             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp,
+             const SparseCols *sp) {
     NttArgs a;
     memset(&a, 0, sizeof a);
     a.in = in;
@@ -782,6 +814,13 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
         a.cos_stage_ws = CT.stage_ws;
         a.cos_stage_w2 = CT.stage_w2;
         a.cos_pass = CT.pass;
+        if (sp) {
+            a.nz = sp->nz;
+            a.sp_last = sp->last;
+            a.sp_fill = sp->lagr_lde;
+            a.sp_fill_stride = n;
+            a.sp_col0 = sp->col0;
+        }
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so
     // one launch drain per pass instead of one per coset
@@ -935,6 +974,28 @@ void hash_rows_block(hipStream_t st, const fe *base, int ncols, int log_n, int l
     ZK_PROF(st, "hash_rows", (64.0 + (blk ? 64.0 : 32.0)) * N,
             hipLaunchKernelGGL(k_hash_rows_block, dim3(cdiv(N, 256)), dim3(256), 0, st, base, log_n, log_b, blk,
                                ncols / 4, leaves));
+}
+
+// Sparse-column detection: nz[c0 + c] |= 1 when column c has a nonzero entry before its last one; last[c0 + c] = its
+// last entry.  One pass over the columns (16 B per element read); nz must be zeroed first.
+__global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last) {
+    const int c = blockIdx.y;
+    const fe *col = trace + (size_t)(c0 + c) * n;
+    uint64_t any = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n - 1; i += (size_t)gridDim.x * blockDim.x) {
+        const fe v = col[i];
+        any |= v.lo | v.hi;
+    }
+    const unsigned long long wave_any = __ballot(any != 0);
+    if (wave_any && (threadIdx.x & 63) == 0) atomicOr(nz + c0 + c, 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0) last[c0 + c] = col[n - 1];
+}
+
+void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp) {
+    const unsigned bx = (unsigned)std::min<size_t>(cdiv(n, 256 * 16), 256);
+    ZK_PROF(st, "sparse_detect", 16.0 * n * nc,
+            hipLaunchKernelGGL(k_sparse_detect, dim3(bx, nc), dim3(256), 0, st, trace, n, c0, const_cast<unsigned *>(sp.nz),
+                               const_cast<fe *>(sp.last)));
 }
 
 // Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).
@@ -1287,6 +1348,9 @@ struct EvalShared {
 #ifndef ZK_EVAL_WAVES
 #define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
 #endif
+#ifndef ZK_EVAL_STASH
+#define ZK_EVAL_STASH 1  // columns read in two sections (the 5 opcode bits, sponge 7 and 8, next-row s0) go through a
+#endif                   // lane-private LDS slot instead of a second global load (the re-read missed L2: 1.21x traffic)
 #ifndef ZK_EVAL_WAVES_EXT
 #define ZK_EVAL_WAVES_EXT 4  // the two-plane (quadratic extension) variant (4: 128 VGPRs, 9 spills; 3: 142, 0)
 #endif
@@ -1300,6 +1364,10 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
                                                           const fe *divs, const AirConsts *K, const AirConsts *K2,
                                                           size_t plane, fe *comp) {
     __shared__ EvalShared S;
+    // lane-private stash of the columns two sections read (ZK_EVAL_STASH): 8 x 256 x 16 B = 32 KiB per block, so four
+    // 256-thread blocks (16 waves, the register budget's 4 per SIMD) still fit a CU's 160 KiB
+    __shared__ fe stash[ZK_EVAL_STASH ? 8 : 1][256];
+    const int tid = threadIdx.x;
     {
         // one LDS slot per thread, every range bounded on both sides
         const int t = threadIdx.x;
@@ -1337,6 +1405,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
 #define NXT(c) cb[(size_t)(c)*cs + qn]
     const fe one = fe_one();
     const fe s0n = NXT(12);
+    if (ZK_EVAL_STASH) stash[5][tid] = s0n;
     fe t = fe_zero();  // sum of coeff_t[k] * C_k (kept reduced: a lazy 288-bit sum here costs 130 spills)
     fe t2 = fe_zero();  // the b-plane sum (KE = 2)
 #define ZK_ACC(k, val)                                                    \
@@ -1352,6 +1421,13 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     // is_push from the flags, so the ten selectors below are never live across it.
     {
         const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
+        if (ZK_EVAL_STASH) {
+            stash[0][tid] = b0;
+            stash[1][tid] = b1;
+            stash[2][tid] = b2;
+            stash[3][tid] = b3;
+            stash[4][tid] = b4;
+        }
         // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4  (Horner by doubling: bits are field elements)
         fe opc = b0;
         opc = fe_add(fe_add(opc, opc), b1);
@@ -1365,7 +1441,11 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         const fe *per = periodic + (i & 127) * 9;
         fe x[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = cube(CUR(7 + k));
+        for (int k = 0; k < 4; k++) {
+            const fe c = CUR(7 + k);
+            if (ZK_EVAL_STASH && k < 2) stash[6 + k][tid] = c;
+            x[k] = cube(c);
+        }
         fe m0[4];
 #pragma unroll
         for (int r2 = 0; r2 < 4; r2++) m0[r2] = fe_add(mds_row(r2, x), per[1 + r2]);
@@ -1401,7 +1481,8 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         if (KE == 2) t2 = fe_add(t2, fe_mul(sR2, fh));
         ZK_SEQ(cb, t.lo);
         {
-            const fe d16 = fe_sub(NXT(7), CUR(7)), d17 = fe_sub(NXT(8), CUR(8)), n9 = NXT(9), n10 = NXT(10);
+            const fe c7 = ZK_EVAL_STASH ? stash[6][tid] : CUR(7), c8 = ZK_EVAL_STASH ? stash[7][tid] : CUR(8);
+            const fe d16 = fe_sub(NXT(7), c7), d17 = fe_sub(NXT(8), c8), n9 = NXT(9), n10 = NXT(10);
             acc288 aC = acc288_zero();
             acc288_madd(aC, S.ct[16], d16);
             acc288_madd(aC, S.ct[17], d17);
@@ -1435,9 +1516,12 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         else ZK_ACC(k, val);                             \
     } while (0)
 #define ZK_SEQS() ZK_SEQ(cb, LZ ? aS.w[0] : (uint32_t)t.lo)
-        const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
+        const fe b0 = ZK_EVAL_STASH ? stash[0][tid] : CUR(5), b1 = ZK_EVAL_STASH ? stash[1][tid] : CUR(4),
+                 b2 = ZK_EVAL_STASH ? stash[2][tid] : CUR(3), b3 = ZK_EVAL_STASH ? stash[3][tid] : CUR(2),
+                 b4 = ZK_EVAL_STASH ? stash[4][tid] : CUR(1);
         const fe nb0 = fe_sub(one, b0), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3), nb4 = fe_sub(one, b4);
         const fe s0 = CUR(12), s1 = CUR(13);
+        const fe s0n = ZK_EVAL_STASH ? stash[5][tid] : NXT(12);  // (shadows the first section's: no live range across)
         // 0 clock, 2 shift
         ZK_ACCS(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
         const fe b01 = fe_mul(b0, b1);

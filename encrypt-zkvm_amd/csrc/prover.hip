@@ -222,6 +222,24 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     ZK_CHECK_HIP(upload(p, &pl->xr_ce, xrce));
     ZK_CHECK_HIP(make_pow_table(p, h_inv(fe_make(3)), n, &pl->inv3));
     ZK_CHECK_HIP(upload(p, &pl->periodic, periodic_table(n)));
+    if (pl->log_n > 12) {
+        // e_(n-1)'s interpolant and coset LDE (the sparse trace columns': SparseCols)
+        ZK_CHECK_HIP(p->arena.alloc(&pl->lagr, n));
+        ZK_CHECK_HIP(p->arena.alloc(&pl->lagr_lde, (size_t)B * n));
+        std::vector<fe> e(n, fe_zero());
+        e[n - 1] = fe_one();
+        fe *de = nullptr;
+        ZK_CHECK_HIP(hipMalloc(&de, n * sizeof(fe)));
+        hipError_t err = hipMemcpy(de, e.data(), n * sizeof(fe), hipMemcpyHostToDevice);
+        if (err == hipSuccess) {
+            const fe inv_n = h_inv(fe_make(n));
+            ntt(p->st, pl->Tn, de, n, pl->lagr, n, 1, true, nullptr, &inv_n, p->tmp);
+            ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, 0, 1, (int)B, pl->lagr_lde, (size_t)B * n, n, p->tmp);
+            err = hipStreamSynchronize(p->st);
+        }
+        (void)hipFree(de);
+        ZK_CHECK_HIP(err);
+    }
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     *out = pl.get();
     p->plans[key] = std::move(pl);
@@ -1081,8 +1099,31 @@ static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c
 // cosets of the LDE domain (coset r: the coefficients scaled by (3 w_N^r)^k) and commit to the rows.
 // A host-resident trace goes up on the upload stream in the column groups of the upload plan; each group's
 // event gates that group's interpolation and coset LDE on the compute stream.
+// Sparse trace columns (SparseCols): a column that is zero in every row but the last (the VM's stack registers past
+// the program's maximum depth, five of the benchmark's 28) interpolates to last * lagr and extends to last * lagr_lde;
+// sparse_detect flags them on the device and the NTT passes skip their DFTs.  Exact: the same polynomials and LDE.
+// ZK_SPARSE=0 transforms every column.
+static bool sparse_on() {
+    static const bool on = [] {
+        const char *e = getenv("ZK_SPARSE");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
 static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
     const fe inv_n = h_inv(fe_make(n));
+    SparseCols spc{};
+    const SparseCols *sp = nullptr;
+    if (sparse_on() && pl->lagr && !src.fixed) {
+        if (!p->sp_nz) {
+            ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, W));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
+        }
+        ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, W * sizeof(unsigned), p->st));
+        spc = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
+        sp = &spc;
+    }
     if (src.dev && src.fixed) {
         // zk_vm_prove: interpolate and extend the dynamic stack columns only; the preprocessed ones by one pass
         const FixedCols &fx = *src.fixed;
@@ -1102,8 +1143,13 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         return d2h_small(p, root, p->nodes + 32, 32);
     }
     if (src.dev) {
-        ntt(p->st, pl->Tn, src.dev, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-        return lde_commit(p, pl, p->polys, W, p->lde, p->leaves, p->nodes, root);
+        if (sp) sparse_detect(p->st, src.dev, n, 0, W, *sp);
+        ntt(p->st, pl->Tn, src.dev, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp, sp);
+        const size_t B = (size_t)1 << pl->log_b;
+        ntt_lde(p->st, pl->Tn, pl->ct, p->polys, n, W, 0, 1, (int)B, p->lde, B * n, n, p->tmp, sp);
+        hash_rows_cosets(p->st, p->lde, W, pl->log_n, pl->log_b, 0, pl->log_b, p->leaves);
+        merkle_tree(p->st, p->leaves, n * B, p->nodes);
+        return d2h_small(p, root, p->nodes + 32, 32);
     }
     const int log_n = pl->log_n, log_b = pl->log_b;
     const size_t B = (size_t)1 << log_b;
@@ -1125,9 +1171,13 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
         }
         ZK_TRY(upload_gate(p, p->ev_up[g]));
-        ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp);
+        SparseCols gsp = spc;
+        gsp.col0 = c0;
+        if (sp) sparse_detect(p->st, p->d_trace, n, c0, nc, spc);
+        ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp,
+            sp ? &gsp : nullptr);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
-                p->tmp);
+                p->tmp, sp ? &gsp : nullptr);
         c0 += nc;
         if (incr)
             for (; 4 * (hashed + 1) <= c0; hashed++) hash_rows_block(p->st, p->lde, W, log_n, log_b, hashed, p->leaves);

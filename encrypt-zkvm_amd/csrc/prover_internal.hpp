@@ -90,6 +90,9 @@ struct Plan {  // everything that depends only on (n, B)
     // 1 / ((x - 1)(x - g^(n-2))) over the CE domain (coset-major): the two boundary divisors
     // depend only on n, so they are inverted once per plan (first proof) and reused
     fe *bnd_inv = nullptr;
+    // four-step plans: the interpolant of e_(n-1) (n coefficients) and its coset LDE (B n, coset-major) -- what a
+    // trace column that is zero but in its random last row interpolates and extends to, times that row (SparseCols)
+    fe *lagr = nullptr, *lagr_lde = nullptr;
 };
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
 // the evaluator's divisor tables for the 8 CE cosets (divisor_tables: 3 planes of 8n), built once per plan
@@ -160,6 +163,8 @@ struct zk_prover {
     uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
     fe *fri_alphas = nullptr;     // the alphas the device coin drew (2 per layer)
     fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
+    unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries
+    fe *sp_last = nullptr;        // ... and the trace's last row
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets

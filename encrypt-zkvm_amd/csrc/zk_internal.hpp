@@ -104,13 +104,25 @@ struct PowTable {
 // out[t] = lo[t & 2047] * hi[t >> 11] for t < n
 void pow_expand(hipStream_t st, const fe *lo, const fe *hi, size_t n, fe *out);
 
+// Sparse columns of a trace batch: column c (flags at nz[col0 + c]) is zero in every row but the last when
+// nz[col0 + c] == 0 (sparse_detect); then its interpolation is last[col0 + c] * lagr (the interpolant of e_(n-1))
+// and its coset LDE last * lagr_lde (coset r at r n): the NTT passes skip its DFTs.  Four-step sizes only.
+struct SparseCols {
+    const unsigned *nz;
+    const fe *last;
+    const fe *lagr, *lagr_lde;
+    int col0;
+};
+void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
+
 // NTT of `batch` polynomials of size 2^log_n, each at in + b*in_stride -> out + b*out_stride.
 //   inverse     : use w^-1 (no 1/n scale; fold it into post_scale)
 //   pre         : optional s^k pre-scale of input coefficient k (coset evaluation), may be null
 //   post_scale  : optional constant multiplied into every output (e.g. 1/n)
 // in and out must not alias.  tmp must hold batch * n elements when log_n > 12.
+// sp (optional, interpolations with post_scale = 1/n only): sparse columns of the batch (SparseCols)
 void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe *out, size_t out_stride,
-         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp);
+         int batch, bool inverse, const PowTable *pre, const fe *post_scale, fe *tmp, const SparseCols *sp = nullptr);
 
 // Coset-LDE tables of one plan (LDE coset r < B, s_r = 3 w_N^r):
 //   n <= 4096 (single pass): full[r*n + k] = s_r^k (input pre-scale)
@@ -125,7 +137,8 @@ struct CosetTables {
 // the n evaluations over coset r to out + c*out_cstride + j*out_jstride.  tmp: ncols*min(ncos, 8)*n
 // (four-step; launches of up to 8 cosets).
 void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
-             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp);
+             int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp,
+             const SparseCols *sp = nullptr);
 
 // grinding: atomicMin into *best_dev of the nonces in [start, start+count) with >= bits trailing zeros
 void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,

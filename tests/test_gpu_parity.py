@@ -540,3 +540,27 @@ def test_host_trace_memory_outlives_its_owner(gpu, oracle):
     assert rc == 0
     ref, _, _ = oracle.prove(np.array(trace), oracle_pub(oracle, pub))
     assert proof == ref
+
+
+@pytest.mark.parametrize("path", ["host", "device"])
+def test_sparse_column_detection(gpu, oracle, path):
+    """Sparse trace columns (zero in every row but the last: SparseCols) skip their NTTs.  A 2^14 trace with the
+    VM's sparse registers (s11..s15), one of them with a zero last row too, one made dense by a single middle entry,
+    and s10 zeroed but for its last row (sparse) -- edits in columns no constraint or assertion reads, so the trace
+    still satisfies the AIR: the proof equals the oracle's, from the host trace (upload groups) and from HBM."""
+    trace, pub = workload_trace(ops_for_trace_len(14, "cipher"), seed=14)
+    n = trace.shape[1]
+    t = trace.copy()
+    assert not t[23:28, : n - 1].any()  # the cipher mix never reaches stack depth 12
+    t[25, n - 1] = 0                     # sparse with a zero last row
+    t[27, 5] = [7, 0]                    # one entry in the middle: dense
+    t[22, : n - 1] = 0                   # s10, zeroed but for its last row: sparse
+    oproof, orec, _ = oracle.prove(t, oracle_pub(oracle, pub))
+    if path == "host":
+        proof, rec, _, rc = gpu.prove(t, pub, ProofOptions(), record=True)
+    else:
+        d, _ = gpu.upload_trace(t)
+        proof, rec, _, rc = gpu.prove_device(d, n, pub, ProofOptions(), record=True)
+    assert rc == 0
+    assert bytes(rec.trace_root) == bytes(orec.trace_root)
+    assert proof == oproof
