@@ -466,17 +466,22 @@ def main():
         verified = orc.verify(proof, opub, min_sec)[0] == 0
     from zkvm_amd.prover import verify as zk_verify
     zk_verified = zk_verify(proof, pub, min_sec)[0] == 0
+    gpu.close()
+    lifetime = None
+    if not args.no_compare:
+        lifetime = lifetime_leg(local, n, trace, pub, opts, proof)
     # every rank: its proof accepted by zk_verify; rank 0's workload (seed 1000) is a committed oracle pin, so its
     # proof must also equal the pin byte for byte (the other ranks' seeds have no pin)
     pin = pin_check(proof, find_pin(args.log_n, 1000 + rank, opts))
     all_verified = all_ranks_true(pg, zk_verified, local)
-    gpu.close()
     trace = None
     host.close()
 
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
-                     zk_verified, pin, all_verified) if rank == 0 else None
+                     zk_verified, pin, all_verified, lifetime) if rank == 0 else None
+    if out is not None and world == 1 and not args.no_compare and os.environ.get("GPU_MAX_HW_QUEUES") != "4":
+        out["default_queues"] = default_queues_leg(args, P)
 
     # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A
     # watchdog bounds it: should a collective never complete, rank 0 still prints the line (with the error) and
@@ -514,6 +519,53 @@ def main():
 
 
 SHARDED_TIMEOUT_S = 240
+
+
+def lifetime_leg(local, n, trace, pub, opts, proof):
+    """The reference builds its prover inside every vm::prove call (ExecutionProver::new, vm/src/lib.rs:24):
+    cold_call_ms = zk_prover_create + the first proof (per-size tables) + zk_prover_destroy; pooled_call_ms = the same
+    call shape through the process-wide pool (zk_prover_acquire + proof + zk_prover_release) once it holds a prover."""
+    from zkvm_amd.prover import GpuProver
+    from zkvm_amd.native import lib
+    cold = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        g = GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor)
+        p = g.prove_host(trace, pub, opts)[0]
+        g.close()
+        cold.append(1e3 * (time.perf_counter() - t0))
+        assert p == proof
+    pooled = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        g = GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor, pooled=True)
+        p = g.prove_host(trace, pub, opts)[0]
+        g.close()
+        pooled.append(1e3 * (time.perf_counter() - t0))
+        assert p == proof
+    lib().zk_prover_pool_trim(local)
+    return {"cold_call_ms": round(min(cold), 3), "cold_calls_ms": [round(x, 1) for x in cold],
+            "pooled_call_ms": round(sorted(pooled[1:])[1], 3), "pooled_first_call_ms": round(pooled[0], 3),
+            "call_shape": "one proof per call from the host-resident trace; cold: create + prove + destroy; pooled: "
+                          "acquire + prove + release (median of 3 after the pool's first fill)"}
+
+
+def default_queues_leg(args, P):
+    """The headline configuration re-run in a child process with HIP's default 4 hardware queues per process
+    (GPU_MAX_HW_QUEUES=4; this process set 16 before its first HIP call): what a host that does not set it gets."""
+    import subprocess
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="4")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--no-verify", "--no-compare",
+           "--sharded-log-n", "0", "--inflight", str(P), "--steps", str(args.steps), "--log-n", str(args.log_n)]
+    if args.config5:
+        cmd.append("--config5")
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        return {"ms_per_step": line["ms_per_step"], "value": line["value"], "gpu_max_hw_queues": 4,
+                "inflight": P, "proof_matches_pin": line.get("proof_matches_pin")}
+    except Exception as e:  # reported, never fatal for the headline
+        return {"error": repr(e)[:300]}
 
 
 def vm_prove_leg(args, prog, src, w, proof, provers, opts, pg, local, rank):
@@ -562,7 +614,7 @@ def vm_prove_leg(args, prog, src, w, proof, provers, opts, pg, local, rank):
 
 def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops, latency_ms,
                dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified, pin,
-               all_verified):
+               all_verified, lifetime):
     """rank 0's JSON line (the driver's contract) from the measurements of main()."""
     dom = max(kstats.items(), key=lambda kv: kv[1][0])
     name, (tot_ms, launches, tot_bytes) = dom
@@ -613,6 +665,7 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
         "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
         "proof_matches_pin": pin["proof_matches_pin"] if pin else None, "pin": pin["pin"] if pin else None,
         "all_ranks_verified_by_zk_verify": all_verified,
+        "prover_lifetime": lifetime,
     }
     return out
 

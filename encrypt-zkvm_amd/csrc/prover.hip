@@ -432,6 +432,72 @@ void zk_prover_destroy(zk_prover *p) {
     delete p;
 }
 
+// ---------------------------------------------------------------- process-wide prover pool
+// The reference builds its prover per call (ExecutionProver::new in vm::prove, vm/src/lib.rs:24).  A zk_prover is
+// ~12.5 GB of HBM at 2^20 plus per-size tables built by its first proof, so the drop-in keeps released provers for
+// the next acquire on the same device instead (zk_prover_acquire / zk_prover_release).
+namespace {
+struct Pool {
+    std::mutex mu;
+    std::vector<zk_prover *> idle;
+};
+Pool &pool() {
+    static Pool *P = new Pool();  // process lifetime (provers released at exit are reclaimed with the process)
+    return *P;
+}
+}  // namespace
+
+int zk_prover_acquire(int device, size_t max_n, uint32_t max_b, zk_prover **out) {
+    if (!out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    {
+        Pool &P = pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        // the smallest idle full prover of this device that fits
+        size_t best = P.idle.size();
+        for (size_t i = 0; i < P.idle.size(); i++) {
+            const zk_prover *q = P.idle[i];
+            if (q->device != device || q->shard_world || q->max_n < max_n || q->max_b < max_b) continue;
+            if (best == P.idle.size() || q->max_n * q->max_b < P.idle[best]->max_n * P.idle[best]->max_b) best = i;
+        }
+        if (best < P.idle.size()) {
+            *out = P.idle[best];
+            P.idle.erase(P.idle.begin() + (long)best);
+            return ZK_OK;
+        }
+    }
+    return zk_prover_create(device, max_n, max_b, out);
+}
+
+void zk_prover_release(zk_prover *p) {
+    if (!p) return;
+    if (p->shard_world) {  // rank-sized provers are not pooled
+        zk_prover_destroy(p);
+        return;
+    }
+    (void)hipSetDevice(p->device);
+    (void)hipStreamSynchronize(p->st);
+    Pool &P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.idle.push_back(p);
+}
+
+int zk_prover_pool_trim(int device) {
+    std::vector<zk_prover *> drop;
+    {
+        Pool &P = pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        for (size_t i = 0; i < P.idle.size();)
+            if (device < 0 || P.idle[i]->device == device) {
+                drop.push_back(P.idle[i]);
+                P.idle.erase(P.idle.begin() + (long)i);
+            } else {
+                i++;
+            }
+    }
+    for (zk_prover *p : drop) zk_prover_destroy(p);
+    return (int)drop.size();
+}
+
 int zk_prover_trace_buffer(zk_prover *p, void **d_trace) {
     if (!p || !d_trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     *d_trace = p->d_trace;

@@ -28,7 +28,8 @@ MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 3
 
 # every symbol include/zkvm_gpu.h declares (checked by tests/test_native_abi.py)
 EXPORTED = (
-    "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_create_shard", "zk_prover_destroy", "zk_prover_trace_buffer",
+    "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_create_shard", "zk_prover_destroy",
+    "zk_prover_acquire", "zk_prover_release", "zk_prover_pool_trim", "zk_prover_trace_buffer",
     "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_prover_exchange_stats", "zk_vm_trace",
@@ -97,6 +98,10 @@ def lib():
         L.zk_prover_create_shard.argtypes = [i32, sz, i32, C.POINTER(vp)]
         L.zk_prover_destroy.argtypes = [vp]
         L.zk_prover_destroy.restype = None
+        L.zk_prover_acquire.argtypes = [i32, sz, u32, C.POINTER(vp)]
+        L.zk_prover_release.argtypes = [vp]
+        L.zk_prover_release.restype = None
+        L.zk_prover_pool_trim.argtypes = [i32]
         L.zk_prover_trace_buffer.argtypes = [vp, C.POINTER(vp)]
         L.zk_prove.argtypes = [vp, vp, sz, C.POINTER(Options), C.POINTER(PubInputs), vp, C.POINTER(sz)]
         L.zk_prove_columns.argtypes = [vp, C.POINTER(vp), sz, C.POINTER(Options), C.POINTER(PubInputs), vp,

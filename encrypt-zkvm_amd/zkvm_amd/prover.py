@@ -60,16 +60,23 @@ def make_pub_inputs(program_hash, stack_outputs, lwe_size: int, delta: int) -> P
 class GpuProver:
     """One GPU's device memory and stream (zk_prover)."""
 
-    def __init__(self, device: int = 0, max_trace_len: int = 1 << 16, max_blowup: int = 8):
+    def __init__(self, device: int = 0, max_trace_len: int = 1 << 16, max_blowup: int = 8, pooled: bool = False):
+        """pooled: take the prover from the process-wide pool (zk_prover_acquire) and hand it back on close
+        (zk_prover_release) instead of creating and freeing it -- the per-call construction of the reference
+        (ExecutionProver::new in vm::prove) at the cost of a pool lookup."""
         h = C.c_void_p()
-        check(lib().zk_prover_create(device, max_trace_len, max_blowup, C.byref(h)), "zk_prover_create")
+        if pooled:
+            check(lib().zk_prover_acquire(device, max_trace_len, max_blowup, C.byref(h)), "zk_prover_acquire")
+        else:
+            check(lib().zk_prover_create(device, max_trace_len, max_blowup, C.byref(h)), "zk_prover_create")
         self.handle = h
         self.max_trace_len = max_trace_len
         self.device = device
+        self.pooled = pooled
 
     def close(self):
         if self.handle:
-            lib().zk_prover_destroy(self.handle)
+            (lib().zk_prover_release if self.pooled else lib().zk_prover_destroy)(self.handle)
             self.handle = None
 
     def __del__(self):

@@ -124,6 +124,14 @@ int zk_prover_create(int device, size_t max_trace_len, uint32_t max_blowup, zk_p
  * with that world size; every single-GPU entry point refuses it (ZK_ERR_INVALID_ARG). */
 int zk_prover_create_shard(int device, size_t max_trace_len, int world, zk_prover **out);
 void zk_prover_destroy(zk_prover *p);
+/* Process-wide pool for callers that build a prover per proof, as the reference does (ExecutionProver::new inside
+ * vm::prove, vm/src/lib.rs:24): zk_prover_acquire returns an idle pooled full prover of this device with at least
+ * these sizes (the smallest such; its per-size tables are already built), else creates one; zk_prover_release hands
+ * it back instead of freeing its ~12.5 GB (2^20).  Thread-safe.  zk_prover_pool_trim frees the idle provers of one
+ * device (-1: every device) and returns how many. */
+int zk_prover_acquire(int device, size_t max_trace_len, uint32_t max_blowup, zk_prover **out);
+void zk_prover_release(zk_prover *p);
+int zk_prover_pool_trim(int device);
 /* device pointer to a scratch region large enough for a 28 x max_trace_len trace (so callers can
  * stage a device-resident trace without their own allocator) */
 int zk_prover_trace_buffer(zk_prover *p, void **d_trace);
