@@ -292,8 +292,9 @@ struct GenMode {
 // The trace of `prog` on `in` into p->d_trace (28 x n column-major; the columns `mode` selects), stream-ordered on
 // p->st: the host stack pass (errors, outputs, the state every S rows, the maximum depth), one upload of the states,
 // inputs and last row, then the kernels.  Nothing waits for them.
+// dp_known: the program's device copy when the caller holds prog->mu (fixed_columns), else null (looked up here)
 int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const fe last[28], GenMode mode,
-                size_t *n_out, fe *outputs, uint32_t *max_depth) {
+                size_t *n_out, fe *outputs, uint32_t *max_depth, const DevProg *dp_known = nullptr) {
     const auto &P = prog->P;
     const size_t n = P.trace_len, len = P.code.size();
     *n_out = n;
@@ -329,7 +330,8 @@ int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const 
     memcpy(h + b_states + b_sec, last, b_last);
     if (in.npub) memcpy(h + b_states + b_sec + b_last, in.pub, in.npub);
     DevProg dp;
-    ZK_TRY(device_program(prog, p->device, &dp));
+    if (dp_known) dp = *dp_known;
+    else ZK_TRY(device_program(prog, p->device, &dp));
     // device staging: the LDE buffer (written by the proof's LDE before anything reads it) holds the upload, the
     // NTT scratch the device states; both are free between proofs
     uint8_t *dv = reinterpret_cast<uint8_t *>(p->lde);
@@ -387,7 +389,8 @@ int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint
     memset(zero, 0, sizeof zero);
     uint32_t md = 0;
     size_t nn = 0;
-    ZK_TRY(vm_generate(p, prog, in, zero, GenMode{true, NREG}, &nn, outs, &md));
+    const DevProg dp{d->code, d->sponge};  // prog->mu is held: no second lookup through device_program
+    ZK_TRY(vm_generate(p, prog, in, zero, GenMode{true, NREG}, &nn, outs, &md, &dp));
     const fe inv_n = h_inv(fe_make(n));
     ntt(p->st, pl->Tn, p->d_trace, n, g.fpolys, n, 12, true, nullptr, &inv_n, p->tmp);
     ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, 0, 1, (int)B, g.flde, B * n, n, p->tmp);
