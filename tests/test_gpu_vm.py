@@ -119,12 +119,27 @@ def test_vm_prove_equals_host_trace_proof(gpu, preprocess, monkeypatch):
 
 
 def test_vm_prove_reports_vm_errors(gpu):
-    prog = Program("read2\nadd\n")
-    w = make_workload("read2\nadd\n", seed=3)
-    with pytest.raises(ZkError) as e:
-        prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
-    assert e.value.code == native.ZK_ERR_STACK and "stack error at 2: add operation stack underflow" in str(e.value)
-    prog.close()
+    for src, msg in [("push.1\nadd\n", "add operation stack underflow"), ("read2\nread2\nread2\nread2\n",
+                                                                          "read2 operation stack overflow"),
+                     ("read\nread\n", "no more inputs to read")]:
+        prog = Program(src)
+        w = make_workload(src, seed=3, n_pub=1)
+        host_err = None
+        try:
+            prog.trace(w.public, w.secret, w.server_key, w.last_row)
+        except ZkError as e:
+            host_err = (e.code, str(e).split("] ", 1)[1])
+        assert host_err is not None and msg in host_err[1], (src, host_err)
+        for pre in ("1", "0"):
+            import os
+            os.environ["ZK_VM_PREPROCESS"] = pre
+            try:
+                with pytest.raises(ZkError) as e:
+                    prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
+            finally:
+                os.environ.pop("ZK_VM_PREPROCESS", None)
+            assert e.value.code == host_err[0] and str(e.value).endswith(host_err[1]), (src, pre, str(e.value))
+        prog.close()
 
 
 @pytest.mark.parametrize("log_n", sorted({c["log_n"] for c in LARGE_CASES if c["options"]["field_extension"] == 1
