@@ -347,6 +347,8 @@ def main():
                     help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the device-resident / pageable / latency comparison legs (profiler passes)")
+    ap.add_argument("--ab", action="store_true",
+                    help="A/B runs: of the comparison legs keep only steady_state, device-resident and latency")
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
@@ -427,12 +429,13 @@ def main():
         run_proofs(dfns, P)
         dev_s = run_proofs_timed(dfns, cmp_steps, pg, local)
         assert all(p_ == proof for p_ in last if p_ is not None), "device-resident proof differs"
-        pageable = np.array(trace)  # ordinary (pageable) host memory
-        pfns = [host_step(k, pageable) for k in range(P)]
-        run_proofs(pfns, P)
-        pag_s = run_proofs_timed(pfns, cmp_steps, pg, local)
-        assert all(p_ == proof for p_ in last if p_ is not None), "pageable-trace proof differs"
-        del pageable
+        if not args.ab:
+            pageable = np.array(trace)  # ordinary (pageable) host memory
+            pfns = [host_step(k, pageable) for k in range(P)]
+            run_proofs(pfns, P)
+            pag_s = run_proofs_timed(pfns, cmp_steps, pg, local)
+            assert all(p_ == proof for p_ in last if p_ is not None), "pageable-trace proof differs"
+            del pageable
         vm_rec.update(vm_prove_leg(args, prog, src, w, proof, provers, opts, pg, local, rank))
     prog.close()
     for g in provers[1:]:
@@ -468,7 +471,7 @@ def main():
     zk_verified = zk_verify(proof, pub, min_sec)[0] == 0
     gpu.close()
     lifetime = None
-    if not args.no_compare:
+    if not args.no_compare and not args.ab:
         lifetime = lifetime_leg(local, n, trace, pub, opts, proof)
     # every rank: its proof accepted by zk_verify; rank 0's workload (seed 1000) is a committed oracle pin, so its
     # proof must also equal the pin byte for byte (the other ranks' seeds have no pin)
@@ -480,7 +483,8 @@ def main():
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
                      zk_verified, pin, all_verified, lifetime) if rank == 0 else None
-    if out is not None and world == 1 and not args.no_compare and os.environ.get("GPU_MAX_HW_QUEUES") != "4":
+    if (out is not None and world == 1 and not args.no_compare and not args.ab
+            and os.environ.get("GPU_MAX_HW_QUEUES") != "4"):
         out["default_queues"] = default_queues_leg(args, P)
 
     # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A

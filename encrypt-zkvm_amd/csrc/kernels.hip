@@ -941,50 +941,58 @@ void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int 
             hipLaunchKernelGGL(k_hash_rows, dim3(cdiv(M, 256)), dim3(256), 0, st, base, ncols, log_n, log_b, r0, log_rc, leaves));
 }
 
-// One BLAKE3 block of every row: columns 4 blk .. 4 blk + 3 (64 bytes) compressed into the row's chaining value,
-// kept in its leaf slot between blocks (IV before block 0; after the last block the slot holds the digest).  The
-// trace rows (28 elements = 7 full blocks) are hashed this way block by block as their columns' LDEs complete, so
-// a host-resident proof hashes its rows under the rest of the upload instead of after it.
-__global__ void __launch_bounds__(256) k_hash_rows_block(const fe *base, int log_n, int log_b, int blk, int nblk,
-                                                         uint8_t *cv_leaves) {
+// BLAKE3 blocks b0 .. b1 - 1 of every row: columns 4 b .. 4 b + 3 (64 bytes) compressed into the row's chaining
+// value, kept in its leaf slot between launches (IV before block 0; after the last block the slot holds the digest).
+// The trace rows (28 elements = 7 full blocks) are hashed this way as their columns' LDEs complete, so a
+// host-resident proof hashes its rows under the rest of the upload instead of after it.
+__global__ void __launch_bounds__(256) k_hash_rows_blocks(const fe *base, int log_n, int log_b, int b0, int b1, int nblk,
+                                                          uint8_t *cv_leaves) {
     const size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= N) return;
     const size_t r = t & (B - 1), q = t >> log_b;
-    const fe *p = base + r * n + q + (size_t)(4 * blk) * B * n;
     uint32_t h[8], m[16];
     uint8_t *slot = cv_leaves + 32 * ((q << log_b) + r);
-    if (blk == 0) b3::iv(h);
+    if (b0 == 0) b3::iv(h);
     else load_digest(slot, h);
+    for (int blk = b0; blk < b1; blk++) {
+        const fe *p = base + r * n + q + (size_t)(4 * blk) * B * n;
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const fe v = p[(size_t)e * B * n];
-        m[4 * e + 0] = (uint32_t)v.lo;
-        m[4 * e + 1] = (uint32_t)(v.lo >> 32);
-        m[4 * e + 2] = (uint32_t)v.hi;
-        m[4 * e + 3] = (uint32_t)(v.hi >> 32);
+        for (int e = 0; e < 4; e++) {
+            const fe v = p[(size_t)e * B * n];
+            m[4 * e + 0] = (uint32_t)v.lo;
+            m[4 * e + 1] = (uint32_t)(v.lo >> 32);
+            m[4 * e + 2] = (uint32_t)v.hi;
+            m[4 * e + 3] = (uint32_t)(v.hi >> 32);
+        }
+        const uint32_t flags = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == nblk - 1 ? (b3::CHUNK_END | b3::ROOT) : 0u);
+        b3::compress(h, m, 0, 0, 64, flags);
     }
-    const uint32_t flags = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == nblk - 1 ? (b3::CHUNK_END | b3::ROOT) : 0u);
-    b3::compress(h, m, 0, 0, 64, flags);
     store_digest(slot, h);
 }
 
-void hash_rows_block(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int blk, uint8_t *leaves) {
+void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves) {
     const size_t N = (size_t)1 << (log_n + log_b);
-    ZK_PROF(st, "hash_rows", (64.0 + (blk ? 64.0 : 32.0)) * N,
-            hipLaunchKernelGGL(k_hash_rows_block, dim3(cdiv(N, 256)), dim3(256), 0, st, base, log_n, log_b, blk,
+    ZK_PROF(st, "hash_rows", (64.0 * (b1 - b0) + (b0 ? 64.0 : 32.0)) * N,
+            hipLaunchKernelGGL(k_hash_rows_blocks, dim3(cdiv(N, 256)), dim3(256), 0, st, base, log_n, log_b, b0, b1,
                                ncols / 4, leaves));
 }
 
 // Sparse-column detection: nz[c0 + c] |= 1 when column c has a nonzero entry before its last one; last[c0 + c] = its
 // last entry.  One pass over the columns (16 B per element read); nz must be zeroed first.
 __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last) {
+    constexpr int PER = 16;  // independent loads per thread (unrolled: all in flight at once)
     const int c = blockIdx.y;
     const fe *col = trace + (size_t)(c0 + c) * n;
+    const size_t base = blockIdx.x * (size_t)(256 * PER) + threadIdx.x;
     uint64_t any = 0;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n - 1; i += (size_t)gridDim.x * blockDim.x) {
-        const fe v = col[i];
-        any |= v.lo | v.hi;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const size_t i = base + (size_t)k * 256;
+        if (i < n - 1) {
+            const fe v = col[i];
+            any |= v.lo | v.hi;
+        }
     }
     const unsigned long long wave_any = __ballot(any != 0);
     if (wave_any && (threadIdx.x & 63) == 0) atomicOr(nz + c0 + c, 1u);
@@ -992,10 +1000,9 @@ __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n
 }
 
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp) {
-    const unsigned bx = (unsigned)std::min<size_t>(cdiv(n, 256 * 16), 256);
     ZK_PROF(st, "sparse_detect", 16.0 * n * nc,
-            hipLaunchKernelGGL(k_sparse_detect, dim3(bx, nc), dim3(256), 0, st, trace, n, c0, const_cast<unsigned *>(sp.nz),
-                               const_cast<fe *>(sp.last)));
+            hipLaunchKernelGGL(k_sparse_detect, dim3(cdiv(n, 256 * 16), nc), dim3(256), 0, st, trace, n, c0,
+                               const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last)));
 }
 
 // Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).

@@ -1245,8 +1245,13 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
                 p->tmp, sp ? &gsp : nullptr);
         c0 += nc;
-        if (incr)
-            for (; 4 * (hashed + 1) <= c0; hashed++) hash_rows_block(p->st, p->lde, W, log_n, log_b, hashed, p->leaves);
+        // the complete blocks so far, at least two per launch but the last (each launch re-reads and re-writes the
+        // 32-byte chaining values: fewer launches, less of that traffic)
+        const int ready = c0 / 4;
+        if (incr && (ready - hashed >= 2 || (c0 == W && ready > hashed))) {
+            hash_rows_blocks(p->st, p->lde, W, log_n, log_b, hashed, ready, p->leaves);
+            hashed = ready;
+        }
     }
     if (!incr) hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);

@@ -153,9 +153,9 @@ void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int 
                       uint8_t *leaves);
 void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, uint8_t *leaves,
                              uint8_t *nodes);
-// block blk of the leaf hashes of all B n rows of a coset-major column set of ncols (a multiple of 4, <= 64)
-// columns: columns 4 blk .. 4 blk + 3 compressed into the chaining value each leaf slot carries between blocks
-void hash_rows_block(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int blk, uint8_t *leaves);
+// blocks b0 .. b1 - 1 of the leaf hashes of all B n rows of a coset-major column set of ncols (a multiple of 4,
+// <= 64) columns: columns 4 b .. 4 b + 3 compressed into the chaining value each leaf slot carries between launches
+void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves);
 // Storage of a FRI layer of L values: natural order (lb = 0), or coset-major over 2^lb cosets of 2^lcn
 // points (natural index i at (i mod 2^lb) 2^lcn + i / 2^lb): layer 0 as the DEEP coset LDE leaves it
 struct FriLayout {

@@ -9,7 +9,7 @@ O=gpurun_out
 mkdir -p $O
 run() {  # name queues stream gate inflight [upload plan]
   GPU_MAX_HW_QUEUES=$2 ZK_UPLOAD_STREAM=$3 ZK_UPLOAD_GATE=$4 ZK_UPLOAD_PLAN=${6:-incr} timeout -k 10 400 python3 bench.py --no-cpu-baseline \
-    --no-verify --inflight $5 ${BENCH_ARGS:-} > $O/abq_$1.json 2> $O/abq_$1.err || { echo "$1 FAILED"; tail -5 $O/abq_$1.err; exit 1; }
+    --no-verify --ab --inflight $5 ${BENCH_ARGS:-} > $O/abq_$1.json 2> $O/abq_$1.err || { echo "$1 FAILED"; tail -5 $O/abq_$1.err; exit 1; }
   python3 - "$1" "$O/abq_$1.json" <<'PY'
 import json, sys
 b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
@@ -20,12 +20,11 @@ PY
 }
 for rep in 1 2; do
   run q16_own_dev_p4_legacy 16 own device 4 legacy
+  run q16_sh_dev_p4_legacy 16 shared device 4 legacy
+  run q16_sh_dev_p4 16 shared device 4
+  run q16_sh_host_p4 16 shared host 4
   run q4_own_dev_p4_legacy 4 own device 4 legacy
-  run q4_own_dev_p4 4 own device 4
   run q4_sh_dev_p4 4 shared device 4
   run q4_sh_host_p4 4 shared host 4
   run q4_sh_dev_p3 4 shared device 3
-  run q16_own_dev_p4 16 own device 4
-  run q16_sh_dev_p4 16 shared device 4
-  run q16_sh_host_p4 16 shared host 4
 done
