@@ -7,7 +7,7 @@ O=gpurun_out
 mkdir -p "$O"
 for v in "$@"; do
   if [ "$v" = base ]; then lib=encrypt-zkvm_amd/lib/libzkvm_gpu.so; else lib=encrypt-zkvm_amd/lib/libzkvm_gpu_$v.so; fi
-  ZKVM_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-verify --steps ${AB_STEPS:-20} --warmup 6 ${BENCH_ARGS:-} \
+  ZKVM_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-verify --steps ${AB_STEPS:-20} --warmup ${AB_WARMUP:-12} ${BENCH_ARGS:-} \
     > "$O/ab_$v.json" 2> "$O/ab_$v.err" || { echo "$v FAILED"; tail -5 "$O/ab_$v.err"; exit 1; }
   python3 - "$v" "$O/ab_$v.json" <<'PY'
 import json, sys
