@@ -309,6 +309,7 @@ int zk::upload_gate(zk_prover *p, hipEvent_t ev) {
 void zk::upload_drain(zk_prover *p) {
     for (auto &e : p->ev_up)
         if (e) (void)hipEventSynchronize(e);
+    if (p->ev_verify) (void)hipEventSynchronize(p->ev_verify);  // the sparse hint's verification upload
 }
 
 // world = 0: a full prover; world = G: one rank of a G-way coset-sharded proof (blowup 8), whose LDE-domain
@@ -428,6 +429,8 @@ void zk_prover_destroy(zk_prover *p) {
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
     if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
     if (p->h_vm) (void)hipHostFree(p->h_vm);
+    if (p->sp_h) (void)hipHostFree(p->sp_h);
+    if (p->ev_verify) (void)hipEventDestroy(p->ev_verify);
     delete p->open;
     delete p;
 }
@@ -1124,6 +1127,7 @@ struct TraceSrc {
     const fe *dev = nullptr;
     const uint8_t *const *cols = nullptr;
     const FixedCols *fixed = nullptr;  // with dev: only the dynamic columns are in dev (zk_vm_prove)
+    bool hint_ok = true;               // host columns: the sparse hint of the previous proof may be used
 };
 
 // Column groups of a host-resident trace upload.  The copy engine streams group g + 1 while the CUs interpolate and
@@ -1185,10 +1189,15 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         if (!p->sp_nz) {
             ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, W));
             ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sp_vz, W));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sp_vlast, W));
+            ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 2 * W * sizeof(unsigned), hipHostMallocDefault));
+            ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_verify, hipEventDisableTiming));
         }
         ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, W * sizeof(unsigned), p->st));
         spc = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
         sp = &spc;
+        p->sp_used = true;
     }
     if (src.dev && src.fixed) {
         // zk_vm_prove: interpolate and extend the dynamic stack columns only; the preprocessed ones by one pass
@@ -1225,36 +1234,97 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
     // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
     const bool incr = upload_plan_incr();
-    const int *plan = incr ? kPlanIncr : kPlanLegacy;
-    const int ngroups = incr ? (int)(sizeof kPlanIncr / sizeof(int)) : (int)(sizeof kPlanLegacy / sizeof(int));
-    static_assert(sizeof kPlanIncr / sizeof(int) <= ZK_UPLOAD_GROUPS_MAX, "upload groups");
-    int c0 = 0, hashed = 0;
-    for (int g = 0; g < ngroups; g++) {
-        const int nc = plan[g];
-        {
-            std::lock_guard<std::mutex> lk(*p->up_mu);
-            ZK_TRY(upload_trace_group(p, src, n, c0, nc));
-            ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
+    // sparse hint: the columns the previous proof of this length found sparse (hint_ok: prove_impl allows it)
+    const uint32_t hint = (sp && incr && src.hint_ok && p->sp_hint_n == n) ? p->sp_hint : 0u;
+    p->sp_hinted = hint;
+    int dense[W], nd = 0, hin[W], nh = 0;
+    for (int c = 0; c < W; c++) {
+        if ((hint >> c) & 1u) hin[nh++] = c;
+        else dense[nd++] = c;
+    }
+    bool ready[W] = {};
+    // contiguous runs of a column list: f(first column, count)
+    auto runs = [](const int *cols, int k, auto f) -> int {
+        for (int i = 0; i < k;) {
+            int j = i + 1;
+            while (j < k && cols[j] == cols[j - 1] + 1) j++;
+            ZK_TRY(f(cols[i], j - i));
+            i = j;
         }
-        ZK_TRY(upload_gate(p, p->ev_up[g]));
+        return ZK_OK;
+    };
+    auto transform = [&](int c0, int nc) -> int {  // interpolation + coset LDE of columns [c0, c0 + nc)
         SparseCols gsp = spc;
         gsp.col0 = c0;
-        if (sp) sparse_detect(p->st, p->d_trace, n, c0, nc, spc);
         ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp,
             sp ? &gsp : nullptr);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
                 p->tmp, sp ? &gsp : nullptr);
-        c0 += nc;
-        // the complete blocks so far, at least two per launch but the last (each launch re-reads and re-writes the
-        // 32-byte chaining values: fewer launches, less of that traffic)
-        const int ready = c0 / 4;
-        if (incr && (ready - hashed >= 2 || (c0 == W && ready > hashed))) {
-            hash_rows_blocks(p->st, p->lde, W, log_n, log_b, hashed, ready, p->leaves);
-            hashed = ready;
+        return ZK_OK;
+    };
+    int hashed = 0;
+    auto hash_ready = [&](bool last) {  // the blocks whose 4 columns are extended, at least two per launch but the last
+        int b = hashed;
+        while (b < W / 4 && ready[4 * b] && ready[4 * b + 1] && ready[4 * b + 2] && ready[4 * b + 3]) b++;
+        if (b - hashed >= 2 || (last && b > hashed)) {
+            hash_rows_blocks(p->st, p->lde, W, log_n, log_b, hashed, b, p->leaves);
+            hashed = b;
         }
+    };
+    if (nh) {
+        // hinted columns: zero but the last row, whose values the host reads from the trace: their coefficients and
+        // LDE are last * e_(n-1)'s (the NTT passes' sparse fill), with nothing uploaded yet
+        fe lastv[W];
+        memset(lastv, 0, sizeof lastv);
+        for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
+        ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
+        ZK_TRY(runs(hin, nh, transform));
+        for (int i = 0; i < nh; i++) ready[hin[i]] = true;
     }
-    if (!incr) hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
+    // upload groups over the dense columns: 4 columns each, the last 4 as 2 + 2 (after the last copy only 2 columns'
+    // NTTs, the last hash blocks and the Merkle tree remain); legacy: 7 groups of 4, all rows hashed at the end
+    int gsz[W], ngroups = 0;
+    for (int left = nd; left > 0;) {
+        const int k = !incr ? std::min(4, left) : left > 4 ? 4 : left > 2 ? 2 : left;
+        gsz[ngroups++] = (incr && left == 4) ? 2 : k;
+        left -= gsz[ngroups - 1];
+    }
+    if (ngroups + (nh ? 1 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
+    int di = 0;
+    for (int g = 0; g < ngroups; g++) {
+        const int *cols = dense + di, nc = gsz[g];
+        {
+            std::lock_guard<std::mutex> lk(*p->up_mu);
+            ZK_TRY(runs(cols, nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
+            ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
+        }
+        ZK_TRY(upload_gate(p, p->ev_up[g]));
+        if (sp) ZK_TRY(runs(cols, nc, [&](int c0, int k) { sparse_detect(p->st, p->d_trace, n, c0, k, spc); return ZK_OK; }));
+        ZK_TRY(runs(cols, nc, transform));
+        for (int i = 0; i < nc; i++) ready[cols[i]] = true;
+        di += nc;
+        if (incr) hash_ready(di == nd);
+    }
+    if (incr) hash_ready(true);
+    else hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);
+    if (sp) ZK_TRY(d2h_small(p, p->sp_h + W, p->sp_nz, W * sizeof(unsigned)));  // for the next proof's hint
+    if (nh) {
+        // the hinted columns go up last, verified by a detection on the upload stream (never waited for by the
+        // compute stream); prove_impl checks the flags before it returns
+        std::lock_guard<std::mutex> lk(*p->up_mu);
+        ZK_TRY(runs(hin, nh, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
+        ZK_CHECK_HIP(hipMemsetAsync(p->sp_vz, 0, W * sizeof(unsigned), p->up));
+        const SparseCols vsp{p->sp_vz, p->sp_vlast, nullptr, nullptr, 0};
+        ZK_TRY(runs(hin, nh, [&](int c0, int k) { sparse_detect(p->up, p->d_trace, n, c0, k, vsp); return ZK_OK; }));
+        CopyList L;
+        L.n = 1;
+        L.src[0] = p->sp_vz;
+        L.dst[0] = p->sp_h;
+        L.words[0] = W;
+        ZK_CHECK_HIP(copy_to_host(p->up, L, W));
+        ZK_CHECK_HIP(hipEventRecord(p->ev_verify, p->up));
+    }
     return d2h_small(p, root, p->nodes + 32, 32);
 }
 
@@ -1347,7 +1417,42 @@ static int check_ood_identity(const std::vector<fe2> &e, int C, const AirConsts 
     return ZK_OK;
 }
 
+static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                      uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump);
+
+// One proof, plus the sparse hint's bookkeeping for host-resident traces: a hinted column that turns out not to be
+// sparse (the upload-stream detection flags it) voids the proof, which is redone without the hint; a completed proof
+// leaves the columns it found sparse as the next proof's hint.
 static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+                      uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
+    p->sp_used = false;
+    p->sp_hinted = 0;
+    int rc = prove_once(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+    if (!src.cols || !p->sp_used) return rc;
+    // (prove_once's CopyGuard drained the uploads, the verification's flag copy included)
+    uint32_t bad = 0;
+    for (int c = 0; c < W; c++)
+        if (((p->sp_hinted >> c) & 1u) && p->sp_h[c]) bad |= 1u << c;
+    if (bad) {
+        p->sp_hint = 0;
+        p->sp_hint_n = 0;
+        TraceSrc s2 = src;
+        s2.hint_ok = false;
+        p->sp_used = false;
+        rc = prove_once(p, s2, n, opt, pub, proof_out, proof_len, rec, dump);
+        if (!p->sp_used) return rc;
+    }
+    if (rc == ZK_OK || rc == ZK_ERR_DEGREE || rc == ZK_ERR_BUFFER_TOO_SMALL) {
+        uint32_t found = 0;
+        for (int c = 0; c < W; c++)
+            if (((p->sp_hinted >> c) & 1u) ? p->sp_h[c] == 0 : p->sp_h[W + c] == 0) found |= 1u << c;
+        p->sp_hint = found;
+        p->sp_hint_n = n;
+    }
+    return rc;
+}
+
+static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     if (!p || !proof_len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
     ZK_REQUIRE_FULL_PROVER(p);
@@ -1754,6 +1859,7 @@ int zk_lde_new(zk_prover *p, const uint8_t *trace, size_t width, size_t n, uint3
     for (int c = 0; c < W; c++) cols[c] = trace + (size_t)c * n * sizeof(fe);
     TraceSrc src;
     src.cols = cols;
+    src.hint_ok = false;  // no proof follows to verify a hint
     uint8_t r[32];
     rc = trace_lde_commit(p, pl, src, n, r);
     if (!rc) rc = d2h_flush(p);

@@ -165,6 +165,16 @@ struct zk_prover {
     fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
     unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries
     fe *sp_last = nullptr;        // ... and the trace's last row
+    // Sparse hint (host-resident traces): the columns the previous proof of the same length found sparse are taken as
+    // sparse from their last row alone and uploaded last, off the critical path, where a detection on the upload
+    // stream verifies them (sp_vz -> pinned sp_h[0..W), event ev_verify); a wrong hint redoes the proof without it
+    uint32_t sp_hint = 0, sp_hinted = 0;
+    bool sp_used = false;  // the last trace_lde_commit ran the sparse detection (its flags are in sp_h)
+    size_t sp_hint_n = 0;
+    unsigned *sp_vz = nullptr;
+    fe *sp_vlast = nullptr;
+    unsigned *sp_h = nullptr;       // pinned: [0, W) verification flags, [W, 2W) the trace root flush's nz flags
+    hipEvent_t ev_verify = nullptr;
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets

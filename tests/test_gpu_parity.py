@@ -564,3 +564,24 @@ def test_sparse_column_detection(gpu, oracle, path):
     assert rc == 0
     assert bytes(rec.trace_root) == bytes(orec.trace_root)
     assert proof == oproof
+
+
+def test_sparse_hint_learned_and_refuted(oracle):
+    """The sparse hint (a host-resident trace's columns that the previous proof of the same length found sparse are
+    taken as sparse from their last row and verified off the critical path): proofs of a trace, of the same trace
+    again (hinted), of an edited trace the hint is wrong for (col 27 dense: the library must notice and redo the
+    proof), and of the first trace once more -- each equal to the oracle's."""
+    trace, pub = workload_trace(ops_for_trace_len(14, "cipher"), seed=15)
+    n = trace.shape[1]
+    edited = trace.copy()
+    edited[27, 9] = [3, 1]     # dense now (no constraint reads s15: the trace still satisfies the AIR)
+    edited[22, : n - 1] = 0    # sparse now
+    g = GpuProver(0, max_trace_len=n)
+    try:
+        for t in (trace, trace, edited, edited, trace):
+            proof, _, _, rc = g.prove(t, pub, ProofOptions())
+            assert rc == 0
+            oproof, _, _ = oracle.prove(t, oracle_pub(oracle, pub))
+            assert proof == oproof
+    finally:
+        g.close()
