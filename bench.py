@@ -356,6 +356,7 @@ def main():
     # streams of several provers share queues, and a compute stream parked on its upload's event then holds up the
     # kernels of another prover queued behind it (A/B, 2 provers: 16.1 ms per proof at 4 queues, 14.3 at 8, 13.8 at
     # 16).  Set before the first HIP call of the process (torch.distributed's included).
+    # (The GPU boxes of this pool export GPU_MAX_HW_QUEUES=4 themselves; an explicit setting is kept and reported.)
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     if args.sharded:
         return run_sharded(args)
@@ -483,9 +484,13 @@ def main():
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
                      zk_verified, pin, all_verified, lifetime) if rank == 0 else None
-    if (out is not None and world == 1 and not args.no_compare and not args.ab
-            and os.environ.get("GPU_MAX_HW_QUEUES") != "4"):
-        out["default_queues"] = default_queues_leg(args, P)
+    if out is not None:
+        out["gpu_max_hw_queues"] = int(os.environ["GPU_MAX_HW_QUEUES"])
+    if out is not None and world == 1 and not args.no_compare and not args.ab:
+        q = queues_leg(args, P)
+        out["queues_ab"] = q
+        out["default_queues_ms"] = (out["ms_per_step"] if out["gpu_max_hw_queues"] == 4
+                                    else q.get("ms_per_step"))
 
     # ---- multi-GPU: the north_star's ONE proof sharded by coset over all ranks (configs[3]) as a sub-record.  A
     # watchdog bounds it: should a collective never complete, rank 0 still prints the line (with the error) and
@@ -554,11 +559,12 @@ def lifetime_leg(local, n, trace, pub, opts, proof):
                           "acquire + prove + release (median of 3 after the pool's first fill)"}
 
 
-def default_queues_leg(args, P):
-    """The headline configuration re-run in a child process with HIP's default 4 hardware queues per process
-    (GPU_MAX_HW_QUEUES=4; this process set 16 before its first HIP call): what a host that does not set it gets."""
+def queues_leg(args, P):
+    """The headline configuration re-run in a child process at the OTHER hardware-queue count (GPU_MAX_HW_QUEUES
+    4 <-> 16; HIP's default is 4 and this pool's boxes export 4): the design must not depend on a host raising it."""
     import subprocess
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="4")
+    other = "16" if os.environ.get("GPU_MAX_HW_QUEUES") == "4" else "4"
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=other)
     cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--no-verify", "--no-compare",
            "--sharded-log-n", "0", "--inflight", str(P), "--steps", str(args.steps), "--log-n", str(args.log_n)]
     if args.config5:
@@ -566,10 +572,10 @@ def default_queues_leg(args, P):
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         line = json.loads(r.stdout.strip().splitlines()[-1])
-        return {"ms_per_step": line["ms_per_step"], "value": line["value"], "gpu_max_hw_queues": 4,
+        return {"gpu_max_hw_queues": int(other), "ms_per_step": line["ms_per_step"], "value": line["value"],
                 "inflight": P, "proof_matches_pin": line.get("proof_matches_pin")}
     except Exception as e:  # reported, never fatal for the headline
-        return {"error": repr(e)[:300]}
+        return {"gpu_max_hw_queues": int(other), "error": repr(e)[:300]}
 
 
 def vm_prove_leg(args, prog, src, w, proof, provers, opts, pg, local, rank):

@@ -994,8 +994,9 @@ __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n
             any |= v.lo | v.hi;
         }
     }
-    const unsigned long long wave_any = __ballot(any != 0);
-    if (wave_any && (threadIdx.x & 63) == 0) atomicOr(nz + c0 + c, 1u);
+    // one flag write per block that saw a nonzero entry (a plain store: every writer stores 1), not one atomic per
+    // wave -- 4096 same-address atomics per 64 MiB column serialised at L2 (0.38 ms per proof)
+    if (__syncthreads_or(any != 0) && threadIdx.x == 0) nz[c0 + c] = 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) last[c0 + c] = col[n - 1];
 }
 
