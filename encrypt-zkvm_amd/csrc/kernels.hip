@@ -2184,13 +2184,14 @@ struct BndPoly {
     fe cb[22];  // one coefficient plane (air/src/lib.rs:170-195 order: step 0 cols 0,7,8,11,12..19; step n-2 cols 7,8,12..19)
     fe bnd1;    // sum_k cb[12+k] v_k
 };
+// [kbase, kend): the coefficient range of this launch (a sharded rank's share; 0, n otherwise); n is the column stride
 __global__ void __launch_bounds__(DIV_T) k_bnd_div_g(const fe *tpolys, size_t n, BndPoly bp, const fe *pw, size_t H,
-                                                    fe *g1, fe *g2, fe *bs) {
+                                                    fe *g1, fe *g2, fe *bs, size_t kbase, size_t kend) {
     __shared__ fe red[DIV_T / 64];
     const size_t per = 2048 + H;
-    const size_t k = blockIdx.x * (size_t)DIV_T + threadIdx.x;
+    const size_t k = kbase + blockIdx.x * (size_t)DIV_T + threadIdx.x;
     fe v1 = fe_zero(), v2 = fe_zero();
-    if (k < n) {
+    if (k < kend) {
         auto T = [&](int c) { return ld_fe(tpolys + (size_t)c * n + k); };
         acc288 a0 = acc288_zero(), a1 = acc288_zero();
         acc288_madd(a0, bp.cb[0], T(0));
@@ -2221,10 +2222,9 @@ __global__ void __launch_bounds__(DIV_T) k_bnd_div_g(const fe *tpolys, size_t n,
     }
 }
 
-void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
-                       unsigned *flag) {
-    const size_t n = (size_t)1 << log_n;
-    const size_t H = n / 2048 + 2, nb = (n + DIV_CH - 1) / DIV_CH, nb1 = (n + DIV_T - 1) / DIV_T;
+static void bnd_tables_phase1(hipStream_t st, const fe *tpolys, size_t n, const AirConsts &K, fe c, fe *scratch,
+                              size_t k0, size_t kn, fe *total) {
+    const size_t H = n / 2048 + 2, nb1 = (kn + DIV_T - 1) / DIV_T;
     fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *bs = g2 + 2 * n;  // layout of deep_poly's scratch
     DeepPowBases pb;
     pb.b[0] = fe_one();
@@ -2235,12 +2235,39 @@ void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirCon
     BndPoly bp;
     memcpy(bp.cb, K.coeff_b, sizeof bp.cb);
     bp.bnd1 = K.bnd1;
-    ZK_PROF(st, "boundary_poly", (16.0 * 12 + 32.0) * n,
-            hipLaunchKernelGGL(k_bnd_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, n, bp, pw, H, g1, g2, bs));
-    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1, nullptr);
-    ZK_PROF(st, "boundary_poly", 64.0 * n,
-            hipLaunchKernelGGL(k_deep_div_q<true>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, n, fe_one(),
-                               c, pw, H, col0, flag, (size_t)0, nullptr));
+    ZK_PROF(st, "boundary_poly", (16.0 * 12 + 32.0) * kn,
+            hipLaunchKernelGGL(k_bnd_div_g, dim3((unsigned)nb1), dim3(DIV_T), 0, st, tpolys, n, bp, pw, H, g1, g2, bs, k0,
+                               k0 + kn));
+    hipLaunchKernelGGL(k_deep_div_scan<2>, dim3(1), dim3(1024), 0, st, bs, (int)nb1, total);
+}
+static void bnd_phase3(hipStream_t st, size_t n, fe c, fe *scratch, size_t k0, size_t kn, const fe *ext, fe *col0,
+                       unsigned *flag) {
+    const size_t H = n / 2048 + 2, nb = (kn + DIV_CH - 1) / DIV_CH, nb1 = (kn + DIV_T - 1) / DIV_T;
+    fe *pw = scratch, *g1 = pw + 4 * (2048 + H), *g2 = g1 + n, *bs = g2 + 2 * n;
+    ZK_PROF(st, "boundary_poly", 64.0 * kn,
+            hipLaunchKernelGGL(k_deep_div_q<true>, dim3((unsigned)nb), dim3(DIV_T), 0, st, g1, g2, bs, (int)nb1, k0 + kn,
+                               fe_one(), c, pw, H, col0, flag, k0, ext));
+}
+
+void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
+                       unsigned *flag) {
+    const size_t n = (size_t)1 << log_n;
+    bnd_tables_phase1(st, tpolys, n, K, c, scratch, 0, n, nullptr);
+    bnd_phase3(st, n, c, scratch, 0, n, nullptr, col0, flag);
+}
+
+// The same over a sharded rank's coefficient range [k0, k0 + kn): begin returns the range's two sums (device); the
+// ranks exchange them and end gets ext = the sums of the later ranks' ranges.  col0 is indexed by global k.
+const fe *boundary_range_begin(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch,
+                               size_t k0, size_t kn) {
+    const size_t n = (size_t)1 << log_n;
+    fe *total = deep_range_total(scratch, n, 2);
+    bnd_tables_phase1(st, tpolys, n, K, c, scratch, k0, kn, total);
+    return total;
+}
+void boundary_range_end(hipStream_t st, int log_n, fe c, fe *scratch, size_t k0, size_t kn, const fe *ext, fe *col0,
+                        unsigned *flag) {
+    bnd_phase3(st, (size_t)1 << log_n, c, scratch, k0, kn, ext, col0, flag);
 }
 
 void deep_coeff_launch(hipStream_t st, const NttTables &Tn, const fe *tpolys, const fe *cpolys, int ccols, int log_n,

@@ -1181,24 +1181,29 @@ static bool sparse_on() {
     return on;
 }
 
+int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp) {
+    *sp = nullptr;
+    if (!sparse_on() || !pl->lagr) return ZK_OK;
+    if (!p->sp_nz) {
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, W));
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_vz, W));
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_vlast, W));
+        ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 2 * W * sizeof(unsigned), hipHostMallocDefault));
+        ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_verify, hipEventDisableTiming));
+    }
+    ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, W * sizeof(unsigned), p->st));
+    *out = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
+    *sp = out;
+    return ZK_OK;
+}
+
 static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
     const fe inv_n = h_inv(fe_make(n));
     SparseCols spc{};
     const SparseCols *sp = nullptr;
-    if (sparse_on() && pl->lagr && !src.fixed) {
-        if (!p->sp_nz) {
-            ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, W));
-            ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
-            ZK_CHECK_HIP(p->arena.alloc(&p->sp_vz, W));
-            ZK_CHECK_HIP(p->arena.alloc(&p->sp_vlast, W));
-            ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 2 * W * sizeof(unsigned), hipHostMallocDefault));
-            ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_verify, hipEventDisableTiming));
-        }
-        ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, W * sizeof(unsigned), p->st));
-        spc = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
-        sp = &spc;
-        p->sp_used = true;
-    }
+    if (!src.fixed) ZK_TRY(sparse_begin(p, pl, &spc, &sp));
+    p->sp_used = sp != nullptr;
     if (src.dev && src.fixed) {
         // zk_vm_prove: interpolate and extend the dynamic stack columns only; the preprocessed ones by one pass
         const FixedCols &fx = *src.fixed;

@@ -239,6 +239,9 @@ struct FixedCols {
     fe last[W];              // the last row
 };
 // zk_prove_device of p->d_trace (whose dynamic columns hold the trace) with the preprocessed columns of fx
+// Sparse trace columns (SparseCols) for this proof: allocates the flags on first use and clears them on p->st; *sp
+// stays null when ZK_SPARSE=0 or the plan is too small for the four-step NTT.
+int sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp);
 int prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inputs *pub, const FixedCols *fx,
                 uint8_t *proof_out, size_t *proof_len);
 // polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip)

@@ -431,8 +431,15 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ntt(p->st, X.pl[l]->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp);
-            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp);
+            // sparse columns (zero but the last row): no DFT, the LDE is last * the unit vector's (every rank
+            // detects them in its own copy of the trace)
+            SparseCols spc{};
+            const SparseCols *sp = nullptr;
+            ZK_TRY(sparse_begin(p, X.pl[l], &spc, &sp));
+            if (sp) sparse_detect(p->st, p->d_trace, n, 0, W, *sp);
+            ntt(p->st, X.pl[l]->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp, sp);
+            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp,
+                    sp);
         }
     }
     stage_mark(P0, "trace_lde");
@@ -452,7 +459,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     stage_mark(P0, "trace_commit");
     coin.reseed(R.trace_root);
 
-    // S3: constraint evaluation over the local CE cosets (CE domain = LDE domain at blowup 8)
+    // S3: constraint evaluation over the local CE cosets (CE domain = LDE domain at blowup 8).  The assertion terms
+    // are not evaluated per row: S4 adds their quotient in coefficient form, each rank over its n / G coefficient
+    // slice (boundary_range_*; traces too short for whole ranges keep the per-row form).
+    const bool bnd_split = (n / G) % ZK_DEEP_RANGE_QUANTUM == 0;
     AirConsts K, Kp[2];
     if (KX == 1) {
         draw_air_consts(coin, pub, n, K, R);
@@ -475,11 +485,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         if (KX == 1) {
             ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
             ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                                 (const AirConsts *)p->air_consts, p->comp));
+                                                 (const AirConsts *)p->air_consts, p->comp, !bnd_split));
         } else {
             ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
             ZK_CHECK_HIP(eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                                     (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp));
+                                                     (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp, !bnd_split));
         }
     }
     stage_mark(P0, "constraints");
@@ -519,6 +529,27 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             }
             fs[l] = p->flag;
             fr[l] = p->sh_flags;
+        }
+        // assertion quotient over this rank's slice of composition column 0 (plane by plane: the division scratch is
+        // shared); the range sums are all-gathered and each rank adds the later ranks' as its carry
+        for (int pln = 0; bnd_split && pln < KX; pln++) {
+            const AirConsts &Kb = KX == 1 ? K : Kp[pln];
+            std::vector<const void *> s2(nlp);
+            std::vector<void *> r2(nlp);
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                s2[l] = boundary_range_begin(p->st, p->polys, log_n, Kb, K.g_last2, p->dscratch, (size_t)X.rank[l] * kg, kg);
+                r2[l] = p->sh_buf;
+            }
+            ZK_TRY(xchg(X, "bnd_totals", AG, s2, r2, 2 * sizeof(fe)));
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                hipLaunchKernelGGL(k_sh_suffix_carry, dim3(1), dim3(64), 0, p->st, p->sh_buf, G, X.rank[l], 2, p->ood);
+                const size_t k0 = (size_t)X.rank[l] * kg;
+                boundary_range_end(p->st, log_n, K.g_last2, p->dscratch, k0, kg, p->ood, CTMP(p) + pln * kg - k0, p->flag);
+            }
         }
         for (int c = 0; c < CK; c++) {
             std::vector<const void *> s2(nlp);

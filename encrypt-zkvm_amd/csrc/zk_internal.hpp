@@ -242,6 +242,13 @@ hipError_t eval_constraints(hipStream_t st, const fe *lde, int log_n, int log_b,
 // c = g^(n-2); scratch: deep_poly's layout; sets *flag when an assertion fails
 void boundary_poly_add(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch, fe *col0,
                        unsigned *flag);
+// boundary_poly_add split over a sharded rank's coefficient range [k0, k0 + kn) (kn a multiple of
+// ZK_DEEP_RANGE_QUANTUM): begin -> the range's 2 sums on the device; end adds the quotient's range into col0
+// (global index) given ext = the sums of every later range.  The remainder flag is raised by the rank with k0 = 0.
+const fe *boundary_range_begin(hipStream_t st, const fe *tpolys, int log_n, const AirConsts &K, fe c, fe *scratch,
+                               size_t k0, size_t kn);
+void boundary_range_end(hipStream_t st, int log_n, fe c, fe *scratch, size_t k0, size_t kn, const fe *ext, fe *col0,
+                        unsigned *flag);
 // cross-coset step of the size-8n interpolation: per k1 < n, from the 8 per-coset inverse NTTs
 // (c_r[k1]), produce coefficients a[k1 + n*k2] = 3^-(k1+n k2) / (8n) * sum_r w8^(-r k2) w_8n^(-r k1) c_r[k1]
 // and write column k2 < ncols of the segmented composition polynomial: polys[k2*n + k1].
