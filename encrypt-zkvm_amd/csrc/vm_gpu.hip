@@ -507,6 +507,39 @@ int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t
     return prove_fixed(p, n, opt, &pub, &fx, proof_out, proof_len);
 }
 
+int zk_vm_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, zk_program *prog, const uint8_t *public_in,
+                        size_t num_public, const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                        const uint8_t *last_row, const zk_options *opt, uint8_t *proof_out, size_t *proof_len,
+                        uint8_t *outputs, uint8_t *program_hash) {
+    if (!comm || !provers || nlocal < 1 || !prog || !opt || !proof_len || (num_secret && !secret) ||
+        (num_public && !public_in))
+        ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (!last_row) ZK_FAIL(ZK_ERR_INVALID_ARG, "zk_vm_prove_sharded: last_row is required (every rank writes the same trace)");
+    for (int l = 0; l < nlocal; l++)
+        if (!provers[l]) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    const zk::vm::Inputs in{public_in, num_public, secret, num_secret, lwe_size, delta};
+    fe outs[NREG], last[28];
+    read_last(last_row, last);
+    size_t n = 0;
+    // Processor::run + trace on every local rank, each into its own trace buffer (the loopback communicator drives
+    // several ranks from one process; one RCCL process holds one)
+    for (int l = 0; l < nlocal; l++) {
+        size_t nl = 0;
+        ZK_TRY(vm_generate(provers[l], prog, in, last, GenMode{true, NREG}, &nl, outs, nullptr));
+        n = nl;
+    }
+    zk_pub_inputs pub;
+    memset(&pub, 0, sizeof pub);
+    fe_to_bytes(prog->P.hash[0], pub.program_hash[0]);
+    fe_to_bytes(prog->P.hash[1], pub.program_hash[1]);
+    for (int i = 0; i < NREG; i++) fe_to_bytes(outs[i], pub.stack_outputs[i]);
+    pub.lwe_size = lwe_size;
+    pub.delta = delta;
+    if (outputs) memcpy(outputs, pub.stack_outputs, sizeof pub.stack_outputs);
+    if (program_hash) memcpy(program_hash, pub.program_hash, sizeof pub.program_hash);
+    return zk_prove_sharded(comm, provers, nlocal, nullptr, n, opt, &pub, proof_out, proof_len, nullptr);
+}
+
 // diagnostics: the host stack pass's states every `stride` rows (CPU tests check them against host-written traces)
 extern "C" int zk_diag_vm_states(const zk_program *prog, const uint8_t *public_in, size_t num_public,
                                  const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,

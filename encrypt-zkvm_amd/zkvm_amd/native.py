@@ -36,6 +36,7 @@ EXPORTED = (
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_prove_sharded",
     "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error", "zk_vm_trace_device",
     "zk_vm_prove",
+    "zk_vm_prove_sharded",
 )
 
 
@@ -147,6 +148,8 @@ def lib():
         L.zk_program_trace.argtypes = [vp, vp, sz, vp, sz, u32, u32, vp, vp, sz, C.POINTER(sz), vp]
         L.zk_vm_trace_device.argtypes = [vp, vp, vp, sz, vp, sz, u32, u32, vp, C.POINTER(sz), vp]
         L.zk_vm_prove.argtypes = [vp, vp, vp, sz, vp, sz, u32, u32, vp, C.POINTER(Options), vp, C.POINTER(sz), vp, vp]
+        L.zk_vm_prove_sharded.argtypes = [vp, vp, C.c_int, vp, vp, sz, vp, sz, u32, u32, vp, C.POINTER(Options), vp,
+                                          C.POINTER(sz), vp, vp]
         L.zk_diag_vm_states.argtypes = [vp, vp, sz, vp, sz, u32, u32, sz, sz, vp, vp]
         L.zk_program_free.argtypes = [vp]
         L.zk_program_free.restype = None

@@ -126,6 +126,24 @@ class ShardedProver:
         check(rc, "zk_prove_sharded")
         return C.string_at(buf, plen.value), rec
 
+    def prove_program(self, prog, inputs, last_row, options: ProofOptions = REFERENCE_OPTIONS):
+        """vm::prove sharded (zk_vm_prove_sharded): every local rank writes the trace of `prog` on `inputs`
+        (Program.encode_inputs) into its own HBM, then one proof over the ranks.  last_row is required (the same
+        on every rank).  Returns (program hash, outputs, proof)."""
+        from .prover import bytes_elems, elems_bytes
+        opt = options.to_c()
+        if getattr(self, "_proof_buf", None) is None:
+            self._proof_buf = C.create_string_buffer(4 << 20)
+        buf = self._proof_buf
+        plen = C.c_size_t(len(buf))
+        outputs = C.create_string_buffer(256)
+        h = C.create_string_buffer(32)
+        arr = (C.c_void_p * len(self.provers))(*[p.value for p in self.provers])
+        rc = lib().zk_vm_prove_sharded(self.comm, arr, len(self.provers), prog.handle, *inputs, elems_bytes(last_row),
+                                       C.byref(opt), buf, C.byref(plen), outputs, h)
+        check(rc, "zk_vm_prove_sharded")
+        return bytes_elems(h.raw), bytes_elems(outputs.raw), C.string_at(buf, plen.value)
+
     def stage_times(self) -> dict:
         names = (C.c_char_p * 32)()
         ms = (C.c_float * 32)()

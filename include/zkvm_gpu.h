@@ -293,6 +293,14 @@ int zk_vm_trace_device(zk_prover *p, zk_program *prog, const uint8_t *public_in,
 int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t num_public, const uint8_t *secret,
                 size_t num_secret, uint32_t lwe_size, uint32_t delta, const uint8_t *last_row, const zk_options *opt,
                 uint8_t *proof_out, size_t *proof_len, uint8_t *outputs, uint8_t *program_hash);
+/* vm::prove as ONE proof sharded over the ranks of `comm`: every local rank writes the trace into its
+ * own HBM (zk_vm_trace_device: the host stack pass is repeated per process, no trace crosses PCIe or xGMI), then
+ * zk_prove_sharded over the device traces.  last_row is REQUIRED (every rank must write the same trace; the caller
+ * draws it once and broadcasts it).  The same proof bytes as zk_vm_prove / zk_prove of that trace, on every rank. */
+int zk_vm_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, zk_program *prog, const uint8_t *public_in,
+                        size_t num_public, const uint8_t *secret, size_t num_secret, uint32_t lwe_size, uint32_t delta,
+                        const uint8_t *last_row, const zk_options *opt, uint8_t *proof_out, size_t *proof_len,
+                        uint8_t *outputs, uint8_t *program_hash);
 
 #ifdef __cplusplus
 }

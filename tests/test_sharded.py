@@ -137,6 +137,40 @@ def test_sharded_rejects_bad_world():
 
 # ---------------------------------------------------------------- full-size pins, sharded
 from golden_large import LARGE_CASES, check_large_proof, large_inputs  # noqa: E402
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,world,ext", [(14, 2, 1), (14, 8, 2), (16, 8, 1), (16, 4, 2)])
+def test_sharded_vm_prove(log_n, world, ext):
+    """vm::prove sharded (zk_vm_prove_sharded): every loopback rank writes the trace on its own device buffer, then
+    one sharded proof over them -- sparse columns (zero but the last row) and the assertion terms split by
+    coefficient range are both on at these sizes.  The bytes equal the single-GPU proof of the host trace."""
+    from zkvm_amd.prover import Program
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(log_n, "cipher")
+    w = make_workload(src, seed=22 + log_n)
+    prog = Program(src)
+    trace, outputs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+    pub = make_pub_inputs(prog.hash, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    opts = ProofOptions(field_extension=ext)
+    g = GpuProver(0, max_trace_len=trace.shape[1])
+    try:
+        single, _, _, rc = g.prove(trace, pub, opts)
+    finally:
+        g.close()
+    assert rc == 0
+    inp = Program.encode_inputs(w.public, w.secret, w.server_key)
+    sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
+    try:
+        h, outs, got = sp.prove_program(prog, inp, w.last_row, opts)
+        assert h == list(prog.hash) and outs == list(outputs)
+        with pytest.raises(native.ZkError):  # the last row must be given: every rank writes the same trace
+            native.check(native.lib().zk_vm_prove_sharded(sp.comm, None, 0, prog.handle, None, 0, None, 0, 4, 1,
+                                                          None, None, None, None, None, None))
+    finally:
+        sp.close()
+        prog.close()
+    assert hashlib.sha256(got).hexdigest() == hashlib.sha256(single).hexdigest()
+
+
 # (case, world): every loopback rank holds its own rank-sized prover (zk_prover_create_shard) on the one test GPU:
 # 2^22 at world 8 is 8 x ~12.6 GB
 LARGE_SHARDED = [(c, w) for c in LARGE_CASES for w in ((8,) if c["log_n"] <= 20 else (2, 8))]

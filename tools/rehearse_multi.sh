@@ -14,5 +14,9 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 sh = d.get("sharded", {})
 print("n_gpus", d["n_gpus"], "value", d["value"], "ms_per_step", d["ms_per_step"], "verified", d.get("proof_verified_by_oracle"))
-print("sharded", {k: sh.get(k) for k in ("n_ranks", "ms_per_proof", "device_resident_ms_per_proof", "device_resident_same_proof", "error")})
+print("replica pin", d.get("proof_matches_pin"), "all ranks verified", d.get("all_ranks_verified_by_zk_verify"))
+print("sharded", {k: sh.get(k) for k in ("n_ranks", "ms_per_proof", "device_resident_ms_per_proof", "vm_prove_ms_per_proof",
+                                         "device_resident_and_vm_prove_same_proof", "proof_matches_pin",
+                                         "all_ranks_verified_by_zk_verify", "error")})
+print("exchange", {k: v for k, v in (sh.get("exchange") or {}).items()})
 PY
