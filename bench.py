@@ -457,6 +457,9 @@ def main():
     kstats = gpu.kernel_stats()
     kops = gpu.kernel_ops()
     gpu.profile(False)
+    upst = gpu.upload_stats()  # that proof's trace upload (sparse / narrow hints learned from the proofs before it)
+    upload = {"mb_per_proof": round(upst["bytes"] / 2**20, 1), "full_trace_mb": round(28 * n * 16 / 2**20, 1),
+              "sparse_cols": upst["sparse"], "narrow8_cols": upst["narrow8"], "narrow32_cols": upst["narrow32"]}
 
     verified = None
     if rank == 0 and not args.no_verify:
@@ -486,6 +489,7 @@ def main():
                      zk_verified, pin, all_verified, lifetime) if rank == 0 else None
     if out is not None:
         out["gpu_max_hw_queues"] = int(os.environ["GPU_MAX_HW_QUEUES"])
+        out["trace_upload"] = upload
     if out is not None and world == 1 and not args.no_compare and not args.ab:
         q = queues_leg(args, P)
         out["queues_ab"] = q

@@ -978,32 +978,75 @@ void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int 
                                ncols / 4, leaves));
 }
 
-// Sparse-column detection: nz[c0 + c] |= 1 when column c has a nonzero entry before its last one; last[c0 + c] = its
-// last entry.  One pass over the columns (16 B per element read); nz must be zeroed first.
-__global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last) {
+// Sparse-column detection: nz[c0 + c] = 1 when column c has a nonzero entry before its last one; last[c0 + c] = its
+// last entry; with wstride > 0 also the width flags of SparseCols.  One pass over the columns (16 B per element read);
+// nz must be zeroed first.
+__global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last,
+                                                       int wstride) {
     constexpr int PER = 16;  // independent loads per thread (unrolled: all in flight at once)
     const int c = blockIdx.y;
     const fe *col = trace + (size_t)(c0 + c) * n;
     const size_t base = blockIdx.x * (size_t)(256 * PER) + threadIdx.x;
-    uint64_t any = 0;
+    uint64_t any = 0, w8 = 0, w32 = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const size_t i = base + (size_t)k * 256;
         if (i < n - 1) {
             const fe v = col[i];
             any |= v.lo | v.hi;
+            w8 |= (v.lo >> 8) | v.hi;
+            w32 |= (v.lo >> 32) | v.hi;
         }
     }
     // one flag write per block that saw a nonzero entry (a plain store: every writer stores 1), not one atomic per
     // wave -- 4096 same-address atomics per 64 MiB column serialised at L2 (0.38 ms per proof)
-    if (__syncthreads_or(any != 0) && threadIdx.x == 0) nz[c0 + c] = 1u;
+    const bool b_any = __syncthreads_or(any != 0);
+    if (wstride) {
+        const bool b8 = __syncthreads_or(w8 != 0), b32 = __syncthreads_or(w32 != 0);
+        if (threadIdx.x == 0) {
+            if (b8) nz[wstride + c0 + c] = 1u;
+            if (b32) nz[2 * wstride + c0 + c] = 1u;
+        }
+    }
+    if (b_any && threadIdx.x == 0) nz[c0 + c] = 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) last[c0 + c] = col[n - 1];
 }
 
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp) {
     ZK_PROF(st, "sparse_detect", 16.0 * n * nc,
             hipLaunchKernelGGL(k_sparse_detect, dim3(cdiv(n, 256 * 16), nc), dim3(256), 0, st, trace, n, c0,
-                               const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last)));
+                               const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last), sp.wstride));
+}
+
+// Packed narrow columns -> field elements: grid (row blocks, column), 4 rows per thread
+__global__ void __launch_bounds__(256) k_expand_narrow(const uint8_t *src, NarrowCols nc, size_t n, fe *trace) {
+    const int k = blockIdx.y;
+    fe *out = trace + (size_t)nc.col[k] * n;
+    const uint8_t *in = src + nc.off[k];
+    const size_t i0 = (blockIdx.x * (size_t)256 + threadIdx.x) * 4;
+    if (i0 >= n) return;
+    uint32_t v[4];
+    if (nc.width[k] == 1) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(in + i0);  // rows i0 .. i0+3 (n is a multiple of 4)
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = (w >> (8 * e)) & 0xffu;
+    } else {
+        const uint4 w = *reinterpret_cast<const uint4 *>(in + 4 * i0);
+        v[0] = w.x;
+        v[1] = w.y;
+        v[2] = w.z;
+        v[3] = w.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const size_t i = i0 + e;
+        out[i] = i == n - 1 ? nc.last[k] : fe{(uint64_t)v[e], 0};
+    }
+}
+
+void expand_narrow(hipStream_t st, const uint8_t *src, const NarrowCols &nc, size_t n, fe *trace) {
+    if (!nc.count) return;
+    hipLaunchKernelGGL(k_expand_narrow, dim3(cdiv(n / 4, 256), nc.count), dim3(256), 0, st, src, nc, n, trace);
 }
 
 // Commit to coset-major rows: leaves + full Merkle tree (nodes[1] = root).

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "host_pool.hpp"
 #include "prover_internal.hpp"
 #include "rescue_consts.hpp"
 
@@ -430,6 +431,7 @@ void zk_prover_destroy(zk_prover *p) {
     if (p->h_gather_out) (void)hipHostFree(p->h_gather_out);
     if (p->h_vm) (void)hipHostFree(p->h_vm);
     if (p->sp_h) (void)hipHostFree(p->sp_h);
+    if (p->h_pack) (void)hipHostFree(p->h_pack);
     if (p->ev_verify) (void)hipEventDestroy(p->ev_verify);
     delete p->open;
     delete p;
@@ -541,6 +543,16 @@ int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, 
         if (ms) ms[i] = p->stage_ms[i].second;
     }
     if (count) *count = k;
+    return ZK_OK;
+}
+
+int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols, uint32_t *narrow8_cols,
+                           uint32_t *narrow32_cols) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    if (bytes) *bytes = p->up_bytes;
+    if (sparse_cols) *sparse_cols = p->up_sparse;
+    if (narrow8_cols) *narrow8_cols = p->up_nw8;
+    if (narrow32_cols) *narrow32_cols = p->up_nw32;
     return ZK_OK;
 }
 
@@ -1155,6 +1167,7 @@ static bool upload_plan_incr() {
 // Columns that are contiguous in host memory (zk_prove's single buffer) go up as one copy per run.
 static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c0, int nc) {
     const size_t col = n * sizeof(fe);
+    p->up_bytes += (uint64_t)nc * col;
     for (int c = c0; c < c0 + nc;) {
         int e = c + 1;
         while (e < c0 + nc && src.cols[e] == src.cols[e - 1] + col) e++;
@@ -1181,18 +1194,48 @@ static bool sparse_on() {
     return on;
 }
 
+// Narrow columns (host-resident traces): ZK_NARROW=0 uploads every column whole.
+static bool narrow_on() {
+    static const bool on = [] {
+        const char *e = getenv("ZK_NARROW");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
+// rows [r0, r1) of a host column as `width`-byte integers (1 or 4) at dst + width * row; false if a value does not fit
+static bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8_t *dst) {
+    const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
+    uint64_t over = 0;
+    if (width == 1) {
+        for (size_t i = r0; i < r1; i++) {
+            const uint64_t lo = v[2 * i], hi = v[2 * i + 1];
+            over |= (lo >> 8) | hi;
+            dst[i] = (uint8_t)lo;
+        }
+    } else {
+        uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+        for (size_t i = r0; i < r1; i++) {
+            const uint64_t lo = v[2 * i], hi = v[2 * i + 1];
+            over |= (lo >> 32) | hi;
+            d[i] = (uint32_t)lo;
+        }
+    }
+    return over == 0;
+}
+
 int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp) {
     *sp = nullptr;
     if (!sparse_on() || !pl->lagr) return ZK_OK;
     if (!p->sp_nz) {
-        ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, W));
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, 3 * W));
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_vz, W));
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_vlast, W));
-        ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 2 * W * sizeof(unsigned), hipHostMallocDefault));
+        ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 4 * W * sizeof(unsigned), hipHostMallocDefault));
         ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_verify, hipEventDisableTiming));
     }
-    ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, W * sizeof(unsigned), p->st));
+    ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, 3 * W * sizeof(unsigned), p->st));
     *out = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
     *sp = out;
     return ZK_OK;
@@ -1239,14 +1282,23 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
     // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
     const bool incr = upload_plan_incr();
-    // sparse hint: the columns the previous proof of this length found sparse (hint_ok: prove_impl allows it)
-    const uint32_t hint = (sp && incr && src.hint_ok && p->sp_hint_n == n) ? p->sp_hint : 0u;
+    // hints of the previous proof of this length (hint_ok: prove_impl allows them): its sparse columns, and its narrow
+    // ones (8- or 32-bit values before the last row), which host threads pack while the wide columns go up
+    const bool fresh = sp && incr && src.hint_ok && p->sp_hint_n == n;
+    const uint32_t hint = fresh ? p->sp_hint : 0u;
+    const uint32_t nw8 = fresh && narrow_on() ? p->nw8_hint & ~hint : 0u;
+    const uint32_t nw32 = fresh && narrow_on() ? p->nw32_hint & ~hint & ~nw8 : 0u;
     p->sp_hinted = hint;
-    int dense[W], nd = 0, hin[W], nh = 0;
+    p->up_bytes = 0;
+    p->up_sparse = hint;
+    p->up_nw8 = p->up_nw32 = 0;
+    int dense[W], nd = 0, hin[W], nh = 0, nar[W], nn = 0;
     for (int c = 0; c < W; c++) {
         if ((hint >> c) & 1u) hin[nh++] = c;
+        else if (((nw8 | nw32) >> c) & 1u) nar[nn++] = c;
         else dense[nd++] = c;
     }
+    if (sp) spc.wstride = W;  // width flags for the next proof's narrow hint
     bool ready[W] = {};
     // contiguous runs of a column list: f(first column, count)
     auto runs = [](const int *cols, int k, auto f) -> int {
@@ -1276,6 +1328,14 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             hashed = b;
         }
     };
+    // the kernels of an uploaded column list: detection (flags for the next proof's hints), transforms, hashing
+    auto process = [&](const int *cols, int nc) -> int {
+        if (sp) ZK_TRY(runs(cols, nc, [&](int c0, int k) { sparse_detect(p->st, p->d_trace, n, c0, k, spc); return ZK_OK; }));
+        ZK_TRY(runs(cols, nc, transform));
+        for (int i = 0; i < nc; i++) ready[cols[i]] = true;
+        if (incr) hash_ready(false);
+        return ZK_OK;
+    };
     if (nh) {
         // hinted columns: zero but the last row, whose values the host reads from the trace: their coefficients and
         // LDE are last * e_(n-1)'s (the NTT passes' sparse fill), with nothing uploaded yet
@@ -1286,7 +1346,49 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         ZK_TRY(runs(hin, nh, transform));
         for (int i = 0; i < nh; i++) ready[hin[i]] = true;
     }
-    // upload groups over the dense columns: 4 columns each, the last 4 as 2 + 2 (after the last copy only 2 columns'
+    // narrow columns: packed rows 0 .. n-2 (1 or 4 bytes each) into pinned h_pack by the host pool, one task per
+    // quarter million rows; the latch is waited for on every way out (the tasks read the caller's columns)
+    NarrowCols NC{};
+    size_t pack_bytes = 0;
+    for (int i = 0; i < nn; i++) {
+        NC.col[i] = nar[i];
+        NC.width[i] = ((nw8 >> nar[i]) & 1u) ? 1 : 4;
+        NC.off[i] = pack_bytes;
+        pack_bytes += ((size_t)NC.width[i] * n + 15) & ~(size_t)15;
+    }
+    NC.count = nn;
+    std::atomic<uint32_t> pack_bad{0};
+    Latch packed;
+    struct PackWait {
+        Latch &l;
+        ~PackWait() { l.wait(); }
+    } pack_wait{packed};
+    if (nn) {
+        if (pack_bytes > p->h_pack_cap) {  // the previous proof's copies from it have drained (CopyGuard)
+            if (p->h_pack) (void)hipHostFree(p->h_pack);
+            p->h_pack = nullptr;
+            p->h_pack_cap = 0;
+            ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocDefault));
+            p->h_pack_cap = pack_bytes;
+        }
+        constexpr size_t R = (size_t)1 << 18;
+        const size_t per = (n - 1 + R - 1) / R;
+        packed.reset((int)(per * nn));
+        for (int i = 0; i < nn; i++)
+            for (size_t t = 0; t < per; t++) {
+                const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
+                const uint8_t *col = src.cols[nar[i]];
+                uint8_t *dst = p->h_pack + NC.off[i];
+                const int width = NC.width[i], c = nar[i];
+                const bool tail = r1 == n - 1;
+                HostPool::get().submit([=, &pack_bad, &packed] {
+                    if (!pack_rows(col, r0, r1, width, dst)) pack_bad.fetch_or(1u << c);
+                    if (tail) memset(dst + (size_t)width * (n - 1), 0, width);  // the last row's slot (not read)
+                    packed.count_down();
+                });
+            }
+    }
+    // upload groups over the wide columns: 4 columns each, the last 4 as 2 + 2 (after the last copy only 2 columns'
     // NTTs, the last hash blocks and the Merkle tree remain); legacy: 7 groups of 4, all rows hashed at the end
     int gsz[W], ngroups = 0;
     for (int left = nd; left > 0;) {
@@ -1294,26 +1396,64 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         gsz[ngroups++] = (incr && left == 4) ? 2 : k;
         left -= gsz[ngroups - 1];
     }
-    if (ngroups + (nh ? 1 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
-    int di = 0;
-    for (int g = 0; g < ngroups; g++) {
-        const int *cols = dense + di, nc = gsz[g];
+    if (ngroups + (nn ? 2 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
+    int ev = 0;  // upload events used
+    auto upload_group = [&](const int *cols, int nc) -> int {
         {
             std::lock_guard<std::mutex> lk(*p->up_mu);
             ZK_TRY(runs(cols, nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
-            ZK_CHECK_HIP(hipEventRecord(p->ev_up[g], p->up));
+            ZK_CHECK_HIP(hipEventRecord(p->ev_up[ev], p->up));
         }
-        ZK_TRY(upload_gate(p, p->ev_up[g]));
-        if (sp) ZK_TRY(runs(cols, nc, [&](int c0, int k) { sparse_detect(p->st, p->d_trace, n, c0, k, spc); return ZK_OK; }));
-        ZK_TRY(runs(cols, nc, transform));
-        for (int i = 0; i < nc; i++) ready[cols[i]] = true;
-        di += nc;
-        if (incr) hash_ready(di == nd);
+        ZK_TRY(upload_gate(p, p->ev_up[ev++]));
+        return process(cols, nc);
+    };
+    int fallback[W], nfb = 0;
+    auto narrow_group = [&]() -> int {  // once the packing is done: the packed bytes up, expanded, then processed
+        packed.wait();
+        const uint32_t bad = pack_bad.load();
+        NarrowCols G{};
+        int good[W], ng = 0;
+        for (int i = 0; i < nn; i++) {
+            if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
+                fallback[nfb++] = nar[i];
+                continue;
+            }
+            G.col[G.count] = nar[i];
+            G.width[G.count] = NC.width[i];
+            G.off[G.count] = NC.off[i];
+            memcpy(&G.last[G.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
+            G.count++;
+            good[ng++] = nar[i];
+        }
+        if (!ng) return ZK_OK;
+        uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
+        {
+            std::lock_guard<std::mutex> lk(*p->up_mu);
+            ZK_CHECK_HIP(hipMemcpyAsync(stage, p->h_pack, pack_bytes, hipMemcpyHostToDevice, p->up));
+            p->up_bytes += pack_bytes;
+            for (int i = 0; i < G.count; i++) (G.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << G.col[i];
+            ZK_CHECK_HIP(hipEventRecord(p->ev_up[ev], p->up));
+        }
+        ZK_TRY(upload_gate(p, p->ev_up[ev++]));
+        expand_narrow(p->st, stage, G, n, p->d_trace);
+        return process(good, ng);
+    };
+    bool narrow_done = nn == 0;
+    int di = 0;
+    for (int g = 0; g < ngroups; g++) {
+        if (!narrow_done && packed.ready()) {
+            ZK_TRY(narrow_group());
+            narrow_done = true;
+        }
+        ZK_TRY(upload_group(dense + di, gsz[g]));
+        di += gsz[g];
     }
+    if (!narrow_done) ZK_TRY(narrow_group());
+    if (nfb) ZK_TRY(upload_group(fallback, nfb));
     if (incr) hash_ready(true);
     else hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);
-    if (sp) ZK_TRY(d2h_small(p, p->sp_h + W, p->sp_nz, W * sizeof(unsigned)));  // for the next proof's hint
+    if (sp) ZK_TRY(d2h_small(p, p->sp_h + W, p->sp_nz, 3 * W * sizeof(unsigned)));  // for the next proof's hints
     if (nh) {
         // the hinted columns go up last, verified by a detection on the upload stream (never waited for by the
         // compute stream); prove_impl checks the flags before it returns
@@ -1448,10 +1588,16 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
         if (!p->sp_used) return rc;
     }
     if (rc == ZK_OK || rc == ZK_ERR_DEGREE || rc == ZK_ERR_BUFFER_TOO_SMALL) {
-        uint32_t found = 0;
-        for (int c = 0; c < W; c++)
-            if (((p->sp_hinted >> c) & 1u) ? p->sp_h[c] == 0 : p->sp_h[W + c] == 0) found |= 1u << c;
+        uint32_t found = 0, w8 = 0, w32 = 0;
+        for (int c = 0; c < W; c++) {
+            const bool hinted = (p->sp_hinted >> c) & 1u;
+            if (hinted ? p->sp_h[c] == 0 : p->sp_h[W + c] == 0) found |= 1u << c;
+            else if (!hinted && p->sp_h[2 * W + c] == 0) w8 |= 1u << c;
+            else if (!hinted && p->sp_h[3 * W + c] == 0) w32 |= 1u << c;
+        }
         p->sp_hint = found;
+        p->nw8_hint = w8;
+        p->nw32_hint = w32;
         p->sp_hint_n = n;
     }
     return rc;

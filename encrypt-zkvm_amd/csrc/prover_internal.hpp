@@ -163,7 +163,7 @@ struct zk_prover {
     uint8_t *fri_seed = nullptr;  // device FRI coin state (32 B)
     fe *fri_alphas = nullptr;     // the alphas the device coin drew (2 per layer)
     fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
-    unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries
+    unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries + 2W width flags
     fe *sp_last = nullptr;        // ... and the trace's last row
     // Sparse hint (host-resident traces): the columns the previous proof of the same length found sparse are taken as
     // sparse from their last row alone and uploaded last, off the critical path, where a detection on the upload
@@ -173,8 +173,16 @@ struct zk_prover {
     size_t sp_hint_n = 0;
     unsigned *sp_vz = nullptr;
     fe *sp_vlast = nullptr;
-    unsigned *sp_h = nullptr;       // pinned: [0, W) verification flags, [W, 2W) the trace root flush's nz flags
+    unsigned *sp_h = nullptr;       // pinned: [0, W) verification flags, [W, 4W) the detection's nz and width flags
     hipEvent_t ev_verify = nullptr;
+    // Narrow hint (host-resident traces): columns the previous proof of the same length found to hold 8-bit (nw8) or
+    // 32-bit (nw32) values in rows 0 .. n-2 are packed by host threads (which check every value: a column that does
+    // not fit goes up whole instead) and go up as 1 or 4 bytes per element (h_pack, pinned), expanded on the device
+    uint32_t nw8_hint = 0, nw32_hint = 0;
+    uint64_t up_bytes = 0;                        // zk_prover_upload_stats of the last host-column proof
+    uint32_t up_sparse = 0, up_nw8 = 0, up_nw32 = 0;
+    uint8_t *h_pack = nullptr;
+    size_t h_pack_cap = 0;
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets

@@ -112,8 +112,21 @@ struct SparseCols {
     const fe *last;
     const fe *lagr, *lagr_lde;
     int col0;
+    // width flags (sparse_detect only): wstride > 0 sets nz[wstride + c] when column c has an entry of 8 bits or more
+    // and nz[2 wstride + c] when one of 32 bits or more (last row excluded) -- the next proof's narrow-upload hint
+    int wstride = 0;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
+// Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte
+// integers (1 or 4) at src + off[k], its last row last[k]; written out as field elements into trace column col[k].
+struct NarrowCols {
+    int count;
+    int col[28];
+    int width[28];
+    size_t off[28];
+    fe last[28];
+};
+void expand_narrow(hipStream_t st, const uint8_t *src, const NarrowCols &nc, size_t n, fe *trace);
 
 // NTT of `batch` polynomials of size 2^log_n, each at in + b*in_stride -> out + b*out_stride.
 //   inverse     : use w^-1 (no 1/n scale; fold it into post_scale)

@@ -234,6 +234,11 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
  * ranks, and the number of calls.  Valid once the proof has returned, until the next proof. */
 int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
                              int *count);
+/* The host-to-device trace traffic of the last proof from host columns (zk_prove / zk_prove_columns): bytes copied,
+ * the columns taken as sparse (zero but the last row: their last value only), and the columns uploaded packed as 8-
+ * or 32-bit integers (narrow; each value checked on the host first).  Bit c = trace column c. */
+int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols, uint32_t *narrow8_cols,
+                           uint32_t *narrow32_cols);
 
 /* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
  * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required

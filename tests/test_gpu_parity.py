@@ -566,6 +566,44 @@ def test_sparse_column_detection(gpu, oracle, path):
     assert proof == oproof
 
 
+def test_narrow_columns_learned_and_refuted(oracle):
+    """Narrow columns (a host-resident trace's columns that the previous proof of the same length found to hold 8- or
+    32-bit values before the last row go up packed, each value checked on the host; one that does not fit goes up
+    whole): the proofs of a trace, of the same trace again (packed), and of edits that break the 8-bit and then the
+    32-bit class of a learned column -- each equal to the oracle's, with the upload shrinking once the hint is
+    learned."""
+    trace, pub = workload_trace(ops_for_trace_len(14, "cipher"), seed=16)
+    n = trace.shape[1]
+    small = trace.copy()
+    small[27, : n - 1] = 0
+    small[27, 5:200, 0] = np.arange(5, 200) % 251 + 1  # s15 (read by no constraint): 8-bit values
+    wide8 = small.copy()
+    wide8[27, 77] = [300, 0]                            # no longer 8-bit
+    wide32 = small.copy()
+    wide32[27, 78] = [1 << 40, 0]                       # no longer 32-bit
+    g = GpuProver(0, max_trace_len=n)
+    try:
+        stats = []
+        for t in (trace, trace, small, small, wide8, wide8, wide32, small):
+            proof, _, _, rc = g.prove(t, pub, ProofOptions())
+            assert rc == 0
+            oproof, _, _ = oracle.prove(t, oracle_pub(oracle, pub))
+            assert proof == oproof
+            stats.append(g.upload_stats())
+    finally:
+        g.close()
+    full = 28 * n * 16
+    assert stats[0]["bytes"] == full and not stats[0]["narrow8"]
+    # learned: the bit columns go up as bytes, the clock (20 bits) as 32-bit words, 5 sparse columns not at all
+    assert set(range(1, 7)) <= set(stats[1]["narrow8"]) and 0 in stats[1]["narrow32"]
+    # (the 5 sparse columns still go up, last, for the off-critical-path check of that hint)
+    assert stats[1]["bytes"] < 0.8 * full
+    assert 27 in stats[3]["narrow8"]                   # small: s15 learned as 8-bit
+    assert 27 not in stats[4]["narrow8"] + stats[4]["narrow32"]  # refuted on the host: went up whole
+    assert 27 in stats[5]["narrow32"]                  # relearned as 32-bit
+    assert 27 not in stats[6]["narrow32"]              # refuted again
+
+
 def test_sparse_hint_learned_and_refuted(oracle):
     """The sparse hint (a host-resident trace's columns that the previous proof of the same length found sparse are
     taken as sparse from their last row and verified off the critical path): proofs of a trace, of the same trace
