@@ -18,13 +18,10 @@ print(f"{sys.argv[1]:>14} {b['ms_per_step']:7.3f} steady {b.get('steady_state_ms
       f"vm_prove {v.get('vm_prove_ms')} (lat {v.get('vm_prove_latency_ms')}, same {v.get('vm_prove_same_proof')}) pin {b.get('proof_matches_pin')}")
 PY
 }
-for rep in 1 2; do
-  run q16_own_dev_p4_legacy 16 own device 4 legacy
-  run q16_sh_dev_p4_legacy 16 shared device 4 legacy
-  run q16_sh_dev_p4 16 shared device 4
-  run q16_sh_host_p4 16 shared host 4
-  run q4_own_dev_p4_legacy 4 own device 4 legacy
+for rep in $(seq 1 ${AB_REPS:-2}); do
   run q4_sh_dev_p4 4 shared device 4
   run q4_sh_host_p4 4 shared host 4
   run q4_sh_dev_p3 4 shared device 3
+  run q4_sh_host_p3 4 shared host 3
+  run q4_sh_dev_p2 4 shared device 2
 done
