@@ -447,6 +447,10 @@ struct NttArgs {
     const fe *sp_last, *sp_fill;
     size_t sp_fill_stride;
     int sp_col0;
+    // fused detection (SparseCols::fused, interpolation pass 1): det[det_col0 + column] = 1 when an entry before the
+    // last is nonzero, det[det_stride + ..] when one has 8 bits or more, det[2 det_stride + ..] when 32 or more
+    unsigned *det;
+    int det_col0, det_stride;
     __device__ __forceinline__ bool sparse(uint32_t b) const {
         return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
     }
@@ -499,6 +503,26 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_single(NttArgs 
 // multiplies per 4 points instead of 1, the pre-scale's 4 are gone) and the line constant s_r^k1, folded
 // into the per-coset pass twiddle (s_r w_n^j2)^k1.  Same outputs, 0.25 multiplies and one 16-B table read
 // fewer per element.
+// fused column detection (NttArgs::det): per-thread ORs of the entries a thread loads, flushed once per block
+struct DetAcc {
+    uint32_t any = 0, w8 = 0, w32 = 0;
+    __device__ __forceinline__ void note(fe v) {
+        const uint32_t h = (uint32_t)v.hi | (uint32_t)(v.hi >> 32) | (uint32_t)(v.lo >> 32);
+        w32 |= h;
+        w8 |= h | ((uint32_t)v.lo >> 8);
+        any |= h | (uint32_t)v.lo;
+    }
+};
+__device__ __forceinline__ void det_flush(const NttArgs &a, uint32_t b, const DetAcc &d) {
+    const bool ba = __syncthreads_or(d.any != 0), b8 = __syncthreads_or(d.w8 != 0), b32 = __syncthreads_or(d.w32 != 0);
+    if (threadIdx.x == 0) {
+        const int c = a.det_col0 + (int)(b / (uint32_t)a.ncos);
+        if (ba) a.det[c] = 1u;
+        if (b8 && a.det_stride) a.det[a.det_stride + c] = 1u;
+        if (b32 && a.det_stride) a.det[2 * a.det_stride + c] = 1u;
+    }
+}
+
 template <int LOGM, int TILE, bool CT>
 __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a, int batch) {
     extern __shared__ fe s[];
@@ -534,8 +558,20 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         const fe_ws *stage_ws = CT ? a.cos_stage_ws + (size_t)r * 4096 : a.tw_ws;
         const fe_w2 *stage_w2 = CT ? a.cos_stage_w2 + (size_t)r * 4096 : a.tw_w2;
         using F = Fuse<LOGM, TILE>;
-        first_round_from<LOGM, TILE, CT, F::LAZY>(
-            s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); }, stage_ws);
+        if (!CT && a.det) {  // (uniform) the interpolation of a host trace: detection fused with the tile load
+            DetAcc d;
+            first_round_from<LOGM, TILE, CT, F::LAZY>(
+                s, [&](int line, int k2) {
+                    const size_t k = k1_0 + line + n1 * (size_t)k2;
+                    const fe v = ld_fe(in + k);
+                    if (k != n - 1) d.note(v);
+                    return v;
+                }, stage_ws);
+            det_flush(a, b, d);
+        } else {
+            first_round_from<LOGM, TILE, CT, F::LAZY>(
+                s, [&](int line, int k2) { return ld_fe(in + k1_0 + line + n1 * (size_t)k2); }, stage_ws);
+        }
         r4_rounds<LOGM, TILE, 3, CT, F::STOP, F::LAZY>(s, stage, stage_ws, stage_w2);
         const fe *ptw = CT ? a.cos_pass + (size_t)r * n : a.pass_tw;
         auto store = [&](int line, int j2, fe v) {
@@ -547,10 +583,12 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         return;
       }
     }
+    DetAcc d;
     for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
         int line = e % LPB, k2 = Lds<LOGM, TILE>::load_k(e / LPB);
         size_t k = k1_0 + line + n1 * (size_t)k2;
         fe v = ld_fe(in + k);
+        if (!CT && a.det && k != n - 1) d.note(v);
         if (!CT) {
             if (a.pre_full) v = fe_mul(v, a.pre_full[(size_t)r * a.pre_stride + k]);
             else if (a.pre_lo) v = fe_mul(v, pow_split(a.pre_lo, a.pre_hi, k));
@@ -558,6 +596,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         s[Lds<LOGM, TILE>::idx(line, (int)(__brev((unsigned)k2) >> (32 - LOGM)))] = v;
     }
     __syncthreads();
+    if (!CT && a.det) det_flush(a, b, d);
     if constexpr (CT)
         lds_dft<LOGM, TILE, true>(s, a.cos_stage + (size_t)r * 4096, a.cos_stage_ws + (size_t)r * 4096, a.cos_stage_w2 + (size_t)r * 4096);
     else lds_dft<LOGM, TILE>(s, a.tw4096, a.tw_ws, a.tw_w2);
@@ -751,11 +790,17 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     a.cos_stage_ws = nullptr;
     a.cos_stage_w2 = nullptr;
     if (sp && T.log_n > 12 && inverse && post_scale && fe_eq(*post_scale, T.inv_n)) {  // interpolation
-        a.nz = sp->nz;
-        a.sp_last = sp->last;
-        a.sp_fill = sp->lagr;
-        a.sp_fill_stride = 0;
-        a.sp_col0 = sp->col0;
+        if (sp->fused) {
+            a.det = const_cast<unsigned *>(sp->nz);
+            a.det_col0 = sp->col0;
+            a.det_stride = sp->wstride;
+        } else {
+            a.nz = sp->nz;
+            a.sp_last = sp->last;
+            a.sp_fill = sp->lagr;
+            a.sp_fill_stride = 0;
+            a.sp_col0 = sp->col0;
+        }
     }
     ntt_run(st, a, batch, tmp);
 }
@@ -814,7 +859,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
         a.cos_stage_ws = CT.stage_ws;
         a.cos_stage_w2 = CT.stage_w2;
         a.cos_pass = CT.pass;
-        if (sp) {
+        if (sp && !sp->fused) {
             a.nz = sp->nz;
             a.sp_last = sp->last;
             a.sp_fill = sp->lagr_lde;

@@ -1310,9 +1310,14 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         }
         return ZK_OK;
     };
+    // with the hints learned, the uploaded columns' flags come from the interpolation's pass 1 (no separate pass over
+    // them; a column found sparse there is transformed in full this time and hinted next time)
+    const bool fuse_det = fresh;
+    bool fused_tf = false;
     auto transform = [&](int c0, int nc) -> int {  // interpolation + coset LDE of columns [c0, c0 + nc)
         SparseCols gsp = spc;
         gsp.col0 = c0;
+        gsp.fused = fused_tf;
         ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp,
             sp ? &gsp : nullptr);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
@@ -1330,8 +1335,12 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     };
     // the kernels of an uploaded column list: detection (flags for the next proof's hints), transforms, hashing
     auto process = [&](const int *cols, int nc) -> int {
-        if (sp) ZK_TRY(runs(cols, nc, [&](int c0, int k) { sparse_detect(p->st, p->d_trace, n, c0, k, spc); return ZK_OK; }));
-        ZK_TRY(runs(cols, nc, transform));
+        if (sp && !fuse_det)
+            ZK_TRY(runs(cols, nc, [&](int c0, int k) { sparse_detect(p->st, p->d_trace, n, c0, k, spc); return ZK_OK; }));
+        fused_tf = sp && fuse_det;
+        const int rc = runs(cols, nc, transform);
+        fused_tf = false;
+        ZK_TRY(rc);
         for (int i = 0; i < nc; i++) ready[cols[i]] = true;
         if (incr) hash_ready(false);
         return ZK_OK;

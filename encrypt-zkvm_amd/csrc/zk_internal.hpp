@@ -115,6 +115,10 @@ struct SparseCols {
     // width flags (sparse_detect only): wstride > 0 sets nz[wstride + c] when column c has an entry of 8 bits or more
     // and nz[2 wstride + c] when one of 32 bits or more (last row excluded) -- the next proof's narrow-upload hint
     int wstride = 0;
+    // fused: the interpolation's pass 1 writes the flags (nz, and with wstride the width flags) of the columns it
+    // reads and skips none; the coset LDE then skips none either (host-resident traces once the hints are learned:
+    // no separate detection pass over the uploaded columns)
+    bool fused = false;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
 // Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte
