@@ -14,13 +14,13 @@ host-resident proofs over a 100-proof window: a 20-proof window pays the run's t
 before the first column group is up, fewer co-runners for the last proofs -- about 4 %,
 tools/inflight_timeline.py).
 
-Proofs in flight (--inflight P, default 4): each GPU holds P independent provers (own HBM buffers and
-streams, zk_prover objects) driven by P host threads, so one prover's trace upload, host-side transcript round
-trips and proof tail overlap the others' kernels (host-resident trace, one box: 13.6-13.8 ms per proof at P = 3,
-13.2-13.4 at P = 4, device-resident 12.7-12.9; 16.1 ms at P = 2 with HIP's default 4 hardware queues).  The
-provers' streams are independent; the copy engines already serve their uploads near-FIFO (a cross-prover upload
-order measured neutral, DESIGN.md section 4 dead ends).  The K timed
-steps are K complete proofs, dealt round-robin to the provers; per-proof latency is stage_ms.
+Proofs in flight (--inflight P, default 3): each GPU holds P independent provers (own HBM buffers and
+compute streams, zk_prover objects; one upload stream per device) driven by P host threads, so one prover's trace
+upload, host-side transcript round trips and proof tail overlap the others' kernels.  P + 1 streams fit HIP's
+default 4 hardware queues at P = 3 (A/B at 4 queues, three passes: 11.53-11.56 ms per proof at P = 3, 11.52-11.58
+at P = 2, 11.75-11.79 at P = 4; profiles/r04_ab_queues.txt), so the line needs no GPU_MAX_HW_QUEUES setting
+(queues_ab re-runs it at 16).  The K timed steps are K complete proofs, dealt round-robin to the provers;
+per-proof latency is stage_ms.
 
 Multi-GPU (one process per GPU, torchrun): every rank proves its own independent trace (weak
 scaling, no data-path collective); the driver's barrier + max-over-ranks timing gives the
@@ -341,7 +341,7 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=-1,
                     help="threads of the all-cores CPU sample (-1: the host share, at most 16; 0: skip it)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--inflight", type=int, default=4, help="independent provers (proofs in flight) per GPU")
+    ap.add_argument("--inflight", type=int, default=3, help="independent provers (proofs in flight) per GPU")
     ap.add_argument("--sharded", action="store_true", help="one proof sharded over all ranks (configs[3])")
     ap.add_argument("--sharded-log-n", type=int, default=22,
                     help="trace length of the sharded sub-record that runs when WORLD_SIZE > 1 (0: skip it)")
@@ -352,12 +352,8 @@ def main():
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
     args = ap.parse_args()
-    # Each prover drives two streams (compute, trace upload); with HIP's default of 4 hardware queues per process the
-    # streams of several provers share queues, and a compute stream parked on its upload's event then holds up the
-    # kernels of another prover queued behind it (A/B, 2 provers: 16.1 ms per proof at 4 queues, 14.3 at 8, 13.8 at
-    # 16).  Set before the first HIP call of the process (torch.distributed's included).
-    # (The GPU boxes of this pool export GPU_MAX_HW_QUEUES=4 themselves; an explicit setting is kept and reported.)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    # HIP's hardware queues per process: whatever the environment gives (the runtime's default is 4, which the GPU
+    # boxes of this pool also export); reported in the line, and queues_ab re-runs the workload at the other setting
     if args.sharded:
         return run_sharded(args)
 
@@ -488,7 +484,7 @@ def main():
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
                      zk_verified, pin, all_verified, lifetime) if rank == 0 else None
     if out is not None:
-        out["gpu_max_hw_queues"] = int(os.environ["GPU_MAX_HW_QUEUES"])
+        out["gpu_max_hw_queues"] = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         out["trace_upload"] = upload
     if out is not None and world == 1 and not args.no_compare and not args.ab:
         q = queues_leg(args, P)
@@ -567,7 +563,7 @@ def queues_leg(args, P):
     """The headline configuration re-run in a child process at the OTHER hardware-queue count (GPU_MAX_HW_QUEUES
     4 <-> 16; HIP's default is 4 and this pool's boxes export 4): the design must not depend on a host raising it."""
     import subprocess
-    other = "16" if os.environ.get("GPU_MAX_HW_QUEUES") == "4" else "4"
+    other = "16" if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4" else "4"
     env = dict(os.environ, GPU_MAX_HW_QUEUES=other)
     cmd = [sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", "--no-verify", "--no-compare",
            "--sharded-log-n", "0", "--inflight", str(P), "--steps", str(args.steps), "--log-n", str(args.log_n)]

@@ -298,19 +298,14 @@ static int shared_upload_stream(int device, hipStream_t *st, std::mutex **mu) {
 }
 
 int zk::upload_gate(zk_prover *p, hipEvent_t ev) {
-    static const bool host_gate = [] {
-        const char *e = getenv("ZK_UPLOAD_GATE");
-        return e && !strcmp(e, "host");
-    }();
-    if (host_gate) ZK_CHECK_HIP(hipEventSynchronize(ev));
-    else ZK_CHECK_HIP(hipStreamWaitEvent(p->st, ev, 0));
+    (void)p;
+    ZK_CHECK_HIP(hipEventSynchronize(ev));
     return ZK_OK;
 }
 
 void zk::upload_drain(zk_prover *p) {
     for (auto &e : p->ev_up)
         if (e) (void)hipEventSynchronize(e);
-    if (p->ev_verify) (void)hipEventSynchronize(p->ev_verify);  // the sparse hint's verification upload
 }
 
 // world = 0: a full prover; world = G: one rank of a G-way coset-sharded proof (blowup 8), whose LDE-domain
@@ -337,16 +332,7 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     p->max_n = max_n;
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
-    {
-        const char *e = getenv("ZK_UPLOAD_STREAM");
-        if (e && !strcmp(e, "own")) {
-            ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->up, hipStreamNonBlocking));
-            p->up_owned = true;
-            p->up_mu = new std::mutex();
-        } else {
-            ZK_TRY(shared_upload_stream(device, &p->up, &p->up_mu));
-        }
-    }
+    ZK_TRY(shared_upload_stream(device, &p->up, &p->up_mu));
     for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
@@ -421,10 +407,6 @@ void zk_prover_destroy(zk_prover *p) {
     for (auto &e : p->xchg_pool) (void)hipEventDestroy(e);
     for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
-    if (p->up_owned) {
-        (void)hipStreamDestroy(p->up);
-        delete p->up_mu;
-    }
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
@@ -432,7 +414,6 @@ void zk_prover_destroy(zk_prover *p) {
     if (p->h_vm) (void)hipHostFree(p->h_vm);
     if (p->sp_h) (void)hipHostFree(p->sp_h);
     if (p->h_pack) (void)hipHostFree(p->h_pack);
-    if (p->ev_verify) (void)hipEventDestroy(p->ev_verify);
     delete p->open;
     delete p;
 }
@@ -1145,20 +1126,11 @@ struct TraceSrc {
 // Column groups of a host-resident trace upload.  The copy engine streams group g + 1 while the CUs interpolate and
 // extend group g; more groups overlap more of the copy but add a launch drain per NTT pass and group.  A/B on one box
 // (3 provers in flight): 1 group 12.73-13.02 ms per proof at 22.7 ms latency, 2 groups 13.15-13.24 / 18.7, 4 groups
-// 13.16-13.32 / 16.8, 7 groups of 4 13.02-13.04 / 15.9 (device-resident 12.15-12.32).
-// Round 4 (ZK_UPLOAD_PLAN=incr, the default): the rows are hashed block by block as their columns' LDEs complete
-// (hash_rows_block: a 28-element row is 7 BLAKE3 blocks of 4 columns), and the last 4 columns go up as two groups of
-// 2, so after the last copy only 2 columns' NTTs, one compression per row and the Merkle tree remain.
-// ZK_UPLOAD_PLAN=legacy: 7 groups of 4, all rows hashed after the last group.
-static const int kPlanLegacy[] = {4, 4, 4, 4, 4, 4, 4};
-static const int kPlanIncr[] = {4, 4, 4, 4, 4, 4, 2, 2};
-static bool upload_plan_incr() {
-    static const bool incr = [] {
-        const char *e = getenv("ZK_UPLOAD_PLAN");
-        return !(e && !strcmp(e, "legacy"));
-    }();
-    return incr;
-}
+// 13.16-13.32 / 16.8, 7 groups of 4 13.02-13.04 / 15.9 (device-resident 12.15-12.32).  Round 4: the rows are hashed
+// block by block as their columns' LDEs complete (hash_rows_blocks: a 28-element row is 7 BLAKE3 blocks of 4
+// columns), and the last 4 columns go up as two groups of 2, so after the last copy only 2 columns' NTTs, one
+// compression per row and the Merkle tree remain (latency 15.3-15.4 -> 13.9-14.2 ms against 7 groups of 4, all rows
+// hashed at the end; profiles/r04_ab_queues_pass1.txt).
 
 // hipMemcpyAsync from page-locked memory (zk_host_alloc, zk_host_register, any hipHostMalloc'd or
 // hipHostRegister'ed buffer) is a DMA in stream order; from pageable memory the runtime stages the copy
@@ -1224,16 +1196,21 @@ static bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8
     return over == 0;
 }
 
+// rows [r0, r1) of a host column all zero
+static bool zero_rows(const uint8_t *col, size_t r0, size_t r1) {
+    const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
+    uint64_t any = 0;
+    for (size_t i = 2 * r0; i < 2 * r1; i++) any |= v[i];
+    return any == 0;
+}
+
 int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp) {
     *sp = nullptr;
     if (!sparse_on() || !pl->lagr) return ZK_OK;
     if (!p->sp_nz) {
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, 3 * W));
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
-        ZK_CHECK_HIP(p->arena.alloc(&p->sp_vz, W));
-        ZK_CHECK_HIP(p->arena.alloc(&p->sp_vlast, W));
-        ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 4 * W * sizeof(unsigned), hipHostMallocDefault));
-        ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_verify, hipEventDisableTiming));
+        ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 3 * W * sizeof(unsigned), hipHostMallocDefault));
     }
     ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, 3 * W * sizeof(unsigned), p->st));
     *out = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
@@ -1278,13 +1255,11 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     const size_t B = (size_t)1 << log_b;
     // The device trace buffer is free: the previous proof on this prover returned only after its stream drained
     // (and the trace is read by the interpolation alone).
-    // Group by group: its copies, then its kernels.  From page-locked memory every call returns at once (the
-    // order is immaterial); from pageable memory each copy returns only once the runtime has staged it, so
-    // issuing group g's kernels before group g + 1's copies lets them run while the host stages the next group.
-    const bool incr = upload_plan_incr();
-    // hints of the previous proof of this length (hint_ok: prove_impl allows them): its sparse columns, and its narrow
-    // ones (8- or 32-bit values before the last row), which host threads pack while the wide columns go up
-    const bool fresh = sp && incr && src.hint_ok && p->sp_hint_n == n;
+    // hints of the previous proof of this length (hint_ok: prove_impl allows them): its sparse columns (zero but the
+    // last row: nothing goes up but that value), and its narrow ones (8- or 32-bit values before the last row), which
+    // go up packed.  Host threads check every hinted value while the other columns go up: a narrow column that does
+    // not fit goes up whole, a sparse one that is not sparse voids the proof (prove_impl redoes it without hints).
+    const bool fresh = sp && src.hint_ok && p->sp_hint_n == n;
     const uint32_t hint = fresh ? p->sp_hint : 0u;
     const uint32_t nw8 = fresh && narrow_on() ? p->nw8_hint & ~hint : 0u;
     const uint32_t nw32 = fresh && narrow_on() ? p->nw32_hint & ~hint & ~nw8 : 0u;
@@ -1342,21 +1317,12 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         fused_tf = false;
         ZK_TRY(rc);
         for (int i = 0; i < nc; i++) ready[cols[i]] = true;
-        if (incr) hash_ready(false);
+        hash_ready(false);
         return ZK_OK;
     };
-    if (nh) {
-        // hinted columns: zero but the last row, whose values the host reads from the trace: their coefficients and
-        // LDE are last * e_(n-1)'s (the NTT passes' sparse fill), with nothing uploaded yet
-        fe lastv[W];
-        memset(lastv, 0, sizeof lastv);
-        for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
-        ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
-        ZK_TRY(runs(hin, nh, transform));
-        for (int i = 0; i < nh; i++) ready[hin[i]] = true;
-    }
-    // narrow columns: packed rows 0 .. n-2 (1 or 4 bytes each) into pinned h_pack by the host pool, one task per
-    // quarter million rows; the latch is waited for on every way out (the tasks read the caller's columns)
+    // host checks of the hints: one pool task per quarter million rows of a hinted column, the narrow ones packing
+    // rows 0 .. n-2 (1 or 4 bytes each) into pinned h_pack as they go; the latch is waited for on every way out (the
+    // tasks read the caller's columns)
     NarrowCols NC{};
     size_t pack_bytes = 0;
     for (int i = 0; i < nn; i++) {
@@ -1366,12 +1332,17 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         pack_bytes += ((size_t)NC.width[i] * n + 15) & ~(size_t)15;
     }
     NC.count = nn;
-    std::atomic<uint32_t> pack_bad{0};
-    Latch packed;
+    std::atomic<uint32_t> pack_bad{0}, sparse_bad{0};
+    Latch packed, checked;
     struct PackWait {
-        Latch &l;
-        ~PackWait() { l.wait(); }
-    } pack_wait{packed};
+        Latch &a, &b;
+        ~PackWait() {
+            a.wait();
+            b.wait();
+        }
+    } pack_wait{packed, checked};
+    constexpr size_t R = (size_t)1 << 18;
+    const size_t per = (n - 1 + R - 1) / R;
     if (nn) {
         if (pack_bytes > p->h_pack_cap) {  // the previous proof's copies from it have drained (CopyGuard)
             if (p->h_pack) (void)hipHostFree(p->h_pack);
@@ -1380,8 +1351,6 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocDefault));
             p->h_pack_cap = pack_bytes;
         }
-        constexpr size_t R = (size_t)1 << 18;
-        const size_t per = (n - 1 + R - 1) / R;
         packed.reset((int)(per * nn));
         for (int i = 0; i < nn; i++)
             for (size_t t = 0; t < per; t++) {
@@ -1397,88 +1366,113 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
                 });
             }
     }
-    // upload groups over the wide columns: 4 columns each, the last 4 as 2 + 2 (after the last copy only 2 columns'
-    // NTTs, the last hash blocks and the Merkle tree remain); legacy: 7 groups of 4, all rows hashed at the end
+    if (nh) {
+        checked.reset((int)(per * nh));
+        for (int i = 0; i < nh; i++)
+            for (size_t t = 0; t < per; t++) {
+                const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
+                const uint8_t *col = src.cols[hin[i]];
+                const int c = hin[i];
+                HostPool::get().submit([=, &sparse_bad, &checked] {
+                    if (!zero_rows(col, r0, r1)) sparse_bad.fetch_or(1u << c);
+                    checked.count_down();
+                });
+            }
+        // hinted sparse columns: their coefficients and LDE are last * e_(n-1)'s (the NTT passes' sparse fill)
+        fe lastv[W];
+        memset(lastv, 0, sizeof lastv);
+        for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
+        ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
+        ZK_TRY(runs(hin, nh, transform));
+        for (int i = 0; i < nh; i++) ready[hin[i]] = true;
+    }
+    // Upload items, each one copy (or a run of column copies) and an event on the shared upload stream: the wide
+    // columns in groups of 4, the last 4 as 2 + 2 (after the last copy only 2 columns' NTTs, the last hash blocks and
+    // the Merkle tree remain); the packed narrow columns as soon as the host threads have packed them; narrow columns
+    // that did not fit, whole, last.  The next item's copy is queued before the host waits for the current one's event
+    // (the compute stream never parks on the upload stream: a parked stream would hold up the kernels of other
+    // provers that share its hardware queue), so the copy engine always has the next group.
     int gsz[W], ngroups = 0;
     for (int left = nd; left > 0;) {
-        const int k = !incr ? std::min(4, left) : left > 4 ? 4 : left > 2 ? 2 : left;
-        gsz[ngroups++] = (incr && left == 4) ? 2 : k;
+        const int k = left > 4 ? 4 : left > 2 ? 2 : left;
+        gsz[ngroups++] = left == 4 ? 2 : k;
         left -= gsz[ngroups - 1];
     }
     if (ngroups + (nn ? 2 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
-    int ev = 0;  // upload events used
-    auto upload_group = [&](const int *cols, int nc) -> int {
-        {
-            std::lock_guard<std::mutex> lk(*p->up_mu);
-            ZK_TRY(runs(cols, nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
-            ZK_CHECK_HIP(hipEventRecord(p->ev_up[ev], p->up));
-        }
-        ZK_TRY(upload_gate(p, p->ev_up[ev++]));
-        return process(cols, nc);
+    struct Item {
+        const int *cols = nullptr;
+        int nc = 0;
+        bool narrow = false;
+        int ev = 0;
     };
-    int fallback[W], nfb = 0;
-    auto narrow_group = [&]() -> int {  // once the packing is done: the packed bytes up, expanded, then processed
-        packed.wait();
-        const uint32_t bad = pack_bad.load();
-        NarrowCols G{};
-        int good[W], ng = 0;
-        for (int i = 0; i < nn; i++) {
-            if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
-                fallback[nfb++] = nar[i];
-                continue;
+    int fallback[W], nfb = 0, good[W], ngood = 0, ev = 0, gi = 0, di = 0;
+    bool narrow_done = nn == 0, fb_done = false;
+    NarrowCols G{};
+    uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
+    auto next_item = [&](Item *it) -> bool {
+        if (!narrow_done && (packed.ready() || gi == ngroups)) {
+            packed.wait();
+            narrow_done = true;
+            const uint32_t bad = pack_bad.load();
+            for (int i = 0; i < nn; i++) {
+                if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
+                    fallback[nfb++] = nar[i];
+                    continue;
+                }
+                G.col[G.count] = nar[i];
+                G.width[G.count] = NC.width[i];
+                G.off[G.count] = NC.off[i];
+                memcpy(&G.last[G.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
+                G.count++;
+                good[ngood++] = nar[i];
             }
-            G.col[G.count] = nar[i];
-            G.width[G.count] = NC.width[i];
-            G.off[G.count] = NC.off[i];
-            memcpy(&G.last[G.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
-            G.count++;
-            good[ng++] = nar[i];
+            if (ngood) {
+                *it = Item{good, ngood, true, ev++};
+                return true;
+            }
         }
-        if (!ng) return ZK_OK;
-        uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
-        {
-            std::lock_guard<std::mutex> lk(*p->up_mu);
+        if (gi < ngroups) {
+            *it = Item{dense + di, gsz[gi], false, ev++};
+            di += gsz[gi++];
+            return true;
+        }
+        if (narrow_done && nfb && !fb_done) {
+            fb_done = true;
+            *it = Item{fallback, nfb, false, ev++};
+            return true;
+        }
+        return false;
+    };
+    auto issue = [&](const Item &it) -> int {
+        std::lock_guard<std::mutex> lk(*p->up_mu);
+        if (it.narrow) {
             ZK_CHECK_HIP(hipMemcpyAsync(stage, p->h_pack, pack_bytes, hipMemcpyHostToDevice, p->up));
             p->up_bytes += pack_bytes;
             for (int i = 0; i < G.count; i++) (G.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << G.col[i];
-            ZK_CHECK_HIP(hipEventRecord(p->ev_up[ev], p->up));
+        } else {
+            ZK_TRY(runs(it.cols, it.nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
         }
-        ZK_TRY(upload_gate(p, p->ev_up[ev++]));
-        expand_narrow(p->st, stage, G, n, p->d_trace);
-        return process(good, ng);
+        ZK_CHECK_HIP(hipEventRecord(p->ev_up[it.ev], p->up));
+        return ZK_OK;
     };
-    bool narrow_done = nn == 0;
-    int di = 0;
-    for (int g = 0; g < ngroups; g++) {
-        if (!narrow_done && packed.ready()) {
-            ZK_TRY(narrow_group());
-            narrow_done = true;
-        }
-        ZK_TRY(upload_group(dense + di, gsz[g]));
-        di += gsz[g];
+    Item cur;
+    bool have = next_item(&cur);
+    if (have) ZK_TRY(issue(cur));
+    while (have) {
+        Item nxt;
+        const bool more = next_item(&nxt);
+        if (more) ZK_TRY(issue(nxt));
+        ZK_CHECK_HIP(hipEventSynchronize(p->ev_up[cur.ev]));
+        if (cur.narrow) expand_narrow(p->st, stage, G, n, p->d_trace);
+        ZK_TRY(process(cur.cols, cur.nc));
+        cur = nxt;
+        have = more;
     }
-    if (!narrow_done) ZK_TRY(narrow_group());
-    if (nfb) ZK_TRY(upload_group(fallback, nfb));
-    if (incr) hash_ready(true);
-    else hash_rows_cosets(p->st, p->lde, W, log_n, log_b, 0, log_b, p->leaves);
+    hash_ready(true);
     merkle_tree(p->st, p->leaves, n * B, p->nodes);
-    if (sp) ZK_TRY(d2h_small(p, p->sp_h + W, p->sp_nz, 3 * W * sizeof(unsigned)));  // for the next proof's hints
-    if (nh) {
-        // the hinted columns go up last, verified by a detection on the upload stream (never waited for by the
-        // compute stream); prove_impl checks the flags before it returns
-        std::lock_guard<std::mutex> lk(*p->up_mu);
-        ZK_TRY(runs(hin, nh, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
-        ZK_CHECK_HIP(hipMemsetAsync(p->sp_vz, 0, W * sizeof(unsigned), p->up));
-        const SparseCols vsp{p->sp_vz, p->sp_vlast, nullptr, nullptr, 0};
-        ZK_TRY(runs(hin, nh, [&](int c0, int k) { sparse_detect(p->up, p->d_trace, n, c0, k, vsp); return ZK_OK; }));
-        CopyList L;
-        L.n = 1;
-        L.src[0] = p->sp_vz;
-        L.dst[0] = p->sp_h;
-        L.words[0] = W;
-        ZK_CHECK_HIP(copy_to_host(p->up, L, W));
-        ZK_CHECK_HIP(hipEventRecord(p->ev_verify, p->up));
-    }
+    if (sp) ZK_TRY(d2h_small(p, p->sp_h, p->sp_nz, 3 * W * sizeof(unsigned)));  // for the next proof's hints
+    checked.wait();
+    p->sp_bad = sparse_bad.load();
     return d2h_small(p, root, p->nodes + 32, 32);
 }
 
@@ -1574,35 +1568,33 @@ static int check_ood_identity(const std::vector<fe2> &e, int C, const AirConsts 
 static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump);
 
-// One proof, plus the sparse hint's bookkeeping for host-resident traces: a hinted column that turns out not to be
-// sparse (the upload-stream detection flags it) voids the proof, which is redone without the hint; a completed proof
-// leaves the columns it found sparse as the next proof's hint.
+// One proof, plus the hints' bookkeeping for host-resident traces: a hinted sparse column that the host check finds
+// nonzero voids the proof, which is redone without hints; a completed proof leaves the columns it found sparse and
+// narrow (8- or 32-bit before the last row) as the next proof's hints.
 static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     p->sp_used = false;
     p->sp_hinted = 0;
+    p->sp_bad = 0;
     int rc = prove_once(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
     if (!src.cols || !p->sp_used) return rc;
-    // (prove_once's CopyGuard drained the uploads, the verification's flag copy included)
-    uint32_t bad = 0;
-    for (int c = 0; c < W; c++)
-        if (((p->sp_hinted >> c) & 1u) && p->sp_h[c]) bad |= 1u << c;
-    if (bad) {
-        p->sp_hint = 0;
+    if (p->sp_bad) {
+        p->sp_hint = p->nw8_hint = p->nw32_hint = 0;
         p->sp_hint_n = 0;
         TraceSrc s2 = src;
         s2.hint_ok = false;
         p->sp_used = false;
+        p->sp_bad = 0;
         rc = prove_once(p, s2, n, opt, pub, proof_out, proof_len, rec, dump);
         if (!p->sp_used) return rc;
     }
     if (rc == ZK_OK || rc == ZK_ERR_DEGREE || rc == ZK_ERR_BUFFER_TOO_SMALL) {
+        // (the hinted sparse columns were not detected on the device: their flags stayed 0, and the host checked them)
         uint32_t found = 0, w8 = 0, w32 = 0;
         for (int c = 0; c < W; c++) {
-            const bool hinted = (p->sp_hinted >> c) & 1u;
-            if (hinted ? p->sp_h[c] == 0 : p->sp_h[W + c] == 0) found |= 1u << c;
-            else if (!hinted && p->sp_h[2 * W + c] == 0) w8 |= 1u << c;
-            else if (!hinted && p->sp_h[3 * W + c] == 0) w32 |= 1u << c;
+            if (p->sp_h[c] == 0) found |= 1u << c;
+            else if (p->sp_h[W + c] == 0) w8 |= 1u << c;
+            else if (p->sp_h[2 * W + c] == 0) w32 |= 1u << c;
         }
         p->sp_hint = found;
         p->nw8_hint = w8;

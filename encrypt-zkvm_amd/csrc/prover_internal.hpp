@@ -107,12 +107,12 @@ struct zk_prover {
     int device = 0;
     hipStream_t st = nullptr;
     // upload stream: a host-resident trace goes up here in column groups, each group's event gating its
-    // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it.  By default one
-    // stream per device shared by all its provers (upload_stream: the link is one resource, and the process then
-    // needs P + 1 hardware queues for P provers instead of 2P; ZK_UPLOAD_STREAM=own gives each prover its own).
+    // interpolation and coset LDE on st (trace_lde_commit), so PCIe overlaps the group before it.  One stream per
+    // device shared by all its provers (shared_upload_stream: the link is one resource, and the process then needs
+    // P + 1 hardware queues for P provers instead of 2P; A/B at HIP's default 4 queues: 12.44 vs 12.64 ms per proof
+    // for a stream per prover, profiles/r04_ab_queues_pass1.txt).
     // up_mu orders one prover's (copy, event) pairs against the other provers' on a shared stream.
     hipStream_t up = nullptr;
-    bool up_owned = false;
     std::mutex *up_mu = nullptr;
     // ... each group's event gating its kernels on st.  Measured (tools/ubench/upload_probe.hip): an event recorded
     // between the 16 MiB column copies of one stream halves their rate (29.7 vs 55 GB/s), but not between 112 MiB
@@ -165,24 +165,21 @@ struct zk_prover {
     fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
     unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries + 2W width flags
     fe *sp_last = nullptr;        // ... and the trace's last row
-    // Sparse hint (host-resident traces): the columns the previous proof of the same length found sparse are taken as
-    // sparse from their last row alone and uploaded last, off the critical path, where a detection on the upload
-    // stream verifies them (sp_vz -> pinned sp_h[0..W), event ev_verify); a wrong hint redoes the proof without it
-    uint32_t sp_hint = 0, sp_hinted = 0;
-    bool sp_used = false;  // the last trace_lde_commit ran the sparse detection (its flags are in sp_h)
+    // Hints (host-resident traces, prove_impl): the columns the previous proof of the same length found sparse are
+    // taken as sparse from their last row alone and never uploaded; host threads check them during the proof (sp_bad:
+    // the hinted columns that were not sparse; the proof is then redone without hints)
+    uint32_t sp_hint = 0, sp_hinted = 0, sp_bad = 0;
+    bool sp_used = false;  // the last trace_lde_commit ran the detection (its flags are in sp_h)
     size_t sp_hint_n = 0;
-    unsigned *sp_vz = nullptr;
-    fe *sp_vlast = nullptr;
-    unsigned *sp_h = nullptr;       // pinned: [0, W) verification flags, [W, 4W) the detection's nz and width flags
-    hipEvent_t ev_verify = nullptr;
+    unsigned *sp_h = nullptr;  // pinned: the detection's flags, [0, W) nonzero, [W, 2W) 8-bit, [2W, 3W) 32-bit
     // Narrow hint (host-resident traces): columns the previous proof of the same length found to hold 8-bit (nw8) or
     // 32-bit (nw32) values in rows 0 .. n-2 are packed by host threads (which check every value: a column that does
     // not fit goes up whole instead) and go up as 1 or 4 bytes per element (h_pack, pinned), expanded on the device
     uint32_t nw8_hint = 0, nw32_hint = 0;
-    uint64_t up_bytes = 0;                        // zk_prover_upload_stats of the last host-column proof
-    uint32_t up_sparse = 0, up_nw8 = 0, up_nw32 = 0;
     uint8_t *h_pack = nullptr;
     size_t h_pack_cap = 0;
+    uint64_t up_bytes = 0;                        // zk_prover_upload_stats of the last host-column proof
+    uint32_t up_sparse = 0, up_nw8 = 0, up_nw32 = 0;
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
@@ -224,10 +221,11 @@ struct zk_prover {
 
 namespace zk {
 
-// Upload gating (trace_lde_commit, shard.hip S2): make the compute stream's next kernels wait for upload event ev.
-// ZK_UPLOAD_GATE=host blocks the host thread on the event before it enqueues them (the compute stream never parks on
-// a cross-stream wait, which with fewer hardware queues than streams holds up the kernels of whatever stream shares
-// its queue); the default is a device-side stream wait.
+// Upload gating (trace_lde_commit, shard.hip S2): the host thread waits for upload event ev before it enqueues the
+// kernels that read the group (the next group's copy is already queued).  The compute stream never parks on a
+// cross-stream wait, which with fewer hardware queues than streams holds up the kernels of whatever stream shares its
+// queue (A/B at 4 queues, 4 provers: 11.77 vs 11.99 ms per proof for a device-side stream wait;
+// profiles/r04_ab_queues.txt).
 int upload_gate(zk_prover *p, hipEvent_t ev);
 // wait until every upload this prover has enqueued has completed (the caller's host buffers are free again)
 void upload_drain(zk_prover *p);
