@@ -55,12 +55,6 @@ constexpr int NTT_THREADS = ZK_NTT_THREADS;
 #ifndef ZK_NTT_J0
 #define ZK_NTT_J0 1  // plain-DFT wave-uniform rounds: the waves with j = 0 skip their three unit-twiddle multiplies
 #endif
-#ifndef ZK_NTT_GRP
-#define ZK_NTT_GRP 1  // group-uniform (16 lanes per twiddle) W-set multiplies in the h = 64 round: 1 for 1024-point lines, 2 for every UNI tile
-#endif
-#ifndef ZK_NTT_GRP_LAST
-#define ZK_NTT_GRP_LAST 0  // the same W-set multiplies in the fused last round (4 lanes per twiddle)
-#endif
 #ifndef ZK_NTT_SWZ
 #define ZK_NTT_SWZ 1  // XOR-swizzled LDS tiles (0: one pad element per line)
 #endif
@@ -158,7 +152,9 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         __syncthreads();
         return;
     }
-    if constexpr (L::UNI && ZK_NTT_GRP && (ZK_NTT_GRP == 2 || LOGM == 10) && h == 64) {
+    // (1024-point lines only: on the 2048- and 4096-point tiles of 2^21 .. 2^23 the same mapping measured no gain,
+    // 51.4-51.6 vs 51.6-51.8 ms per 2^22 proof, device-resident 50.3-50.5 vs 50.1-50.3; profiles/r04_ab_grp2_2p22.txt)
+    if constexpr (L::UNI && LOGM == 10 && h == 64) {
         // group-uniform twiddles (h = 64): wave w takes the 4 butterfly classes j = 4w .. 4w+3, one per quarter-wave,
         // each of the 16 (line, group) pairs a 4096-element tile holds (any M of a UNI tile), so the 16 lanes of a
         // quarter-wave share one twiddle and its W set (vector loads of one 64-B entry; fe_mul_wsv, 80 issue slots
@@ -370,22 +366,13 @@ __device__ __forceinline__ void last_round_to(const fe *s, const fe_ws *ws, cons
     const int p = L::idx(line, j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
     const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
     fe t1, t3, u2, u3, a0, a1, a2, a3;
-    if constexpr (ZK_NTT_GRP_LAST && LPB == 4) {
-        // the LPB lanes of one j (its lines) share the twiddle: W sets through vector loads (fe_mul_wsv)
-        const fe_ws W1 = ws[CT ? h + j : j << (12 - LG)];
-        t1 = fe_mul_wsv(x1, W1);
-        t3 = fe_mul_wsv(x3, W1);
-        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        u2 = fe_mul_wsv(a2, ws[CT ? 2 * h + j : j << (11 - LG)]);
-        u3 = fe_mul_wsv(a3, ws[CT ? 3 * h + j : (j + h) << (11 - LG)]);
-    } else {
-        const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
-        t1 = fe_mul_w2(x1, w1);
-        t3 = fe_mul_w2(x3, w1);
-        addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
-        u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
-    }
+    // (W sets through vector loads for the 4 lanes of one j measured within noise: profiles/r04_ab_kernels_2p20.txt)
+    const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
+    t1 = fe_mul_w2(x1, w1);
+    t3 = fe_mul_w2(x3, w1);
+    addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
+    u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
+    u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
     fe o0, o1, o2, o3;
     addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);  // LZ: the store canonicalises (a multiply or fe_canon)
     store(line, j, o0);
@@ -1444,9 +1431,6 @@ struct EvalShared {
 #ifndef ZK_EVAL_WAVES
 #define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
 #endif
-#ifndef ZK_EVAL_STASH
-#define ZK_EVAL_STASH 1  // columns read in two sections (the 5 opcode bits, sponge 7 and 8, next-row s0) go through a
-#endif                   // lane-private LDS slot instead of a second global load (the re-read missed L2: 1.21x traffic)
 #ifndef ZK_EVAL_WAVES_EXT
 #define ZK_EVAL_WAVES_EXT 4  // the two-plane (quadratic extension) variant (4: 128 VGPRs, 9 spills; 3: 142, 0)
 #endif
@@ -1460,9 +1444,11 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
                                                           const fe *divs, const AirConsts *K, const AirConsts *K2,
                                                           size_t plane, fe *comp) {
     __shared__ EvalShared S;
-    // lane-private stash of the columns two sections read (ZK_EVAL_STASH): 8 x 256 x 16 B = 32 KiB per block, so four
+    // lane-private stash of the columns two sections read (the 5 opcode bits, sponge 7 and 8, next-row s0): an LDS
+    // slot instead of a second global load, which missed L2 (PMC: 4.30 GB per launch without, 3.42 with, against
+    // 3.52 GB algorithmic; profiles/r04_pmc_traffic_eval_stash.txt).  8 x 256 x 16 B = 32 KiB per block, so four
     // 256-thread blocks (16 waves, the register budget's 4 per SIMD) still fit a CU's 160 KiB
-    __shared__ fe stash[ZK_EVAL_STASH ? 8 : 1][256];
+    __shared__ fe stash[8][256];
     const int tid = threadIdx.x;
     {
         // one LDS slot per thread, every range bounded on both sides
@@ -1501,7 +1487,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
 #define NXT(c) cb[(size_t)(c)*cs + qn]
     const fe one = fe_one();
     const fe s0n = NXT(12);
-    if (ZK_EVAL_STASH) stash[5][tid] = s0n;
+    stash[5][tid] = s0n;
     fe t = fe_zero();  // sum of coeff_t[k] * C_k (kept reduced: a lazy 288-bit sum here costs 130 spills)
     fe t2 = fe_zero();  // the b-plane sum (KE = 2)
 #define ZK_ACC(k, val)                                                    \
@@ -1517,13 +1503,11 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     // is_push from the flags, so the ten selectors below are never live across it.
     {
         const fe b0 = CUR(5), b1 = CUR(4), b2 = CUR(3), b3 = CUR(2), b4 = CUR(1);
-        if (ZK_EVAL_STASH) {
-            stash[0][tid] = b0;
-            stash[1][tid] = b1;
-            stash[2][tid] = b2;
-            stash[3][tid] = b3;
-            stash[4][tid] = b4;
-        }
+        stash[0][tid] = b0;
+        stash[1][tid] = b1;
+        stash[2][tid] = b2;
+        stash[3][tid] = b3;
+        stash[4][tid] = b4;
         // opcode = 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4  (Horner by doubling: bits are field elements)
         fe opc = b0;
         opc = fe_add(fe_add(opc, opc), b1);
@@ -1539,7 +1523,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const fe c = CUR(7 + k);
-            if (ZK_EVAL_STASH && k < 2) stash[6 + k][tid] = c;
+            if (k < 2) stash[6 + k][tid] = c;
             x[k] = cube(c);
         }
         fe m0[4];
@@ -1577,7 +1561,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         if (KE == 2) t2 = fe_add(t2, fe_mul(sR2, fh));
         ZK_SEQ(cb, t.lo);
         {
-            const fe c7 = ZK_EVAL_STASH ? stash[6][tid] : CUR(7), c8 = ZK_EVAL_STASH ? stash[7][tid] : CUR(8);
+            const fe c7 = stash[6][tid], c8 = stash[7][tid];
             const fe d16 = fe_sub(NXT(7), c7), d17 = fe_sub(NXT(8), c8), n9 = NXT(9), n10 = NXT(10);
             acc288 aC = acc288_zero();
             acc288_madd(aC, S.ct[16], d16);
@@ -1612,12 +1596,10 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
         else ZK_ACC(k, val);                             \
     } while (0)
 #define ZK_SEQS() ZK_SEQ(cb, LZ ? aS.w[0] : (uint32_t)t.lo)
-        const fe b0 = ZK_EVAL_STASH ? stash[0][tid] : CUR(5), b1 = ZK_EVAL_STASH ? stash[1][tid] : CUR(4),
-                 b2 = ZK_EVAL_STASH ? stash[2][tid] : CUR(3), b3 = ZK_EVAL_STASH ? stash[3][tid] : CUR(2),
-                 b4 = ZK_EVAL_STASH ? stash[4][tid] : CUR(1);
+        const fe b0 = stash[0][tid], b1 = stash[1][tid], b2 = stash[2][tid], b3 = stash[3][tid], b4 = stash[4][tid];
         const fe nb0 = fe_sub(one, b0), nb2 = fe_sub(one, b2), nb3 = fe_sub(one, b3), nb4 = fe_sub(one, b4);
         const fe s0 = CUR(12), s1 = CUR(13);
-        const fe s0n = ZK_EVAL_STASH ? stash[5][tid] : NXT(12);  // (shadows the first section's: no live range across)
+        const fe s0n = stash[5][tid];  // (shadows the first section's: no live range across)
         // 0 clock, 2 shift
         ZK_ACCS(0, fe_sub(NXT(0), fe_add(CUR(0), one)));
         const fe b01 = fe_mul(b0, b1);
