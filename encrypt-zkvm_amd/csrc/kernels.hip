@@ -438,6 +438,7 @@ struct NttArgs {
     // last is nonzero, det[det_stride + ..] when one has 8 bits or more, det[2 det_stride + ..] when 32 or more
     unsigned *det;
     int det_col0, det_stride;
+    int sp_all;  // (host) every batch entry is sparse: no pass 1, pass 2 fills only (SparseCols::all)
     __device__ __forceinline__ bool sparse(uint32_t b) const {
         return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
     }
@@ -714,6 +715,11 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
+    if (a.nz && a.sp_all) {  // fills only: read the fill table, write last * fill
+        ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el, 0.0,
+                    hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
+        return;
+    }
     ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) - uniform_mul_discount<LOGM, TILE>(false) + (a.has_post ? 1 : 0)),
                 el * LOGM,
                 hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
@@ -787,6 +793,7 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
             a.sp_fill = sp->lagr;
             a.sp_fill_stride = 0;
             a.sp_col0 = sp->col0;
+            a.sp_all = sp->all;
         }
     }
     ntt_run(st, a, batch, tmp);
@@ -806,7 +813,7 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     a1.out = tmp;
     a1.out_stride = (size_t)1 << L;
     a1.has_post = 0;
-    ZK_DISPATCH_LOGM(log_n2, launch_pass1, st, a1, batch);
+    if (!(a.nz && a.sp_all)) ZK_DISPATCH_LOGM(log_n2, launch_pass1, st, a1, batch);  // (all sparse: pass 1 would skip every block)
     NttArgs a2 = a;
     a2.in = tmp;
     a2.in_stride = (size_t)1 << L;
@@ -852,6 +859,7 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
             a.sp_fill = sp->lagr_lde;
             a.sp_fill_stride = n;
             a.sp_col0 = sp->col0;
+            a.sp_all = sp->all;
         }
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so

@@ -1288,11 +1288,12 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // with the hints learned, the uploaded columns' flags come from the interpolation's pass 1 (no separate pass over
     // them; a column found sparse there is transformed in full this time and hinted next time)
     const bool fuse_det = fresh;
-    bool fused_tf = false;
+    bool fused_tf = false, all_tf = false;
     auto transform = [&](int c0, int nc) -> int {  // interpolation + coset LDE of columns [c0, c0 + nc)
         SparseCols gsp = spc;
         gsp.col0 = c0;
         gsp.fused = fused_tf;
+        gsp.all = all_tf;
         ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n, p->tmp,
             sp ? &gsp : nullptr);
         ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n, B * n, n,
@@ -1383,7 +1384,10 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         memset(lastv, 0, sizeof lastv);
         for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
         ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
-        ZK_TRY(runs(hin, nh, transform));
+        all_tf = true;  // no pass 1: the fills alone
+        const int rc = runs(hin, nh, transform);
+        all_tf = false;
+        ZK_TRY(rc);
         for (int i = 0; i < nh; i++) ready[hin[i]] = true;
     }
     // Upload items, each one copy (or a run of column copies) and an event on the shared upload stream: the wide

@@ -119,6 +119,9 @@ struct SparseCols {
     // reads and skips none; the coset LDE then skips none either (host-resident traces once the hints are learned:
     // no separate detection pass over the uploaded columns)
     bool fused = false;
+    // all: the host knows every column of the call is sparse (the hinted columns of a host trace): pass 1 is not
+    // launched at all, pass 2 only writes last * fill (and the profiler counts that work, not a transform's)
+    bool all = false;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
 // Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte
