@@ -1062,7 +1062,7 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
         }
     }
     // one rank: nothing to shard or exchange, so the single-GPU path proves it (the same proof bytes; its
-    // seven-coset evaluation and coefficient-form assertions only pay off without ranks to balance)
+    // seven-coset evaluation only pays off without ranks to balance: DESIGN.md section 7, round 4)
     if (X.G == 1) return prove_single(X.P[0], trace, n, opt, pub, proof_out, proof_len, rec);
     // drop any staged reads an earlier failed proof left behind, and again on every way out of this one
     std::vector<std::unique_ptr<IoScope>> io_scopes;
