@@ -1397,17 +1397,9 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // (the compute stream never parks on the upload stream: a parked stream would hold up the kernels of other
     // provers that share its hardware queue), so the copy engine always has the next group.
     int gsz[W], ngroups = 0;
-    // ZK_UPLOAD_FIRST = k (1..4): a first group of k columns, so the first kernels start after a shorter copy
-    static const int first_k = [] {
-        const char *e = getenv("ZK_UPLOAD_FIRST");
-        const int v = e ? atoi(e) : 4;
-        return v >= 1 && v <= 4 ? v : 4;
-    }();
+    // (a first group of 1 or 2 columns, so the first kernels start after a shorter copy, measured slower: latency
+    // 13.90-13.95 vs 13.73-13.79 ms, throughput unchanged; profiles/r04h_ab_first_group.txt)
     int left = nd;
-    if (left > 4 + first_k) {
-        gsz[ngroups++] = first_k;
-        left -= first_k;
-    }
     while (left > 0) {
         const int k = left > 4 ? 4 : left > 2 ? 2 : left;
         gsz[ngroups++] = left == 4 ? 2 : k;

@@ -250,8 +250,16 @@ struct FixedCols {
 int sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp);
 int prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inputs *pub, const FixedCols *fx,
                 uint8_t *proof_out, size_t *proof_len);
-// polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip)
+// polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip); B: the LDE
+// cosets held (fx's flde / lagr_lde and lde alike)
 void fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t n, size_t B, fe *polys, fe *lde);
+// zk_prove_sharded, and with `fixed` (one FixedCols per local rank, its own cosets; trace must be null) the sharded
+// proof of zk_vm_prove_sharded's device traces (shard.hip)
+int prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
+                        const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
+                        zk_record *rec, const FixedCols *fixed);
+// the rank of local prover l of a sharded proof over comm
+int shard_rank_of(const zk_comm *comm, int l);
 
 // the single-GPU prove path (prover.hip) for a sharded proof over one rank: trace = host column-major trace, or
 // NULL when it already sits in p->d_trace

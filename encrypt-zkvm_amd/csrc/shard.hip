@@ -262,6 +262,9 @@ struct Ctx {
     std::vector<Plan *> pl;
     int G, Bl, log_n, C;
     size_t n;
+    // zk_vm_prove_sharded: the preprocessed columns of each local rank (its own cosets), or null: the device trace
+    // then holds only the dynamic stack columns 12 .. 12 + md - 1
+    const FixedCols *fixed = nullptr;
 };
 
 
@@ -426,6 +429,25 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, nc, X.rank[l], G, Bl,
                         p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
             }
+        }
+    } else if (X.fixed) {
+        // vm::prove: interpolate and extend only the dynamic stack columns; the program-only columns and the zero
+        // registers from the per-program preprocessed columns of this rank's cosets (one streaming pass)
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            const FixedCols &fx = X.fixed[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            constexpr size_t c0 = 12;
+            if (fx.md > 0) {
+                ntt(p->st, X.pl[l]->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, fx.md, true, nullptr, &inv_n, p->tmp);
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + c0 * n, n, fx.md, X.rank[l], G, Bl,
+                        p->lde + c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+            }
+            if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
+            fe_ws ws[W];
+            for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
+            ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
+            fixed_axpy(p->st, fx, p->fix_ws, n, (size_t)Bl, p->polys, p->lde);
         }
     } else {
         for (int l = 0; l < nlp; l++) {
@@ -1022,7 +1044,16 @@ void zk_comm_destroy(zk_comm *c) { delete c; }
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec) {
+    return zk::prove_sharded_entry(comm, provers, nlocal, trace, n, opt, pub, proof_out, proof_len, rec, nullptr);
+}
+
+int zk::shard_rank_of(const zk_comm *comm, int l) { return comm->loopback() ? l : comm->rank; }
+
+int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
+                            const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
+                            zk_record *rec, const FixedCols *fixed) {
     if (!comm || !provers || !proof_len || nlocal <= 0) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    if (fixed && trace) ZK_FAIL(ZK_ERR_INVALID_ARG, "preprocessed columns go with a device trace");
     if (comm->loopback() ? nlocal != comm->world : nlocal != 1)
         ZK_FAIL(ZK_ERR_INVALID_ARG,
                 "a loopback communicator needs one prover per rank, an RCCL or host-exchange one exactly one");
@@ -1063,7 +1094,10 @@ int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8
     }
     // one rank: nothing to shard or exchange, so the single-GPU path proves it (the same proof bytes; its
     // seven-coset evaluation only pays off without ranks to balance: DESIGN.md section 7, round 4)
-    if (X.G == 1) return prove_single(X.P[0], trace, n, opt, pub, proof_out, proof_len, rec);
+    if (X.G == 1)
+        return fixed ? prove_fixed(X.P[0], n, opt, pub, fixed, proof_out, proof_len)
+                     : prove_single(X.P[0], trace, n, opt, pub, proof_out, proof_len, rec);
+    X.fixed = fixed;
     // drop any staged reads an earlier failed proof left behind, and again on every way out of this one
     std::vector<std::unique_ptr<IoScope>> io_scopes;
     for (auto *p : X.P) {

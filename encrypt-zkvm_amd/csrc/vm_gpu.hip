@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.hpp"
 #include "prover_internal.hpp"
 #include "vm_internal.hpp"
 
@@ -365,25 +366,28 @@ int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const 
 // The preprocessed columns of (prog, lwe_size, blowup) on p's device (zk_program::Fixed), built on first use with
 // this call's inputs: the full trace with a zero last row, its columns 0..11 interpolated and extended, and the
 // Lagrange polynomial of the last row.  Returned by value (the cache may grow while the caller proves).
-int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint32_t B, zk_program::Fixed *out) {
+// r0, rstride: the LDE cosets to hold (a sharded rank's r0 + rstride j, j < B / rstride; 0, 1 for all of them).
+int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint32_t B, zk_program::Fixed *out,
+                  int r0 = 0, int rstride = 1) {
     std::lock_guard<std::mutex> lk(prog->mu);
     zk_program::Device *d = nullptr;
     ZK_TRY(device_program_locked(prog, p->device, &d));
     for (const auto &f : d->fixed)
-        if (f.L == in.L && f.B == B) {
+        if (f.L == in.L && f.B == B && f.r0 == r0 && f.rstride == rstride) {
             *out = f;
             return ZK_OK;
         }
     const size_t n = prog->P.trace_len;
+    const uint32_t nb = B / (uint32_t)rstride;  // cosets held
     Plan *pl = nullptr;
     ZK_TRY(get_plan(p, n, B, &pl));
-    zk_program::Fixed f{in.L, B, 0, nullptr, nullptr, nullptr, nullptr};
+    zk_program::Fixed f{in.L, B, 0, nullptr, nullptr, nullptr, nullptr, r0, rstride};
     ZK_CHECK_HIP(hipMalloc(&f.fpolys, 12 * n * sizeof(fe)));
     d->fixed.push_back(f);  // freed by ~zk_program; completed below
     zk_program::Fixed &g = d->fixed.back();
-    ZK_CHECK_HIP(hipMalloc(&g.flde, 12 * B * n * sizeof(fe)));
+    ZK_CHECK_HIP(hipMalloc(&g.flde, 12 * nb * n * sizeof(fe)));
     ZK_CHECK_HIP(hipMalloc(&g.lagr, n * sizeof(fe)));
-    ZK_CHECK_HIP(hipMalloc(&g.lagr_lde, B * n * sizeof(fe)));
+    ZK_CHECK_HIP(hipMalloc(&g.lagr_lde, nb * n * sizeof(fe)));
     // f_0 .. f_11: the program-only columns with the last row zeroed
     fe zero[28], outs[NREG];
     memset(zero, 0, sizeof zero);
@@ -393,13 +397,13 @@ int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint
     ZK_TRY(vm_generate(p, prog, in, zero, GenMode{true, NREG}, &nn, outs, &md, &dp));
     const fe inv_n = h_inv(fe_make(n));
     ntt(p->st, pl->Tn, p->d_trace, n, g.fpolys, n, 12, true, nullptr, &inv_n, p->tmp);
-    ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, 0, 1, (int)B, g.flde, B * n, n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, r0, rstride, (int)nb, g.flde, nb * n, n, p->tmp);
     // e_(n-1): zeros but a one in the last row
     ZK_CHECK_HIP(hipMemsetAsync(p->polys, 0, n * sizeof(fe), p->st));
     const fe one = fe_one();
     ZK_TRY(h2d_small(p, p->polys + (n - 1), &one, sizeof one));
     ntt(p->st, pl->Tn, p->polys, n, g.lagr, n, 1, true, nullptr, &inv_n, p->tmp);
-    ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, 0, 1, (int)B, g.lagr_lde, B * n, n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, r0, rstride, (int)nb, g.lagr_lde, nb * n, n, p->tmp);
     ZK_TRY(io_rewind(p));  // sync: the cache is complete, the staging area starts over
     g.md = (int)md;
     *out = g;
@@ -521,11 +525,31 @@ int zk_vm_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, zk_progr
     fe outs[NREG], last[28];
     read_last(last_row, last);
     size_t n = 0;
+    const int G = comm->world;
+    // ZK_VM_PREPROCESS=0: every column from the device trace, as zk_vm_prove
+    const char *pe = getenv("ZK_VM_PREPROCESS");
+    const bool pre = !(pe && !strcmp(pe, "0")) && opt->blowup == 8 && (G == 1 || G == 2 || G == 4 || G == 8);
+    std::vector<FixedCols> fx(pre ? nlocal : 0);
     // Processor::run + trace on every local rank, each into its own trace buffer (the loopback communicator drives
-    // several ranks from one process; one RCCL process holds one)
+    // several ranks from one process; one RCCL process holds one); with the preprocessed columns (built once per
+    // program and rank, for the rank's own cosets) only the stack registers the program uses are generated
     for (int l = 0; l < nlocal; l++) {
         size_t nl = 0;
-        ZK_TRY(vm_generate(provers[l], prog, in, last, GenMode{true, NREG}, &nl, outs, nullptr));
+        if (pre) {
+            zk_program::Fixed f{};
+            ZK_TRY(fixed_columns(provers[l], prog, in, opt->blowup, &f, shard_rank_of(comm, l), G));
+            uint32_t md = 0;
+            ZK_TRY(vm_generate(provers[l], prog, in, last, GenMode{false, f.md}, &nl, outs, &md));
+            if ((int)md != f.md) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the stack depth depends on the inputs");
+            fx[l].md = f.md;
+            fx[l].fpolys = f.fpolys;
+            fx[l].flde = f.flde;
+            fx[l].lagr = f.lagr;
+            fx[l].lagr_lde = f.lagr_lde;
+            memcpy(fx[l].last, last, sizeof fx[l].last);
+        } else {
+            ZK_TRY(vm_generate(provers[l], prog, in, last, GenMode{true, NREG}, &nl, outs, nullptr));
+        }
         n = nl;
     }
     zk_pub_inputs pub;
@@ -537,7 +561,8 @@ int zk_vm_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, zk_progr
     pub.delta = delta;
     if (outputs) memcpy(outputs, pub.stack_outputs, sizeof pub.stack_outputs);
     if (program_hash) memcpy(program_hash, pub.program_hash, sizeof pub.program_hash);
-    return zk_prove_sharded(comm, provers, nlocal, nullptr, n, opt, &pub, proof_out, proof_len, nullptr);
+    return prove_sharded_entry(comm, provers, nlocal, nullptr, n, opt, &pub, proof_out, proof_len, nullptr,
+                               pre ? fx.data() : nullptr);
 }
 
 // diagnostics: the host stack pass's states every `stride` rows (CPU tests check them against host-written traces)

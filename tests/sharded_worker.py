@@ -118,6 +118,21 @@ def main():
             proof, _ = sp.prove(trace, pub, opts)
             res[name] = {"sha256": hashlib.sha256(proof).hexdigest(), "want": want, "bytes": len(proof)}
             print(f"rank {rank}/{world} {name}: {len(proof)} B", flush=True)
+        # vm::prove sharded (zk_vm_prove_sharded): this rank writes the 2^16 job's trace into its own HBM and builds the
+        # preprocessed columns of its own cosets; the proof must equal the host-trace job's
+        from zkvm_amd.prover import Program, ProofOptions
+        from zkvm_amd.workloads import make_workload, ops_for_trace_len
+        src = ops_for_trace_len(16, "cipher")
+        w = make_workload(src, seed=31 + 16)
+        prog = Program(src)
+        try:
+            for k in range(2):  # the second call reuses the rank's preprocessed columns
+                _, _, proof = sp.prove_program(prog, Program.encode_inputs(w.public, w.secret, w.server_key),
+                                               w.last_row, ProofOptions())
+                res[f"vm_cipher_2p16_call{k}"] = {"sha256": hashlib.sha256(proof).hexdigest(),
+                                                  "want": res["cipher_2p16_ext1"]["want"], "bytes": len(proof)}
+        finally:
+            prog.close()
     finally:
         sp.close()
     (out / f"rank{rank}.json").write_text(json.dumps(res))

@@ -138,11 +138,15 @@ def test_sharded_rejects_bad_world():
 # ---------------------------------------------------------------- full-size pins, sharded
 from golden_large import LARGE_CASES, check_large_proof, large_inputs  # noqa: E402
 @pytest.mark.gpu
-@pytest.mark.parametrize("log_n,world,ext", [(14, 2, 1), (14, 8, 2), (16, 8, 1), (16, 4, 2)])
-def test_sharded_vm_prove(log_n, world, ext):
+@pytest.mark.parametrize("log_n,world,ext,pre", [(14, 2, 1, True), (14, 8, 2, True), (16, 8, 1, True), (16, 4, 2, True),
+                                                 (16, 1, 1, True), (16, 8, 1, False), (14, 2, 2, False)])
+def test_sharded_vm_prove(log_n, world, ext, pre, monkeypatch):
     """vm::prove sharded (zk_vm_prove_sharded): every loopback rank writes the trace on its own device buffer, then
-    one sharded proof over them -- sparse columns (zero but the last row) and the assertion terms split by
-    coefficient range are both on at these sizes.  The bytes equal the single-GPU proof of the host trace."""
+    one sharded proof over them -- with the per-program preprocessed columns of each rank's own cosets (the default;
+    pre=False: every column from the device trace, ZK_VM_PREPROCESS=0), and the assertion terms split by coefficient
+    range.  The bytes equal the single-GPU proof of the host trace; a second call reuses the preprocessed columns."""
+    if not pre:
+        monkeypatch.setenv("ZK_VM_PREPROCESS", "0")
     from zkvm_amd.prover import Program
     from zkvm_amd.workloads import make_workload, ops_for_trace_len
     src = ops_for_trace_len(log_n, "cipher")
@@ -162,6 +166,7 @@ def test_sharded_vm_prove(log_n, world, ext):
     try:
         h, outs, got = sp.prove_program(prog, inp, w.last_row, opts)
         assert h == list(prog.hash) and outs == list(outputs)
+        assert sp.prove_program(prog, inp, w.last_row, opts)[2] == got
         with pytest.raises(native.ZkError):  # the last row must be given: every rank writes the same trace
             native.check(native.lib().zk_vm_prove_sharded(sp.comm, None, 0, prog.handle, None, 0, None, 0, 4, 1,
                                                           None, None, None, None, None, None))
