@@ -438,7 +438,7 @@ struct NttArgs {
     // last is nonzero, det[det_stride + ..] when one has 8 bits or more, det[2 det_stride + ..] when 32 or more
     unsigned *det;
     int det_col0, det_stride;
-    int sp_all;  // (host) every batch entry is sparse: no pass 1, pass 2 fills only (SparseCols::all)
+    int sp_all;  // (host) every batch entry is sparse: no transform, one fill pass (SparseCols::all, k_sparse_fill)
     __device__ __forceinline__ bool sparse(uint32_t b) const {
         return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
     }
@@ -715,11 +715,6 @@ static void launch_pass2(hipStream_t st, const NttArgs &a, int batch) {
     size_t sh = Lds<LOGM, TILE>::bytes();
     hipFuncSetAttribute((const void *)ntt_pass2<LOGM, TILE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const double el = (double)batch * ((size_t)1 << a.log_n);
-    if (a.nz && a.sp_all) {  // fills only: read the fill table, write last * fill
-        ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el, 0.0,
-                    hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
-        return;
-    }
     ZK_PROF_OPS(st, "ntt_pass2", 32.0 * el, el * (dft_muls_per_elem(LOGM) - uniform_mul_discount<LOGM, TILE>(false) + (a.has_post ? 1 : 0)),
                 el * LOGM,
                 hipLaunchKernelGGL((ntt_pass2<LOGM, TILE>), dim3(cdiv(n2, LPB), batch), dim3(NTT_THREADS), sh, st, a));
@@ -799,10 +794,32 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
     ntt_run(st, a, batch, tmp);
 }
 
+// Sparse columns the host knows of (SparseCols::all: the hinted columns of a host trace): the transform of column c
+// is last[c] * fill (fill: the transform of e_(n-1), coset r's at fill + r * fill_stride), so one streaming pass reads
+// each fill value once and writes it scaled into every column of the batch (instead of a pass-2 launch that re-read
+// the fill per column: 32 B per output element -> 16 + 16 / ncols)
+__global__ void __launch_bounds__(256) k_sparse_fill(NttArgs a, int ncols, int log_n) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)a.ncos << log_n)) return;
+    const uint32_t j = (uint32_t)(t >> log_n);
+    const size_t k = t & (n - 1);
+    const fe f = a.sp_fill[(size_t)a.coset_of(j) * a.sp_fill_stride + k];
+    fe *o = a.out + (size_t)j * a.out_jstride + k;
+    for (int c = 0; c < ncols; c++) o[(size_t)c * a.out_stride] = fe_mul(a.sp_last[a.sp_col0 + c], f);
+}
+
 // the passes of one NTT call (single pass for n <= 4096, else four-step through tmp)
 void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     constexpr int TILE = ZK_NTT_TILE;
     const int L = a.log_n;
+    if (a.nz && a.sp_all) {
+        const int ncols = batch / a.ncos;
+        const double pts = (double)a.ncos * (double)((size_t)1 << L);
+        ZK_PROF_OPS(st, "sparse_fill", 16.0 * pts * (1 + ncols), pts * ncols, 0.0,
+                    hipLaunchKernelGGL(k_sparse_fill, dim3(cdiv((size_t)a.ncos << L, 256)), dim3(256), 0, st, a, ncols, L));
+        return;
+    }
     if (L <= 12) {
         ZK_DISPATCH_LOGM(L, launch_single, st, a, batch);
         return;
@@ -813,7 +830,7 @@ void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     a1.out = tmp;
     a1.out_stride = (size_t)1 << L;
     a1.has_post = 0;
-    if (!(a.nz && a.sp_all)) ZK_DISPATCH_LOGM(log_n2, launch_pass1, st, a1, batch);  // (all sparse: pass 1 would skip every block)
+    ZK_DISPATCH_LOGM(log_n2, launch_pass1, st, a1, batch);
     NttArgs a2 = a;
     a2.in = tmp;
     a2.in_stride = (size_t)1 << L;
