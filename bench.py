@@ -455,7 +455,8 @@ def main():
     gpu.profile(False)
     upst = gpu.upload_stats()  # that proof's trace upload (sparse / narrow hints learned from the proofs before it)
     upload = {"mb_per_proof": round(upst["bytes"] / 2**20, 1), "full_trace_mb": round(28 * n * 16 / 2**20, 1),
-              "sparse_cols": upst["sparse"], "narrow8_cols": upst["narrow8"], "narrow32_cols": upst["narrow32"]}
+              "sparse_cols": upst["sparse"], "narrow8_cols": upst["narrow8"], "narrow32_cols": upst["narrow32"],
+              "derived_cols": upst["derived"]}
 
     verified = None
     if rank == 0 and not args.no_verify:

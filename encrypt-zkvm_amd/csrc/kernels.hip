@@ -809,6 +809,17 @@ __global__ void __launch_bounds__(256) k_sparse_fill(NttArgs a, int ncols, int l
     for (int c = 0; c < ncols; c++) o[(size_t)c * a.out_stride] = fe_mul(a.sp_last[a.sp_col0 + c], f);
 }
 
+// out[i] = F[i] + d * L[i], d wave-uniform (its W set a kernel argument): the clock column's coefficients / LDE from the
+// identity column's and e_(n-1)'s (trace_lde_commit)
+__global__ void __launch_bounds__(256) k_axpy_fill(const fe *F, const fe *L, fe_ws d, size_t cnt, fe *out) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i < cnt) out[i] = fe_add(F[i], fe_mul_uniform(L[i], d));
+}
+void axpy_fill(hipStream_t st, const fe *F, const fe *L, const fe_ws &d, size_t cnt, fe *out) {
+    ZK_PROF_OPS(st, "sparse_fill", 48.0 * cnt, (double)cnt, (double)cnt,
+                hipLaunchKernelGGL(k_axpy_fill, dim3(cdiv(cnt, 256)), dim3(256), 0, st, F, L, d, cnt, out));
+}
+
 // the passes of one NTT call (single pass for n <= 4096, else four-step through tmp)
 void ntt_run(hipStream_t st, const NttArgs &a, int batch, fe *tmp) {
     constexpr int TILE = ZK_NTT_TILE;

@@ -537,6 +537,12 @@ int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols,
     return ZK_OK;
 }
 
+int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols) {
+    if (!p || !derived_cols) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    *derived_cols = p->clk_used ? 1u : 0u;
+    return ZK_OK;
+}
+
 int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
                              int *count) {
     if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
@@ -1175,6 +1181,48 @@ static bool narrow_on() {
     return on;
 }
 
+// The AIR clock (ZK_CLOCK=0 turns its derivation off)
+static bool clock_on() {
+    static const bool on = [] {
+        const char *e = getenv("ZK_CLOCK");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
+// the identity column 0, 1, ..., n-1 interpolated and extended over the B cosets (Plan::id_poly / id_lde), once per plan
+static int clock_tables(zk_prover *p, Plan *pl) {
+    if (pl->id_poly) return ZK_OK;
+    const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b;
+    fe *poly = nullptr, *lde = nullptr;
+    ZK_CHECK_HIP(p->arena.alloc(&poly, n));
+    ZK_CHECK_HIP(p->arena.alloc(&lde, B * n));
+    std::vector<fe> id(n);
+    for (size_t i = 0; i < n; i++) id[i] = fe_make(i);
+    fe *d = nullptr;
+    ZK_CHECK_HIP(hipMalloc(&d, n * sizeof(fe)));
+    hipError_t err = hipMemcpy(d, id.data(), n * sizeof(fe), hipMemcpyHostToDevice);
+    if (err == hipSuccess) {
+        const fe inv_n = h_inv(fe_make(n));
+        ntt(p->st, pl->Tn, d, n, poly, n, 1, true, nullptr, &inv_n, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, poly, n, 1, 0, 1, (int)B, lde, B * n, n, p->tmp);
+        err = hipStreamSynchronize(p->st);
+    }
+    (void)hipFree(d);
+    ZK_CHECK_HIP(err);
+    pl->id_poly = poly;
+    pl->id_lde = lde;
+    return ZK_OK;
+}
+
+// rows [r0, r1) of a host column: row i holds i (the AIR clock)
+static bool clock_rows(const uint8_t *col, size_t r0, size_t r1) {
+    const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
+    uint64_t bad = 0;
+    for (size_t i = r0; i < r1; i++) bad |= (v[2 * i] ^ (uint64_t)i) | v[2 * i + 1];
+    return bad == 0;
+}
+
 // rows [r0, r1) of a host column as `width`-byte integers (1 or 4) at dst + width * row; false if a value does not fit
 static bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8_t *dst) {
     const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
@@ -1262,13 +1310,23 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     const bool fresh = sp && src.hint_ok && p->sp_hint_n == n;
     const uint32_t hint = fresh ? p->sp_hint : 0u;
     const uint32_t nw8 = fresh && narrow_on() ? p->nw8_hint & ~hint : 0u;
-    const uint32_t nw32 = fresh && narrow_on() ? p->nw32_hint & ~hint & ~nw8 : 0u;
+    uint32_t nw32 = fresh && narrow_on() ? p->nw32_hint & ~hint & ~nw8 : 0u;
+    // The AIR clock: constraint 0 (clk' = clk + 1, air/src/constrains.rs) and the assertion clk[0] = 0 force rows
+    // 0 .. n-2 of column 0 of any trace the AIR accepts to 0 .. n-2, so its interpolant and LDE are the identity
+    // column's (per plan) plus (last - (n - 1)) times e_(n-1)'s: no upload, no transform.  Taken once the previous
+    // proof found column 0 narrow (32-bit), checked by host threads while the other columns go up; a column that is
+    // not 0 .. n-2 voids the proof, which is redone without hints (and this length is not speculated again).
+    const bool clk = fresh && clock_on() && (nw32 & 1u) && p->clk_off_n != n;
+    if (clk) nw32 &= ~1u;
+    p->clk_used = clk;
+    p->clk_bad = false;
     p->sp_hinted = hint;
     p->up_bytes = 0;
     p->up_sparse = hint;
     p->up_nw8 = p->up_nw32 = 0;
     int dense[W], nd = 0, hin[W], nh = 0, nar[W], nn = 0;
     for (int c = 0; c < W; c++) {
+        if (clk && c == 0) continue;
         if ((hint >> c) & 1u) hin[nh++] = c;
         else if (((nw8 | nw32) >> c) & 1u) nar[nn++] = c;
         else dense[nd++] = c;
@@ -1333,15 +1391,16 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         pack_bytes += ((size_t)NC.width[i] * n + 15) & ~(size_t)15;
     }
     NC.count = nn;
-    std::atomic<uint32_t> pack_bad{0}, sparse_bad{0};
-    Latch packed, checked;
+    std::atomic<uint32_t> pack_bad{0}, sparse_bad{0}, clock_bad{0};
+    Latch packed, checked, clocked;
     struct PackWait {
-        Latch &a, &b;
+        Latch &a, &b, &c;
         ~PackWait() {
             a.wait();
             b.wait();
+            c.wait();
         }
-    } pack_wait{packed, checked};
+    } pack_wait{packed, checked, clocked};
     constexpr size_t R = (size_t)1 << 18;
     const size_t per = (n - 1 + R - 1) / R;
     if (nn) {
@@ -1384,11 +1443,29 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         memset(lastv, 0, sizeof lastv);
         for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
         ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
-        all_tf = true;  // no pass 1: the fills alone
+        all_tf = true;  // no transform: the fills alone
         const int rc = runs(hin, nh, transform);
         all_tf = false;
         ZK_TRY(rc);
         for (int i = 0; i < nh; i++) ready[hin[i]] = true;
+    }
+    if (clk) {
+        ZK_TRY(clock_tables(p, pl));
+        clocked.reset((int)per);
+        const uint8_t *col = src.cols[0];
+        for (size_t t = 0; t < per; t++) {
+            const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
+            HostPool::get().submit([=, &clock_bad, &clocked] {
+                if (!clock_rows(col, r0, r1)) clock_bad.store(1u);
+                clocked.count_down();
+            });
+        }
+        fe last0;
+        memcpy(&last0, col + (n - 1) * sizeof(fe), sizeof(fe));
+        const fe_ws d = make_fe_ws(fe_sub(last0, fe_make(n - 1)));
+        axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
+        axpy_fill(p->st, pl->id_lde, pl->lagr_lde, d, B * n, p->lde);
+        ready[0] = true;
     }
     // Upload items, each one copy (or a run of column copies) and an event on the shared upload stream: the wide
     // columns in groups of 4, the last 4 as 2 + 2 (after the last copy only 2 columns' NTTs, the last hash blocks and
@@ -1479,7 +1556,9 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     merkle_tree(p->st, p->leaves, n * B, p->nodes);
     if (sp) ZK_TRY(d2h_small(p, p->sp_h, p->sp_nz, 3 * W * sizeof(unsigned)));  // for the next proof's hints
     checked.wait();
+    clocked.wait();
     p->sp_bad = sparse_bad.load();
+    p->clk_bad = clock_bad.load() != 0;
     return d2h_small(p, root, p->nodes + 32, 32);
 }
 
@@ -1583,9 +1662,12 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     p->sp_used = false;
     p->sp_hinted = 0;
     p->sp_bad = 0;
+    p->clk_used = p->clk_bad = false;
     int rc = prove_once(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
     if (!src.cols || !p->sp_used) return rc;
-    if (p->sp_bad) {
+    if (p->sp_bad || p->clk_bad) {
+        if (p->clk_bad) p->clk_off_n = n;
+        p->clk_used = p->clk_bad = false;
         p->sp_hint = p->nw8_hint = p->nw32_hint = 0;
         p->sp_hint_n = 0;
         TraceSrc s2 = src;
@@ -1602,6 +1684,11 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
             if (p->sp_h[c] == 0) found |= 1u << c;
             else if (p->sp_h[W + c] == 0) w8 |= 1u << c;
             else if (p->sp_h[2 * W + c] == 0) w32 |= 1u << c;
+        }
+        if (p->clk_used) {  // (its flags were not detected on the device) the clock stays in the 32-bit class
+            found &= ~1u;
+            w8 &= ~1u;
+            w32 |= 1u;
         }
         p->sp_hint = found;
         p->nw8_hint = w8;

@@ -93,6 +93,9 @@ struct Plan {  // everything that depends only on (n, B)
     // four-step plans: the interpolant of e_(n-1) (n coefficients) and its coset LDE (B n, coset-major) -- what a
     // trace column that is zero but in its random last row interpolates and extends to, times that row (SparseCols)
     fe *lagr = nullptr, *lagr_lde = nullptr;
+    // ... and the column 0, 1, ..., n-1's (the AIR clock of a valid trace but for its random last row), built on first
+    // use (clock_tables)
+    fe *id_poly = nullptr, *id_lde = nullptr;
 };
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
 // the evaluator's divisor tables for the 8 CE cosets (divisor_tables: 3 planes of 8n), built once per plan
@@ -180,6 +183,11 @@ struct zk_prover {
     size_t h_pack_cap = 0;
     uint64_t up_bytes = 0;                        // zk_prover_upload_stats of the last host-column proof
     uint32_t up_sparse = 0, up_nw8 = 0, up_nw32 = 0;
+    // Clock column (host-resident traces, trace_lde_commit): column 0 derived from the AIR's clock instead of
+    // uploaded and transformed (clk_used: the last proof did; clk_bad: the host check refuted it; clk_off_n: a length
+    // whose traces refuted it, not speculated again)
+    bool clk_used = false, clk_bad = false;
+    size_t clk_off_n = 0;
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets

@@ -119,8 +119,8 @@ struct SparseCols {
     // reads and skips none; the coset LDE then skips none either (host-resident traces once the hints are learned:
     // no separate detection pass over the uploaded columns)
     bool fused = false;
-    // all: the host knows every column of the call is sparse (the hinted columns of a host trace): pass 1 is not
-    // launched at all, pass 2 only writes last * fill (and the profiler counts that work, not a transform's)
+    // all: the host knows every column of the call is sparse (the hinted columns of a host trace): no transform is
+    // launched, one streaming pass writes last * fill into every column (k_sparse_fill)
     bool all = false;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
@@ -159,6 +159,8 @@ struct CosetTables {
 void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe *in, size_t in_stride, int ncols,
              int r0, int rstride, int ncos, fe *out, size_t out_cstride, size_t out_jstride, fe *tmp,
              const SparseCols *sp = nullptr);
+// out[i] = F[i] + d * L[i] for i < cnt (d given by its W set)
+void axpy_fill(hipStream_t st, const fe *F, const fe *L, const fe_ws &d, size_t cnt, fe *out);
 
 // grinding: atomicMin into *best_dev of the nonces in [start, start+count) with >= bits trailing zeros
 void grind_launch(hipStream_t st, const uint32_t *seed_dev, uint64_t start, uint32_t count, int bits,

@@ -167,13 +167,16 @@ class GpuProver:
         return {names[i].decode(): ms[i] for i in range(min(cnt.value, 32))}
 
     def upload_stats(self) -> dict:
-        """The last host-column proof's trace upload (zk_prover_upload_stats): bytes, and the columns taken as sparse
-        or uploaded packed as 8- / 32-bit integers."""
+        """The last host-column proof's trace upload (zk_prover_upload_stats): bytes, and the columns taken as sparse,
+        uploaded packed as 8- / 32-bit integers, or derived from the AIR (the clock, zk_prover_upload_derived)."""
         b = C.c_uint64(0)
         sp, n8, n32 = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
         check(lib().zk_prover_upload_stats(self.handle, C.byref(b), C.byref(sp), C.byref(n8), C.byref(n32)))
+        dv = C.c_uint32(0)
+        check(lib().zk_prover_upload_derived(self.handle, C.byref(dv)))
         cols = lambda m: [c for c in range(28) if (m >> c) & 1]  # noqa: E731
-        return {"bytes": b.value, "sparse": cols(sp.value), "narrow8": cols(n8.value), "narrow32": cols(n32.value)}
+        return {"bytes": b.value, "sparse": cols(sp.value), "narrow8": cols(n8.value), "narrow32": cols(n32.value),
+                "derived": cols(dv.value)}
 
     def profile(self, on: bool):
         check(lib().zk_prover_profile(self.handle, 1 if on else 0))

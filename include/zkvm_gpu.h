@@ -239,6 +239,10 @@ int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double
  * or 32-bit integers (narrow; each value checked on the host first).  Bit c = trace column c. */
 int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols, uint32_t *narrow8_cols,
                            uint32_t *narrow32_cols);
+/* the columns of the last host-column proof that were derived from the AIR instead of uploaded and transformed: bit 0,
+ * the clock (rows 0 .. n-2 of any accepted trace hold 0 .. n-2: air/src/constrains.rs clock constraint and the
+ * clk[0] = 0 assertion), checked against the caller's column by host threads */
+int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols);
 
 /* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
  * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required

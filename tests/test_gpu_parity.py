@@ -594,17 +594,48 @@ def test_narrow_columns_learned_and_refuted(oracle):
         g.close()
     full = 28 * n * 16
     assert stats[0]["bytes"] == full and not stats[0]["narrow8"]
-    # learned: the bit columns go up as bytes, the clock (20 bits) as 32-bit words, 5 sparse columns not at all
-    assert set(range(1, 7)) <= set(stats[1]["narrow8"]) and 0 in stats[1]["narrow32"]
-    # nothing of the sparse columns goes up (their last row aside), the narrow ones as 1 or 4 bytes per row
+    # learned: the bit columns go up as bytes, the clock (learned as 32-bit) is derived from the AIR, 5 sparse columns
+    # not at all
+    assert set(range(1, 7)) <= set(stats[1]["narrow8"]) and stats[1]["derived"] == [0]
+    # nothing of the sparse or derived columns goes up (their last row aside), the narrow ones as 1 or 4 bytes per row
     st = stats[1]
-    wide = 28 - len(st["sparse"]) - len(st["narrow8"]) - len(st["narrow32"])
+    wide = 28 - len(st["sparse"]) - len(st["narrow8"]) - len(st["narrow32"]) - len(st["derived"])
     assert len(st["sparse"]) >= 5
     assert st["bytes"] == wide * n * 16 + (len(st["narrow8"]) + 4 * len(st["narrow32"])) * n
     assert 27 in stats[3]["narrow8"]                   # small: s15 learned as 8-bit
     assert 27 not in stats[4]["narrow8"] + stats[4]["narrow32"]  # refuted on the host: went up whole
     assert 27 in stats[5]["narrow32"]                  # relearned as 32-bit
     assert 27 not in stats[6]["narrow32"]              # refuted again
+
+
+def test_clock_column_derived_and_refuted(oracle):
+    """The AIR clock (column 0 of an accepted trace holds 0 .. n-2 before its random last row): once learned, a
+    host-resident trace's clock is neither uploaded nor transformed but derived (identity column + last-row
+    correction) and checked by host threads.  A trace whose clock is not 0 .. n-2 (an invalid trace) must not be
+    proved as the derived one: the host check refutes the derivation, the proof is redone from the caller's column
+    and fails the AIR exactly as without the derivation; valid traces keep proving to the oracle's bytes."""
+    trace, pub = workload_trace(ops_for_trace_len(14, "cipher"), seed=17)
+    n = trace.shape[1]
+    bad = trace.copy()
+    bad[0, 1000] = [7, 0]  # clk[1000] = 7: not the clock
+    other = trace.copy()
+    other[0, n - 1] = [12345, 6789]  # another random last row: still a clock
+    g = GpuProver(0, max_trace_len=n)
+    try:
+        derived = []
+        for t in (trace, trace, other):
+            proof, _, _, rc = g.prove(t, pub, ProofOptions())
+            assert rc == 0
+            assert proof == oracle.prove(t, oracle_pub(oracle, pub))[0]
+            derived.append(g.upload_stats()["derived"])
+        assert derived == [[], [0], [0]]
+        _, _, _, rc = g.prove(bad, pub, ProofOptions(), allow_degree_error=True)
+        assert rc == native.ZK_ERR_DEGREE
+        proof, _, _, rc = g.prove(trace, pub, ProofOptions())  # not speculated again at this length
+        assert rc == 0 and proof == oracle.prove(trace, oracle_pub(oracle, pub))[0]
+        assert g.upload_stats()["derived"] == []
+    finally:
+        g.close()
 
 
 def test_sparse_hint_learned_and_refuted(oracle):
