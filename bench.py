@@ -214,9 +214,9 @@ def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0, repeats:
            "runs_s": [round(r, 2) for r in runs],
            "sample": f"oracle or_prove (C, 1 thread), median of {len(runs)} proofs of one 2^{log_n}-step trace of the "
                      f"same cipher-mix generator, {'config-5' if config5 else 'reference'} options: {dt:.1f} s; a "
-                     f"2^{log_n} sample of the 2^20 config (the CPU prover's time per step grows with log n: the "
-                     f"2^20 pin took 246.9 s in the build container, tests/golden/large/cases.json), so this figure "
-                     f"flatters the CPU"}
+                     f"2^{log_n} sample of the 2^20 config (the CPU prover's time per step grows with log n: on a "
+                     f"GPU box's host one proof of configs[2]'s own 2^20 trace took 95.8 s, 10.9 k trace-steps/s, "
+                     f"profiles/r04n_cpu_baseline_2p20.json), so this figure flatters the CPU by ~10-20 %"}
     if all_cores > 1:
         # the reference prover is single-threaded (no rayon), so its whole-host throughput is one proof per
         # core: all_cores threads each prove the same trace at once (ctypes releases the GIL; the oracle
