@@ -439,8 +439,14 @@ struct NttArgs {
     unsigned *det;
     int det_col0, det_stride;
     int sp_all;  // (host) every batch entry is sparse: no transform, one fill pass (SparseCols::all, k_sparse_fill)
+    // the AIR clock (SparseCols::idoff): column 0 found to hold 0 .. n-2 transforms to sp_id + (last - (n-1)) * fill
+    const fe *sp_id;
+    int sp_idoff;
     __device__ __forceinline__ bool sparse(uint32_t b) const {
         return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
+    }
+    __device__ __forceinline__ bool clock(uint32_t b) const {
+        return nz && sp_idoff && sp_col0 + (int)(b / (uint32_t)ncos) == 0 && nz[sp_idoff] == 0;
     }
     // (32-bit: batch entries and grid sizes are < 2^32; 64-bit division is a long VALU sequence)
     __device__ __forceinline__ int coset_of(uint32_t b) const { return cos_r0 + (int)(b % (uint32_t)ncos) * cos_rstride; }
@@ -535,7 +541,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass1(NttArgs a
         k1_0 = (size_t)(lin32 / (uint32_t)batch) * LPB;
         b = lin32 % (uint32_t)batch;
     }
-    if (a.sparse(b)) return;  // pass 2 writes its output
+    if (a.sparse(b) || a.clock(b)) return;  // pass 2 writes its output
     const fe *in = a.in + (size_t)(b / (uint32_t)a.ncos) * a.in_stride;
     const int r = a.coset_of(b);
     fe *out = a.out + b * a.out_stride;
@@ -624,6 +630,18 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
         for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
             const size_t o = n2 * (size_t)(e / LPB) + j2_0 + (size_t)(e % LPB);
             out[o] = fe_mul(last, fill[o]);
+        }
+        return;
+    }
+    if (a.clock((uint32_t)b)) {
+        // the identity column's transform + (last - (n-1)) * (the transform of e_(n-1))
+        const fe d = fe_sub(a.sp_last[0], fe_make(n - 1));
+        const size_t off = (size_t)a.coset_of((uint32_t)b) * a.sp_fill_stride;
+        const fe *fill = a.sp_fill + off, *id = a.sp_id + off;
+        fe *out = a.out_of((uint32_t)b);
+        for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+            const size_t o = n2 * (size_t)(e / LPB) + j2_0 + (size_t)(e % LPB);
+            out[o] = fe_add(id[o], fe_mul(d, fill[o]));
         }
         return;
     }
@@ -789,6 +807,8 @@ void ntt(hipStream_t st, const NttTables &T, const fe *in, size_t in_stride, fe 
             a.sp_fill_stride = 0;
             a.sp_col0 = sp->col0;
             a.sp_all = sp->all;
+            a.sp_id = sp->id_poly;
+            a.sp_idoff = sp->id_poly ? sp->idoff : 0;
         }
     }
     ntt_run(st, a, batch, tmp);
@@ -888,6 +908,8 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
             a.sp_fill_stride = n;
             a.sp_col0 = sp->col0;
             a.sp_all = sp->all;
+            a.sp_id = sp->id_lde;
+            a.sp_idoff = sp->id_lde ? sp->idoff : 0;
         }
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so
@@ -1050,12 +1072,12 @@ void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int 
 // last entry; with wstride > 0 also the width flags of SparseCols.  One pass over the columns (16 B per element read);
 // nz must be zeroed first.
 __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last,
-                                                       int wstride) {
+                                                       int wstride, int idoff) {
     constexpr int PER = 16;  // independent loads per thread (unrolled: all in flight at once)
     const int c = blockIdx.y;
     const fe *col = trace + (size_t)(c0 + c) * n;
     const size_t base = blockIdx.x * (size_t)(256 * PER) + threadIdx.x;
-    uint64_t any = 0, w8 = 0, w32 = 0;
+    uint64_t any = 0, w8 = 0, w32 = 0, nid = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const size_t i = base + (size_t)k * 256;
@@ -1064,7 +1086,12 @@ __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n
             any |= v.lo | v.hi;
             w8 |= (v.lo >> 8) | v.hi;
             w32 |= (v.lo >> 32) | v.hi;
+            nid |= (v.lo ^ (uint64_t)i) | v.hi;
         }
+    }
+    if (idoff && c0 + c == 0) {  // (block-uniform) the AIR clock check of column 0
+        const bool b_nid = __syncthreads_or(nid != 0);
+        if (b_nid && threadIdx.x == 0) nz[idoff] = 1u;
     }
     // one flag write per block that saw a nonzero entry (a plain store: every writer stores 1), not one atomic per
     // wave -- 4096 same-address atomics per 64 MiB column serialised at L2 (0.38 ms per proof)
@@ -1083,7 +1110,8 @@ __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp) {
     ZK_PROF(st, "sparse_detect", 16.0 * n * nc,
             hipLaunchKernelGGL(k_sparse_detect, dim3(cdiv(n, 256 * 16), nc), dim3(256), 0, st, trace, n, c0,
-                               const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last), sp.wstride));
+                               const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last), sp.wstride,
+                               sp.id_poly ? sp.idoff : 0));
 }
 
 // Packed narrow columns -> field elements: grid (row blocks, column), 4 rows per thread

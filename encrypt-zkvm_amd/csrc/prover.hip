@@ -1256,12 +1256,18 @@ int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols *
     *sp = nullptr;
     if (!sparse_on() || !pl->lagr) return ZK_OK;
     if (!p->sp_nz) {
-        ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, 3 * W));
+        ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, 4 * W));  // nonzero, 8-bit, 32-bit flags; [3W]: column 0 not the clock
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
         ZK_CHECK_HIP(hipHostMalloc((void **)&p->sp_h, 3 * W * sizeof(unsigned), hipHostMallocDefault));
     }
-    ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, 3 * W * sizeof(unsigned), p->st));
+    ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, 4 * W * sizeof(unsigned), p->st));
     *out = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
+    if (clock_on()) {  // the AIR clock of column 0, detected with the sparse columns (device-side traces)
+        ZK_TRY(clock_tables(p, pl));
+        out->id_poly = pl->id_poly;
+        out->id_lde = pl->id_lde;
+        out->idoff = 3 * W;
+    }
     *sp = out;
     return ZK_OK;
 }

@@ -122,6 +122,11 @@ struct SparseCols {
     // all: the host knows every column of the call is sparse (the hinted columns of a host trace): no transform is
     // launched, one streaming pass writes last * fill into every column (k_sparse_fill)
     bool all = false;
+    // idoff > 0: column 0 is also checked for being the AIR clock (rows 0 .. n-2 hold 0 .. n-2; nz[idoff] = 1 when it
+    // is not); such a column transforms to id + (last - (n-1)) * fill (id_poly / id_lde: the identity column's
+    // interpolant and coset LDE, like lagr / lagr_lde) and skips its DFTs like a sparse one
+    const fe *id_poly = nullptr, *id_lde = nullptr;
+    int idoff = 0;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
 // Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte
