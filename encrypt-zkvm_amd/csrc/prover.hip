@@ -1164,7 +1164,7 @@ static int upload_trace_group(zk_prover *p, const TraceSrc &src, size_t n, int c
 // the program's maximum depth, five of the benchmark's 28) interpolates to last * lagr and extends to last * lagr_lde;
 // sparse_detect flags them on the device and the NTT passes skip their DFTs.  Exact: the same polynomials and LDE.
 // ZK_SPARSE=0 transforms every column.
-static bool sparse_on() {
+bool zk::sparse_on() {
     static const bool on = [] {
         const char *e = getenv("ZK_SPARSE");
         return !(e && !strcmp(e, "0"));
@@ -1182,7 +1182,7 @@ static bool narrow_on() {
 }
 
 // The AIR clock (ZK_CLOCK=0 turns its derivation off)
-static bool clock_on() {
+bool zk::clock_on() {
     static const bool on = [] {
         const char *e = getenv("ZK_CLOCK");
         return !(e && !strcmp(e, "0"));
@@ -1191,7 +1191,7 @@ static bool clock_on() {
 }
 
 // the identity column 0, 1, ..., n-1 interpolated and extended over the B cosets (Plan::id_poly / id_lde), once per plan
-static int clock_tables(zk_prover *p, Plan *pl) {
+int zk::clock_tables(zk_prover *p, Plan *pl) {
     if (pl->id_poly) return ZK_OK;
     const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b;
     fe *poly = nullptr, *lde = nullptr;
@@ -1216,7 +1216,7 @@ static int clock_tables(zk_prover *p, Plan *pl) {
 }
 
 // rows [r0, r1) of a host column: row i holds i (the AIR clock)
-static bool clock_rows(const uint8_t *col, size_t r0, size_t r1) {
+bool zk::clock_rows(const uint8_t *col, size_t r0, size_t r1) {
     const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
     uint64_t bad = 0;
     for (size_t i = r0; i < r1; i++) bad |= (v[2 * i] ^ (uint64_t)i) | v[2 * i + 1];
@@ -1245,7 +1245,7 @@ static bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8
 }
 
 // rows [r0, r1) of a host column all zero
-static bool zero_rows(const uint8_t *col, size_t r0, size_t r1) {
+bool zk::zero_rows(const uint8_t *col, size_t r0, size_t r1) {
     const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
     uint64_t any = 0;
     for (size_t i = 2 * r0; i < 2 * r1; i++) any |= v[i];
@@ -1669,6 +1669,7 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     p->sp_hinted = 0;
     p->sp_bad = 0;
     p->clk_used = p->clk_bad = false;
+    const size_t cap = proof_len ? *proof_len : 0;  // (in/out: a voided attempt has overwritten it with its length)
     int rc = prove_once(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
     if (!src.cols || !p->sp_used) return rc;
     if (p->sp_bad || p->clk_bad) {
@@ -1680,6 +1681,7 @@ static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
         s2.hint_ok = false;
         p->sp_used = false;
         p->sp_bad = 0;
+        *proof_len = cap;
         rc = prove_once(p, s2, n, opt, pub, proof_out, proof_len, rec, dump);
         if (!p->sp_used) return rc;
     }

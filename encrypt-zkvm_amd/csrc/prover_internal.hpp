@@ -188,6 +188,12 @@ struct zk_prover {
     // whose traces refuted it, not speculated again)
     bool clk_used = false, clk_bad = false;
     size_t clk_off_n = 0;
+    // Sharded host-trace hints (shard.hip S2): the sparse columns and the clock a previous sharded proof of this length
+    // and world found (from all-gathered flags, so every rank holds the same), checked by the ranks' host threads
+    uint32_t sh_sparse = 0;
+    bool sh_clock = false;
+    size_t sh_hint_n = 0, sh_clock_off_n = 0;
+    int sh_hint_g = 0;
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
@@ -261,6 +267,14 @@ int prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inpu
 // polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip); B: the LDE
 // cosets held (fx's flde / lagr_lde and lde alike)
 void fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t n, size_t B, fe *polys, fe *lde);
+// Host-trace column classes shared by the single-GPU and the sharded prover (prover.hip): ZK_SPARSE / ZK_CLOCK
+// switches, the identity column's tables of a plan (the AIR clock: built once), and the host checks of a column's
+// rows [r0, r1): all zero, or row i holding i
+bool sparse_on();
+bool clock_on();
+int clock_tables(zk_prover *p, Plan *pl);
+bool zero_rows(const uint8_t *col, size_t r0, size_t r1);
+bool clock_rows(const uint8_t *col, size_t r0, size_t r1);
 // zk_prove_sharded, and with `fixed` (one FixedCols per local rank, its own cosets; trace must be null) the sharded
 // proof of zk_vm_prove_sharded's device traces (shard.hip)
 int prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,

@@ -20,11 +20,14 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "blake3.hpp"
 #include "comm.hpp"
+#include "host_pool.hpp"
 #include "prover_internal.hpp"
 
 using namespace zk;
@@ -265,7 +268,13 @@ struct Ctx {
     // zk_vm_prove_sharded: the preprocessed columns of each local rank (its own cosets), or null: the device trace
     // then holds only the dynamic stack columns 12 .. 12 + md - 1
     const FixedCols *fixed = nullptr;
+    // host traces: the previous proof's column hints may be used (hint_ok); this proof's hinted columns (sh_hinted, bit
+    // c: column c taken from its last row) and the ones the ranks' checks refuted (sh_refuted: prove_sharded returned
+    // ZK_SH_REDO, and prove_sharded_entry proves again without hints)
+    bool hint_ok = true, sh_clock = false;
+    uint32_t sh_hinted = 0, sh_refuted = 0;
 };
+constexpr int ZK_SH_REDO = 1000;  // (internal) a refuted column hint voided the proof on every rank
 
 
 // One collective of the proof, timed: events on local rank 0's stream before and after it (the time includes any
@@ -388,46 +397,204 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             }
         }
     } copy_guard{X.P, trace != nullptr};
+    // host checks of the hinted columns (below): the tasks read the caller's trace, so every way out waits for them
+    Latch checked;
+    std::unique_ptr<std::atomic<uint32_t>[]> bad(new std::atomic<uint32_t>[nlp]);
+    for (int l = 0; l < nlp; l++) bad[l].store(0);
+    struct CheckWait {
+        Latch &a;
+        ~CheckWait() { a.wait(); }
+    } check_wait{checked};
     if (trace) {
-        const int rounds = (W + G - 1) / G;
+        // Column classes (round 4, as the single-GPU host path): the sparse columns (zero but the last row) and the AIR
+        // clock (rows 0 .. n-2 = 0 .. n-2) that the previous sharded proof of this length and world found -- the same
+        // hints on every rank, learned from all-gathered flags -- are neither uploaded, interpolated nor all-gathered:
+        // every rank forms their coefficients and local LDE from the last row (fills).  Each rank's host threads check
+        // its 1/G row range of them; the flags are all-gathered with the hints of the next proof, and a refuted hint
+        // voids the proof on every rank (prove_sharded_entry redoes it without hints).
+        zk_prover *H = X.P[0];
+        const bool fresh = X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G;
+        const uint32_t S = fresh ? H->sh_sparse : 0u;
+        const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
+        X.sh_hinted = S | (K ? 1u : 0u);
+        X.sh_clock = K;
+        int U[W], nu = 0;  // the uploaded columns, ascending
+        for (int c = 0; c < W; c++)
+            if (!((S >> c) & 1u) && !(K && c == 0)) U[nu++] = c;
+        const int rounds = (nu + G - 1) / G;
         static_assert((W + 1) / 2 <= ZK_UPLOAD_GROUPS_MAX, "one upload event per round at G = 2");
         const size_t col = n * sizeof(fe);
+        std::vector<SparseCols> spc(nlp);
+        std::vector<const SparseCols *> spp(nlp, nullptr);
+        for (int l = 0; l < nlp; l++) {
+            ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
+            ZK_TRY(sparse_begin(X.P[l], X.pl[l], &spc[l], &spp[l]));  // the flags the interpolation's pass 1 sets
+            if (spp[l]) spc[l].wstride = W;
+            if (K) ZK_TRY(clock_tables(X.P[l], X.pl[l]));
+        }
+        if (S | (K ? 1u : 0u)) {
+            constexpr size_t R = (size_t)1 << 18;
+            std::vector<std::pair<int, size_t>> tasks;  // (local rank, first row)
+            for (int l = 0; l < nlp; l++) {
+                const size_t r0 = n * (size_t)X.rank[l] / (size_t)G, r1 = std::min(n - 1, n * (size_t)(X.rank[l] + 1) / G);
+                for (size_t t = r0; t < r1; t += R) tasks.push_back({l, t});
+            }
+            int nt = 0;
+            for (int c = 0; c < W; c++) nt += ((S >> c) & 1u) || (K && c == 0) ? 1 : 0;
+            checked.reset(nt * (int)tasks.size());
+            for (int c = 0; c < W; c++) {
+                const bool sparse = (S >> c) & 1u, clock = K && c == 0;
+                if (!sparse && !clock) continue;
+                const uint8_t *cp = trace + (size_t)c * col;
+                for (const auto &tk : tasks) {
+                    const int l = tk.first;
+                    const size_t t0 = tk.second;
+                    const size_t r1 = std::min(n - 1, std::min(n * (size_t)(X.rank[l] + 1) / G, t0 + R));
+                    std::atomic<uint32_t> *b = &bad[l];
+                    HostPool::get().submit([=, &checked] {
+                        if (!(clock ? clock_rows(cp, t0, r1) : zero_rows(cp, t0, r1))) b->fetch_or(1u << c);
+                        checked.count_down();
+                    });
+                }
+            }
+        }
         auto upload = [&](int k) -> int {
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
-                const int c = X.rank[l] + G * k;
+                const int i = X.rank[l] + G * k;
                 ZK_CHECK_HIP(hipSetDevice(p->device));
                 std::lock_guard<std::mutex> lk(*p->up_mu);
-                if (c < W)
-                    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)c * n, trace + (size_t)c * col, col,
+                if (i < nu)
+                    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)U[i] * n, trace + (size_t)U[i] * col, col,
                                                 hipMemcpyHostToDevice, p->up));
                 ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->up));
             }
             return ZK_OK;
         };
-        ZK_TRY(upload(0));
+        if (rounds) ZK_TRY(upload(0));
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
         for (int k = 0; k < rounds; k++) {
             if (k + 1 < rounds) ZK_TRY(upload(k + 1));
+            const int i0 = G * k, real = std::min(G, nu - i0), first = U[i0];
+            // in place when the round's columns are consecutive (the padding slots of a short last round then land on
+            // columns nobody uploads -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns); else
+            // through the composition scratch (free until S4) and copied out
+            const bool inplace = U[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
-                const size_t c = (size_t)X.rank[l] + (size_t)G * k;
+                const int i = i0 + X.rank[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
                 ZK_TRY(upload_gate(p, p->ev_up[k]));
-                if (c < (size_t)W) ntt(p->st, X.pl[l]->Tn, p->d_trace + c * n, n, p->polys + c * n, n, 1, true, nullptr, &inv_n, p->tmp);
-                snd[l] = p->polys + c * n;
-                rcv[l] = p->polys + (size_t)G * k * n;
+                if (i < nu) {
+                    SparseCols g = spc[l];
+                    g.col0 = U[i];
+                    g.fused = true;
+                    ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)U[i] * n, n, p->polys + (size_t)U[i] * n, n, 1, true, nullptr,
+                        &inv_n, p->tmp, spp[l] ? &g : nullptr);
+                }
+                snd[l] = inplace ? p->polys + (size_t)(first + X.rank[l]) * n : p->polys + (size_t)(i < nu ? U[i] : 0) * n;
+                rcv[l] = inplace ? p->polys + (size_t)first * n : CTMP(p);
             }
             ZK_TRY(xchg(X, "trace_coeffs", AG, snd, rcv, col));
-            // this round's G columns are complete on every rank: extend them over the local cosets now, so the
-            // LDE runs under the next round's upload instead of after the last one
-            const int c0 = G * k, nc = std::min(G, W - c0);
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, nc, X.rank[l], G, Bl,
-                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+                if (!inplace)
+                    for (int g = 0; g < real; g++)
+                        if (g != X.rank[l])
+                            ZK_CHECK_HIP(hipMemcpyAsync(p->polys + (size_t)U[i0 + g] * n, CTMP(p) + (size_t)g * n, col,
+                                                        hipMemcpyDeviceToDevice, p->st));
+                // this round's columns are complete on every rank: extend them over the local cosets now, so the LDE
+                // runs under the next round's upload instead of after the last one
+                for (int a = 0; a < real;) {
+                    int b = a + 1;
+                    while (b < real && U[i0 + b] == U[i0 + b - 1] + 1) b++;
+                    const int c0 = U[i0 + a];
+                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
+                            p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+                    a = b;
+                }
+            }
+        }
+        // the hinted columns from the last row (after the last round: a short round's padding may have landed there)
+        if (S | (K ? 1u : 0u)) {
+            fe lastv[W];
+            for (int c = 0; c < W; c++) memcpy(&lastv[c], trace + (size_t)c * col + (n - 1) * sizeof(fe), sizeof(fe));
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                if (S) {
+                    ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
+                    for (int c = 0; c < W;) {
+                        if (!((S >> c) & 1u)) {
+                            c++;
+                            continue;
+                        }
+                        int e = c + 1;
+                        while (e < W && ((S >> e) & 1u)) e++;
+                        SparseCols g = spc[l];
+                        g.col0 = c;
+                        g.fused = false;
+                        g.all = true;  // fills only
+                        ntt(p->st, X.pl[l]->Tn, p->polys + (size_t)c * n, n, p->polys + (size_t)c * n, n, e - c, true, nullptr,
+                            &inv_n, p->tmp, &g);
+                        ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c * n, n, e - c, X.rank[l], G, Bl,
+                                p->lde + (size_t)c * Bl * n, (size_t)Bl * n, n, p->tmp, &g);
+                        c = e;
+                    }
+                }
+                if (K) {
+                    const fe_ws d = make_fe_ws(fe_sub(lastv[0], fe_make(n - 1)));
+                    const Plan *pl = X.pl[l];
+                    axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
+                    for (int j = 0; j < Bl; j++) {
+                        const size_t r = (size_t)X.rank[l] + (size_t)G * j;
+                        axpy_fill(p->st, pl->id_lde + r * n, pl->lagr_lde + r * n, d, n, p->lde + (size_t)j * n);
+                    }
+                }
+            }
+        }
+        // the flags of the columns each rank interpolated (for the next proof's hints) and each rank's check of the
+        // hinted ones, all-gathered: every rank then holds the same view
+        if (spp[0]) {
+            checked.wait();
+            std::vector<const void *> fs(nlp);
+            std::vector<void *> fr(nlp);
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                const uint32_t b = bad[l].load();
+                ZK_TRY(h2d_small(p, p->sp_nz + 3 * W + 1, &b, sizeof b));
+                fs[l] = p->sp_nz;
+                fr[l] = p->sh_buf;
+            }
+            ZK_TRY(xchg(X, "column_flags", AG, fs, fr, 4 * W * sizeof(unsigned)));
+            std::vector<unsigned> f((size_t)G * 4 * W);
+            ZK_TRY(d2h_small(P0, f.data(), P0->sh_buf, f.size() * sizeof(unsigned)));
+            ZK_TRY(d2h_flush(P0));
+            unsigned nz[3 * W] = {};
+            uint32_t refuted = 0;
+            for (int g = 0; g < G; g++) {
+                for (int c = 0; c < 3 * W; c++) nz[c] |= f[(size_t)g * 4 * W + c];
+                refuted |= f[(size_t)g * 4 * W + 3 * W + 1];
+            }
+            if (refuted) {
+                X.sh_refuted = refuted;
+                return ZK_SH_REDO;
+            }
+            // next proof: the columns found sparse (uploaded ones with no nonzero entry before the last row, and the
+            // hinted ones, which the checks confirmed), and the clock when column 0 was found 32-bit (or derived)
+            uint32_t sp_next = S;
+            for (int i = 0; i < nu; i++)
+                if (nz[U[i]] == 0) sp_next |= 1u << U[i];
+            bool clk_next = K;
+            if (!K && !(sp_next & 1u) && nu > 0 && U[0] == 0) clk_next = nz[W] != 0 && nz[2 * W] == 0;
+            for (zk_prover *p : X.P) {
+                p->sh_sparse = sp_next;
+                p->sh_clock = clk_next;
+                p->sh_hint_n = n;
+                p->sh_hint_g = G;
             }
         }
     } else if (X.fixed) {
@@ -1104,5 +1271,21 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         ZK_CHECK_HIP(hipSetDevice(p->device));
         io_scopes.push_back(std::make_unique<IoScope>(p));
     }
-    return prove_sharded(X, trace, opt, pub, proof_out, proof_len, rec);
+    const size_t cap = *proof_len;  // (in/out)
+    int rc = prove_sharded(X, trace, opt, pub, proof_out, proof_len, rec);
+    if (rc == ZK_SH_REDO) {
+        *proof_len = cap;
+        // a hinted column was not what the previous proof found (every rank saw the same all-gathered checks): forget
+        // the hints (and stop speculating the clock at this length if it was refuted), prove from every column
+        for (zk_prover *p : X.P) {
+            p->sh_hint_n = 0;
+            p->sh_sparse = 0;
+            p->sh_clock = false;
+            if (X.sh_clock && (X.sh_refuted & 1u)) p->sh_clock_off_n = n;
+        }
+        X.hint_ok = false;
+        X.sh_refuted = 0;
+        rc = prove_sharded(X, trace, opt, pub, proof_out, proof_len, rec);
+    }
+    return rc;
 }

@@ -226,3 +226,44 @@ def test_shard_prover_refuses_single_gpu_calls():
     finally:
         L.zk_prover_destroy(h)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,ext", [(2, 1), (8, 1), (4, 2)])
+def test_sharded_host_column_hints(world, ext):
+    """Host-trace sharded proofs with the column hints of the previous sharded proof (shard.hip S2): the sparse columns
+    and the AIR clock are taken from the last row (not uploaded, interpolated or all-gathered) and checked by every
+    rank's host threads over its row range.  A trace the hints are wrong for (a hinted sparse column made dense in a
+    column no constraint reads) is refuted on every rank and proved again from every column; a trace whose clock is
+    not 0 .. n-2 is not proved as the derived one (it fails the AIR as without the hints).  Every proof equals the
+    single-GPU prover's."""
+    from zkvm_amd.prover import vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(16, "cipher")
+    w = make_workload(src, seed=81 + world)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    n = trace.shape[1]
+    dense = trace.copy()
+    dense[27, 9] = [3, 1]        # s15 (read by no constraint): dense now
+    other = trace.copy()
+    other[0, n - 1] = [4242, 17]  # another last row: still a clock
+    bad = trace.copy()
+    bad[0, 1000] = [7, 0]        # not a clock
+    opts = ProofOptions(field_extension=ext)
+    g = GpuProver(0, max_trace_len=n)
+    sp = ShardedProver.loopback(world, max_trace_len=n)
+    try:
+        for t in (trace, trace, trace, dense, dense, other, trace):
+            want, _, _, rc = g.prove(t, pub, opts)
+            assert rc == 0
+            got, _ = sp.prove(t, pub, opts)
+            assert hashlib.sha256(got).hexdigest() == hashlib.sha256(want).hexdigest()
+        with pytest.raises(native.ZkError) as e:
+            sp.prove(bad, pub, opts)
+        assert e.value.code == native.ZK_ERR_DEGREE
+        got, _ = sp.prove(trace, pub, opts)  # (the clock is not speculated again at this length)
+        assert got == g.prove(trace, pub, opts)[0]
+    finally:
+        sp.close()
+        g.close()
