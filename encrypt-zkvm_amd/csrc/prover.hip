@@ -1173,7 +1173,7 @@ bool zk::sparse_on() {
 }
 
 // Narrow columns (host-resident traces): ZK_NARROW=0 uploads every column whole.
-static bool narrow_on() {
+bool zk::narrow_on() {
     static const bool on = [] {
         const char *e = getenv("ZK_NARROW");
         return !(e && !strcmp(e, "0"));
@@ -1224,7 +1224,7 @@ bool zk::clock_rows(const uint8_t *col, size_t r0, size_t r1) {
 }
 
 // rows [r0, r1) of a host column as `width`-byte integers (1 or 4) at dst + width * row; false if a value does not fit
-static bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8_t *dst) {
+bool zk::pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8_t *dst) {
     const uint64_t *v = reinterpret_cast<const uint64_t *>(col);
     uint64_t over = 0;
     if (width == 1) {

@@ -190,7 +190,7 @@ struct zk_prover {
     size_t clk_off_n = 0;
     // Sharded host-trace hints (shard.hip S2): the sparse columns and the clock a previous sharded proof of this length
     // and world found (from all-gathered flags, so every rank holds the same), checked by the ranks' host threads
-    uint32_t sh_sparse = 0;
+    uint32_t sh_sparse = 0, sh_nw8 = 0, sh_nw32 = 0;  // (and the narrow ones: the owner rank uploads them packed)
     bool sh_clock = false;
     size_t sh_hint_n = 0, sh_clock_off_n = 0;
     int sh_hint_g = 0;
@@ -272,6 +272,9 @@ void fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t
 // rows [r0, r1): all zero, or row i holding i
 bool sparse_on();
 bool clock_on();
+bool narrow_on();
+// rows [r0, r1) of a host column as `width`-byte integers (1 or 4) at dst + width * row; false if a value does not fit
+bool pack_rows(const uint8_t *col, size_t r0, size_t r1, int width, uint8_t *dst);
 int clock_tables(zk_prover *p, Plan *pl);
 bool zero_rows(const uint8_t *col, size_t r0, size_t r1);
 bool clock_rows(const uint8_t *col, size_t r0, size_t r1);

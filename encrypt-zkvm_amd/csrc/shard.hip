@@ -398,13 +398,19 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
     } copy_guard{X.P, trace != nullptr};
     // host checks of the hinted columns (below): the tasks read the caller's trace, so every way out waits for them
-    Latch checked;
-    std::unique_ptr<std::atomic<uint32_t>[]> bad(new std::atomic<uint32_t>[nlp]);
-    for (int l = 0; l < nlp; l++) bad[l].store(0);
+    Latch checked, packed;
+    std::unique_ptr<std::atomic<uint32_t>[]> bad(new std::atomic<uint32_t>[nlp]), pack_bad(new std::atomic<uint32_t>[nlp]);
+    for (int l = 0; l < nlp; l++) {
+        bad[l].store(0);
+        pack_bad[l].store(0);
+    }
     struct CheckWait {
-        Latch &a;
-        ~CheckWait() { a.wait(); }
-    } check_wait{checked};
+        Latch &a, &b;
+        ~CheckWait() {
+            a.wait();
+            b.wait();
+        }
+    } check_wait{checked, packed};
     if (trace) {
         // Column classes (round 4, as the single-GPU host path): the sparse columns (zero but the last row) and the AIR
         // clock (rows 0 .. n-2 = 0 .. n-2) that the previous sharded proof of this length and world found -- the same
@@ -418,6 +424,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
         X.sh_hinted = S | (K ? 1u : 0u);
         X.sh_clock = K;
+        const uint32_t derived = S | (K ? 1u : 0u);
+        const uint32_t N8 = fresh && narrow_on() ? H->sh_nw8 & ~derived : 0u;
+        const uint32_t N32 = fresh && narrow_on() ? H->sh_nw32 & ~derived & ~N8 : 0u;
         int U[W], nu = 0;  // the uploaded columns, ascending
         for (int c = 0; c < W; c++)
             if (!((S >> c) & 1u) && !(K && c == 0)) U[nu++] = c;
@@ -458,15 +467,78 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 }
             }
         }
+        // narrow columns (8- or 32-bit before the last row): their owner's host threads pack rows 0 .. n-2 into its
+        // pinned staging while the other columns go up; a column goes up packed (expanded on the device), or whole if a
+        // value does not fit
+        std::vector<NarrowCols> nar(nlp);
+        for (int l = 0; l < nlp; l++) {
+            NarrowCols &nc = nar[l];
+            nc.count = 0;
+            size_t bytes = 0;
+            for (int i = X.rank[l]; i < nu; i += G) {
+                const int c = U[i];
+                if (!(((N8 | N32) >> c) & 1u)) continue;
+                nc.col[nc.count] = c;
+                nc.width[nc.count] = ((N8 >> c) & 1u) ? 1 : 4;
+                nc.off[nc.count] = bytes;
+                memcpy(&nc.last[nc.count], trace + (size_t)c * col + (n - 1) * sizeof(fe), sizeof(fe));
+                bytes += ((size_t)nc.width[nc.count] * n + 15) & ~(size_t)15;
+                nc.count++;
+            }
+            zk_prover *p = X.P[l];
+            if (nc.count && bytes > p->h_pack_cap) {  // (the previous proof's copies from it have drained: CopyGuard)
+                if (p->h_pack) (void)hipHostFree(p->h_pack);
+                p->h_pack = nullptr;
+                p->h_pack_cap = 0;
+                ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, bytes, hipHostMallocDefault));
+                p->h_pack_cap = bytes;
+            }
+        }
+        {
+            constexpr size_t R = (size_t)1 << 18;
+            const size_t per = (n - 1 + R - 1) / R;
+            int total = 0;
+            for (int l = 0; l < nlp; l++) total += nar[l].count * (int)per;
+            packed.reset(total);
+            for (int l = 0; l < nlp; l++)
+                for (int k = 0; k < nar[l].count; k++)
+                    for (size_t t = 0; t < per; t++) {
+                        const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
+                        const uint8_t *cp = trace + (size_t)nar[l].col[k] * col;
+                        uint8_t *dst = X.P[l]->h_pack + nar[l].off[k];
+                        const int width = nar[l].width[k], c = nar[l].col[k];
+                        std::atomic<uint32_t> *b = &pack_bad[l];
+                        HostPool::get().submit([=, &packed] {
+                            if (!pack_rows(cp, r0, r1, width, dst)) b->fetch_or(1u << c);
+                            if (r1 == n - 1) memset(dst + (size_t)width * (n - 1), 0, width);  // (the last row's slot)
+                            packed.count_down();
+                        });
+                    }
+        }
+        // the narrow column k of local rank l, or -1
+        auto narrow_of = [&](int l, int c) {
+            for (int k = 0; k < nar[l].count; k++)
+                if (nar[l].col[k] == c) return k;
+            return -1;
+        };
+        std::vector<uint32_t> went_packed(nlp, 0u);
         auto upload = [&](int k) -> int {
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 const int i = X.rank[l] + G * k;
                 ZK_CHECK_HIP(hipSetDevice(p->device));
+                const int q = i < nu ? narrow_of(l, U[i]) : -1;
+                if (q >= 0) packed.wait();  // (before the lock: the packing does not need it)
                 std::lock_guard<std::mutex> lk(*p->up_mu);
-                if (i < nu)
+                if (q >= 0 && !((pack_bad[l].load() >> U[i]) & 1u)) {
+                    const size_t w = (size_t)nar[l].width[q] * n;
+                    ZK_CHECK_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t *>(CLDE(p)) + nar[l].off[q],
+                                                p->h_pack + nar[l].off[q], w, hipMemcpyHostToDevice, p->up));
+                    went_packed[l] |= 1u << U[i];
+                } else if (i < nu) {
                     ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)U[i] * n, trace + (size_t)U[i] * col, col,
                                                 hipMemcpyHostToDevice, p->up));
+                }
                 ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->up));
             }
             return ZK_OK;
@@ -486,6 +558,16 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 const int i = i0 + X.rank[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
                 ZK_TRY(upload_gate(p, p->ev_up[k]));
+                if (i < nu && ((went_packed[l] >> U[i]) & 1u)) {
+                    const int q = narrow_of(l, U[i]);
+                    NarrowCols one{};
+                    one.count = 1;
+                    one.col[0] = U[i];
+                    one.width[0] = nar[l].width[q];
+                    one.off[0] = nar[l].off[q];
+                    one.last[0] = nar[l].last[q];
+                    expand_narrow(p->st, reinterpret_cast<const uint8_t *>(CLDE(p)), one, n, p->d_trace);
+                }
                 if (i < nu) {
                     SparseCols g = spc[l];
                     g.col0 = U[i];
@@ -584,14 +666,21 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 return ZK_SH_REDO;
             }
             // next proof: the columns found sparse (uploaded ones with no nonzero entry before the last row, and the
-            // hinted ones, which the checks confirmed), and the clock when column 0 was found 32-bit (or derived)
-            uint32_t sp_next = S;
-            for (int i = 0; i < nu; i++)
-                if (nz[U[i]] == 0) sp_next |= 1u << U[i];
-            bool clk_next = K;
-            if (!K && !(sp_next & 1u) && nu > 0 && U[0] == 0) clk_next = nz[W] != 0 && nz[2 * W] == 0;
+            // hinted ones, which the checks confirmed), narrow (8- / 32-bit before the last row), and the clock when
+            // column 0 was found 32-bit (or was derived)
+            uint32_t sp_next = S, w8 = 0, w32 = 0;
+            for (int i = 0; i < nu; i++) {
+                const int c = U[i];
+                if (nz[c] == 0) sp_next |= 1u << c;
+                else if (nz[W + c] == 0) w8 |= 1u << c;
+                else if (nz[2 * W + c] == 0) w32 |= 1u << c;
+            }
+            const bool clk_next = K || (!(sp_next & 1u) && (w32 & 1u));
+            if (clk_next) w32 &= ~1u;
             for (zk_prover *p : X.P) {
                 p->sh_sparse = sp_next;
+                p->sh_nw8 = w8;
+                p->sh_nw32 = w32;
                 p->sh_clock = clk_next;
                 p->sh_hint_n = n;
                 p->sh_hint_g = G;
@@ -1279,7 +1368,7 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         // the hints (and stop speculating the clock at this length if it was refuted), prove from every column
         for (zk_prover *p : X.P) {
             p->sh_hint_n = 0;
-            p->sh_sparse = 0;
+            p->sh_sparse = p->sh_nw8 = p->sh_nw32 = 0;
             p->sh_clock = false;
             if (X.sh_clock && (X.sh_refuted & 1u)) p->sh_clock_off_n = n;
         }
