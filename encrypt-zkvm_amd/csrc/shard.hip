@@ -419,7 +419,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         // its 1/G row range of them; the flags are all-gathered with the hints of the next proof, and a refuted hint
         // voids the proof on every rank (prove_sharded_entry redoes it without hints).
         zk_prover *H = X.P[0];
-        const bool fresh = X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G;
+        static const bool hints_on = [] {  // ZK_SHARD_HINTS=0: every column uploaded, interpolated and all-gathered
+            const char *e = getenv("ZK_SHARD_HINTS");
+            return !(e && !strcmp(e, "0"));
+        }();
+        const bool fresh = hints_on && X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G;
         const uint32_t S = fresh ? H->sh_sparse : 0u;
         const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
         X.sh_hinted = S | (K ? 1u : 0u);
