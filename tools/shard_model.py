@@ -5,7 +5,8 @@ Loopback ranks run every rank of a G-way sharded proof on ONE GPU, so the wall t
 with R the work every rank repeats (interpolation, DEEP coefficients, FRI layers >= 1, host steps), S the work that
 is divided among the ranks (LDEs, evaluation, hashing, layer 0) and X the in-process exchange copies (device-local,
 small).  From G = 2, 4, 8 this fits R and S (least squares); the per-rank time on G separate GPUs is then
-R + S / G + exchange(G), the exchange priced from its volume at an assumed xGMI rate.
+R + S / G + exchange(G), the exchange priced from the bytes rank 0 received in the loopback proof at an assumed xGMI
+rate ("projection").
     python3 tools/shard_model.py [log_n] [steps]      (GPU box; prints one JSON object)
 """
 import json
@@ -51,8 +52,10 @@ def main():
         sp = ShardedProver.loopback(G, max_trace_len=n)
         try:
             res["loopback_host_ms"][G] = timed(sp, lambda: sp.prove(host.array, pub, ProofOptions())[0])
+            res.setdefault("received", {}).setdefault("host", {})[G] = sp.exchange_stats()
             sp.upload_trace(trace)
             res["loopback_ms"][G] = timed(sp, lambda: sp.prove(None, pub, ProofOptions(), n=n)[0])
+            res["received"].setdefault("device", {})[G] = sp.exchange_stats()
             res["stage_ms"][G] = {k: round(v, 3) for k, v in sp.stage_times().items()}
             # vm::prove sharded: every loopback rank also writes its own trace (zk_vm_prove_sharded), so the VM's
             # host stack pass and row kernels are counted once per rank, like the replicated work they are
@@ -73,6 +76,24 @@ def main():
         (R, S), *_ = np.linalg.lstsq(A, T, rcond=None)
         res[name] = {"replicated_ms_R": round(float(R), 3), "divided_ms_S": round(float(S), 3),
                      "residuals_ms": [round(float(x), 3) for x in (T - A @ np.array([R, S]))]}
+    # Per rank on G separate GPUs: R + S / G + the exchanges, priced from the bytes rank 0 received in the loopback
+    # proof (the same collectives and volumes an RCCL rank sees) at the link model of DESIGN.md section 7: per-direction
+    # xGMI 76.8 GB/s per link, 70 % collective efficiency, G - 1 links, 50 us per collective, no overlap with compute
+    link = 76.8e9 * 0.7
+    res["projection"] = {}
+    for kind, fit in (("device", "fit"), ("host", "fit_host")):
+        R, S = res[fit]["replicated_ms_R"], res[fit]["divided_ms_S"]
+        proj = {}
+        for G in (2, 4, 8):
+            st = res["received"][kind][G]
+            nbytes = sum(v[1] for v in st.values())
+            calls = sum(v[2] for v in st.values())
+            x_ms = 1e3 * nbytes / ((G - 1) * link) + 0.05 * calls
+            proj[G] = {"per_rank_ms": round(R + S / G + x_ms, 2), "exchange_ms": round(x_ms, 2),
+                       "received_mb": round(nbytes / 1e6, 1), "collectives": calls}
+        res["projection"][kind] = proj
+    res["received"] = {k: {G: {c: [round(v[1] / 1e6, 2), v[2]] for c, v in d.items()} for G, d in m.items()}
+                       for k, m in res["received"].items()}
     print(json.dumps(res))
 
 
