@@ -268,11 +268,11 @@ struct Ctx {
     // zk_vm_prove_sharded: the preprocessed columns of each local rank (its own cosets), or null: the device trace
     // then holds only the dynamic stack columns 12 .. 12 + md - 1
     const FixedCols *fixed = nullptr;
-    // host traces: the previous proof's column hints may be used (hint_ok); this proof's hinted columns (sh_hinted, bit
-    // c: column c taken from its last row) and the ones the ranks' checks refuted (sh_refuted: prove_sharded returned
+    // host traces: the previous proof's column hints may be used (hint_ok); whether this proof derives the clock
+    // (sh_clock), and the hinted columns the ranks' checks refuted (sh_refuted, bit c: prove_sharded returned
     // ZK_SH_REDO, and prove_sharded_entry proves again without hints)
     bool hint_ok = true, sh_clock = false;
-    uint32_t sh_hinted = 0, sh_refuted = 0;
+    uint32_t sh_refuted = 0;
 };
 constexpr int ZK_SH_REDO = 1000;  // (internal) a refuted column hint voided the proof on every rank
 
@@ -426,7 +426,6 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         const bool fresh = hints_on && X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G;
         const uint32_t S = fresh ? H->sh_sparse : 0u;
         const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
-        X.sh_hinted = S | (K ? 1u : 0u);
         X.sh_clock = K;
         const uint32_t derived = S | (K ? 1u : 0u);
         const uint32_t N8 = fresh && narrow_on() ? H->sh_nw8 & ~derived : 0u;
