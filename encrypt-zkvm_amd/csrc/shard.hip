@@ -394,6 +394,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             for (zk_prover *p : P) {
                 (void)hipSetDevice(p->device);
                 upload_drain(p);
+                // (and the kernels of a failed proof: the next proof's uploads into d_trace must not overtake them)
+                (void)hipStreamSynchronize(p->st);
             }
         }
     } copy_guard{X.P, trace != nullptr};
