@@ -1036,7 +1036,7 @@ void hash_rows_cosets(hipStream_t st, const fe *base, int ncols, int log_n, int 
 // The trace rows (28 elements = 7 full blocks) are hashed this way as their columns' LDEs complete, so a
 // host-resident proof hashes its rows under the rest of the upload instead of after it.
 __global__ void __launch_bounds__(256) k_hash_rows_blocks(const fe *base, int log_n, int log_b, int b0, int b1, int nblk,
-                                                          uint8_t *cv_leaves) {
+                                                          uint8_t *cv_leaves, VirtCols virt) {
     const size_t N = (size_t)1 << (log_n + log_b), n = (size_t)1 << log_n, B = (size_t)1 << log_b;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= N) return;
@@ -1045,11 +1045,14 @@ __global__ void __launch_bounds__(256) k_hash_rows_blocks(const fe *base, int lo
     uint8_t *slot = cv_leaves + 32 * ((q << log_b) + r);
     if (b0 == 0) b3::iv(h);
     else load_digest(slot, h);
+    const uint32_t vmask = virt.mask >> (4 * b0) << (4 * b0) & ((b1 >= 8 ? 0u : 1u << (4 * b1)) - 1u);
+    const fe lg = vmask ? virt.lagr_lde[r * n + q] : fe_zero();  // e_(n-1)'s LDE at this row (virtual columns)
     for (int blk = b0; blk < b1; blk++) {
         const fe *p = base + r * n + q + (size_t)(4 * blk) * B * n;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            const fe v = p[(size_t)e * B * n];
+            const int c = 4 * blk + e;
+            const fe v = ((vmask >> c) & 1u) ? fe_mul(lg, virt.last[c]) : p[(size_t)e * B * n];
             m[4 * e + 0] = (uint32_t)v.lo;
             m[4 * e + 1] = (uint32_t)(v.lo >> 32);
             m[4 * e + 2] = (uint32_t)v.hi;
@@ -1061,11 +1064,12 @@ __global__ void __launch_bounds__(256) k_hash_rows_blocks(const fe *base, int lo
     store_digest(slot, h);
 }
 
-void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves) {
+void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves,
+                      VirtCols virt) {
     const size_t N = (size_t)1 << (log_n + log_b);
     ZK_PROF(st, "hash_rows", (64.0 * (b1 - b0) + (b0 ? 64.0 : 32.0)) * N,
             hipLaunchKernelGGL(k_hash_rows_blocks, dim3(cdiv(N, 256)), dim3(256), 0, st, base, log_n, log_b, b0, b1,
-                               ncols / 4, leaves));
+                               ncols / 4, leaves, virt));
 }
 
 // Sparse-column detection: nz[c0 + c] = 1 when column c has a nonzero entry before its last one; last[c0 + c] = its

@@ -1127,7 +1127,20 @@ struct TraceSrc {
     const uint8_t *const *cols = nullptr;
     const FixedCols *fixed = nullptr;  // with dev: only the dynamic columns are in dev (zk_vm_prove)
     bool hint_ok = true;               // host columns: the sparse hint of the previous proof may be used
+    bool no_virtual = false;           // every trace LDE column written (stage dumps read them)
 };
+
+// Virtual columns: the first trace column no transition constraint or assertion reads -- the evaluator reads columns
+// 0 .. 12 + 2 lwe_size - 1 <= 21 (enforce_add2 reads 2 lwe_size stack items, lwe_size <= 5; constrains.rs) -- so a
+// hinted sparse column from here on needs no LDE in memory (ZK_VIRTUAL=0 writes it)
+constexpr int ZK_VIRT_MIN_COL = 22;
+static bool virtual_on() {
+    static const bool on = [] {
+        const char *e = getenv("ZK_VIRTUAL");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
 
 // Column groups of a host-resident trace upload.  The copy engine streams group g + 1 while the CUs interpolate and
 // extend group g; more groups overlap more of the copy but add a launch drain per NTT pass and group.  A/B on one box
@@ -1274,6 +1287,7 @@ int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols *
 
 static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t n, uint8_t root[32]) {
     const fe inv_n = h_inv(fe_make(n));
+    p->virt = 0;  // every LDE column is written unless the host path below takes some as virtual
     SparseCols spc{};
     const SparseCols *sp = nullptr;
     if (!src.fixed) ZK_TRY(sparse_begin(p, pl, &spc, &sp));
@@ -1326,6 +1340,8 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     if (clk) nw32 &= ~1u;
     p->clk_used = clk;
     p->clk_bad = false;
+    const uint32_t virt = !src.no_virtual && virtual_on() ? hint & ~((1u << ZK_VIRT_MIN_COL) - 1u) : 0u;
+    p->virt = 0;  // (set once the hinted columns' last rows are on the device)
     p->sp_hinted = hint;
     p->up_bytes = 0;
     p->up_sparse = hint;
@@ -1369,7 +1385,8 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         int b = hashed;
         while (b < W / 4 && ready[4 * b] && ready[4 * b + 1] && ready[4 * b + 2] && ready[4 * b + 3]) b++;
         if (b - hashed >= 2 || (last && b > hashed)) {
-            hash_rows_blocks(p->st, p->lde, W, log_n, log_b, hashed, b, p->leaves);
+            hash_rows_blocks(p->st, p->lde, W, log_n, log_b, hashed, b, p->leaves,
+                             VirtCols{p->virt, p->sp_last, pl->lagr_lde});
             hashed = b;
         }
     };
@@ -1449,10 +1466,28 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         memset(lastv, 0, sizeof lastv);
         for (int i = 0; i < nh; i++) memcpy(&lastv[hin[i]], src.cols[hin[i]] + (n - 1) * sizeof(fe), sizeof(fe));
         ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
-        all_tf = true;  // no transform: the fills alone
-        const int rc = runs(hin, nh, transform);
-        all_tf = false;
-        ZK_TRY(rc);
+        // no transform: the fills alone -- the coefficients of every hinted column, the LDE of the non-virtual ones
+        int hnv[W], nhv = 0;
+        for (int i = 0; i < nh; i++)
+            if (!((virt >> hin[i]) & 1u)) hnv[nhv++] = hin[i];
+        SparseCols gsp = spc;
+        gsp.fused = false;
+        gsp.all = true;
+        ZK_TRY(runs(hin, nh, [&](int c0, int nc) {
+            gsp.col0 = c0;
+            ntt(p->st, pl->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, nc, true, nullptr, &inv_n,
+                p->tmp, &gsp);
+            return ZK_OK;
+        }));
+        ZK_TRY(runs(hnv, nhv, [&](int c0, int nc) {
+            gsp.col0 = c0;
+            ntt_lde(p->st, pl->Tn, pl->ct, p->polys + (size_t)c0 * n, n, nc, 0, 1, (int)B, p->lde + (size_t)c0 * B * n,
+                    B * n, n, p->tmp, &gsp);
+            return ZK_OK;
+        }));
+        p->virt = virt;
+        memcpy(p->virt_last, lastv, sizeof lastv);
+        p->virt_lagr = pl->lagr_lde;
         for (int i = 0; i < nh; i++) ready[hin[i]] = true;
     }
     if (clk) {
@@ -1663,8 +1698,10 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
 // One proof, plus the hints' bookkeeping for host-resident traces: a hinted sparse column that the host check finds
 // nonzero voids the proof, which is redone without hints; a completed proof leaves the columns it found sparse and
 // narrow (8- or 32-bit before the last row) as the next proof's hints.
-static int prove_impl(zk_prover *p, const TraceSrc &src, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
+static int prove_impl(zk_prover *p, const TraceSrc &src_in, size_t n, const zk_options *opt, const zk_pub_inputs *pub,
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
+    TraceSrc src = src_in;
+    if (dump) src.no_virtual = true;  // the stage dumps read every trace LDE column
     p->sp_used = false;
     p->sp_hinted = 0;
     p->sp_bad = 0;
@@ -1931,7 +1968,10 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     size_t na = 0;
     auto fe_at = [&](const fe *base, size_t idx) { addr[na++] = (uint64_t)(uintptr_t)(base + idx); };
     auto row_at = [&](const fe *base, int ncols, uint64_t i) {  // coset-major LDE row i
-        for (int c = 0; c < ncols; c++) fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
+        for (int c = 0; c < ncols; c++) {
+            if (base == p->lde && ((p->virt >> c) & 1u)) fe_at(p->virt_lagr, (i & (B - 1)) * n + (i >> log_b));
+            else fe_at(base, ((size_t)c * B + (i & (B - 1))) * n + (i >> log_b));
+        }
     };
     size_t need = nu * (W + CK);
     for (int l = 0; l < nl; l++) need += fri_pos[l].size() * fold * KX;
@@ -1968,6 +2008,10 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
         const fe *got = p->h_gather_out;
         size_t off = 0;
         O.trace_rows.assign(got, got + nu * W);
+        if (p->virt)  // virtual columns: the gather read e_(n-1)'s LDE there; times the column's last row
+            for (size_t q = 0; q < nu; q++)
+                for (int c = 0; c < W; c++)
+                    if ((p->virt >> c) & 1u) O.trace_rows[q * W + c] = fe_mul(O.trace_rows[q * W + c], p->virt_last[c]);
         off += nu * W;
         O.comp_rows.assign(got + off, got + off + nu * CK);
         off += nu * CK;

@@ -188,6 +188,12 @@ struct zk_prover {
     // whose traces refuted it, not speculated again)
     bool clk_used = false, clk_bad = false;
     size_t clk_off_n = 0;
+    // Virtual columns of the last host-trace commitment (trace_lde_commit): hinted sparse columns no constraint reads,
+    // whose LDE is never written -- the row hashing and the openings form their values from the last row and e_(n-1)'s
+    // LDE (virt_lagr) instead
+    uint32_t virt = 0;
+    fe virt_last[28] = {};
+    const fe *virt_lagr = nullptr;
     // Sharded host-trace hints (shard.hip S2): the sparse columns and the clock a previous sharded proof of this length
     // and world found (from all-gathered flags, so every rank holds the same), checked by the ranks' host threads
     uint32_t sh_sparse = 0, sh_nw8 = 0, sh_nw32 = 0;  // (and the narrow ones: the owner rank uploads them packed)

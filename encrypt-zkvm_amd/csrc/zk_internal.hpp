@@ -182,7 +182,14 @@ void commit_rows_coset_major(hipStream_t st, const fe *base, int ncols, int log_
                              uint8_t *nodes);
 // blocks b0 .. b1 - 1 of the leaf hashes of all B n rows of a coset-major column set of ncols (a multiple of 4,
 // <= 64) columns: columns 4 b .. 4 b + 3 compressed into the chaining value each leaf slot carries between launches
-void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves);
+// Virtual trace columns (host traces, prover.hip): sparse columns whose LDE is never written; the row hashing forms
+// column c's value at LDE point (coset r, position q) as last[c] * lagr_lde[r n + q]
+struct VirtCols {
+    uint32_t mask = 0;
+    const fe *last = nullptr, *lagr_lde = nullptr;
+};
+void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int log_b, int b0, int b1, uint8_t *leaves,
+                      VirtCols virt = VirtCols());
 // Storage of a FRI layer of L values: natural order (lb = 0), or coset-major over 2^lb cosets of 2^lcn
 // points (natural index i at (i mod 2^lb) 2^lcn + i / 2^lb): layer 0 as the DEEP coset LDE leaves it
 struct FriLayout {
