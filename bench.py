@@ -18,7 +18,8 @@ Proofs in flight (--inflight P, default 3): each GPU holds P independent provers
 compute streams, zk_prover objects; one upload stream per device) driven by P host threads, so one prover's trace
 upload, host-side transcript round trips and proof tail overlap the others' kernels.  P + 1 streams fit HIP's
 default 4 hardware queues at P = 3 (A/B at 4 queues, three passes: 11.53-11.56 ms per proof at P = 3, 11.52-11.58
-at P = 2, 11.75-11.79 at P = 4; profiles/r04_ab_queues.txt), so the line needs no GPU_MAX_HW_QUEUES setting
+at P = 2, 11.75-11.79 at P = 4; profiles/r04_ab_queues.txt; final round-4 tree: 11.30-11.37 at P = 3 against
+11.41-12.32 at P = 2 and 11.65-11.68 at P = 4, profiles/r04v_ab_inflight.txt), so the line needs no GPU_MAX_HW_QUEUES setting
 (queues_ab re-runs it at 16).  The K timed steps are K complete proofs, dealt round-robin to the provers;
 per-proof latency is stage_ms.
 
