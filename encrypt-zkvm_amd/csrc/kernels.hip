@@ -1706,18 +1706,21 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
             is_add2 = fe_mul(Y, b4);
             const fe is_sadd = fe_sub(Y, is_add2);
             const fe is_smul = fe_mul(fe_mul(n0_1_b2, nb3), nb4);
-            // sum_k (sn_k - s1_k * s0) = sum sn_k - s0 * sum s1_k  (one multiply instead of L)
-            fe acc4 = fe_zero(), acc5 = fe_zero(), sum_sn = fe_zero(), sum_s1 = fe_zero();
+            // Three column sums carry all three constraints (exact regrouping of the per-limb terms):
+            //   4: sum_k (sn_k - s1_k) - delta s0           = sum_sn - sum_s1 - delta s0
+            //   5: sum_k (sn_k - s_k - s_(L+k))             = sum_sn - sum_s1 - s0 - sum_hi
+            //      (s_0..s_(L-1) and s_(L)..s_(2L-1) overlap s_1..s_L in all but s0 and s_(L+1)..s_(2L-1))
+            //   7: sum_k (sn_k - s1_k * s0)                 = sum_sn - s0 * sum_s1
+            fe sum_sn = fe_zero(), sum_s1 = fe_zero(), sum_hi = fe_zero();
             for (int k = 0; k < L; k++) {
-                fe sn = NXT(12 + k);
-                fe s1k = CUR(13 + k);
-                acc4 = fe_add(acc4, fe_sub(sn, s1k));
-                acc5 = fe_add(acc5, fe_sub(sn, fe_add(CUR(12 + k), CUR(12 + L + k))));
-                sum_sn = fe_add(sum_sn, sn);
-                sum_s1 = fe_add(sum_s1, s1k);
+                sum_sn = fe_add(sum_sn, NXT(12 + k));
+                sum_s1 = fe_add(sum_s1, CUR(13 + k));
             }
+            for (int k = 1; k < L; k++) sum_hi = fe_add(sum_hi, CUR(12 + L + k));
+            const fe base = fe_sub(sum_sn, sum_s1);
             const fe acc7 = fe_sub(sum_sn, fe_mul(sum_s1, s0));
-            acc4 = fe_sub(acc4, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
+            const fe acc4 = fe_sub(base, fe_mul(S.delta, s0));  // encrypt_trivial body delta * s0 in limb L-1
+            const fe acc5 = fe_sub(base, fe_add(s0, sum_hi));
             ZK_ACCS(4, fe_mul(is_sadd, acc4));
             ZK_ACCS(5, fe_mul(is_add2, acc5));
             ZK_ACCS(7, fe_mul(is_smul, acc7));
