@@ -1497,10 +1497,10 @@ struct EvalShared {
 #define ZK_EVAL_LAZY 1  // lazy 288-bit sum over the selector section's terms (base field)
 #endif
 #ifndef ZK_EVAL_WAVES
-#define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1)
+#define ZK_EVAL_WAVES 4  // waves per SIMD the register budget targets (measured: 4 > 3 > 1; the LDS stash also caps a CU at 4 blocks)
 #endif
 #ifndef ZK_EVAL_WAVES_EXT
-#define ZK_EVAL_WAVES_EXT 4  // the two-plane (quadratic extension) variant (4: 128 VGPRs, 9 spills; 3: 142, 0)
+#define ZK_EVAL_WAVES_EXT 4  // the two-plane (quadratic extension) variant (4: 110 VGPRs, no spills since the limb sums)
 #endif
 // KE coefficient planes: KE = 2 for FieldExtension::Quadratic, where the composition coefficients are
 // E values; the composition is linear in them, so each constraint value is folded into two
