@@ -66,35 +66,34 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# ZK_BENCH_REHEARSE=1: rehearse the multi-GPU flow on fewer GPUs than ranks (several ranks per GPU): the process group
-# is gloo instead of RCCL, ranks share GPUs round robin and the sharded leg exchanges through zk_comm_create_host over
-# that group.  Same code path otherwise (barriers, max over ranks, rank 0's line, the sharded sub-record).
+# ZK_BENCH_REHEARSE=1: rehearse the multi-GPU flow on fewer GPUs than ranks (several ranks per GPU): ranks share GPUs
+# round robin and the sharded leg exchanges through zk_comm_create_host over the TCP host group instead of RCCL (which
+# refuses two ranks on one device).  Same code path otherwise (barriers, max over ranks, rank 0's line, the sharded sub-record).
 REHEARSE = os.environ.get("ZK_BENCH_REHEARSE", "0") == "1"
 
 
 def setup_dist(n_gpus):
+    """One process per GPU, torch-free: the library's own HIP runtime and RCCL (native.runtime_info(), recorded in the
+    line) and a TCP host group for barriers, max over ranks and the RCCL id (zkvm_amd.hostgroup; torchrun's
+    environment).  torch is never imported -- it bundles another libamdhip64 / librccl (ROCm 7.0), and the library
+    would run on whichever copy came first.  --torch-runtime imports it first on purpose (the runtime A/B)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    from zkvm_amd import native
+    native.lib()  # fail loudly without the HIP library
+    ndev = native.device_count()
+    if REHEARSE:
+        local %= max(1, ndev)
     pg = None
     if world > 1:
-        import torch
-        import torch.distributed as dist
+        from zkvm_amd.hostgroup import HostGroup
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if REHEARSE:
-            local %= max(1, torch.cuda.device_count())
-        backend = "nccl" if torch.cuda.is_available() and not REHEARSE else "gloo"
-        if torch.cuda.is_available():
-            torch.cuda.set_device(local)
-            if os.environ.get("ZK_NUMA_BIND", "1") != "0":
-                HOST["numa_node"] = bind_to_gpu_numa_node(local)
-                log(f"[rank {rank}] GPU {local}: host threads on NUMA node {HOST['numa_node']}")
-        dist.init_process_group(backend=backend)
-        pg = dist
-    elif os.environ.get("ZK_NUMA_BIND", "1") != "0":
-        import torch
-        if torch.cuda.is_available():
-            HOST["numa_node"] = bind_to_gpu_numa_node(local)
+        pg = HostGroup.from_env()
+    if ndev > 0 and os.environ.get("ZK_NUMA_BIND", "1") != "0":
+        HOST["numa_node"] = bind_to_gpu_numa_node(local)
+        if world > 1:
+            log(f"[rank {rank}] GPU {local}: host threads on NUMA node {HOST['numa_node']}")
     return world, rank, local, pg
 
 
@@ -113,12 +112,12 @@ def _cpulist(text):
 def bind_to_gpu_numa_node(local):
     """Pin this rank's host threads to the NUMA node its GPU hangs off (with several GPUs per host): the page-locked
     trace is then allocated and written on that node, and each upload reads memory behind its own PCIe root rather
-    than across the socket link.  Threads started later (the VM's) inherit it.  Returns the node, or None where the
-    topology is not exposed (nothing changes then)."""
+    than across the socket link.  Threads started later (the VM's) inherit it.  The device's PCI address comes from
+    the library's runtime (zk_device_pci_bus_id).  Returns the node, or None where the topology is not exposed
+    (nothing changes then)."""
     try:
-        import torch
-        pr = torch.cuda.get_device_properties(local)
-        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        from zkvm_amd import native
+        bdf = native.pci_bus_id(local).lower()
         node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
         if node < 0:
             return None
@@ -131,25 +130,22 @@ def bind_to_gpu_numa_node(local):
         return None
 
 
+def _sync(local):
+    from zkvm_amd import native
+    if native.device_count() > 0:
+        native.synchronize(local)
+
+
 def barrier(pg, local):
-    if pg is None:
-        return
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.synchronize(local)
-    pg.barrier()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize(local)
+    """Device sync, host barrier over every rank, device sync (the timed region's brackets)."""
+    _sync(local)
+    if pg is not None:
+        pg.barrier()
+        _sync(local)
 
 
 def max_over_ranks(pg, value, local):
-    if pg is None:
-        return value
-    import torch
-    dev = f"cuda:{local}" if torch.cuda.is_available() and not REHEARSE else "cpu"
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    return value if pg is None else pg.max(value)
 
 
 def timed_loop(step, steps: int, warmup: int, pg, local: int) -> float:
@@ -205,7 +201,8 @@ def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0, repeats:
     pub = orc.make_pub(h, outputs)
     opts = orc.default_options(num_queries=43, field_extension=2) if config5 else orc.default_options()
     runs = []
-    for _ in range(max(1, repeats)):  # each CPU config timed 3x in the same invocation, median
+    for k in range(max(1, repeats)):  # each CPU config timed 3x in the same invocation, median
+        log(f"cpu baseline: 2^{log_n} sample, proof {k + 1} of {repeats} ...")
         t0 = time.perf_counter()
         orc.prove(trace, pub, opts)
         runs.append(time.perf_counter() - t0)
@@ -231,6 +228,7 @@ def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0, repeats:
                 errs.append(e)
 
         ths = [threading.Thread(target=one) for _ in range(all_cores)]
+        log(f"cpu baseline: {all_cores} concurrent 2^{log_n} proofs ...")
         t0 = time.perf_counter()
         for t in ths:
             t.start()
@@ -243,6 +241,30 @@ def cpu_baseline(log_n: int, config5: bool = False, all_cores: int = 0, repeats:
                             "sample": f"{all_cores} concurrent single-thread oracle proofs of the same 2^{log_n} "
                                       f"trace: {dta:.1f} s"}
     return out
+
+
+def cpu_headline(trace, pub, opts, gpu_proof: bytes, log_n: int):
+    """cpu_baseline.value: ONE proof of the headline workload's own 2^log_n trace by the oracle's single-threaded
+    or_prove (the build's C restatement of the reference prover, which cannot be built here), on this host's
+    cores; the proof must equal the GPU's byte for byte."""
+    import ctypes as C
+    from oracle import oracle as orc
+    orc.build()
+    opub = orc.PubInputs()
+    C.memmove(opub.program_hash, bytes(pub.program_hash), 32)
+    C.memmove(opub.stack_outputs, bytes(pub.stack_outputs), 256)
+    opub.lwe_size, opub.delta = pub.lwe_size, pub.delta
+    oopts = orc.default_options(num_queries=opts.num_queries, field_extension=opts.field_extension)
+    log(f"cpu baseline: one single-thread oracle proof of the 2^{log_n} workload trace ...")
+    t0 = time.perf_counter()
+    oproof = orc.prove(trace, opub, oopts)[0]
+    dt = time.perf_counter() - t0
+    n = trace.shape[1]
+    return {"value": n / dt, "unit": "trace-steps/s", "cores": 1, "kind": "port", "runs_s": [round(dt, 2)],
+            "proof_equals_gpu_proof": oproof == gpu_proof,
+            "sample": f"oracle or_prove (C, 1 thread): one proof of the timed workload's own 2^{log_n}-step trace "
+                      f"(input set 0, the configs[2] pin's trace) with the same options, {dt:.1f} s; the reference "
+                      f"prover (winterfell 0.9, single-threaded) cannot be built here"}
 
 
 def host_cores(req: int) -> int:
@@ -352,7 +374,15 @@ def main():
                     help="A/B runs: of the comparison legs keep only steady_state, device-resident and latency")
     ap.add_argument("--config5", action="store_true",
                     help="128-bit security options (configs[4]): 43 queries, FieldExtension::Quadratic")
+    ap.add_argument("--input-sets", type=int, default=4,
+                    help="input sets of the workload program the timed proofs rotate through (fresh secrets, public "
+                         "inputs and random last rows; set 0 is the pinned seed-1000 workload)")
+    ap.add_argument("--torch-runtime", action="store_true",
+                    help="import torch before the library (runtime A/B only): the library then runs on torch's bundled "
+                         "HIP runtime and RCCL instead of the /opt/rocm copies it links")
     args = ap.parse_args()
+    if args.torch_runtime:
+        import torch  # noqa: F401  (maps torch/lib/libamdhip64.so first; the library shares it)
     # HIP's hardware queues per process: whatever the environment gives (the runtime's default is 4, which the GPU
     # boxes of this pool also export); reported in the line, and queues_ab re-runs the workload at the other setting
     if args.sharded:
@@ -372,6 +402,7 @@ def main():
     # the VM writes its TraceTable straight into page-locked host memory (zk_host_alloc): the host-resident
     # trace the timed region starts from (vm/src/lib.rs:18 builds it, :26 hands it to prove)
     host = HostTrace(n)
+    S = max(1, args.input_sets)
     # vm::prove's front half (vm/src/lib.rs:13-18) in the reference's two steps: Program::compile (parse, pad,
     # hash: the sequential Rescue sponge, once per program) and Processor::run + trace on this run's inputs
     # (a sequential stack pass plus threaded row writes), timed separately; neither is in the timed region
@@ -385,6 +416,16 @@ def main():
               "threads": os.environ.get("ZK_VM_THREADS") or os.environ.get("OMP_NUM_THREADS") or os.cpu_count()}
     log(f"[rank {rank}] VM: n={n} compile {vm_rec['compile_ms']} ms, trace {vm_rec['trace_ms']} ms")
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    # the other input sets of the same program: fresh secrets, public inputs and random last rows, each trace in its
+    # own page-locked buffer (the timed proofs rotate through all S, as a server proving fresh inputs would)
+    sets = [(trace, pub)]
+    extra_hosts = []
+    for k in range(1, S):
+        wk = make_workload(src, seed=5000 + 16 * rank + k)
+        hk = HostTrace(n)
+        extra_hosts.append(hk)
+        tk, ok = prog.trace(wk.public, wk.secret, wk.server_key, wk.last_row, out=hk)
+        sets.append((tk, make_pub_inputs(h, ok, wk.server_key.lwe_size(), wk.server_key.parameters.delta)))
     opts = ProofOptions(43, 8, 0, 2, 8, 127) if args.config5 else ProofOptions()
     min_sec = 128 if args.config5 else 95
     opts_str = "ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5 else "ProofOptions(32, 8, 0, None, 8, 127)"
@@ -398,16 +439,46 @@ def main():
             last[k] = provers[k].prove_host(tr, pub, opts)[0]
         return f
 
-    # ---- value: zk_prove from the host-resident (page-locked) trace to proof bytes, P proofs in flight
-    fns = [host_step(k, trace) for k in range(P)]
+    # proofs per input set: every proof of a set must be the same bytes, whichever prover made it
+    set_proofs = [None] * S
+    nxt = [0]
+    lock = threading.Lock()
+
+    def rotating_step(k):
+        def f():
+            with lock:
+                i = nxt[0] % S
+                nxt[0] += 1
+            tr, pb = sets[i]
+            pr = provers[k].prove_host(tr, pb, opts)[0]
+            with lock:
+                if set_proofs[i] is None:
+                    set_proofs[i] = pr
+                elif set_proofs[i] != pr:
+                    raise AssertionError(f"input set {i}: two proofs of the same trace differ")
+            if i == 0:
+                last[k] = pr
+        return f
+
+    # ---- value: zk_prove from the host-resident (page-locked) traces to proof bytes, P proofs in flight, rotating
+    # through the S input sets
+    fns = [rotating_step(k) for k in range(P)]
     # warm-up: exactly --warmup untimed proofs, dealt round-robin (each prover's first proof builds its per-size
     # tables; the next ones pay page faults and clock ramp-up: 18.9, 14.5, 14.2, then 13.9 ms,
     # tools/proof_times.py); the default is three per prover
     warm = args.warmup if args.warmup is not None else 3 * P
     run_proofs(fns, warm)
     elapsed = run_proofs_timed(fns, args.steps, pg, local)
-    proof = last[0]
-    assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
+    proof = set_proofs[0]
+    assert proof is not None and all(p_ == proof for p_ in last if p_ is not None), \
+        "provers disagree on the proof bytes"
+    set_proofs_ok = all(set_proofs)
+    # the single-trace window beside it (the round-4 headline's form): every proof from set 0
+    sfns = [host_step(k, trace) for k in range(P)]
+    single_s = None
+    if not args.no_compare:
+        single_s = run_proofs_timed(sfns, args.steps, pg, local)
+        assert all(p_ == proof for p_ in last if p_ is not None), "provers disagree on the proof bytes"
 
     # ---- comparison legs (same provers, same count, outside the headline): the trace already in HBM
     # (zk_prove_device), and the host trace in pageable memory (runtime-staged copies)
@@ -479,15 +550,29 @@ def main():
     # proof must also equal the pin byte for byte (the other ranks' seeds have no pin)
     pin = pin_check(proof, find_pin(args.log_n, 1000 + rank, opts))
     all_verified = all_ranks_true(pg, zk_verified, local)
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        # the reported CPU baseline: one single-thread oracle proof of the headline workload's own trace (input set
+        # 0, the pinned configs[2] trace) -- its proof must be the GPU's bytes -- plus the bounded 2^18 samples
+        cpu = cpu_headline(trace, pub, opts, proof, args.log_n)
+        cpu["sample_2p18"] = cpu_baseline(args.cpu_log_n, args.config5, host_cores(args.cpu_cores))
+        if "all_cores" in cpu["sample_2p18"]:
+            cpu["all_cores"] = cpu["sample_2p18"].pop("all_cores")
     trace = None
+    sets = None
     host.close()
+    for hk in extra_hosts:
+        hk.close()
 
     out = build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops,
                      latency_ms, dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified,
-                     zk_verified, pin, all_verified, lifetime) if rank == 0 else None
+                     zk_verified, pin, all_verified, lifetime, cpu) if rank == 0 else None
     if out is not None:
         out["gpu_max_hw_queues"] = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         out["trace_upload"] = upload
+        out["input_sets"] = {"count": S, "timed_proofs_rotate": True, "all_sets_proved_and_consistent": set_proofs_ok,
+                             "single_trace_ms": round(1e3 * single_s / args.steps, 3) if single_s else None}
+        out["runtime"] = native.runtime_info()
     if out is not None and world == 1 and not args.no_compare and not args.ab:
         q = queues_leg(args, P)
         out["queues_ab"] = q
@@ -498,8 +583,8 @@ def main():
     # watchdog bounds it: should a collective never complete, rank 0 still prints the line (with the error) and
     # every rank exits, so the replica measurement above is never lost.
     if world > 1 and args.sharded_log_n:
-        import torch
-        if torch.cuda.is_available():
+        from zkvm_amd import native
+        if native.device_count() > 0:
             done = threading.Event()
 
             def watchdog():
@@ -526,7 +611,7 @@ def main():
     if out is not None:
         print(json.dumps(out), flush=True)
     if pg is not None:
-        pg.destroy_process_group()
+        pg.close()
 
 
 SHARDED_TIMEOUT_S = 240
@@ -626,7 +711,7 @@ def vm_prove_leg(args, prog, src, w, proof, provers, opts, pg, local, rank):
 
 def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, program_ops, padded_ops, latency_ms,
                dev_s, pag_s, steady_s, cmp_steps, stages, kstats, kops, vm_rec, proof, verified, zk_verified, pin,
-               all_verified, lifetime):
+               all_verified, lifetime, cpu):
     """rank 0's JSON line (the driver's contract) from the measurements of main()."""
     dom = max(kstats.items(), key=lambda kv: kv[1][0])
     name, (tot_ms, launches, tot_bytes) = dom
@@ -649,9 +734,6 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
                             "achieved_fe_mul_per_s": round(muls / (tot_ms / 1e3), 1), "peak_fe_mul_per_s": FE_MUL_PEAK,
                             "floor_ms_per_launch": round(floor_ms / launches, 4), "frac": round(floor_ms / tot_ms, 4)}
     roofline["valu_hw"] = pmc_valu(name)
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_log_n, args.config5, host_cores(args.cpu_cores))
     value = world * n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
@@ -702,14 +784,14 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
     pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
     opts = ProofOptions(43, 8, 0, 2, 8, 127) if config5 else ProofOptions()
     if REHEARSE and world > 1:
-        from zkvm_amd.sharded import torch_exchange
-        sp = ShardedProver.host(rank, world, torch_exchange(), local, n)
+        # several ranks on one GPU: exchanges through host memory over the TCP host group (RCCL refuses a
+        # communicator with two ranks on one device)
+        sp = ShardedProver.host(rank, world, pg.exchange_fn(), local, n)
     else:
+        # RCCL from the library's own runtime (native.runtime_info()["rccl"]); the id travels over the host group
         uid = ShardedProver.unique_id() if rank == 0 else None
         if pg is not None:
-            box = [uid]
-            pg.broadcast_object_list(box, src=0)
-            uid = box[0]
+            uid = pg.broadcast(uid, src=0)
         sp = ShardedProver.rccl(rank, world, uid, local, n)
     last = {}
 
@@ -822,7 +904,7 @@ def run_sharded(args):
         }
         print(json.dumps(out), flush=True)
     if pg is not None:
-        pg.destroy_process_group()
+        pg.close()
 
 
 if __name__ == "__main__":

@@ -13,24 +13,31 @@
 
 namespace zk {
 
+// The count is read and written only under mu_, and count_down() notifies while it still holds mu_: a waiter can
+// only observe zero after the last count_down() has released the mutex for good, so a Latch that lives on the
+// waiter's stack may go out of scope as soon as wait() or ready() reports zero.
 class Latch {
 public:
     explicit Latch(int count = 0) : left_(count) {}
-    void reset(int count) { left_.store(count); }
-    void count_down() {
-        if (left_.fetch_sub(1) == 1) {
-            std::lock_guard<std::mutex> lk(mu_);
-            cv_.notify_all();
-        }
+    void reset(int count) {
+        std::lock_guard<std::mutex> lk(mu_);
+        left_ = count;
     }
-    bool ready() const { return left_.load() <= 0; }
+    void count_down() {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--left_ == 0) cv_.notify_all();
+    }
+    bool ready() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return left_ <= 0;
+    }
     void wait() {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return left_.load() <= 0; });
+        cv_.wait(lk, [&] { return left_ <= 0; });
     }
 
 private:
-    std::atomic<int> left_;
+    int left_;
     std::mutex mu_;
     std::condition_variable cv_;
 };

@@ -1570,6 +1570,9 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     };
     auto issue = [&](const Item &it) -> int {
         std::lock_guard<std::mutex> lk(*p->up_mu);
+        // a copy that fails part-way through the item still gets the item's event behind the copies queued before
+        // it, so upload_drain (CopyGuard) waits for every DMA that reads the caller's columns
+        UploadEvent rec{p->ev_up[it.ev], p->up};
         if (it.narrow) {
             ZK_CHECK_HIP(hipMemcpyAsync(stage, p->h_pack, pack_bytes, hipMemcpyHostToDevice, p->up));
             p->up_bytes += pack_bytes;
@@ -1577,8 +1580,7 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         } else {
             ZK_TRY(runs(it.cols, it.nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
         }
-        ZK_CHECK_HIP(hipEventRecord(p->ev_up[it.ev], p->up));
-        return ZK_OK;
+        return rec.record();
     };
     Item cur;
     bool have = next_item(&cur);

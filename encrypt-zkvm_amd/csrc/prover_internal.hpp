@@ -250,6 +250,23 @@ int upload_gate(zk_prover *p, hipEvent_t ev);
 // wait until every upload this prover has enqueued has completed (the caller's host buffers are free again)
 void upload_drain(zk_prover *p);
 
+// The event that closes one upload item on the shared upload stream (taken under up_mu).  record() records it and
+// reports the status; an item left early by a failed copy records it from the destructor, so the copies already
+// queued for the item are covered by an event upload_drain waits for.
+struct UploadEvent {
+    hipEvent_t ev;
+    hipStream_t st;
+    bool done = false;
+    int record() {
+        done = true;
+        ZK_CHECK_HIP(hipEventRecord(ev, st));
+        return ZK_OK;
+    }
+    ~UploadEvent() {
+        if (!done) (void)hipEventRecord(ev, st);
+    }
+};
+
 // vm::prove's preprocessed trace columns (vm_gpu.hip, zk_vm_prove).  Columns 0..11 (clk, opcode bits, hash flag,
 // sponge, stack depth) depend on the program and lwe_size only, and a stack register column 12 + i with i >= the
 // program's maximum depth is zero: every such column c is f_c + last[c] e_(n-1), with f_c fixed per program (f_c = 0

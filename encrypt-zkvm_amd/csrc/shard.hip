@@ -535,6 +535,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 const int q = i < nu ? narrow_of(l, U[i]) : -1;
                 if (q >= 0) packed.wait();  // (before the lock: the packing does not need it)
                 std::lock_guard<std::mutex> lk(*p->up_mu);
+                UploadEvent rec{p->ev_up[k], p->up};  // recorded on the error path too (CopyGuard drains it)
                 if (q >= 0 && !((pack_bad[l].load() >> U[i]) & 1u)) {
                     const size_t w = (size_t)nar[l].width[q] * n;
                     ZK_CHECK_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t *>(CLDE(p)) + nar[l].off[q],
@@ -544,7 +545,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                     ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)U[i] * n, trace + (size_t)U[i] * col, col,
                                                 hipMemcpyHostToDevice, p->up));
                 }
-                ZK_CHECK_HIP(hipEventRecord(p->ev_up[k], p->up));
+                ZK_TRY(rec.record());
             }
             return ZK_OK;
         };

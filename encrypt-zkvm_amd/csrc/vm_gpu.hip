@@ -381,10 +381,20 @@ int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint
     const uint32_t nb = B / (uint32_t)rstride;  // cosets held
     Plan *pl = nullptr;
     ZK_TRY(get_plan(p, n, B, &pl));
-    zk_program::Fixed f{in.L, B, 0, nullptr, nullptr, nullptr, nullptr, r0, rstride};
-    ZK_CHECK_HIP(hipMalloc(&f.fpolys, 12 * n * sizeof(fe)));
-    d->fixed.push_back(f);  // freed by ~zk_program; completed below
-    zk_program::Fixed &g = d->fixed.back();
+    // built in a local entry and cached only once complete: a call whose inputs the VM refuses (too few inputs, ...)
+    // leaves no half-built entry behind for the program's later calls
+    zk_program::Fixed g{in.L, B, 0, nullptr, nullptr, nullptr, nullptr, r0, rstride};
+    struct Unwind {
+        zk_program::Fixed *g;
+        ~Unwind() {
+            if (!g) return;
+            (void)hipFree(g->fpolys);
+            (void)hipFree(g->flde);
+            (void)hipFree(g->lagr);
+            (void)hipFree(g->lagr_lde);
+        }
+    } unwind{&g};
+    ZK_CHECK_HIP(hipMalloc(&g.fpolys, 12 * n * sizeof(fe)));
     ZK_CHECK_HIP(hipMalloc(&g.flde, 12 * nb * n * sizeof(fe)));
     ZK_CHECK_HIP(hipMalloc(&g.lagr, n * sizeof(fe)));
     ZK_CHECK_HIP(hipMalloc(&g.lagr_lde, nb * n * sizeof(fe)));
@@ -406,6 +416,8 @@ int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint
     ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, r0, rstride, (int)nb, g.lagr_lde, nb * n, n, p->tmp);
     ZK_TRY(io_rewind(p));  // sync: the cache is complete, the staging area starts over
     g.md = (int)md;
+    d->fixed.push_back(g);  // freed by ~zk_program from here on
+    unwind.g = nullptr;
     *out = g;
     return ZK_OK;
 }

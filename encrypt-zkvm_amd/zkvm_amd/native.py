@@ -28,7 +28,8 @@ MAX_COLS, MAX_TCONS, MAX_ASSERTS, MAX_CCOLS, MAX_FRI, MAX_REM, MAX_Q = 32, 32, 3
 
 # every symbol include/zkvm_gpu.h declares (checked by tests/test_native_abi.py)
 EXPORTED = (
-    "zk_last_error", "zk_device_count", "zk_prover_create", "zk_prover_create_shard", "zk_prover_destroy",
+    "zk_last_error", "zk_device_count", "zk_runtime_versions", "zk_device_pci_bus_id", "zk_device_synchronize",
+    "zk_prover_create", "zk_prover_create_shard", "zk_prover_destroy",
     "zk_prover_acquire", "zk_prover_release", "zk_prover_pool_trim", "zk_prover_trace_buffer",
     "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
@@ -84,17 +85,69 @@ class Dump(C.Structure):
 
 
 _lib = None
+_runtime = None
+
+
+def mapped_files(prefix: str) -> list:
+    """Distinct files (resolved paths) mapped into this process whose name starts with `prefix`."""
+    found = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split(None, 5)
+            if len(parts) == 6 and os.path.basename(parts[5].strip()).startswith(prefix):
+                found.add(os.path.realpath(parts[5].strip()))
+    return sorted(found)
+
+
+class _RefuseSecondRuntime:
+    """sys.meta_path guard installed once the library has mapped the HIP runtime it links (/opt/rocm): importing
+    torch afterwards would map torch's bundled libamdhip64 as a SECOND runtime (torch asks for the soname
+    libamdhip64.so, which the loaded libamdhip64.so.7 does not satisfy).  A process that needs both must import
+    torch first; the library then shares torch's copy (one runtime, recorded by runtime_info())."""
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch" or name.startswith("torch."):
+            raise ImportError(
+                f"zkvm_amd: {LIB_PATH.name} has already mapped {runtime_info()['hip_runtime']}; importing torch now "
+                f"would load torch's own HIP runtime as a second one -- import torch before the first native.lib() "
+                f"call, or keep GPU work torch-free")
+        return None
+
+
+def runtime_info() -> dict:
+    """The HIP runtime and RCCL this process's library runs on: the mapped files and their versions."""
+    global _runtime
+    if _runtime is None:
+        L = lib()
+        hv, rv = C.c_int(0), C.c_int(0)
+        rc = L.zk_runtime_versions(C.byref(hv), C.byref(rv))
+        hips, rccls = mapped_files("libamdhip64.so"), mapped_files("librccl.so")
+        _runtime = {"hip_runtime": hips[0] if len(hips) == 1 else hips, "rccl": rccls[0] if len(rccls) == 1 else rccls,
+                    "hip_runtime_version": hv.value if rc == ZK_OK else None,
+                    "rccl_version": rv.value if rc == ZK_OK else None,
+                    "torch_loaded_first": "torch" in __import__("sys").modules}
+    return dict(_runtime)
 
 
 def lib():
     global _lib
     if _lib is None:
+        import sys
         if not LIB_PATH.exists():
             raise ZkError(ZK_ERR_DEVICE, f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C encrypt-zkvm_amd)")
         L = C.CDLL(str(LIB_PATH))
+        hips = mapped_files("libamdhip64.so")
+        if len(hips) != 1:
+            raise ZkError(ZK_ERR_DEVICE, f"{len(hips)} HIP runtimes mapped into this process ({hips}): exactly one "
+                                         f"must serve {LIB_PATH.name}")
+        if "torch" not in sys.modules and not any(isinstance(f, _RefuseSecondRuntime) for f in sys.meta_path):
+            sys.meta_path.insert(0, _RefuseSecondRuntime())
         vp, sz, u32, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_int
         L.zk_last_error.restype = C.c_char_p
         L.zk_device_count.argtypes = [C.POINTER(i32)]
+        L.zk_runtime_versions.argtypes = [C.POINTER(i32), C.POINTER(i32)]
+        L.zk_device_pci_bus_id.argtypes = [i32, C.c_char_p, i32]
+        L.zk_device_synchronize.argtypes = [i32]
         L.zk_prover_create.argtypes = [i32, sz, u32, C.POINTER(vp)]
         L.zk_prover_create_shard.argtypes = [i32, sz, i32, C.POINTER(vp)]
         L.zk_prover_destroy.argtypes = [vp]
@@ -178,3 +231,21 @@ def device_count() -> int:
     c = C.c_int(0)
     lib().zk_device_count(C.byref(c))
     return c.value
+
+
+def pci_bus_id(device: int) -> str:
+    buf = C.create_string_buffer(32)
+    check(lib().zk_device_pci_bus_id(device, buf, len(buf)), "zk_device_pci_bus_id")
+    return buf.value.decode()
+
+
+def synchronize(device: int):
+    check(lib().zk_device_synchronize(device), "zk_device_synchronize")
+
+
+def hip_runtime():
+    """ctypes handle of the HIP runtime the library runs on (the same mapped file: dlopen returns its handle)."""
+    path = runtime_info()["hip_runtime"]
+    h = C.CDLL(path)
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return h

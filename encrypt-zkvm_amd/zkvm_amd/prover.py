@@ -261,8 +261,7 @@ _hip_lib = None
 def _hip():
     global _hip_lib
     if _hip_lib is None:
-        _hip_lib = C.CDLL("libamdhip64.so")
-        _hip_lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip_lib = native.hip_runtime()  # the runtime the library runs on, never a second copy
     return _hip_lib
 
 

@@ -5,12 +5,12 @@ FRI layer 1 and the openings are exchanged through a communicator:
 
   * ShardedProver.loopback(world)       -- every rank driven from this process (one prover per rank,
                                            in-process copies); used by the tests on one GPU;
-  * ShardedProver.rccl(rank, world, id) -- one process per GPU, RCCL over xGMI; the 128-byte id comes
-                                           from ShardedProver.unique_id() on rank 0 and is shared out of
-                                           band (bench.py uses torch.distributed);
+  * ShardedProver.rccl(rank, world, id) -- one process per GPU, RCCL over xGMI (the librccl the library
+                                           links); the 128-byte id comes from ShardedProver.unique_id() on
+                                           rank 0 and is shared out of band (bench.py: HostGroup.broadcast);
   * ShardedProver.host(rank, world, fn)  -- one process per rank, exchanges staged through host memory and
-                                           a caller transport (torch_exchange(): a torch.distributed
-                                           group, e.g. gloo; MPI or TCP through the same C callback).
+                                           a caller transport (zkvm_amd.hostgroup.HostGroup.exchange_fn():
+                                           TCP; MPI or any other transport through the same C callback).
 Every rank returns the same proof bytes, identical to the single-GPU prover's.
 """
 from __future__ import annotations
@@ -22,36 +22,6 @@ import numpy as np
 from . import native
 from .native import Record, check, lib
 from .prover import REFERENCE_OPTIONS, ProofOptions
-
-
-def torch_exchange(group=None):
-    """A zk_exchange_fn over a torch.distributed process group (any backend that takes CPU tensors: gloo).
-
-    Returns the ctypes callback; keep it alive as long as the communicator (ShardedProver.host does)."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-
-    def view(addr, nbytes):
-        return torch.frombuffer((C.c_uint8 * nbytes).from_address(addr), dtype=torch.uint8)
-
-    def fn(_ctx, op, send, recv, nbytes):
-        try:
-            if nbytes:
-                out = view(recv, nbytes * world)
-                if op == native.XCHG_ALL_TO_ALL:
-                    dist.all_to_all_single(out, view(send, nbytes * world), group=group)
-                elif op == native.XCHG_ALL_GATHER:
-                    dist.all_gather_into_tensor(out, view(send, nbytes), group=group)
-                else:
-                    return 2
-            return 0
-        except Exception as e:  # an exception must not unwind through the C frames
-            import sys
-            print(f"zk exchange callback: {type(e).__name__}: {e}", file=sys.stderr)
-            return 1
-
-    return native.EXCHANGE_FN(fn)
 
 
 class ShardedProver:
@@ -86,7 +56,7 @@ class ShardedProver:
 
     @classmethod
     def host(cls, rank: int, world: int, fn, device: int, max_trace_len: int) -> "ShardedProver":
-        """One rank per process over a caller transport: fn is a native.EXCHANGE_FN (see torch_exchange)."""
+        """One rank per process over a caller transport: fn is a native.EXCHANGE_FN (see HostGroup.exchange_fn)."""
         comm = C.c_void_p()
         check(lib().zk_comm_create_host(rank, world, fn, None, C.byref(comm)), "zk_comm_create_host")
         p = C.c_void_p()

@@ -112,6 +112,17 @@ typedef struct zk_trace_lde zk_trace_lde;
 const char *zk_last_error(void);
 int zk_device_count(int *count);
 
+/* ---- the runtime this library is linked against (no reference counterpart: host plumbing) ----
+ * The library needs libamdhip64.so.7 and librccl.so.1 (RUNPATH /opt/rocm/lib).  A host that also loads another
+ * copy of either (PyTorch bundles its own) must load it first, or the process maps two HIP runtimes; these calls let a
+ * host get what it needs from the copy the library uses instead.  zk_runtime_versions: hipRuntimeGetVersion and
+ * ncclGetVersion of the mapped copies.  zk_device_pci_bus_id: "dddd:bb:dd.f" of a device (the host's NUMA binding
+ * reads /sys/bus/pci/devices/<id>/numa_node).  zk_device_synchronize: hipDeviceSynchronize on one device (the bench's
+ * barriers). */
+int zk_runtime_versions(int *hip_runtime, int *rccl);
+int zk_device_pci_bus_id(int device, char *bus_id, int len);
+int zk_device_synchronize(int device);
+
 /* ---- prover object: device memory sized for traces up to max_trace_len rows ----
  * Process-wide side effect: the first zk_prover_create on a device that the process has not used yet
  * sets hipDeviceScheduleSpin for that device, so every host thread waiting on a stream of that device

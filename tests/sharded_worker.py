@@ -1,8 +1,8 @@
-"""One rank of a multi-process coset-sharded proof (zk_prove_sharded over zk_comm_create_host + gloo).
+"""One rank of a multi-process coset-sharded proof (zk_prove_sharded over zk_comm_create_host + a TCP host group).
 
 Started by tests/test_sharded_multiprocess.py, `world` copies at once, all on GPU 0 of the test box: every process
-holds one rank-sized prover and exchanges through torch.distributed (gloo over 127.0.0.1), which is the code path an
-RCCL rank runs (one local rank per process, rank-dependent ownership of cosets, openings and FRI layers) with the
+holds one rank-sized prover and exchanges through zkvm_amd.hostgroup (TCP over 127.0.0.1; torch-free, so the library
+runs on the HIP runtime it links), which is the code path an RCCL rank runs (one local rank per process, rank-dependent ownership of cosets, openings and FRI layers) with the
 transport swapped.  Each job's proof sha256 goes to <out>/rank<r>.json; the test compares them with the golden
 proofs and, for the generated traces, with the single-GPU prover's proof (computed on rank 0).
 
@@ -10,7 +10,6 @@ usage: python tests/sharded_worker.py RANK WORLD PORT OUTDIR [selftest | large:<
 """
 import hashlib
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -84,14 +83,13 @@ def selftest(rank, world, fn):
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], Path(sys.argv[4])
     mode = sys.argv[5] if len(sys.argv) > 5 else "prove"
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-    import torch.distributed as dist
-    from zkvm_amd.sharded import ShardedProver, torch_exchange
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    fn = torch_exchange()
+    from zkvm_amd.hostgroup import HostGroup
+    from zkvm_amd.sharded import ShardedProver
+    dist = HostGroup(rank, world, port=int(port), timeout=120)
+    fn = dist.exchange_fn()
     if mode == "selftest":
         (out / f"rank{rank}.json").write_text(json.dumps(selftest(rank, world, fn)))
-        dist.destroy_process_group()
+        dist.close()
         return
     if mode.startswith("large:"):  # one full-size pinned case (tests/golden/large), checked here on every rank
         sys.path.insert(0, str(ROOT / "tests"))
@@ -108,7 +106,7 @@ def main():
         check_large_proof(c, proof, rec, pub, oracle)  # the parent test built the oracle library
         (out / f"rank{rank}.json").write_text(json.dumps({c["name"]: {"sha256": hashlib.sha256(proof).hexdigest(),
                                                                        "want": c["proof_sha256"]}}))
-        dist.destroy_process_group()
+        dist.close()
         return
     jobs = golden_jobs(world) + generated_jobs(rank)
     res = {}
@@ -135,8 +133,10 @@ def main():
             prog.close()
     finally:
         sp.close()
+    from zkvm_amd import native
+    res["runtime"] = native.runtime_info()
     (out / f"rank{rank}.json").write_text(json.dumps(res))
-    dist.destroy_process_group()
+    dist.close()
 
 
 if __name__ == "__main__":

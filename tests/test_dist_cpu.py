@@ -1,20 +1,65 @@
-"""Multi-rank bench harness on CPU (gloo, world_size 2).
+"""Multi-rank bench harness on CPU (world_size 2 and 4, separate processes, no GPU, no torch).
 
-bench.py at N > 1 runs one process per GPU; each rank proves its own independent trace (weak
-scaling, no data-path collective) and the timing is barrier-bracketed with the max taken over
-ranks.  Here the same code (bench.setup_dist / timed_loop / max_over_ranks) runs under gloo with
-a stand-in step of rank-dependent duration: every rank must report the slowest rank's time.
+bench.py at N > 1 runs one process per GPU (torchrun's environment); each rank proves its own independent trace (weak
+scaling, no data-path collective) and the timing is barrier-bracketed with the max taken over ranks.  The host side of
+that runs over zkvm_amd.hostgroup (a TCP group; torch is never imported, so the library keeps its own HIP runtime and
+RCCL).  Here the same code (bench.setup_dist / timed_loop / max_over_ranks) runs with a stand-in step of
+rank-dependent duration: every rank must report the slowest rank's time.  The host group's collectives and its
+zk_exchange_fn are checked byte for byte.
 """
+import json
 import os
 import socket
+import subprocess
 import sys
-import time
 from pathlib import Path
 
 import pytest
-import torch.multiprocessing as mp
 
 ROOT = Path(__file__).resolve().parent.parent
+
+WORKER = r'''
+import json, os, sys, time
+sys.path[:0] = [{root!r}, {pkg!r}]
+mode = sys.argv[1]
+if mode == "bench":
+    import bench
+    w, r, local, pg = bench.setup_dist(int(os.environ["WORLD_SIZE"]))
+    calls = []
+    def step():
+        calls.append(1)
+        time.sleep(0.03 * (r + 1))
+    elapsed = bench.timed_loop(step, steps=4, warmup=2, pg=pg, local=local)
+    ok = bench.all_ranks_true(pg, r != 1, local)
+    out = {{"rank": r, "world": w, "elapsed": elapsed, "calls": len(calls), "all_true": ok,
+            "torch": "torch" in sys.modules}}
+    pg.close()
+else:
+    import ctypes as C
+    from zkvm_amd import native
+    from zkvm_amd.hostgroup import HostGroup
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    g = HostGroup.from_env(timeout=60)
+    ag = g.all_gather(bytes([rank]) * (rank + 1))
+    a2a = g.all_to_all([bytes([16 * rank + d]) * 3 for d in range(world)])
+    big = g.all_gather(bytes([rank]) * (3 << 20))
+    fn = g.exchange_fn()
+    nb = 5
+    send = (C.c_uint8 * (nb * world))(*[(16 * rank + d) & 255 for d in range(world) for _ in range(nb)])
+    recv = (C.c_uint8 * (nb * world))()
+    rc1 = fn(None, native.XCHG_ALL_TO_ALL, C.addressof(send), C.addressof(recv), nb)
+    xa2a = list(recv)
+    one = (C.c_uint8 * nb)(*[rank + 100] * nb)
+    rc2 = fn(None, native.XCHG_ALL_GATHER, C.addressof(one), C.addressof(recv), nb)
+    xag = list(recv)
+    bad = fn(None, 7, C.addressof(one), C.addressof(recv), nb)
+    uid = g.broadcast(b"id-from-rank-0" if rank == 0 else None)
+    out = {{"ag": [list(x) for x in ag], "a2a": [list(x) for x in a2a], "big_ok": all(
+        b == bytes([s]) * (3 << 20) for s, b in enumerate(big)), "x_a2a": xa2a, "x_ag": xag, "rc": [rc1, rc2],
+        "bad_rc": bad, "uid": uid.decode(), "max": g.max(float(rank) * 1.5), "torch": "torch" in sys.modules}}
+    g.close()
+print("RESULT " + json.dumps(out), flush=True)
+'''
 
 
 def free_port():
@@ -23,41 +68,59 @@ def free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
-                      LOCAL_RANK=str(rank))
-    sys.path.insert(0, str(ROOT))
-    import bench
-    w, r, local, pg = bench.setup_dist(world)
-    assert (w, r) == (world, rank) and pg is not None
-    calls = []
+def run_world(world, mode, tmp_path):
+    """world processes with torchrun's environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT, run id)."""
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=str(ROOT), pkg=str(ROOT / "encrypt-zkvm_amd")))
+    port, run_id = free_port(), f"t{os.getpid()}-{world}-{mode}"
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TORCHELASTIC_RUN_ID=run_id, ZK_NUMA_BIND="0")
+        procs.append(subprocess.Popen([sys.executable, str(script), mode], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=120)[0])
+    finally:
+        for p in procs:  # only the processes started here
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    res = []
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"rank {r}: {o}"
+        res.append(json.loads(next(ln for ln in o.splitlines() if ln.startswith("RESULT "))[7:]))
+    return res
 
-    def step():
-        calls.append(1)
-        time.sleep(0.03 * (rank + 1))
 
-    elapsed = bench.timed_loop(step, steps=4, warmup=2, pg=pg, local=local)
-    q.put((rank, elapsed, len(calls)))
-    pg.destroy_process_group()
+@pytest.mark.parametrize("world", [2, 4])
+def test_timed_loop_max_over_ranks(world, tmp_path):
+    res = sorted(run_world(world, "bench", tmp_path), key=lambda x: x["rank"])
+    times = [x["elapsed"] for x in res]
+    assert all(x["calls"] == 6 for x in res)                    # warmup 2 + steps 4 on every rank
+    assert max(times) - min(times) < 1e-9                        # every rank reports the same (max) time
+    assert times[0] >= 4 * 0.03 * world * 0.95                   # ... which is the slowest rank's
+    assert all(x["all_true"] is False for x in res)             # rank 1's False reaches every rank
+    assert not any(x["torch"] for x in res)                      # the bench process never imports torch
 
 
-@pytest.mark.parametrize("world", [2])
-def test_timed_loop_max_over_ranks_gloo(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    res.sort()
-    times = [t for _, t, _ in res]
-    assert all(c == 6 for _, _, c in res)            # warmup 2 + steps 4 on every rank
-    assert abs(times[0] - times[1]) < 1e-9           # every rank reports the same (max) time
-    assert times[0] >= 4 * 0.03 * world * 0.95       # ... which is the slowest rank's
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_group_collectives(world, tmp_path):
+    res = run_world(world, "group", tmp_path)
+    nb = 5
+    for r, x in enumerate(res):
+        assert x["ag"] == [[s] * (s + 1) for s in range(world)]
+        assert x["a2a"] == [[16 * s + r] * 3 for s in range(world)]
+        assert x["big_ok"]
+        assert x["rc"] == [0, 0] and x["bad_rc"] != 0
+        # the zk_exchange_fn layout: all-to-all chunk s of rank r's recv is chunk r of rank s's send
+        assert x["x_a2a"] == [16 * s + r for s in range(world) for _ in range(nb)]
+        assert x["x_ag"] == [100 + s for s in range(world) for _ in range(nb)]
+        assert x["uid"] == "id-from-rank-0"
+        assert x["max"] == 1.5 * (world - 1)
+        assert not x["torch"]
 
 
 def test_workload_seeds_differ_per_rank():
@@ -74,7 +137,7 @@ def test_numa_cpulist_parsing():
     import bench
     assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
     assert bench._cpulist("") == set()
-    # no GPU here: the binding is a no-op and leaves the affinity alone
+    # no GPU here: the binding finds no device and leaves the affinity alone
     before = os.sched_getaffinity(0)
     assert bench.bind_to_gpu_numa_node(0) is None
     assert os.sched_getaffinity(0) == before

@@ -27,6 +27,16 @@ def gpu():
     g.close()
 
 
+def test_runtime_is_the_one_the_library_links(gpu):
+    """This GPU test process runs the library on the HIP runtime and RCCL it links (/opt/rocm), one copy of each:
+    nothing in the suite imports torch, whose bundled ROCm 7.0 copies would otherwise serve it."""
+    rt = native.runtime_info()
+    print(rt)
+    assert isinstance(rt["hip_runtime"], str) and rt["hip_runtime"].startswith("/opt/rocm"), rt
+    assert isinstance(rt["rccl"], str) and rt["rccl"].startswith("/opt/rocm"), rt
+    assert not rt["torch_loaded_first"] and len(native.mapped_files("libamdhip64.so")) == 1
+
+
 def test_field_ops(gpu):
     rnd = random.Random(5)
     edge = [0, 1, 2, P - 1, P - 2, 2**64 - 1, 2**64, 2**127, P - 2**64, 45 * 2**40]

@@ -184,3 +184,70 @@ def test_vm_prove_preprocessed_columns_across_provers_and_inputs(gpu):
     finally:
         g2.close()
         prog.close()
+
+
+def test_vm_prove_first_call_fails_then_succeeds(gpu):
+    """The per-program preprocessed columns are built by the first zk_vm_prove call with that call's inputs: a first
+    call the VM refuses (too few public inputs) must leave nothing cached, so the next call with valid inputs builds
+    them afresh and proves exactly the host-trace proof."""
+    src = cipher_mix_program(200)[0]
+    w = make_workload(src, seed=21)
+    short = make_workload(src, seed=21, n_pub=0)
+    prog = Program(src)
+    try:
+        with pytest.raises(ZkError) as e:
+            prog.prove_device(gpu, Program.encode_inputs(short.public, short.secret, short.server_key), w.last_row)
+        assert "no more inputs to read" in str(e.value)
+        trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+        pub = make_pub_inputs(prog.hash, outs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+        ref, _, _, rc = gpu.prove(trace, pub, ProofOptions())
+        assert rc == 0
+        for _ in range(2):  # built by the first successful call, reused by the second
+            _, _, proof = prog.prove_device(gpu, Program.encode_inputs(w.public, w.secret, w.server_key), w.last_row)
+            assert proof == ref
+    finally:
+        prog.close()
+
+
+def test_vm_prove_concurrent_first_calls():
+    """Three provers on three host threads call zk_vm_prove at once on a freshly compiled program: one of them builds
+    the program's preprocessed columns under the program lock while the others wait for it (the recursive-lock
+    deadlock of round 4's first version would hang here); every proof equals the host-trace proof of its inputs."""
+    import threading
+    src = ops_for_trace_len(14, "cipher")
+    prog = Program(src)
+    provers = [GpuProver(0, max_trace_len=1 << 14) for _ in range(3)]
+    try:
+        ws = [make_workload(src, seed=60 + k) for k in range(3)]
+        refs = []
+        for k, w in enumerate(ws):
+            trace, outs = prog.trace(w.public, w.secret, w.server_key, w.last_row)
+            pub = make_pub_inputs(prog.hash, outs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+            ref, _, _, rc = provers[k].prove(trace, pub, ProofOptions())
+            assert rc == 0
+            refs.append(ref)
+        prog.close()
+        prog = Program(src)  # fresh: no device copy, no preprocessed columns yet
+        got, errs = [None] * 3, []
+        start = threading.Barrier(3)
+
+        def run(k):
+            try:
+                start.wait()
+                got[k] = prog.prove_device(provers[k], Program.encode_inputs(ws[k].public, ws[k].secret,
+                                                                               ws[k].server_key), ws[k].last_row)[2]
+            except BaseException as ex:  # re-raised below
+                errs.append(ex)
+
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=90)
+        assert not any(t.is_alive() for t in ths), "zk_vm_prove hung on the concurrent first call"
+        assert not errs, errs
+        assert got == refs
+    finally:
+        for g in provers:
+            g.close()
+        prog.close()

@@ -1,0 +1,66 @@
+"""The off path of every column-hint kill switch, against the oracle's full-size pin.
+
+The single-GPU host path learns column classes from one proof and uses them for the next (prover.hip):
+sparse columns skip their NTTs (ZK_SPARSE), narrow columns go up packed (ZK_NARROW), the AIR clock is derived instead
+of uploaded (ZK_CLOCK), hinted sparse columns get no LDE in memory (ZK_VIRTUAL); the sharded host path has the same
+hints (ZK_SHARD_HINTS).  The switches are read once per process, so each off path runs in a child process: the
+configs[2] trace (2^20, the c2_cipher_2p20 pin) proved three times from the host trace -- the first proof unhinted,
+the later ones with whatever the switch leaves on -- must give the pinned proof every time, and the upload record must
+show the switched-off class absent.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+pytestmark = pytest.mark.gpu
+
+CHILD = r'''
+import hashlib, json, sys
+sys.path[:0] = [{root!r}, {pkg!r}, {tests!r}]
+from golden_large import LARGE_CASES, large_inputs
+from zkvm_amd.prover import GpuProver
+c = next(c for c in LARGE_CASES if c["name"] == "c2_cipher_2p20")
+ht, trace, pub, opts = large_inputs(c)
+n = trace.shape[1]
+out = {{"want": c["proof_sha256"], "single": [], "uploads": []}}
+g = GpuProver(0, max_trace_len=n)
+for _ in range(3):
+    out["single"].append(hashlib.sha256(g.prove_host(trace, pub, opts)[0]).hexdigest())
+    out["uploads"].append(g.upload_stats())
+g.close()
+if {sharded!r}:
+    from zkvm_amd.sharded import ShardedProver
+    sp = ShardedProver.loopback(2, 0, n)
+    out["sharded"] = [hashlib.sha256(sp.prove(trace, pub, opts)[0]).hexdigest() for _ in range(3)]
+    sp.close()
+ht.close()
+print("RESULT " + json.dumps(out), flush=True)
+'''
+
+SWITCHES = ["ZK_SPARSE", "ZK_NARROW", "ZK_CLOCK", "ZK_VIRTUAL", "ZK_SHARD_HINTS"]
+
+
+@pytest.mark.parametrize("switch", SWITCHES)
+def test_kill_switch_off_path_matches_pin(switch, tmp_path):
+    script = tmp_path / "child.py"
+    script.write_text(CHILD.format(root=str(ROOT), pkg=str(ROOT / "encrypt-zkvm_amd"), tests=str(ROOT / "tests"),
+                                   sharded=switch == "ZK_SHARD_HINTS"))
+    env = dict(os.environ, **{switch: "0"})
+    r = subprocess.run([sys.executable, "-u", str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads(next(ln for ln in r.stdout.splitlines() if ln.startswith("RESULT "))[7:])
+    assert out["single"] == [out["want"]] * 3
+    hinted = out["uploads"][-1]  # the third proof: hints learned by the first two
+    if switch == "ZK_SPARSE":
+        assert hinted["sparse"] == []
+    elif switch == "ZK_NARROW":
+        assert hinted["narrow8"] == [] and hinted["narrow32"] == [] and hinted["sparse"]
+    elif switch == "ZK_CLOCK":
+        assert hinted["derived"] == [] and hinted["sparse"]
+    elif switch == "ZK_SHARD_HINTS":
+        assert out["sharded"] == [out["want"]] * 3

@@ -108,3 +108,48 @@ def test_reference_vm_program_output():
     last_row = [rand_field(np.random.default_rng(5), lo=1) for _ in range(28)]
     trace, output, h = vm_trace(src, [1, 3], [x], sk, last_row)
     assert trace.shape[0] == 28 and sk.decrypt(output[:5]) == 9
+
+
+def _in_fresh_process(code: str) -> dict:
+    import json
+    import subprocess
+    import sys
+    pre = f"import json, sys; sys.path[:0] = [{str(ROOT)!r}, {str(ROOT / 'encrypt-zkvm_amd')!r}]\n"
+    r = subprocess.run([sys.executable, "-c", pre + code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_one_hip_runtime_the_one_the_library_links():
+    """native.lib() in a torch-free process maps exactly one libamdhip64 -- /opt/rocm's, the RUNPATH the library was
+    linked with (what a Rust host would load) -- and refuses a later `import torch`, which would map torch's bundled
+    copy as a second runtime."""
+    out = _in_fresh_process(
+        "from zkvm_amd import native\n"
+        "native.lib()\n"
+        "info = native.runtime_info()\n"
+        "hips = native.mapped_files('libamdhip64.so')\n"
+        "try:\n"
+        "    import torch\n"
+        "    refused = False\n"
+        "except ImportError:\n"
+        "    refused = True\n"
+        "print(json.dumps({'info': info, 'hips': hips, 'after': native.mapped_files('libamdhip64.so'),"
+        " 'refused': refused}))\n")
+    assert len(out["hips"]) == 1 and out["hips"] == out["after"]
+    assert out["info"]["hip_runtime"] == out["hips"][0]
+    assert out["info"]["hip_runtime"].startswith("/opt/rocm") and "/torch/" not in out["info"]["hip_runtime"]
+    assert out["info"]["rccl"].startswith("/opt/rocm")
+    assert out["info"]["hip_runtime_version"] >= 70200000 and out["info"]["rccl_version"] > 0
+    assert out["refused"] and not out["info"]["torch_loaded_first"]
+
+
+def test_torch_first_gives_one_shared_runtime():
+    """A host that imports torch first: the library shares torch's runtime (still one mapping), and says so."""
+    out = _in_fresh_process(
+        "import torch\n"
+        "from zkvm_amd import native\n"
+        "native.lib()\n"
+        "print(json.dumps({'info': native.runtime_info(), 'hips': native.mapped_files('libamdhip64.so')}))\n")
+    assert len(out["hips"]) == 1 and out["info"]["hip_runtime"] == out["hips"][0]
+    assert out["info"]["torch_loaded_first"]

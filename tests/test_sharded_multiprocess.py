@@ -1,10 +1,11 @@
-"""The sharded prover with one rank per PROCESS (zk_comm_create_host + a gloo transport), as an RCCL job runs it.
+"""The sharded prover with one rank per PROCESS (zk_comm_create_host + a TCP host group), as an RCCL job runs it.
 
 The loopback tests (tests/test_sharded.py) drive every rank from one process; here `world` separate processes on
 the one test GPU each hold a single rank-sized prover, so every rank-dependent branch of shard.hip (coset ownership,
 the openings each rank serves, FRI layers >= 1 on rank 0, the per-process transcript) runs as in a multi-GPU job --
-only the transport differs (gloo over 127.0.0.1 instead of RCCL over xGMI).  The CPU tests check the exchange
-callback's chunk order at world 2 with gloo, and the communicator's argument checks.
+only the transport differs (zkvm_amd.hostgroup over 127.0.0.1 instead of RCCL over xGMI).  The CPU tests check the
+exchange callback's chunk order at world 2, and the communicator's argument checks.  No process imports torch: every
+rank runs on the HIP runtime the library links (checked in the rank records).
 """
 import ctypes as C
 import json
@@ -45,7 +46,7 @@ def run_ranks(world, out, mode="prove", timeout=240, env=None):
     return [json.loads((out / f"rank{r}.json").read_text()) for r in range(world)]
 
 
-def test_host_exchange_callback_gloo_world2(tmp_path):
+def test_host_exchange_callback_world2(tmp_path):
     res = run_ranks(2, tmp_path, "selftest", timeout=120)
     nb, world = 5, 2
     for r, x in enumerate(res):
@@ -70,6 +71,9 @@ def test_host_comm_argument_checks():
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_one_rank_per_process(tmp_path, world):
     res = run_ranks(world, tmp_path)
+    for x in res:
+        rt = x.pop("runtime")
+        assert isinstance(rt["hip_runtime"], str) and not rt["torch_loaded_first"], rt
     names = sorted(res[0])
     assert len(names) >= 3 and all(sorted(x) == names for x in res)
     for name in names:
@@ -80,7 +84,7 @@ def test_sharded_one_rank_per_process(tmp_path, world):
 
 
 # full-size pinned configs with every rank in its own process: configs[2] (2^20) over 8 ranks, configs[4] (2^20, quadratic
-# extension, 128 bits) over 4, configs[3] (2^22) over 8 -- the north_star's sharded proof, with gloo in place of RCCL;
+# extension, 128 bits) over 4, configs[3] (2^22) over 8 -- the north_star's sharded proof, with TCP host exchanges in place of RCCL;
 # each rank regenerates the trace with the product VM (2 threads: the box's CPU share is split between the processes)
 # and checks the proof against the oracle's pin and both verifiers
 FULL_SIZE_MP = [("c2_cipher_2p20", 8), ("c4_cipher_2p20_quad", 4), ("c3_cipher_2p22", 8)]

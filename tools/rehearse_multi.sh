@@ -1,6 +1,6 @@
 #!/bin/bash
 # Rehearse the driver's multi-GPU bench flow (torchrun, N ranks) on a one-GPU box: ZK_BENCH_REHEARSE=1 puts every
-# rank on the one GPU, the process group on gloo and the sharded leg on the host-exchange communicator.
+# rank on the one GPU and the sharded leg on the host-exchange communicator over the TCP host group (no torch).
 # Usage (GPU box): bash tools/rehearse_multi.sh N
 set -eo pipefail
 N=${1:-2}
