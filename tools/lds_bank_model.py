@@ -124,3 +124,36 @@ def check12(sw, LOGM=12):
 new12 = lambda x: x ^ ((x >> 4) & 15) ^ ((x >> 8) & 3) ^ (((x >> 10) & 3) << 2)
 print('LOGM 12 round-1 swizzle      :', check12(old))
 print('LOGM 12 current swizzle      :', check12(new12))
+
+
+# ---- round 5: the wave-local tile (kernels.hip Wl, ZK_NTT_WL) and the lane maps of its phases
+def wl_idx(line, pos):
+    f = (((pos >> 4) ^ (pos >> 6) ^ (pos >> 8)) & 3) << 2
+    return (line << 10) | (pos ^ line ^ f)
+
+
+def wl_phases():
+    out = {}
+    def run(name, lanes):  # lanes(w, l) -> list of (line, pos) the lane touches, one per access
+        m = 1
+        for w in range(16):
+            per = [lanes(w, l) for l in range(64)]
+            for k in range(len(per[0])):
+                m = max(m, worst([wl_idx(*per[l][k]) for l in range(64)]))
+        out[name] = m
+    # round 1 (first_round_from's lane order: line = q % 4, g = q / 4; positions 4g .. 4g+3)
+    run('r1 write (A)', lambda w, l: [(l & 3, 4 * ((w << 4) | (l >> 2)) + t) for t in range(4)])
+    # round 2 (A): j = quarter, line = l & 3, grp = (w << 2) | bits 4-5
+    run('r2 (A)', lambda w, l: [(l & 3, ((w << 2) | ((l >> 2) & 3)) * 16 + (l >> 4) + 4 * t) for t in range(4)])
+    # round 3 (B): j = w, line = l & 3, grp = l >> 2 (bits 6-9)
+    run('r3 (B)', lambda w, l: [(l & 3, (l >> 2) * 64 + w + 16 * t) for t in range(4)])
+    # round 4 (B): j = w | bits 4-5 from the quarter, grp = bits 8-9
+    run('r4 (B)', lambda w, l: [(l & 3, ((l >> 2) & 3) * 256 + (w | (((l >> 4) & 3) << 4)) + 64 * t) for t in range(4)])
+    # round 5, pass 2 (B): j = w | (l >> 2) << 4
+    run('r5 pass 2 (B)', lambda w, l: [(l & 3, (w | ((l >> 2) << 4)) + 256 * t) for t in range(4)])
+    # round 5, pass 1 (C): line = l >> 4, j = (w << 4) | (l & 15)
+    run('r5 pass 1 (C)', lambda w, l: [(l >> 4, ((w << 4) | (l & 15)) + 256 * t) for t in range(4)])
+    return out
+
+
+print('wave-local tile (Wl), round-5 kernels :', wl_phases())
