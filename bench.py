@@ -312,14 +312,22 @@ def all_ranks_true(pg, ok: bool, local: int) -> bool:
 
 
 def pmc_traffic(kernel: str, config5: bool = False):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary of the same configuration
-    (tools/pmc_traffic.py), if any."""
+    """HBM traffic of the kernel from the committed rocprofv3 --pmc passes of the same configuration
+    (tools/pmc_traffic.py, tools/gpu_profile.sh): per launch and per proof over the LAST (steady-state, hinted) proof
+    of a one-prover run, the ratio to that proof's algorithmic bytes, and whether the profile was taken on the
+    sources this bench runs (source hash, zkvm_amd.treehash)."""
     f = ROOT / "profiles" / ("pmc_traffic_config5.json" if config5 else "pmc_traffic.json")
     if not f.exists():
         return None
     try:
+        from zkvm_amd.treehash import source_hash
         d = json.loads(f.read_text())
-        return d.get("per_launch_bytes", {}).get(kernel)
+        return {"per_launch_bytes": d.get("per_launch_bytes", {}).get(kernel),
+                "per_proof_bytes": d.get("per_proof_bytes", {}).get(kernel),
+                "alg_per_proof_bytes": d.get("alg_per_proof_bytes", {}).get(kernel),
+                "traffic_ratio": d.get("traffic_ratio", {}).get(kernel), "scope": d.get("scope"),
+                "profile": f"profiles/{f.name}", "profile_tree": d.get("tree"),
+                "profile_tree_matches": d.get("tree") == source_hash()}
     except Exception:
         return None
 
@@ -341,14 +349,17 @@ def pmc_valu(kernel: str):
     if not f.exists():
         return None
     try:
-        k = json.loads(f.read_text())["kernels"].get(kernel)
+        from zkvm_amd.treehash import source_hash
+        d = json.loads(f.read_text())
+        k = d["kernels"].get(kernel)
     except Exception:
         return None
     if not k:
         return None
     return {"bound": "valu-issue", "slot_util": round(k["slot_util"], 3), "clock_ghz": round(k["clock_ghz"], 2),
             "valu_instr_per_launch": k["valu_instr"] / k["launches"], "peak": "1024 SIMDs x 1 wave64 VALU instr / 2 cycles",
-            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE, tools/pmc_valu.py)"}
+            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE, tools/pmc_valu.py)",
+            "profile_tree": d.get("tree"), "profile_tree_matches": d.get("tree") == source_hash()}
 
 
 def main():
@@ -718,8 +729,10 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
     avg_ms = tot_ms / launches
     achieved = tot_bytes / (tot_ms / 1e3) / 1e9
     prove_total_ms = sum(v[0] for v in kstats.values())
+    tr = pmc_traffic(name, args.config5)
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name, args.config5),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["per_launch_bytes"] if tr else None,
+                "traffic_ratio": tr["traffic_ratio"] if tr else None, "traffic_source": tr,
                 "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
                 "alg_bytes_per_launch": tot_bytes / launches,
                 "kernel_share_of_device_time": round(tot_ms / prove_total_ms, 3)}
@@ -755,6 +768,8 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
         "roofline": roofline, "cpu_baseline": cpu,
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "kernel_ms": {k: round(v[0], 3) for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+        "kernel_launches": {k: v[1] for k, v in kstats.items()},
+        "kernel_alg_bytes": {k: v[2] for k, v in kstats.items()},
         "vm": vm_rec,
         "proof_bytes": len(proof), "proof_verified_by_oracle": verified, "proof_verified_by_zk_verify": zk_verified,
         "proof_matches_pin": pin["proof_matches_pin"] if pin else None, "pin": pin["pin"] if pin else None,

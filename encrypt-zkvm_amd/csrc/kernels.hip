@@ -442,6 +442,7 @@ struct NttArgs {
     // the AIR clock (SparseCols::idoff): column 0 found to hold 0 .. n-2 transforms to sp_id + (last - (n-1)) * fill
     const fe *sp_id;
     int sp_idoff;
+    int sp_r0, sp_rshift;  // the fill tables' cosets: coset r at slot (r - sp_r0) >> sp_rshift (Plan::lde_slot)
     __device__ __forceinline__ bool sparse(uint32_t b) const {
         return nz && nz[sp_col0 + (int)(b / (uint32_t)ncos)] == 0;
     }
@@ -450,6 +451,7 @@ struct NttArgs {
     }
     // (32-bit: batch entries and grid sizes are < 2^32; 64-bit division is a long VALU sequence)
     __device__ __forceinline__ int coset_of(uint32_t b) const { return cos_r0 + (int)(b % (uint32_t)ncos) * cos_rstride; }
+    __device__ __forceinline__ size_t fill_slot(uint32_t b) const { return (size_t)((coset_of(b) - sp_r0) >> sp_rshift); }
     __device__ __forceinline__ fe *out_of(uint32_t b) const {
         return out + (size_t)(b / (uint32_t)ncos) * out_stride + (size_t)(b % (uint32_t)ncos) * out_jstride;
     }
@@ -625,7 +627,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
         // last * (the transform of e_(n-1)) over this block's outputs
         const int col = a.sp_col0 + (int)(b / (uint32_t)a.ncos);
         const fe last = a.sp_last[col];
-        const fe *fill = a.sp_fill + (size_t)a.coset_of((uint32_t)b) * a.sp_fill_stride;
+        const fe *fill = a.sp_fill + a.fill_slot((uint32_t)b) * a.sp_fill_stride;
         fe *out = a.out_of((uint32_t)b);
         for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
             const size_t o = n2 * (size_t)(e / LPB) + j2_0 + (size_t)(e % LPB);
@@ -636,7 +638,7 @@ __global__ void __launch_bounds__(NTT_THREADS, ZK_NTT_WAVES) ntt_pass2(NttArgs a
     if (a.clock((uint32_t)b)) {
         // the identity column's transform + (last - (n-1)) * (the transform of e_(n-1))
         const fe d = fe_sub(a.sp_last[0], fe_make(n - 1));
-        const size_t off = (size_t)a.coset_of((uint32_t)b) * a.sp_fill_stride;
+        const size_t off = a.fill_slot((uint32_t)b) * a.sp_fill_stride;
         const fe *fill = a.sp_fill + off, *id = a.sp_id + off;
         fe *out = a.out_of((uint32_t)b);
         for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
@@ -824,7 +826,7 @@ __global__ void __launch_bounds__(256) k_sparse_fill(NttArgs a, int ncols, int l
     if (t >= ((size_t)a.ncos << log_n)) return;
     const uint32_t j = (uint32_t)(t >> log_n);
     const size_t k = t & (n - 1);
-    const fe f = a.sp_fill[(size_t)a.coset_of(j) * a.sp_fill_stride + k];
+    const fe f = a.sp_fill[a.fill_slot(j) * a.sp_fill_stride + k];
     fe *o = a.out + (size_t)j * a.out_jstride + k;
     for (int c = 0; c < ncols; c++) o[(size_t)c * a.out_stride] = fe_mul(a.sp_last[a.sp_col0 + c], f);
 }
@@ -910,6 +912,8 @@ void ntt_lde(hipStream_t st, const NttTables &T, const CosetTables &CT, const fe
             a.sp_all = sp->all;
             a.sp_id = sp->id_lde;
             a.sp_idoff = sp->id_lde ? sp->idoff : 0;
+            a.sp_r0 = sp->lde_r0;
+            a.sp_rshift = sp->lde_shift;
         }
     }
     // up to 8 cosets per launch (tmp holds ncols * 8 * n): every column of 8 cosets in one grid, so

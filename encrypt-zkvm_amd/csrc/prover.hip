@@ -224,9 +224,14 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
     ZK_CHECK_HIP(make_pow_table(p, h_inv(fe_make(3)), n, &pl->inv3));
     ZK_CHECK_HIP(upload(p, &pl->periodic, periodic_table(n)));
     if (pl->log_n > 12) {
-        // e_(n-1)'s interpolant and coset LDE (the sparse trace columns': SparseCols)
+        // e_(n-1)'s interpolant and coset LDE (the sparse trace columns': SparseCols).  A rank-sized prover holds the
+        // LDE of its own cosets only (plan_rank_tables, once its rank is known)
         ZK_CHECK_HIP(p->arena.alloc(&pl->lagr, n));
-        ZK_CHECK_HIP(p->arena.alloc(&pl->lagr_lde, (size_t)B * n));
+        const bool full = p->shard_world <= 1;
+        if (full) {
+            ZK_CHECK_HIP(p->arena.alloc(&pl->lagr_lde, (size_t)B * n));
+            pl->lde_cos = (int)B;
+        }
         std::vector<fe> e(n, fe_zero());
         e[n - 1] = fe_one();
         fe *de = nullptr;
@@ -235,7 +240,7 @@ int zk::get_plan(zk_prover *p, size_t n, uint32_t B, Plan **out) {
         if (err == hipSuccess) {
             const fe inv_n = h_inv(fe_make(n));
             ntt(p->st, pl->Tn, de, n, pl->lagr, n, 1, true, nullptr, &inv_n, p->tmp);
-            ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, 0, 1, (int)B, pl->lagr_lde, (size_t)B * n, n, p->tmp);
+            if (full) ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, 0, 1, (int)B, pl->lagr_lde, (size_t)B * n, n, p->tmp);
             err = hipStreamSynchronize(p->st);
         }
         (void)hipFree(de);
@@ -1203,13 +1208,30 @@ bool zk::clock_on() {
     return on;
 }
 
-// the identity column 0, 1, ..., n-1 interpolated and extended over the B cosets (Plan::id_poly / id_lde), once per plan
+int zk::plan_rank_tables(zk_prover *p, Plan *pl, int r0, int G) {
+    if (p->shard_world <= 1 || !pl->lagr) return ZK_OK;  // a full prover's tables hold every coset
+    const int shift = ilog2((size_t)G);
+    if (pl->lagr_lde && pl->lde_r0 == r0 && pl->lde_shift == shift) return ZK_OK;
+    const size_t n = (size_t)1 << pl->log_n, Bl = ((size_t)1 << pl->log_b) >> shift;
+    if (!pl->lagr_lde) ZK_CHECK_HIP(p->arena.alloc(&pl->lagr_lde, Bl * n));
+    ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, r0, G, (int)Bl, pl->lagr_lde, Bl * n, n, p->tmp);
+    if (pl->id_lde) ntt_lde(p->st, pl->Tn, pl->ct, pl->id_poly, n, 1, r0, G, (int)Bl, pl->id_lde, Bl * n, n, p->tmp);
+    pl->lde_r0 = r0;
+    pl->lde_shift = shift;
+    pl->lde_cos = (int)Bl;
+    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    return ZK_OK;
+}
+
+// the identity column 0, 1, ..., n-1 interpolated and extended over the cosets the plan's fill tables hold
+// (Plan::id_poly / id_lde, lde_r0 / lde_shift / lde_cos: all B for a full prover), once per plan
 int zk::clock_tables(zk_prover *p, Plan *pl) {
     if (pl->id_poly) return ZK_OK;
-    const size_t n = (size_t)1 << pl->log_n, B = (size_t)1 << pl->log_b;
+    if (!pl->lde_cos) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the plan's rank tables are not built");
+    const size_t n = (size_t)1 << pl->log_n, nc = (size_t)pl->lde_cos;
     fe *poly = nullptr, *lde = nullptr;
     ZK_CHECK_HIP(p->arena.alloc(&poly, n));
-    ZK_CHECK_HIP(p->arena.alloc(&lde, B * n));
+    ZK_CHECK_HIP(p->arena.alloc(&lde, nc * n));
     std::vector<fe> id(n);
     for (size_t i = 0; i < n; i++) id[i] = fe_make(i);
     fe *d = nullptr;
@@ -1218,7 +1240,7 @@ int zk::clock_tables(zk_prover *p, Plan *pl) {
     if (err == hipSuccess) {
         const fe inv_n = h_inv(fe_make(n));
         ntt(p->st, pl->Tn, d, n, poly, n, 1, true, nullptr, &inv_n, p->tmp);
-        ntt_lde(p->st, pl->Tn, pl->ct, poly, n, 1, 0, 1, (int)B, lde, B * n, n, p->tmp);
+        ntt_lde(p->st, pl->Tn, pl->ct, poly, n, 1, pl->lde_r0, 1 << pl->lde_shift, (int)nc, lde, nc * n, n, p->tmp);
         err = hipStreamSynchronize(p->st);
     }
     (void)hipFree(d);
@@ -1267,7 +1289,7 @@ bool zk::zero_rows(const uint8_t *col, size_t r0, size_t r1) {
 
 int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols **sp) {
     *sp = nullptr;
-    if (!sparse_on() || !pl->lagr) return ZK_OK;
+    if (!sparse_on() || !pl->lagr || !pl->lagr_lde) return ZK_OK;
     if (!p->sp_nz) {
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_nz, 4 * W));  // nonzero, 8-bit, 32-bit flags; [3W]: column 0 not the clock
         ZK_CHECK_HIP(p->arena.alloc(&p->sp_last, W));
@@ -1275,6 +1297,8 @@ int zk::sparse_begin(zk_prover *p, Plan *pl, SparseCols *out, const SparseCols *
     }
     ZK_CHECK_HIP(hipMemsetAsync(p->sp_nz, 0, 4 * W * sizeof(unsigned), p->st));
     *out = SparseCols{p->sp_nz, p->sp_last, pl->lagr, pl->lagr_lde, 0};
+    out->lde_r0 = pl->lde_r0;
+    out->lde_shift = pl->lde_shift;
     if (clock_on()) {  // the AIR clock of column 0, detected with the sparse columns (device-side traces)
         ZK_TRY(clock_tables(p, pl));
         out->id_poly = pl->id_poly;
@@ -1518,6 +1542,15 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // (a first group of 1 or 2 columns, so the first kernels start after a shorter copy, measured slower: latency
     // 13.90-13.95 vs 13.73-13.79 ms, throughput unchanged; profiles/r04h_ab_first_group.txt)
     int left = nd;
+    static const int first = [] {  // (round-5 experiment: the first group's size)
+        const char *e = getenv("ZK_UPLOAD_FIRST");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 4 ? v : 0;
+    }();
+    if (first && left > first) {
+        gsz[ngroups++] = first;
+        left -= first;
+    }
     while (left > 0) {
         const int k = left > 4 ? 4 : left > 2 ? 2 : left;
         gsz[ngroups++] = left == 4 ? 2 : k;
@@ -1534,8 +1567,12 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     bool narrow_done = nn == 0, fb_done = false;
     NarrowCols G{};
     uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
+    static const bool narrow_first = [] {  // (round-5 experiment: the packed narrow columns go up first)
+        const char *e = getenv("ZK_NARROW_FIRST");
+        return e && !strcmp(e, "1");
+    }();
     auto next_item = [&](Item *it) -> bool {
-        if (!narrow_done && (packed.ready() || gi == ngroups)) {
+        if (!narrow_done && (packed.ready() || gi == ngroups || narrow_first)) {
             packed.wait();
             narrow_done = true;
             const uint32_t bad = pack_bad.load();

@@ -96,7 +96,14 @@ struct Plan {  // everything that depends only on (n, B)
     // ... and the column 0, 1, ..., n-1's (the AIR clock of a valid trace but for its random last row), built on first
     // use (clock_tables)
     fe *id_poly = nullptr, *id_lde = nullptr;
+    // the LDE cosets lagr_lde / id_lde hold: slot j is coset lde_r0 + (j << lde_shift), lde_cos of them -- all B for
+    // a full prover; a rank-sized prover's own B / G (plan_rank_tables), so its tables are sized like its LDE buffers
+    int lde_r0 = 0, lde_shift = 0, lde_cos = 0;
+    size_t lde_slot(int r) const { return (size_t)((r - lde_r0) >> lde_shift); }
 };
+// A rank-sized prover's lagr_lde / id_lde over the cosets of rank r0 of G (r0 + G j): built on the first sharded proof
+// of the plan, rebuilt if the prover serves another rank
+int plan_rank_tables(zk_prover *p, Plan *pl, int r0, int G);
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
 // the evaluator's divisor tables for the 8 CE cosets (divisor_tables: 3 planes of 8n), built once per plan
 const fe *boundary_inverses(zk_prover *p, Plan *pl);

@@ -638,7 +638,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                     axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
                     for (int j = 0; j < Bl; j++) {
                         const size_t r = (size_t)X.rank[l] + (size_t)G * j;
-                        axpy_fill(p->st, pl->id_lde + r * n, pl->lagr_lde + r * n, d, n, p->lde + (size_t)j * n);
+                        axpy_fill(p->st, pl->id_lde + pl->lde_slot((int)r) * n, pl->lagr_lde + pl->lde_slot((int)r) * n, d,
+                                  n, p->lde + (size_t)j * n);
                     }
                 }
             }
@@ -1343,6 +1344,7 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         ZK_CHECK_HIP(hipSetDevice(p->device));
         Plan *pl = nullptr;
         ZK_TRY(get_plan(p, n, 8, &pl));
+        ZK_TRY(plan_rank_tables(p, pl, X.rank[X.pl.size()], X.G));  // its fill tables over this rank's cosets
         X.pl.push_back(pl);
         if (opt->field_extension == 2) ZK_TRY(ensure_ext(p));
         if (!p->sh_buf) {

@@ -127,6 +127,8 @@ struct SparseCols {
     // interpolant and coset LDE, like lagr / lagr_lde) and skips its DFTs like a sparse one
     const fe *id_poly = nullptr, *id_lde = nullptr;
     int idoff = 0;
+    // the cosets lagr_lde / id_lde hold: coset r at slot (r - lde_r0) >> lde_shift (Plan::lde_slot)
+    int lde_r0 = 0, lde_shift = 0;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
 // Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte

@@ -126,7 +126,8 @@ print('LOGM 12 round-1 swizzle      :', check12(old))
 print('LOGM 12 current swizzle      :', check12(new12))
 
 
-# ---- round 5: the wave-local tile (kernels.hip Wl, ZK_NTT_WL) and the lane maps of its phases
+# ---- round 5 experiment (measured, removed: DESIGN.md §4 dead ends, profiles/r05b_ab_wave_local_ntt.txt): a tile
+# layout for wave-local NTT rounds (one block barrier per pass-2 tile instead of four) and the lane maps of its phases
 def wl_idx(line, pos):
     f = (((pos >> 4) ^ (pos >> 6) ^ (pos >> 8)) & 3) << 2
     return (line << 10) | (pos ^ line ^ f)
@@ -156,4 +157,4 @@ def wl_phases():
     return out
 
 
-print('wave-local tile (Wl), round-5 kernels :', wl_phases())
+print('wave-local tile (round-5 experiment)   :', wl_phases())

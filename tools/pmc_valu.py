@@ -64,7 +64,10 @@ def main():
     lines = ["| kernel | launches | time (ms) | clock (GHz) | VALU instr (G) | slot_util |",
              "|---|---|---|---|---|---|"]
     tot = collections.Counter()
-    js = {"source": os.path.abspath(path), "n_xcd": N_XCD, "simds": SIMDS, "kernels": {}}
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "encrypt-zkvm_amd"))
+    from zkvm_amd.treehash import source_hash
+    js = {"source": os.path.abspath(path), "n_xcd": N_XCD, "simds": SIMDS, "tree": source_hash(), "kernels": {}}
     for g, a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
         cyc = a["GRBM_GUI_ACTIVE"] / N_XCD
         issue = a["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc) if cyc else 0.0

@@ -7,7 +7,10 @@ is divided among the ranks (LDEs, evaluation, hashing, layer 0) and X the in-pro
 small).  From G = 2, 4, 8 this fits R and S (least squares); the per-rank time on G separate GPUs is then
 R + S / G + exchange(G), the exchange priced from the bytes rank 0 received in the loopback proof at an assumed xGMI
 rate ("projection").
+The same fit per proof stage (stage_split: the stage marks of the loopback proofs, each stage's time summed over the
+G ranks the process drives) says where R and S sit.
     python3 tools/shard_model.py [log_n] [steps]      (GPU box; prints one JSON object)
+    python3 tools/shard_model.py --from profiles/<run>.json   (the per-stage split of a committed run, no GPU)
 """
 import json
 import sys
@@ -19,12 +22,35 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "encrypt-zkvm_amd"))
 
-from zkvm_amd.prover import HostTrace, Program, ProofOptions, make_pub_inputs, vm_trace  # noqa: E402
-from zkvm_amd.sharded import ShardedProver  # noqa: E402
-from zkvm_amd.workloads import make_workload, ops_for_trace_len  # noqa: E402
+
+def stage_split(res):
+    """Per stage s: T_s(G) = G R_s + S_s over G = 2, 4, 8 (least squares) for each stage-time record of the run."""
+    Gs = np.array([2.0, 4.0, 8.0])
+    A = np.stack([Gs, np.ones(3)], axis=1)
+    out = {}
+    for key in ("stage_ms", "stage_ms_host", "stage_ms_vm"):
+        if key not in res:
+            continue
+        rec = {str(g): v for g, v in res[key].items()}
+        stages = sorted(set().union(*[set(rec[str(g)]) for g in (2, 4, 8)]), key=lambda k: -rec["2"].get(k, 0))
+        split = {}
+        for st in stages:
+            T = np.array([rec[str(g)].get(st, 0.0) for g in (2, 4, 8)])
+            (R, S), *_ = np.linalg.lstsq(A, T, rcond=None)
+            split[st] = {"R_ms": round(float(R), 3), "S_ms": round(float(S), 3), "per_rank_g8_ms": round(float(R + S / 8), 3)}
+        split["total"] = {k: round(sum(v[k] for v in split.values()), 3) for k in ("R_ms", "S_ms", "per_rank_g8_ms")}
+        out[key] = split
+    return out
 
 
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--from":
+        res = json.loads(Path(sys.argv[2]).read_text())
+        print(json.dumps({"source": sys.argv[2], "stage_split": stage_split(res)}, indent=1))
+        return
+    from zkvm_amd.prover import HostTrace, Program, ProofOptions, make_pub_inputs, vm_trace
+    from zkvm_amd.sharded import ShardedProver
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
     log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 22
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     src = ops_for_trace_len(log_n, "cipher")
@@ -53,6 +79,7 @@ def main():
         try:
             res["loopback_host_ms"][G] = timed(sp, lambda: sp.prove(host.array, pub, ProofOptions())[0])
             res.setdefault("received", {}).setdefault("host", {})[G] = sp.exchange_stats()
+            res.setdefault("stage_ms_host", {})[G] = {k: round(v, 3) for k, v in sp.stage_times().items()}
             sp.upload_trace(trace)
             res["loopback_ms"][G] = timed(sp, lambda: sp.prove(None, pub, ProofOptions(), n=n)[0])
             res["received"].setdefault("device", {})[G] = sp.exchange_stats()
@@ -94,6 +121,7 @@ def main():
         res["projection"][kind] = proj
     res["received"] = {k: {G: {c: [round(v[1] / 1e6, 2), v[2]] for c, v in d.items()} for G, d in m.items()}
                        for k, m in res["received"].items()}
+    res["stage_split"] = stage_split(res)
     print(json.dumps(res))
 
 
