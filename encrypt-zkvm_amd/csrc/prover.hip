@@ -1439,15 +1439,18 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     }
     NC.count = nn;
     std::atomic<uint32_t> pack_bad{0}, sparse_bad{0}, clock_bad{0};
-    Latch packed, checked, clocked;
+    // the narrow columns go up in two parts (the first half of them, the rest), each as soon as its packing is done
+    Latch packed[2], checked, clocked;
     struct PackWait {
-        Latch &a, &b, &c;
+        Latch &a, &a2, &b, &c;
         ~PackWait() {
             a.wait();
+            a2.wait();
             b.wait();
             c.wait();
         }
-    } pack_wait{packed, checked, clocked};
+    } pack_wait{packed[0], packed[1], checked, clocked};
+    const int nA = (nn + 1) / 2;  // narrow columns of part 0
     constexpr size_t R = (size_t)1 << 18;
     const size_t per = (n - 1 + R - 1) / R;
     if (nn) {
@@ -1458,7 +1461,8 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocDefault));
             p->h_pack_cap = pack_bytes;
         }
-        packed.reset((int)(per * nn));
+        packed[0].reset((int)(per * nA));
+        packed[1].reset((int)(per * (nn - nA)));
         for (int i = 0; i < nn; i++)
             for (size_t t = 0; t < per; t++) {
                 const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
@@ -1466,10 +1470,11 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
                 uint8_t *dst = p->h_pack + NC.off[i];
                 const int width = NC.width[i], c = nar[i];
                 const bool tail = r1 == n - 1;
-                HostPool::get().submit([=, &pack_bad, &packed] {
+                Latch *lt = &packed[i < nA ? 0 : 1];
+                HostPool::get().submit([=, &pack_bad] {
                     if (!pack_rows(col, r0, r1, width, dst)) pack_bad.fetch_or(1u << c);
                     if (tail) memset(dst + (size_t)width * (n - 1), 0, width);  // the last row's slot (not read)
-                    packed.count_down();
+                    lt->count_down();
                 });
             }
     }
@@ -1534,73 +1539,68 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     }
     // Upload items, each one copy (or a run of column copies) and an event on the shared upload stream: the wide
     // columns in groups of 4, the last 4 as 2 + 2 (after the last copy only 2 columns' NTTs, the last hash blocks and
-    // the Merkle tree remain); the packed narrow columns as soon as the host threads have packed them; narrow columns
-    // that did not fit, whole, last.  The next item's copy is queued before the host waits for the current one's event
+    // the Merkle tree remain); the packed narrow columns first, in two parts (below); narrow columns that did not fit,
+    // whole, last.  The next item's copy is queued before the host waits for the current one's event
     // (the compute stream never parks on the upload stream: a parked stream would hold up the kernels of other
     // provers that share its hardware queue), so the copy engine always has the next group.
     int gsz[W], ngroups = 0;
     // (a first group of 1 or 2 columns, so the first kernels start after a shorter copy, measured slower: latency
-    // 13.90-13.95 vs 13.73-13.79 ms, throughput unchanged; profiles/r04h_ab_first_group.txt)
+    // 13.90-13.95 vs 13.73-13.79 ms, throughput unchanged; profiles/r04h_ab_first_group.txt; round 5, 3 x 31 single
+    // calls: 14.75-14.78 / 14.67-14.70 vs 14.76-14.84 ms, profiles/r05d_latency_ab.txt)
     int left = nd;
-    static const int first = [] {  // (round-5 experiment: the first group's size)
-        const char *e = getenv("ZK_UPLOAD_FIRST");
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= 4 ? v : 0;
-    }();
-    if (first && left > first) {
-        gsz[ngroups++] = first;
-        left -= first;
-    }
     while (left > 0) {
         const int k = left > 4 ? 4 : left > 2 ? 2 : left;
         gsz[ngroups++] = left == 4 ? 2 : k;
         left -= gsz[ngroups - 1];
     }
-    if (ngroups + (nn ? 2 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
+    if (ngroups + (nn ? 3 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
     struct Item {
         const int *cols = nullptr;
         int nc = 0;
-        bool narrow = false;
+        int part = -1;  // narrow part 0 / 1 (packed), or -1 (whole columns)
         int ev = 0;
     };
-    int fallback[W], nfb = 0, good[W], ngood = 0, ev = 0, gi = 0, di = 0;
-    bool narrow_done = nn == 0, fb_done = false;
-    NarrowCols G{};
+    int fallback[W], nfb = 0, good[2][W], ngood[2] = {0, 0}, ev = 0, gi = 0, di = 0;
+    bool narrow_done[2] = {nA == 0, nn - nA == 0}, fb_done = false;
+    NarrowCols G[2] = {};
+    size_t part_off[3] = {0, nA < nn ? NC.off[nA] : pack_bytes, pack_bytes};  // byte range of each part in h_pack
     uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
-    static const bool narrow_first = [] {  // (round-5 experiment: the packed narrow columns go up first)
-        const char *e = getenv("ZK_NARROW_FIRST");
-        return e && !strcmp(e, "1");
-    }();
-    auto next_item = [&](Item *it) -> bool {
-        if (!narrow_done && (packed.ready() || gi == ngroups || narrow_first)) {
-            packed.wait();
-            narrow_done = true;
-            const uint32_t bad = pack_bad.load();
-            for (int i = 0; i < nn; i++) {
-                if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
-                    fallback[nfb++] = nar[i];
-                    continue;
-                }
-                G.col[G.count] = nar[i];
-                G.width[G.count] = NC.width[i];
-                G.off[G.count] = NC.off[i];
-                memcpy(&G.last[G.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
-                G.count++;
-                good[ngood++] = nar[i];
+    // Order: the first narrow part before anything else (packed by the host threads in ~0.3 ms, a few MB over PCIe:
+    // the first kernels start then instead of after a 64-MB dense group; one call alone -0.45 ms, 14.32-14.36 vs
+    // 14.76-14.84 ms over 3 x 31 calls, profiles/r05d_latency_ab.txt), the second as soon as it is packed, the
+    // dense groups in between.
+    auto narrow_item = [&](int k, Item *it) -> bool {
+        packed[k].wait();
+        narrow_done[k] = true;
+        const uint32_t bad = pack_bad.load();
+        for (int i = k ? nA : 0; i < (k ? nn : nA); i++) {
+            if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
+                fallback[nfb++] = nar[i];
+                continue;
             }
-            if (ngood) {
-                *it = Item{good, ngood, true, ev++};
-                return true;
-            }
+            NarrowCols &g = G[k];
+            g.col[g.count] = nar[i];
+            g.width[g.count] = NC.width[i];
+            g.off[g.count] = NC.off[i];
+            memcpy(&g.last[g.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
+            g.count++;
+            good[k][ngood[k]++] = nar[i];
         }
+        if (!ngood[k]) return false;
+        *it = Item{good[k], ngood[k], k, ev++};
+        return true;
+    };
+    auto next_item = [&](Item *it) -> bool {
+        if (!narrow_done[0] && narrow_item(0, it)) return true;
+        if (!narrow_done[1] && (packed[1].ready() || gi == ngroups) && narrow_item(1, it)) return true;
         if (gi < ngroups) {
-            *it = Item{dense + di, gsz[gi], false, ev++};
+            *it = Item{dense + di, gsz[gi], -1, ev++};
             di += gsz[gi++];
             return true;
         }
-        if (narrow_done && nfb && !fb_done) {
+        if (narrow_done[0] && narrow_done[1] && nfb && !fb_done) {
             fb_done = true;
-            *it = Item{fallback, nfb, false, ev++};
+            *it = Item{fallback, nfb, -1, ev++};
             return true;
         }
         return false;
@@ -1610,10 +1610,12 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         // a copy that fails part-way through the item still gets the item's event behind the copies queued before
         // it, so upload_drain (CopyGuard) waits for every DMA that reads the caller's columns
         UploadEvent rec{p->ev_up[it.ev], p->up};
-        if (it.narrow) {
-            ZK_CHECK_HIP(hipMemcpyAsync(stage, p->h_pack, pack_bytes, hipMemcpyHostToDevice, p->up));
-            p->up_bytes += pack_bytes;
-            for (int i = 0; i < G.count; i++) (G.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << G.col[i];
+        if (it.part >= 0) {
+            const size_t a = part_off[it.part], bytes = part_off[it.part + 1] - a;
+            ZK_CHECK_HIP(hipMemcpyAsync(stage + a, p->h_pack + a, bytes, hipMemcpyHostToDevice, p->up));
+            p->up_bytes += bytes;
+            const NarrowCols &g = G[it.part];
+            for (int i = 0; i < g.count; i++) (g.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << g.col[i];
         } else {
             ZK_TRY(runs(it.cols, it.nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
         }
@@ -1627,7 +1629,7 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         const bool more = next_item(&nxt);
         if (more) ZK_TRY(issue(nxt));
         ZK_CHECK_HIP(hipEventSynchronize(p->ev_up[cur.ev]));
-        if (cur.narrow) expand_narrow(p->st, stage, G, n, p->d_trace);
+        if (cur.part >= 0) expand_narrow(p->st, stage, G[cur.part], n, p->d_trace);
         ZK_TRY(process(cur.cols, cur.nc));
         cur = nxt;
         have = more;
