@@ -1,4 +1,4 @@
-"""Multi-rank bench harness on CPU (world_size 2 and 4, separate processes, no GPU, no torch).
+"""Multi-rank bench harness on CPU (2, 4 and 8 separate processes, no GPU, no torch in the ranks).
 
 bench.py at N > 1 runs one process per GPU (torchrun's environment); each rank proves its own independent trace (weak
 scaling, no data-path collective) and the timing is barrier-bracketed with the max taken over ranks.  The host side of
@@ -95,7 +95,7 @@ def run_world(world, mode, tmp_path):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_timed_loop_max_over_ranks(world, tmp_path):
     res = sorted(run_world(world, "bench", tmp_path), key=lambda x: x["rank"])
     times = [x["elapsed"] for x in res]
@@ -121,6 +121,22 @@ def test_host_group_collectives(world, tmp_path):
         assert x["uid"] == "id-from-rank-0"
         assert x["max"] == 1.5 * (world - 1)
         assert not x["torch"]
+
+
+def test_under_torchrun(tmp_path):
+    """The driver's launch form: torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1
+    --master-port P.  The launcher's agent holds MASTER_PORT (its TCPStore); the torch-free ranks meet through the
+    host group's rendezvous file instead and report the same max-over-ranks time."""
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=str(ROOT), pkg=str(ROOT / "encrypt-zkvm_amd")))
+    env = dict(os.environ, ZK_NUMA_BIND="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script), "bench"],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = [json.loads(ln.split("RESULT ", 1)[1]) for ln in r.stdout.splitlines() if "RESULT " in ln]
+    assert sorted(x["rank"] for x in res) == [0, 1]
+    assert res[0]["elapsed"] == res[1]["elapsed"] and not any(x["torch"] for x in res)
 
 
 def test_workload_seeds_differ_per_rank():
