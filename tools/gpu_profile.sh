@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box session (kernel traces and counters with one prover, so no launch overlaps another): parity tests, rocprofv3 kernel-trace stats of the bench, two PMC passes
 # (FETCH_SIZE / WRITE_SIZE, separately) -> pmc_traffic.json, then the default bench line.
-# Usage (from the repo root, via gpurun):  bash tools/gpu_profile.sh <tag> [tests|notests]
+# Usage (from the repo root, via gpurun):  bash tools/gpu_profile.sh <tag> [tests|notests] [bench|nobench]
+# (nobench: the profiles and counters only; the bench lines in a session of their own)
 set -eo pipefail
 TAG=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -44,8 +45,11 @@ python3 "$R/tools/pmc_stall.py" "$O/pmc_stall_$TAG" -o "$O/pmc_stall_$TAG.md"
 echo "pmc stall ok"
 # keep only the summaries (the per-dispatch counter CSVs are large)
 find "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
-(cd "$R" && timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err")
-echo "bench ok"
+BENCH=${3:-bench}
+if [ "$BENCH" = bench ]; then
+  (cd "$R" && timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err")
+  echo "bench ok"
+fi
 # config 5 (128-bit options, quadratic extension): kernel trace + bench line
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c5_$TAG" -o "c5_$TAG" -- \
   python3 "$R/bench.py" --config5 $BENCH_ARGS > "$O/prof_bench_c5_$TAG.json" 2> "$O/prof_bench_c5_$TAG.err"
@@ -59,6 +63,8 @@ python3 "$R/tools/pmc_traffic.py" "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" 
 cp "$O/pmc_traffic_c5_$TAG.json" "$R/profiles/pmc_traffic_config5.json"
 find "$O/pmc_fetch_c5_$TAG" "$O/pmc_write_c5_$TAG" -name '*counter_collection.csv' -size +20M -delete || true
 echo "config5 pmc ok"
-(cd "$R" && timeout -k 10 600 python3 bench.py --config5 > "$O/bench_c5_$TAG.json" 2> "$O/bench_c5_$TAG.err")
-echo "config5 bench ok"
-cat "$O/bench_$TAG.json"
+if [ "$BENCH" = bench ]; then
+  (cd "$R" && timeout -k 10 600 python3 bench.py --config5 --no-cpu-baseline > "$O/bench_c5_$TAG.json" 2> "$O/bench_c5_$TAG.err")
+  echo "config5 bench ok"
+  cat "$O/bench_$TAG.json"
+fi
