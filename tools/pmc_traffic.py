@@ -26,7 +26,8 @@ from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "encrypt-zkvm_amd"))
 
-ALIASES = {"k_merge_level": "merkle_level", "k_merge_top": "merkle_top", "k_batch_inv_pairs": "batch_inv"}
+ALIASES = {"k_merge_level": "merkle_level", "k_merge_top": "merkle_top", "k_batch_inv_pairs": "batch_inv",
+           "k_hash_rows_blocks": "hash_rows"}  # (the library profiler counts both row-hashing kernels as hash_rows)
 
 
 def short_name(kernel: str) -> str:
