@@ -139,6 +139,38 @@ def test_under_torchrun(tmp_path):
     assert res[0]["elapsed"] == res[1]["elapsed"] and not any(x["torch"] for x in res)
 
 
+def test_host_group_peer_death_is_an_error_not_a_hang(tmp_path):
+    """A rank that dies mid-run (a crashed or killed GPU process) makes the others' next collective raise
+    ConnectionError promptly instead of waiting forever (the bench's watchdog is the second line)."""
+    code = r'''
+import os, sys, time, json
+sys.path[:0] = [{pkg!r}]
+from zkvm_amd.hostgroup import HostGroup
+rank = int(os.environ["RANK"])
+g = HostGroup.from_env(timeout=60)
+g.barrier()
+if rank == 1:
+    os._exit(0)
+t0 = time.monotonic()
+try:
+    g.all_gather(b"x" * 1024)
+    print("RESULT " + json.dumps({{"raised": False}}))
+except ConnectionError as e:
+    print("RESULT " + json.dumps({{"raised": True, "s": time.monotonic() - t0}}))
+'''.format(pkg=str(ROOT / "encrypt-zkvm_amd"))
+    script = tmp_path / "die.py"
+    script.write_text(code)
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(os.environ, RANK=str(r), WORLD_SIZE="2",
+                                                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                                                                       TORCHELASTIC_RUN_ID=f"die{os.getpid()}"),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    out = procs[0].communicate(timeout=60)[0]
+    procs[1].communicate(timeout=60)
+    res = json.loads(next(ln for ln in out.splitlines() if ln.startswith("RESULT "))[7:])
+    assert res["raised"] and res["s"] < 10, out
+
+
 def test_workload_seeds_differ_per_rank():
     """Each rank proves an independent trace: bench seeds the generator with 1000 + rank."""
     sys.path.insert(0, str(ROOT / "encrypt-zkvm_amd"))
