@@ -283,10 +283,11 @@ int zk_device_count(int *count) {
 
 // One upload stream per device for the process (created on first use, kept for the process's lifetime), shared by
 // every prover on that device, with the mutex that keeps one prover's copy and its event record adjacent.
-static int shared_upload_stream(int device, hipStream_t *st, std::mutex **mu) {
+static int shared_upload_stream(int device, hipStream_t *st, std::mutex **mu, std::atomic<int> **busy) {
     struct Up {
         hipStream_t st = nullptr;
         std::mutex mu;
+        std::atomic<int> busy{0};
     };
     static std::mutex reg_mu;
     static std::map<int, Up *> reg;  // process lifetime: never freed
@@ -299,6 +300,7 @@ static int shared_upload_stream(int device, hipStream_t *st, std::mutex **mu) {
     }
     *st = u->st;
     *mu = &u->mu;
+    *busy = &u->busy;
     return ZK_OK;
 }
 
@@ -337,7 +339,7 @@ static int create_prover(int device, size_t max_n, uint32_t max_b, int world, zk
     p->max_n = max_n;
     p->max_b = max_b;
     ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
-    ZK_TRY(shared_upload_stream(device, &p->up, &p->up_mu));
+    ZK_TRY(shared_upload_stream(device, &p->up, &p->up_mu, &p->dev_busy));
     for (auto &e : p->ev_up) ZK_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ZK_CHECK_HIP(upload_rescue_consts(p->st));
     const size_t n = max_n, N = max_n * max_b, CE = 8 * max_n;
@@ -1199,6 +1201,16 @@ bool zk::narrow_on() {
     return on;
 }
 
+// The upload schedule of a host-resident trace (trace_lde_commit): 0 the throughput schedule always, 1 (default) the
+// latency schedule for a proof that starts with no other proof in flight on its device, 2 the latency one always
+static int latency_sched() {
+    static const int v = [] {
+        const char *e = getenv("ZK_LATENCY_SCHED");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 // The AIR clock (ZK_CLOCK=0 turns its derivation off)
 bool zk::clock_on() {
     static const bool on = [] {
@@ -1439,20 +1451,41 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     }
     NC.count = nn;
     std::atomic<uint32_t> pack_bad{0}, sparse_bad{0}, clock_bad{0};
-    // the narrow columns go up in two parts (the first half of them, the rest), each as soon as its packing is done
-    Latch packed[2], checked, clocked;
+    // Two upload schedules (set per proof by prove_once, see zk_prover::lat_sched):
+    //  - throughput (other proofs in flight on the device): the narrow columns go up in two parts (the first half of
+    //    them, the rest) through the copy engine, each as soon as its packing is done, in quarter-million-row tasks;
+    //  - latency (this proof alone on the device): dense groups 0 and 1 start crossing the link at once; the narrow
+    //    columns are packed in parts of 1, 2, 2, ... columns (16 K-row tasks, so each part is ready in ~0.1-0.2 ms)
+    //    and each part's expansion kernel reads the pinned packed bytes itself (no copy engine: that is busy with the
+    //    dense groups), so the first kernels start ~0.3 ms into the call and the device has the narrow columns' work
+    //    while the first dense groups cross.
+    const bool lat = p->lat_sched && nn > 0;
+    int pb[W + 1], np = 0;  // part k: narrow columns pb[k] .. pb[k+1]-1
+    pb[0] = 0;
+    if (lat) {
+        for (int i = 0; i < nn;) {
+            i = std::min(nn, i + (np == 0 ? 1 : 2));
+            pb[++np] = i;
+        }
+    } else if (nn) {
+        pb[1] = (nn + 1) / 2;
+        pb[2] = nn;
+        np = pb[1] < nn ? 2 : 1;
+    }
+    Latch packed[W], checked, clocked;
     struct PackWait {
-        Latch &a, &a2, &b, &c;
+        Latch *parts;
+        const int &np;
+        Latch &b, &c;
         ~PackWait() {
-            a.wait();
-            a2.wait();
+            for (int k = 0; k < np; k++) parts[k].wait();
             b.wait();
             c.wait();
         }
-    } pack_wait{packed[0], packed[1], checked, clocked};
-    const int nA = (nn + 1) / 2;  // narrow columns of part 0
+    } pack_wait{packed, np, checked, clocked};
     constexpr size_t R = (size_t)1 << 18;
     const size_t per = (n - 1 + R - 1) / R;
+    const size_t Rp = lat ? (size_t)1 << 16 : R, perp = (n - 1 + Rp - 1) / Rp;  // packing task rows
     if (nn) {
         if (pack_bytes > p->h_pack_cap) {  // the previous proof's copies from it have drained (CopyGuard)
             if (p->h_pack) (void)hipHostFree(p->h_pack);
@@ -1461,22 +1494,23 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocDefault));
             p->h_pack_cap = pack_bytes;
         }
-        packed[0].reset((int)(per * nA));
-        packed[1].reset((int)(per * (nn - nA)));
-        for (int i = 0; i < nn; i++)
-            for (size_t t = 0; t < per; t++) {
-                const size_t r0 = t * R, r1 = std::min(n - 1, r0 + R);
+        for (int k = 0; k < np; k++) packed[k].reset((int)(perp * (pb[k + 1] - pb[k])));
+        for (int i = 0, k = 0; i < nn; i++) {
+            if (i == pb[k + 1]) k++;  // part k holds narrow column i
+            for (size_t t = 0; t < perp; t++) {
+                const size_t r0 = t * Rp, r1 = std::min(n - 1, r0 + Rp);
                 const uint8_t *col = src.cols[nar[i]];
                 uint8_t *dst = p->h_pack + NC.off[i];
                 const int width = NC.width[i], c = nar[i];
                 const bool tail = r1 == n - 1;
-                Latch *lt = &packed[i < nA ? 0 : 1];
+                Latch *lt = &packed[k];
                 HostPool::get().submit([=, &pack_bad] {
                     if (!pack_rows(col, r0, r1, width, dst)) pack_bad.fetch_or(1u << c);
                     if (tail) memset(dst + (size_t)width * (n - 1), 0, width);  // the last row's slot (not read)
                     lt->count_down();
                 });
             }
+        }
     }
     if (nh) {
         checked.reset((int)(per * nh));
@@ -1553,46 +1587,104 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         gsz[ngroups++] = left == 4 ? 2 : k;
         left -= gsz[ngroups - 1];
     }
-    if (ngroups + (nn ? 3 : 0) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
+    if (ngroups + (lat ? 1 : np + 1) > ZK_UPLOAD_GROUPS_MAX) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many upload groups");
     struct Item {
         const int *cols = nullptr;
         int nc = 0;
-        int part = -1;  // narrow part 0 / 1 (packed), or -1 (whole columns)
+        int part = -1;  // narrow part (packed), or -1 (whole columns)
         int ev = 0;
     };
-    int fallback[W], nfb = 0, good[2][W], ngood[2] = {0, 0}, ev = 0, gi = 0, di = 0;
-    bool narrow_done[2] = {nA == 0, nn - nA == 0}, fb_done = false;
-    NarrowCols G[2] = {};
-    size_t part_off[3] = {0, nA < nn ? NC.off[nA] : pack_bytes, pack_bytes};  // byte range of each part in h_pack
+    int fallback[W], nfb = 0, good[W], ev = 0, gi = 0, di = 0;
+    bool narrow_done[2] = {np < 1, np < 2}, fb_done = false;
+    NarrowCols G[W] = {};
+    size_t part_off[W + 1];  // byte range of each part in h_pack
+    for (int k = 0; k <= np; k++) part_off[k] = pb[k] < nn ? NC.off[pb[k]] : pack_bytes;
     uint8_t *stage = reinterpret_cast<uint8_t *>(p->ctmp);  // composition scratch: free until S4
-    // Order: the first narrow part before anything else (packed by the host threads in ~0.3 ms, a few MB over PCIe:
-    // the first kernels start then instead of after a 64-MB dense group; one call alone -0.45 ms, 14.32-14.36 vs
-    // 14.76-14.84 ms over 3 x 31 calls, profiles/r05d_latency_ab.txt), the second as soon as it is packed, the
-    // dense groups in between.
+    // part k's columns once packed (the host waits for its packing), its unpackable ones to the fallback list
     auto narrow_item = [&](int k, Item *it) -> bool {
         packed[k].wait();
-        narrow_done[k] = true;
+        if (k < 2) narrow_done[k] = true;
         const uint32_t bad = pack_bad.load();
-        for (int i = k ? nA : 0; i < (k ? nn : nA); i++) {
+        NarrowCols &g = G[k];
+        int *gd = good + pb[k], ng = 0;
+        for (int i = pb[k]; i < pb[k + 1]; i++) {
             if ((bad >> nar[i]) & 1u) {  // a value that does not fit: this column goes up whole
                 fallback[nfb++] = nar[i];
                 continue;
             }
-            NarrowCols &g = G[k];
             g.col[g.count] = nar[i];
             g.width[g.count] = NC.width[i];
             g.off[g.count] = NC.off[i];
             memcpy(&g.last[g.count], src.cols[nar[i]] + (n - 1) * sizeof(fe), sizeof(fe));
             g.count++;
-            good[k][ngood[k]++] = nar[i];
+            gd[ng++] = nar[i];
         }
-        if (!ngood[k]) return false;
-        *it = Item{good[k], ngood[k], k, ev++};
+        if (!ng) return false;
+        *it = Item{gd, ng, k, -1};
         return true;
     };
+    auto count_part = [&](int k) {  // part k's packed bytes cross the link
+        p->up_bytes += part_off[k + 1] - part_off[k];
+        const NarrowCols &g = G[k];
+        for (int i = 0; i < g.count; i++) (g.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << g.col[i];
+    };
+    auto issue = [&](const Item &it) -> int {
+        std::lock_guard<std::mutex> lk(*p->up_mu);
+        // a copy that fails part-way through the item still gets the item's event behind the copies queued before
+        // it, so upload_drain (CopyGuard) waits for every DMA that reads the caller's columns
+        UploadEvent rec{p->ev_up[it.ev], p->up};
+        if (it.part >= 0) {
+            const size_t a = part_off[it.part];
+            ZK_CHECK_HIP(hipMemcpyAsync(stage + a, p->h_pack + a, part_off[it.part + 1] - a, hipMemcpyHostToDevice,
+                                        p->up));
+            count_part(it.part);
+        } else {
+            ZK_TRY(runs(it.cols, it.nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
+        }
+        return rec.record();
+    };
+    if (lat) {
+        // the latency schedule: dense groups 0 and 1 go up at once, group g + 2 once group g has landed; the narrow
+        // parts in order as they are packed, each expanded straight from the pinned buffer; then the dense groups
+        int gev[W];
+        auto issue_dense = [&]() -> int {
+            if (gi >= ngroups) return ZK_OK;
+            gev[gi] = ev++;
+            const Item d{dense + di, gsz[gi], -1, gev[gi]};
+            di += gsz[gi++];
+            return issue(d);
+        };
+        ZK_TRY(issue_dense());
+        ZK_TRY(issue_dense());
+        uint8_t *hp = nullptr;
+        ZK_CHECK_HIP(hipHostGetDevicePointer((void **)&hp, p->h_pack, 0));
+        for (int k = 0; k < np; k++) {
+            Item it;
+            if (!narrow_item(k, &it)) continue;
+            count_part(k);
+            expand_narrow(p->st, hp, G[k], n, p->d_trace);
+            ZK_TRY(process(it.cols, it.nc));
+        }
+        for (int g = 0, d0 = 0; g < ngroups; d0 += gsz[g++]) {
+            ZK_CHECK_HIP(hipEventSynchronize(p->ev_up[gev[g]]));
+            ZK_TRY(issue_dense());
+            ZK_TRY(process(dense + d0, gsz[g]));
+        }
+        narrow_done[0] = narrow_done[1] = true;  // (the fallback columns, if any, go through the loop below)
+    }
+    // The throughput schedule: the first narrow part before anything else (packed by the host threads in ~0.3 ms, a
+    // few MB over PCIe: the first kernels start then instead of after a 64-MB dense group; one call alone -0.45 ms,
+    // 14.32-14.36 vs 14.76-14.84 ms over 3 x 31 calls, profiles/r05d_latency_ab.txt), the second as soon as it is
+    // packed, the dense groups in between.
     auto next_item = [&](Item *it) -> bool {
-        if (!narrow_done[0] && narrow_item(0, it)) return true;
-        if (!narrow_done[1] && (packed[1].ready() || gi == ngroups) && narrow_item(1, it)) return true;
+        if (!narrow_done[0] && narrow_item(0, it)) {
+            it->ev = ev++;
+            return true;
+        }
+        if (!narrow_done[1] && (packed[1].ready() || gi == ngroups) && narrow_item(1, it)) {
+            it->ev = ev++;
+            return true;
+        }
         if (gi < ngroups) {
             *it = Item{dense + di, gsz[gi], -1, ev++};
             di += gsz[gi++];
@@ -1604,22 +1696,6 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             return true;
         }
         return false;
-    };
-    auto issue = [&](const Item &it) -> int {
-        std::lock_guard<std::mutex> lk(*p->up_mu);
-        // a copy that fails part-way through the item still gets the item's event behind the copies queued before
-        // it, so upload_drain (CopyGuard) waits for every DMA that reads the caller's columns
-        UploadEvent rec{p->ev_up[it.ev], p->up};
-        if (it.part >= 0) {
-            const size_t a = part_off[it.part], bytes = part_off[it.part + 1] - a;
-            ZK_CHECK_HIP(hipMemcpyAsync(stage + a, p->h_pack + a, bytes, hipMemcpyHostToDevice, p->up));
-            p->up_bytes += bytes;
-            const NarrowCols &g = G[it.part];
-            for (int i = 0; i < g.count; i++) (g.width[i] == 1 ? p->up_nw8 : p->up_nw32) |= 1u << g.col[i];
-        } else {
-            ZK_TRY(runs(it.cols, it.nc, [&](int c0, int k) { return upload_trace_group(p, src, n, c0, k); }));
-        }
-        return rec.record();
     };
     Item cur;
     bool have = next_item(&cur);
@@ -1800,6 +1876,14 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
             (void)hipStreamSynchronize(p->st);
         }
     } copy_guard{p};
+    // proofs in flight on the device: alone, the trace goes up on the latency schedule (trace_lde_commit)
+    struct Busy {
+        std::atomic<int> *b;
+        int others;
+        explicit Busy(std::atomic<int> *x) : b(x), others(x->fetch_add(1)) {}
+        ~Busy() { b->fetch_sub(1); }
+    } busy{p->dev_busy};
+    p->lat_sched = latency_sched() == 2 || (latency_sched() == 1 && busy.others == 0);
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));

@@ -3,7 +3,8 @@
 The single-GPU host path learns column classes from one proof and uses them for the next (prover.hip):
 sparse columns skip their NTTs (ZK_SPARSE), narrow columns go up packed (ZK_NARROW), the AIR clock is derived instead
 of uploaded (ZK_CLOCK), hinted sparse columns get no LDE in memory (ZK_VIRTUAL); the sharded host path has the same
-hints (ZK_SHARD_HINTS).  The switches are read once per process, so each off path runs in a child process: the
+hints (ZK_SHARD_HINTS).  ZK_LATENCY_SCHED=0 keeps a proof that runs alone on the throughput upload schedule (the
+narrow columns in two parts through the copy engine) instead of the latency one.  The switches are read once per process, so each off path runs in a child process: the
 configs[2] trace (2^20, the c2_cipher_2p20 pin) proved three times from the host trace -- the first proof unhinted,
 the later ones with whatever the switch leaves on -- must give the pinned proof every time, and the upload record must
 show the switched-off class absent.
@@ -42,7 +43,7 @@ ht.close()
 print("RESULT " + json.dumps(out), flush=True)
 '''
 
-SWITCHES = ["ZK_SPARSE", "ZK_NARROW", "ZK_CLOCK", "ZK_VIRTUAL", "ZK_SHARD_HINTS"]
+SWITCHES = ["ZK_SPARSE", "ZK_NARROW", "ZK_CLOCK", "ZK_VIRTUAL", "ZK_SHARD_HINTS", "ZK_LATENCY_SCHED"]
 
 
 @pytest.mark.parametrize("switch", SWITCHES)
@@ -62,5 +63,7 @@ def test_kill_switch_off_path_matches_pin(switch, tmp_path):
         assert hinted["narrow8"] == [] and hinted["narrow32"] == [] and hinted["sparse"]
     elif switch == "ZK_CLOCK":
         assert hinted["derived"] == [] and hinted["sparse"]
+    elif switch == "ZK_LATENCY_SCHED":
+        assert hinted["narrow8"] and hinted["sparse"] and hinted["derived"]
     elif switch == "ZK_SHARD_HINTS":
         assert out["sharded"] == [out["want"]] * 3
