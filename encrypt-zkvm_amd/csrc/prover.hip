@@ -414,6 +414,7 @@ void zk_prover_destroy(zk_prover *p) {
     for (auto &e : p->xchg_pool) (void)hipEventDestroy(e);
     for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
+    if (p->ev_vm) (void)hipEventDestroy(p->ev_vm);
     (void)hipStreamDestroy(p->st);
     if (p->h_io) (void)hipHostFree(p->h_io);
     if (p->h_gather_idx) (void)hipHostFree(p->h_gather_idx);
@@ -1337,12 +1338,18 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             ntt_lde(p->st, pl->Tn, pl->ct, p->polys + c0 * n, n, fx.md, 0, 1, (int)B, p->lde + c0 * B * n, B * n, n,
                     p->tmp);
         }
-        if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
-        fe_ws ws[W];
-        for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
-        ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
-        fixed_axpy(p->st, fx, p->fix_ws, n, B, p->polys, p->lde);
-        hash_rows_cosets(p->st, p->lde, W, pl->log_n, pl->log_b, 0, pl->log_b, p->leaves);
+        const int pre = p->fix_prefix_blocks;  // (zk_vm_prove: the preprocessed part went first, fixed_prefix)
+        p->fix_prefix_blocks = 0;
+        if (pre) {
+            hash_rows_blocks(p->st, p->lde, W, pl->log_n, pl->log_b, pre, W / 4, p->leaves);
+        } else {
+            if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
+            fe_ws ws[W];
+            for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
+            ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
+            fixed_axpy(p->st, fx, p->fix_ws, n, B, p->polys, p->lde);
+            hash_rows_cosets(p->st, p->lde, W, pl->log_n, pl->log_b, 0, pl->log_b, p->leaves);
+        }
         merkle_tree(p->st, p->leaves, n * B, p->nodes);
         return d2h_small(p, root, p->nodes + 32, 32);
     }
@@ -2190,6 +2197,21 @@ int zk_prove_device(zk_prover *p, const void *d_trace, size_t n, const zk_option
     TraceSrc src;
     src.dev = (const fe *)d_trace;
     return prove_impl(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
+}
+
+int zk::fixed_prefix(zk_prover *p, size_t n, uint32_t B, const FixedCols &fx) {
+    p->fix_prefix_blocks = 0;
+    Plan *pl = nullptr;
+    ZK_TRY(get_plan(p, n, B, &pl));
+    if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
+    fe_ws ws[W];
+    for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
+    ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
+    fixed_axpy(p->st, fx, p->fix_ws, n, (size_t)1 << pl->log_b, p->polys, p->lde);
+    constexpr int nb = 12 / 4;  // columns 0 .. 11 are preprocessed whatever the program's stack depth
+    hash_rows_blocks(p->st, p->lde, W, pl->log_n, pl->log_b, 0, nb, p->leaves);
+    p->fix_prefix_blocks = nb;
+    return ZK_OK;
 }
 
 int zk::prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inputs *pub, const FixedCols *fx,

@@ -171,6 +171,12 @@ struct zk_prover {
     // on demand
     uint8_t *h_vm = nullptr;
     size_t h_vm_cap = 0;
+    hipEvent_t ev_vm = nullptr;  // recorded behind the last upload from h_vm (it is rewritten only once that is done)
+    bool ev_vm_live = false;
+    // zk_vm_prove: the preprocessed columns' polys / LDE and their BLAKE3 blocks 0 .. fix_prefix_blocks - 1 were
+    // enqueued before the host stack pass (fixed_prefix); the next prove_fixed skips them.  Cleared by zk_vm_prove on
+    // every way out.
+    int fix_prefix_blocks = 0;
     zk::Openings *open = nullptr;      // per-proof openings, storage kept across proofs
     std::vector<uint8_t> proof_bytes;  // the serialized proof, storage kept across proofs
     unsigned *flag = nullptr;
@@ -302,6 +308,9 @@ int prove_fixed(zk_prover *p, size_t n, const zk_options *opt, const zk_pub_inpu
 // polys / lde of the preprocessed columns (all but 12 .. 12 + md - 1): f_c + last[c] e_(n-1) (vm_gpu.hip); B: the LDE
 // cosets held (fx's flde / lagr_lde and lde alike)
 void fixed_axpy(hipStream_t st, const FixedCols &fx, const fe_ws *ws_dev, size_t n, size_t B, fe *polys, fe *lde);
+// zk_vm_prove, before its host stack pass: fixed_axpy of fx into p->polys / p->lde and the BLAKE3 blocks of the rows'
+// first columns that hold no live stack register (0 .. 2: columns 0 .. 11), on p->st; sets p->fix_prefix_blocks
+int fixed_prefix(zk_prover *p, size_t n, uint32_t B, const FixedCols &fx);
 // Host-trace column classes shared by the single-GPU and the sharded prover (prover.hip): ZK_SPARSE / ZK_CLOCK
 // switches, the identity column's tables of a plan (the AIR clock: built once), and the host checks of a column's
 // rows [r0, r1): all zero, or row i holding i

@@ -309,10 +309,14 @@ int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const 
         return (v >= VM_K && v % VM_K == 0 && v <= 4096) ? (size_t)v : (size_t)VM_S;
     }();
     const size_t S = std::min<size_t>(seg_env, n), nseg = n / S, nf = n / VM_K;
-    // the staging area is reused: the previous upload from it must have completed
-    ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+    // the staging area is reused: the previous upload from it must have completed (an event, not a stream sync: the
+    // stream may hold zk_vm_prove's preprocessed-column work, which runs while this host pass does)
+    if (p->ev_vm_live) ZK_CHECK_HIP(hipEventSynchronize(p->ev_vm));
+    p->ev_vm_live = false;
+    if (!p->ev_vm) ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_vm, hipEventDisableTiming));
     const size_t b_states = nseg * sizeof(VmState), b_sec = in.nsec * in.L * sizeof(fe), b_last = 28 * sizeof(fe);
     const size_t bytes = b_states + b_sec + b_last + in.npub;
+    if (bytes > 8 * p->max_n * sizeof(fe)) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many inputs for the prover's staging area");
     if (bytes + 64 > p->h_vm_cap) {
         if (p->h_vm) (void)hipHostFree(p->h_vm);
         p->h_vm = nullptr;
@@ -333,10 +337,12 @@ int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const 
     DevProg dp;
     if (dp_known) dp = *dp_known;
     else ZK_TRY(device_program(prog, p->device, &dp));
-    // device staging: the LDE buffer (written by the proof's LDE before anything reads it) holds the upload, the
-    // NTT scratch the device states; both are free between proofs
-    uint8_t *dv = reinterpret_cast<uint8_t *>(p->lde);
+    // device staging: the composition scratch (8 n elements, free until the composition step) holds the upload, the
+    // NTT scratch the device states; neither is touched by the preprocessed columns' work queued before this pass
+    uint8_t *dv = reinterpret_cast<uint8_t *>(p->ctmp);
     ZK_CHECK_HIP(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, p->st));
+    ZK_CHECK_HIP(hipEventRecord(p->ev_vm, p->st));
+    p->ev_vm_live = true;
     const VmState *dH = reinterpret_cast<const VmState *>(dv);
     const fe *dsec = reinterpret_cast<const fe *>(dv + b_states);
     const fe *dlast = reinterpret_cast<const fe *>(dv + b_states + b_sec);
@@ -493,10 +499,28 @@ int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t
     size_t n = 0;
     zk_program::Fixed f{};
     uint32_t md = 0;
+    FixedCols fx;
+    struct ClearPrefix {  // a prefix not consumed by this call's proof must not reach another one
+        zk_prover *p;
+        ~ClearPrefix() { p->fix_prefix_blocks = 0; }
+    } clear_prefix{p};
     if (pre) {
         // Processor::run + trace (vm/src/lib.rs:14-18): the program-only columns come from the program's preprocessed
         // coefficients / LDE; only the stack registers the program ever uses are generated
         ZK_TRY(fixed_columns(p, prog, in, opt->blowup, &f));
+        fx.md = f.md;
+        fx.fpolys = f.fpolys;
+        fx.flde = f.flde;
+        fx.lagr = f.lagr;
+        fx.lagr_lde = f.lagr_lde;
+        memcpy(fx.last, last, sizeof fx.last);
+        // their share of the trace commitment needs only the last row: queued now, the GPU runs it while the host
+        // runs the stack pass below (one call alone: the pass and this work no longer add up)
+        static const bool prefix_on = [] {  // ZK_VM_PREFIX=0: all of it inside the proof, after the pass
+            const char *e = getenv("ZK_VM_PREFIX");
+            return !(e && !strcmp(e, "0"));
+        }();
+        if (prefix_on && prog->P.trace_len <= p->max_n) ZK_TRY(fixed_prefix(p, prog->P.trace_len, opt->blowup, fx));
         ZK_TRY(vm_generate(p, prog, in, last, GenMode{false, f.md}, &n, outs, &md));
         if ((int)md != f.md) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the stack depth depends on the inputs");
     } else {
@@ -513,13 +537,6 @@ int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t
     if (outputs) memcpy(outputs, pub.stack_outputs, sizeof pub.stack_outputs);
     if (program_hash) memcpy(program_hash, pub.program_hash, sizeof pub.program_hash);
     if (!pre) return zk_prove_device(p, p->d_trace, n, opt, &pub, proof_out, proof_len, nullptr, nullptr);
-    FixedCols fx;
-    fx.md = f.md;
-    fx.fpolys = f.fpolys;
-    fx.flde = f.flde;
-    fx.lagr = f.lagr;
-    fx.lagr_lde = f.lagr_lde;
-    memcpy(fx.last, last, sizeof fx.last);
     return prove_fixed(p, n, opt, &pub, &fx, proof_out, proof_len);
 }
 
