@@ -67,3 +67,35 @@ def test_kill_switch_off_path_matches_pin(switch, tmp_path):
         assert hinted["narrow8"] and hinted["sparse"] and hinted["derived"]
     elif switch == "ZK_SHARD_HINTS":
         assert out["sharded"] == [out["want"]] * 3
+
+
+VM_CHILD = r'''
+import hashlib, json, sys
+sys.path[:0] = [{root!r}, {pkg!r}, {tests!r}]
+from golden_large import LARGE_CASES
+from zkvm_amd.prover import GpuProver, Program, ProofOptions
+from zkvm_amd.workloads import make_workload, ops_for_trace_len
+c = next(c for c in LARGE_CASES if c["name"] == "c2_cipher_2p20")
+src = ops_for_trace_len(c["log_n"], c["generator"])
+w = make_workload(src, seed=c["seed"])
+prog = Program(src)
+g = GpuProver(0, max_trace_len=prog.trace_len)
+inputs = Program.encode_inputs(w.public, w.secret, w.server_key)
+got = [hashlib.sha256(prog.prove_device(g, inputs, w.last_row, ProofOptions())[2]).hexdigest() for _ in range(3)]
+g.close()
+prog.close()
+print("RESULT " + json.dumps({{"want": c["proof_sha256"], "got": got}}), flush=True)
+'''
+
+
+@pytest.mark.parametrize("prefix", ["0", "1"])
+def test_vm_prove_prefix_switch_matches_pin(prefix, tmp_path):
+    """zk_vm_prove queues the preprocessed columns' commitment work ahead of the host stack pass (ZK_VM_PREFIX, on by
+    default); both orders give configs[2]'s pinned proof, call after call (the first call builds the columns)."""
+    script = tmp_path / "vm_child.py"
+    script.write_text(VM_CHILD.format(root=str(ROOT), pkg=str(ROOT / "encrypt-zkvm_amd"), tests=str(ROOT / "tests")))
+    env = dict(os.environ, ZK_VM_PREFIX=prefix)
+    r = subprocess.run([sys.executable, "-u", str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads(next(ln for ln in r.stdout.splitlines() if ln.startswith("RESULT "))[7:])
+    assert out["got"] == [out["want"]] * 3
