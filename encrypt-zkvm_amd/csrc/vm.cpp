@@ -411,10 +411,11 @@ int slow_pass_error(const CompiledProgram &P, const Machine &M) {
 
 // The stack pass (vm_internal.hpp stack_pass): states[c] = the state row row_of(c) - 1 shows.  The stack is kept
 // bottom first (b[0..d)), so a push is one store, a pop a decrement and the ciphertext ops touch their L slots only.
-template <class RowOf>
-int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, RowOf row_of, VmState *states,
-                    fe *outputs, uint32_t *max_depth = nullptr) {
-    const size_t len = P.code.size(), L = in.L;
+// LT: the ciphertext width L as a compile-time constant (1 .. 5, the ciphertext loops unrolled), or 0 (in.L).
+template <int LT, class RowOf>
+int stack_pass_run(const CompiledProgram &P, const Inputs &in, size_t nstates, RowOf row_of, VmState *states,
+                   fe *outputs, uint32_t *max_depth) {
+    const size_t len = P.code.size(), L = LT ? (size_t)LT : in.L;
     const fe delta = fe_make(in.delta);
     fe b[MAX_STACK];
     size_t d = 0, ta = 0, tb = 0, c = 0, md = 0;
@@ -427,6 +428,7 @@ int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, 
     };
     auto sec = [&](size_t i) { return fe_from_bytes(in.sec + 16 * i); };
     while (c < nstates && row_of(c) <= 1) snap(states[c++]);  // rows -1 and 0 show the zero state
+    size_t next = c < nstates ? row_of(c) : SIZE_MAX;  // the row of the next state to keep
     bool err = false;
     for (size_t k = 1; k <= len && !err; k++) {
         const Op o = P.code[k - 1];
@@ -483,7 +485,12 @@ int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, 
         }
         if (P.chiplet_err == k) err = true;
         md = std::max(md, d);
-        while (!err && c < nstates && row_of(c) == k + 1) snap(states[c++]);
+        if (k + 1 == next && !err) {
+            do
+                snap(states[c++]);
+            while (c < nstates && row_of(c) == k + 1);
+            next = c < nstates ? row_of(c) : SIZE_MAX;
+        }
     }
     if (err || len % CYCLE) {
         std::vector<fe> sv(in.nsec * L);
@@ -495,6 +502,18 @@ int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, 
     if (outputs)
         for (size_t i = 0; i < (size_t)MAX_STACK; i++) outputs[i] = i < d ? b[d - 1 - i] : fe_zero();
     return ZK_OK;
+}
+template <class RowOf>
+int stack_pass_impl(const CompiledProgram &P, const Inputs &in, size_t nstates, RowOf row_of, VmState *states,
+                    fe *outputs, uint32_t *max_depth = nullptr) {
+    switch (in.L) {
+    case 1: return stack_pass_run<1>(P, in, nstates, row_of, states, outputs, max_depth);
+    case 2: return stack_pass_run<2>(P, in, nstates, row_of, states, outputs, max_depth);
+    case 3: return stack_pass_run<3>(P, in, nstates, row_of, states, outputs, max_depth);
+    case 4: return stack_pass_run<4>(P, in, nstates, row_of, states, outputs, max_depth);
+    case 5: return stack_pass_run<5>(P, in, nstates, row_of, states, outputs, max_depth);
+    default: return stack_pass_run<0>(P, in, nstates, row_of, states, outputs, max_depth);
+    }
 }
 
 int run_program(const CompiledProgram &P, const Inputs &in, fe *t, size_t n, const fe *last, fe *outputs) {

@@ -4,7 +4,8 @@ Run (GPU box):
   cd /tmp && rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $R/gpurun_out/lat -o lat -- \
       python3 $R/tools/latency_timeline.py --out $R/gpurun_out/lat_marks.json
   python3 $R/tools/latency_timeline.py --analyze $R/gpurun_out/lat --marks $R/gpurun_out/lat_marks.json
-The run part proves the configs[2] trace (2^20, seed 1000, page-locked) with one prover: 5 warm-up calls, then 3
+The run part proves the configs[2] trace (2^20, seed 1000, page-locked; --vm: the same program and inputs through
+zk_vm_prove) with one prover: 5 warm-up calls, then 3
 timed calls 100 ms apart, each bracketed by CLOCK_MONOTONIC stamps (the clock rocprofv3's timestamps use).  The
 analysis takes the last timed call and reports: call start -> first copy, -> first kernel; the last copy's end; the
 device-idle gaps between kernels (host round trips of the transcript) with the kernel after each; busy time; and the
@@ -24,23 +25,35 @@ for p in (ROOT, ROOT / "encrypt-zkvm_amd", ROOT / "tests"):
     sys.path.insert(0, str(p))
 
 
-def run(out):
+def run(out, vm=False):
     from golden_large import LARGE_CASES, large_inputs
-    from zkvm_amd.prover import GpuProver
+    from zkvm_amd.prover import GpuProver, Program, ProofOptions
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
     c = next(c for c in LARGE_CASES if c["name"] == "c2_cipher_2p20")
-    ht, trace, pub, opts = large_inputs(c)
-    g = GpuProver(0, max_trace_len=trace.shape[1])
+    if vm:  # zk_vm_prove: the same program and inputs, the trace written on the GPU
+        src = ops_for_trace_len(c["log_n"], c["generator"])
+        w = make_workload(src, seed=c["seed"])
+        prog = Program(src)
+        inputs = Program.encode_inputs(w.public, w.secret, w.server_key)
+        g = GpuProver(0, max_trace_len=prog.trace_len)
+        call = lambda: prog.prove_device(g, inputs, w.last_row, ProofOptions())  # noqa: E731
+        ht = None
+    else:
+        ht, trace, pub, opts = large_inputs(c)
+        g = GpuProver(0, max_trace_len=trace.shape[1])
+        call = lambda: g.prove_host(trace, pub, opts)  # noqa: E731
     for _ in range(5):
-        g.prove_host(trace, pub, opts)
+        call()
     marks = []
     for _ in range(3):
         time.sleep(0.1)
         t0 = time.monotonic_ns()
-        g.prove_host(trace, pub, opts)
+        call()
         t1 = time.monotonic_ns()
         marks.append((t0, t1))
     g.close()
-    ht.close()
+    if ht:
+        ht.close()
     Path(out).write_text(json.dumps({"calls": marks}))
     print("calls (ms):", [round((b - a) / 1e6, 3) for a, b in marks])
 
@@ -101,8 +114,9 @@ if __name__ == "__main__":
     ap.add_argument("--out")
     ap.add_argument("--analyze")
     ap.add_argument("--marks")
+    ap.add_argument("--vm", action="store_true", help="time zk_vm_prove (vm::prove's shape) instead of prove_host")
     a = ap.parse_args()
     if a.analyze:
         analyze(a.analyze, a.marks)
     else:
-        run(a.out)
+        run(a.out, a.vm)
