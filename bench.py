@@ -388,6 +388,10 @@ def main():
     ap.add_argument("--input-sets", type=int, default=4,
                     help="input sets of the workload program the timed proofs rotate through (fresh secrets, public "
                          "inputs and random last rows; set 0 is the pinned seed-1000 workload)")
+    ap.add_argument("--upload-schedule", choices=["auto", "throughput", "latency"], default="auto",
+                    help="how the host trace goes up (zk_prover_set_upload_schedule) in the timed proofs; auto: the "
+                         "latency schedule for a proof alone on the GPU, else the throughput one (profile passes with "
+                         "--inflight 1 pass throughput, so their proofs are those of the default P = 3 line)")
     ap.add_argument("--torch-runtime", action="store_true",
                     help="import torch before the library (runtime A/B only): the library then runs on torch's bundled "
                          "HIP runtime and RCCL instead of the /opt/rocm copies it links")
@@ -442,6 +446,10 @@ def main():
     opts_str = "ProofOptions(43, 8, 0, Quadratic, 8, 127)" if args.config5 else "ProofOptions(32, 8, 0, None, 8, 127)"
     P = max(1, args.inflight)
     provers = [GpuProver(local, max_trace_len=n, max_blowup=opts.blowup_factor) for _ in range(P)]
+    for g_ in provers:
+        g_.set_upload_schedule(args.upload_schedule)
+    # the schedule the timed proofs ran (auto: three provers in flight keep each other company)
+    timed_sched = args.upload_schedule if args.upload_schedule != "auto" else ("throughput" if P > 1 else "latency")
     gpu = provers[0]
     last = [None] * P
 
@@ -530,16 +538,21 @@ def main():
         latency_ms = 1e3 * sorted(lat)[len(lat) // 2]
     stages = gpu.stage_times()
 
-    # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream)
+    # one extra, untimed, profiled proof: per-kernel device time (HIP events on the prover stream), on the schedule the
+    # timed proofs ran (it runs alone, which AUTO would give the latency schedule's smaller launches)
+    gpu.set_upload_schedule(timed_sched)
     gpu.profile(True)
     gpu.prove_host(trace, pub, opts)
     kstats = gpu.kernel_stats()
     kops = gpu.kernel_ops()
     gpu.profile(False)
+    gpu.set_upload_schedule(args.upload_schedule)
     upst = gpu.upload_stats()  # that proof's trace upload (sparse / narrow hints learned from the proofs before it)
     upload = {"mb_per_proof": round(upst["bytes"] / 2**20, 1), "full_trace_mb": round(28 * n * 16 / 2**20, 1),
               "sparse_cols": upst["sparse"], "narrow8_cols": upst["narrow8"], "narrow32_cols": upst["narrow32"],
-              "derived_cols": upst["derived"]}
+              "derived_cols": upst["derived"],
+              "schedule": {"timed_proofs": timed_sched, "profiled_proof": timed_sched,
+                           "latency_leg": args.upload_schedule if args.upload_schedule != "auto" else "latency"}}
 
     verified = None
     if rank == 0 and not args.no_verify:

@@ -585,6 +585,13 @@ int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double
     return ZK_OK;
 }
 
+int zk_prover_set_upload_schedule(zk_prover *p, int schedule) {
+    if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
+    if (schedule < ZK_SCHED_AUTO || schedule > ZK_SCHED_LATENCY) ZK_FAIL(ZK_ERR_INVALID_ARG, "unknown upload schedule");
+    p->upload_sched = schedule;
+    return ZK_OK;
+}
+
 int zk_prover_profile(zk_prover *p, int enable) {
     if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
     profiler().on = enable != 0;
@@ -1202,8 +1209,9 @@ bool zk::narrow_on() {
     return on;
 }
 
-// The upload schedule of a host-resident trace (trace_lde_commit): 0 the throughput schedule always, 1 (default) the
-// latency schedule for a proof that starts with no other proof in flight on its device, 2 the latency one always
+// The process-wide default of ZK_SCHED_AUTO provers (zk_prover_set_upload_schedule): ZK_LATENCY_SCHED=0 the throughput
+// schedule always, 1 (unset) the latency schedule for a proof that starts with no other proof in flight on its device,
+// 2 the latency one always
 static int latency_sched() {
     static const int v = [] {
         const char *e = getenv("ZK_LATENCY_SCHED");
@@ -1890,7 +1898,11 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
         explicit Busy(std::atomic<int> *x) : b(x), others(x->fetch_add(1)) {}
         ~Busy() { b->fetch_sub(1); }
     } busy{p->dev_busy};
-    p->lat_sched = latency_sched() == 2 || (latency_sched() == 1 && busy.others == 0);
+    const int sched = p->upload_sched != ZK_SCHED_AUTO ? p->upload_sched
+                      : latency_sched() == 0                ? ZK_SCHED_THROUGHPUT
+                      : latency_sched() == 2                ? ZK_SCHED_LATENCY
+                                                            : ZK_SCHED_AUTO;
+    p->lat_sched = sched == ZK_SCHED_LATENCY || (sched == ZK_SCHED_AUTO && busy.others == 0);
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));

@@ -126,9 +126,11 @@ struct zk_prover {
     hipStream_t up = nullptr;
     std::mutex *up_mu = nullptr;
     // proofs in flight on this device (process-wide, beside the upload stream), and whether this proof started alone:
-    // then trace_lde_commit takes the latency schedule (ZK_LATENCY_SCHED: 0 never, 2 always, default when alone)
+    // then trace_lde_commit takes the latency schedule (upload_sched: zk_prover_set_upload_schedule; AUTO follows
+    // ZK_LATENCY_SCHED: 0 never, 2 always, default when alone)
     std::atomic<int> *dev_busy = nullptr;
     bool lat_sched = false;
+    int upload_sched = ZK_SCHED_AUTO;  // zk_prover_set_upload_schedule
     // ... each group's event gating its kernels on st.  Measured (tools/ubench/upload_probe.hip): an event recorded
     // between the 16 MiB column copies of one stream halves their rate (29.7 vs 55 GB/s), but not between 112 MiB
     // copies (56.8 GB/s), so contiguous columns go up as one copy per group.  (Stream write / wait-value packets

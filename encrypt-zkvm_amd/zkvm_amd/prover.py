@@ -178,6 +178,13 @@ class GpuProver:
         return {"bytes": b.value, "sparse": cols(sp.value), "narrow8": cols(n8.value), "narrow32": cols(n32.value),
                 "derived": cols(dv.value)}
 
+    UPLOAD_SCHEDULES = {"auto": 0, "throughput": 1, "latency": 2}
+
+    def set_upload_schedule(self, schedule: str):
+        """zk_prover_set_upload_schedule: "auto" (latency when no other proof is in flight on the device), "throughput"
+        or "latency" -- how a host-resident trace goes up; the proof bytes are the same."""
+        check(lib().zk_prover_set_upload_schedule(self.handle, self.UPLOAD_SCHEDULES[schedule]))
+
     def profile(self, on: bool):
         check(lib().zk_prover_profile(self.handle, 1 if on else 0))
         check(lib().zk_prover_kernel_stats(self.handle, None, None, None, None, 0, None))  # reset

@@ -254,6 +254,15 @@ int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols,
  * the clock (rows 0 .. n-2 of any accepted trace hold 0 .. n-2: air/src/constrains.rs clock constraint and the
  * clk[0] = 0 assertion), checked against the caller's column by host threads */
 int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols);
+/* How a host-resident trace goes up (zk_prove / zk_prove_columns).  ZK_SCHED_AUTO (the default): the latency schedule
+ * for a proof that starts with no other proof in flight on its device, else the throughput schedule.
+ * ZK_SCHED_THROUGHPUT: the narrow (packed) columns in two parts through the copy engine between 64-MB column groups.
+ * ZK_SCHED_LATENCY: the first two column groups start crossing at once and the packed narrow columns are expanded by a
+ * kernel reading the pinned bytes, in small parts, so the first kernels start ~0.3 ms into the call.  Same proof bytes.
+ * (No reference counterpart: winterfell's prover has no upload; a tuning knob for servers, ZK_LATENCY_SCHED=0 / 2 in
+ * the environment sets the AUTO default process-wide.) */
+enum { ZK_SCHED_AUTO = 0, ZK_SCHED_THROUGHPUT = 1, ZK_SCHED_LATENCY = 2 };
+int zk_prover_set_upload_schedule(zk_prover *p, int schedule);
 
 /* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
  * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required

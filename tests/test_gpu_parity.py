@@ -576,12 +576,15 @@ def test_sparse_column_detection(gpu, oracle, path):
     assert proof == oproof
 
 
-def test_narrow_columns_learned_and_refuted(oracle):
+@pytest.mark.parametrize("schedule", ["auto", "throughput", "latency"])
+def test_narrow_columns_learned_and_refuted(oracle, schedule):
     """Narrow columns (a host-resident trace's columns that the previous proof of the same length found to hold 8- or
     32-bit values before the last row go up packed, each value checked on the host; one that does not fit goes up
     whole): the proofs of a trace, of the same trace again (packed), and of edits that break the 8-bit and then the
     32-bit class of a learned column -- each equal to the oracle's, with the upload shrinking once the hint is
-    learned."""
+    learned.  On each upload schedule (zk_prover_set_upload_schedule: auto -- latency, this prover being alone --,
+    throughput: two packed parts through the copy engine; latency: parts of 1, 2, 2, .. columns expanded from pinned
+    memory)."""
     trace, pub = workload_trace(ops_for_trace_len(14, "cipher"), seed=16)
     n = trace.shape[1]
     small = trace.copy()
@@ -592,6 +595,7 @@ def test_narrow_columns_learned_and_refuted(oracle):
     wide32 = small.copy()
     wide32[27, 78] = [1 << 40, 0]                       # no longer 32-bit
     g = GpuProver(0, max_trace_len=n)
+    g.set_upload_schedule(schedule)
     try:
         stats = []
         for t in (trace, trace, small, small, wide8, wide8, wide32, small):

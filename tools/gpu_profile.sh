@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-BENCH_ARGS="--steps 4 --warmup 2 --inflight 1 --no-cpu-baseline --no-verify --no-compare"
+BENCH_ARGS="--steps 4 --warmup 2 --inflight 1 --no-cpu-baseline --no-verify --no-compare --upload-schedule throughput"
 
 if [ "${2:-tests}" = "tests" ]; then
   (cd "$R" && timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$O/gpu_tests_$TAG.log" 2>&1)
@@ -19,8 +19,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
   python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench_$TAG.json" 2> "$O/prof_bench_$TAG.err"
 echo "kernel trace ok"
 # (3 warm-up proofs first: the profiled last proof is a steady-state one, column hints in use; pmc_traffic.py counts
-# that proof's dispatches only, against its algorithmic bytes from the same run's bench line)
-PMC_ARGS="--steps 1 --warmup 3 --inflight 1 --no-cpu-baseline --no-verify --no-compare --input-sets 1"
+# that proof's dispatches only, against its algorithmic bytes from the same run's bench line.  One prover, on the
+# throughput upload schedule: the launches of the default line's three-in-flight proofs, not of one proof alone)
+PMC_ARGS="--steps 1 --warmup 3 --inflight 1 --no-cpu-baseline --no-verify --no-compare --input-sets 1 --upload-schedule throughput"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o f -- \
   python3 "$R/bench.py" $PMC_ARGS > "$O/pmc_fetch_bench_$TAG.json" 2> "$O/pmc_fetch_$TAG.err"
 echo "pmc fetch ok"
