@@ -1671,6 +1671,9 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
         };
         ZK_TRY(issue_dense());
         ZK_TRY(issue_dense());
+        // (h_pack is pinned and mapped; part k's bytes are written by the pool threads before packed[k] opens and the
+        // expansion kernel is launched after that, and a kernel dispatch acquires at system scope, so the kernel
+        // reads this proof's bytes -- tests/test_gpu_parity.py changes a narrow column between proofs on this path)
         uint8_t *hp = nullptr;
         ZK_CHECK_HIP(hipHostGetDevicePointer((void **)&hp, p->h_pack, 0));
         for (int k = 0; k < np; k++) {
