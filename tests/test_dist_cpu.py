@@ -59,6 +59,9 @@ else:
         "bad_rc": bad, "uid": uid.decode(), "max": g.max(float(rank) * 1.5), "torch": "torch" in sys.modules}}
     g.close()
 print("RESULT " + json.dumps(out), flush=True)
+if os.environ.get("ZK_TEST_RESULT_DIR"):  # (under torchrun the ranks' stdout lines can interleave)
+    with open(os.path.join(os.environ["ZK_TEST_RESULT_DIR"], "rank%d.json" % int(os.environ["RANK"])), "w") as f:
+        json.dump(out, f)
 '''
 
 
@@ -129,12 +132,12 @@ def test_under_torchrun(tmp_path):
     host group's rendezvous file instead and report the same max-over-ranks time."""
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=str(ROOT), pkg=str(ROOT / "encrypt-zkvm_amd")))
-    env = dict(os.environ, ZK_NUMA_BIND="0")
+    env = dict(os.environ, ZK_NUMA_BIND="0", ZK_TEST_RESULT_DIR=str(tmp_path))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script), "bench"],
                        env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    res = [json.loads(ln.split("RESULT ", 1)[1]) for ln in r.stdout.splitlines() if "RESULT " in ln]
+    res = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(2)]
     assert sorted(x["rank"] for x in res) == [0, 1]
     assert res[0]["elapsed"] == res[1]["elapsed"] and not any(x["torch"] for x in res)
 
