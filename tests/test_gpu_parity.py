@@ -622,6 +622,19 @@ def test_narrow_columns_learned_and_refuted(oracle, schedule):
     assert 27 not in stats[6]["narrow32"]              # refuted again
 
 
+def test_upload_schedule_rejects_unknown_values():
+    g = GpuProver(0, max_trace_len=1 << 10)
+    try:
+        for bad in (-1, 3, 99):
+            assert native.lib().zk_prover_set_upload_schedule(g.handle, bad) == native.ZK_ERR_INVALID_ARG
+        for ok in ("auto", "throughput", "latency"):
+            g.set_upload_schedule(ok)
+        with pytest.raises(KeyError):
+            g.set_upload_schedule("fastest")
+    finally:
+        g.close()
+
+
 def test_clock_column_derived_and_refuted(oracle):
     """The AIR clock (column 0 of an accepted trace holds 0 .. n-2 before its random last row): once learned, a
     host-resident trace's clock is neither uploaded nor transformed but derived (identity column + last-row

@@ -36,6 +36,14 @@ def test_library_exports_header_symbols():
     assert set(native.EXPORTED) <= set(declared)
 
 
+def test_prover_setters_reject_bad_arguments_without_gpu():
+    """zk_prover_set_upload_schedule and zk_prover_profile check their arguments before touching a device: a null
+    prover is refused (no GPU needed to reach the check)."""
+    L = native.lib()
+    assert L.zk_prover_set_upload_schedule(None, 0) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_prover_profile(None, 1) == native.ZK_ERR_INVALID_ARG
+
+
 def edge_values():
     vals = [0, 1, 2, P - 1, P - 2, 2**64 - 1, 2**64, 2**127, P - 2**64, 45 * 2**40, 2**96 - 1, 2**128 - 45 * 2**40]
     vals += [P - 1 - (1 << k) for k in range(0, 127, 7)]
