@@ -1470,9 +1470,9 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     //  - throughput (other proofs in flight on the device): the narrow columns go up in two parts (the first half of
     //    them, the rest) through the copy engine, each as soon as its packing is done, in quarter-million-row tasks;
     //  - latency (this proof alone on the device): dense groups 0 and 1 start crossing the link at once; the narrow
-    //    columns are packed in parts of 1, 2, 2, ... columns (16 K-row tasks, so each part is ready in ~0.1-0.2 ms)
+    //    columns are packed in parts of 1, 2, 2, ... columns (64 K-row tasks, so each part is ready in ~0.1-0.2 ms)
     //    and each part's expansion kernel reads the pinned packed bytes itself (no copy engine: that is busy with the
-    //    dense groups), so the first kernels start ~0.3 ms into the call and the device has the narrow columns' work
+    //    dense groups), so the first kernels start ~0.2 ms into the call and the device has the narrow columns' work
     //    while the first dense groups cross.
     const bool lat = p->lat_sched && nn > 0;
     int pb[W + 1], np = 0;  // part k: narrow columns pb[k] .. pb[k+1]-1

@@ -258,7 +258,7 @@ int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols);
  * for a proof that starts with no other proof in flight on its device, else the throughput schedule.
  * ZK_SCHED_THROUGHPUT: the narrow (packed) columns in two parts through the copy engine between 64-MB column groups.
  * ZK_SCHED_LATENCY: the first two column groups start crossing at once and the packed narrow columns are expanded by a
- * kernel reading the pinned bytes, in small parts, so the first kernels start ~0.3 ms into the call.  Same proof bytes.
+ * kernel reading the pinned bytes, in small parts, so the first kernels start ~0.2 ms into the call.  Same proof bytes.
  * (No reference counterpart: winterfell's prover has no upload; a tuning knob for servers, ZK_LATENCY_SCHED=0 / 2 in
  * the environment sets the AUTO default process-wide.) */
 enum { ZK_SCHED_AUTO = 0, ZK_SCHED_THROUGHPUT = 1, ZK_SCHED_LATENCY = 2 };
