@@ -444,6 +444,33 @@ def test_grinding_factor_bound(gpu, grinding):
     assert e.value.code == native.ZK_ERR_INVALID_ARG and "grinding" in str(e.value)
 
 
+@pytest.mark.parametrize("field,value", [("field_extension", 3), ("blowup_factor", 4), ("blowup_factor", 12),
+                                         ("fri_folding_factor", 3), ("fri_remainder_max_degree", 100),
+                                         ("num_queries", 0)])
+def test_unsupported_options_refused(gpu, field, value):
+    """Options winterfell 0.9 would not accept (or this prover does not implement) are refused with
+    ZK_ERR_INVALID_ARG before any device work."""
+    trace, pub = workload_trace(LR_PROGRAM, seed=4)
+    with pytest.raises(native.ZkError) as e:
+        gpu.prove(trace, pub, ProofOptions(**{field: value}))
+    assert e.value.code == native.ZK_ERR_INVALID_ARG
+
+
+def test_proof_buffer_too_small_then_proof(gpu, oracle):
+    """A proof buffer too small for the proof gives ZK_ERR_BUFFER_TOO_SMALL (nothing written past it); the next
+    proof with room is the oracle's."""
+    trace, pub = workload_trace(LR_PROGRAM, seed=5)
+    gpu._proof_buf = C.create_string_buffer(64)
+    try:
+        with pytest.raises(native.ZkError) as e:
+            gpu.prove(trace, pub, ProofOptions())
+        assert e.value.code == native.ZK_ERR_BUFFER_TOO_SMALL
+    finally:
+        gpu._proof_buf = None
+    proof, _, _, rc = gpu.prove(trace, pub, ProofOptions())
+    assert rc == 0 and proof == oracle.prove(trace, oracle_pub(oracle, pub))[0]
+
+
 def test_error_then_proof_is_unchanged(gpu, oracle):
     """A proof that fails part-way (degree error after staged reads) leaves nothing pending in the
     prover's pinned staging area: the next proof is byte-identical to the oracle's."""
