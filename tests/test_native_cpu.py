@@ -36,12 +36,20 @@ def test_library_exports_header_symbols():
     assert set(native.EXPORTED) <= set(declared)
 
 
-def test_prover_setters_reject_bad_arguments_without_gpu():
-    """zk_prover_set_upload_schedule and zk_prover_profile check their arguments before touching a device: a null
-    prover is refused (no GPU needed to reach the check)."""
+def test_null_arguments_refused_without_gpu():
+    """The setters and the prove entry points check their arguments before touching a device: null provers, traces
+    and columns are refused with ZK_ERR_INVALID_ARG (no GPU needed to reach the checks)."""
     L = native.lib()
     assert L.zk_prover_set_upload_schedule(None, 0) == native.ZK_ERR_INVALID_ARG
     assert L.zk_prover_profile(None, 1) == native.ZK_ERR_INVALID_ARG
+    # the prove entry points check their pointers before the prover: a null trace, a null column among 28
+    plen = C.c_size_t(0)
+    assert L.zk_prove(None, None, 16, None, None, None, C.byref(plen)) == native.ZK_ERR_INVALID_ARG
+    cols = (C.c_void_p * 28)(*([C.c_void_p(1)] * 27 + [None]))
+    assert L.zk_prove_columns(None, cols, 16, None, None, None, C.byref(plen)) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_prove_columns(None, None, 16, None, None, None, C.byref(plen)) == native.ZK_ERR_INVALID_ARG
+    assert L.zk_vm_prove(None, None, None, 0, None, 0, 5, 16, None, None, None, C.byref(plen), None, None) \
+        == native.ZK_ERR_INVALID_ARG
 
 
 def edge_values():
