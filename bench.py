@@ -742,7 +742,9 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
     avg_ms = tot_ms / launches
     achieved = tot_bytes / (tot_ms / 1e3) / 1e9
     prove_total_ms = sum(v[0] for v in kstats.values())
-    tr = pmc_traffic(name, args.config5)
+    # the committed PMC profiles are taken at 2^20 (tools/gpu_profile.sh): other sizes report no traffic
+    PROFILED_LOG_N = 20
+    tr = pmc_traffic(name, args.config5) if args.log_n == PROFILED_LOG_N else None
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["per_launch_bytes"] if tr else None,
                 "traffic_ratio": tr["traffic_ratio"] if tr else None, "traffic_source": tr,
@@ -759,7 +761,7 @@ def build_line(args, rank, world, n, elapsed, warm, opts, opts_str, min_sec, P, 
         roofline["valu"] = {"bound": "valu", "fe_mul_equiv_per_launch": muls / launches, "fe_addsub_per_launch": addsubs / launches,
                             "achieved_fe_mul_per_s": round(muls / (tot_ms / 1e3), 1), "peak_fe_mul_per_s": FE_MUL_PEAK,
                             "floor_ms_per_launch": round(floor_ms / launches, 4), "frac": round(floor_ms / tot_ms, 4)}
-    roofline["valu_hw"] = pmc_valu(name)
+    roofline["valu_hw"] = pmc_valu(name) if args.log_n == PROFILED_LOG_N else None
     value = world * n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "trace-steps/s", "n_gpus": world, "steps": args.steps,
