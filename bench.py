@@ -10,9 +10,10 @@ builds a TraceTable in host memory and hands it to Prover::prove).  The library 
 on a copy stream, overlapped with the interpolation and, with two provers in flight, with the other proof's
 kernels.  Beside `value` the line reports device_resident_ms (the trace already in HBM), pageable_host_ms
 (the trace in ordinary pageable memory), latency_ms (one prove() call alone on the GPU) and steady_state_ms (the
-host-resident proofs over a 100-proof window: a 20-proof window pays the run's two ends -- nothing to compute
-before the first column group is up, fewer co-runners for the last proofs -- about 4 %,
-tools/inflight_timeline.py).
+host-resident proofs over a 100-proof window).  The default window is 60 proofs: a 20-proof window pays the run's two
+ends -- nothing to compute before the first column group is up, fewer co-runners for the last proofs -- about 1 %
+on the round-5 path (11.11 / 11.17 ms per proof against 11.06 / 11.04 at 60 and 11.02 / 11.05 at 100, one box;
+tools/inflight_timeline.py), and 60 proofs are 0.7 s of GPU time.
 
 Proofs in flight (--inflight P, default 3): each GPU holds P independent provers (own HBM buffers and
 compute streams, zk_prover objects; one upload stream per device) driven by P host threads, so one prover's trace
@@ -365,7 +366,7 @@ def pmc_valu(kernel: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed proofs before the timed region (default 3 per prover in flight; the first proof of "
                          "each prover builds its per-size tables)")
