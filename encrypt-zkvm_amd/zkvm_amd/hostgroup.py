@@ -71,13 +71,15 @@ class HostGroup:
         if world == 1:
             return
         deadline = time.monotonic() + timeout
-        # every rank's own listener for the mesh connections of the ranks above it
-        lst = socket.create_server((addr, 0))
-        lst.settimeout(timeout)
-        my_port = lst.getsockname()[1]
+        # every rank's own listener for the mesh connections of the ranks above it, on an ephemeral port -- created
+        # only once rank 0's hub is bound (rank 0: after binding it; the others: after reaching it), so that no
+        # listener can take an explicitly given hub port first
         if rank == 0:
-            hub = socket.create_server((addr, port or 0), backlog=world)
+            hub = self._bind_hub(addr, port, world, deadline)
             hub.settimeout(timeout)
+            lst = socket.create_server((addr, 0))
+            lst.settimeout(timeout)
+            my_port = lst.getsockname()[1]
             nonce = secrets.token_hex(8)
             path = None
             if port is None:
@@ -112,7 +114,7 @@ class HostGroup:
                     pass
             self.peers.update(conns)  # the hub connections are rank 0's mesh links
         else:
-            c, table = self._connect_hub(addr, port, rdzv_key, my_port, deadline)
+            c, table, lst = self._connect_hub(addr, port, rdzv_key, deadline, timeout)
             self.peers[0] = c
             # mesh: rank r connects to every rank s in (0, r) and accepts from every rank above it
             for s in range(1, rank):
@@ -129,10 +131,23 @@ class HostGroup:
             c.settimeout(None)
             c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
 
-    def _connect_hub(self, addr, port, rdzv_key, my_port, deadline):
-        """Connect to rank 0's hub and wait for the table of every rank's mesh port.  Retried while rank 0 is not
-        listening yet or the rendezvous file is a stale one (refused, or closed by a hub with another nonce)."""
-        last = None
+    @staticmethod
+    def _bind_hub(addr, port, world, deadline):
+        """Rank 0's hub socket on `port` (None: an ephemeral one).  A given port that is briefly taken (another
+        process's outgoing connection can hold it as its ephemeral port for a moment) is retried until the deadline."""
+        while True:
+            try:
+                return socket.create_server((addr, port or 0), backlog=world)
+            except OSError as e:
+                if port is None or e.errno not in (98, 48) or time.monotonic() > deadline:  # EADDRINUSE
+                    raise
+                time.sleep(0.05)
+
+    def _connect_hub(self, addr, port, rdzv_key, deadline, timeout):
+        """Connect to rank 0's hub, create this rank's mesh listener, and wait for the table of every rank's mesh
+        port; returns (hub connection, table, listener).  Retried while rank 0 is not listening yet or the rendezvous
+        file is a stale one (refused, or closed by a hub with another nonce)."""
+        last, lst = None, None
         while time.monotonic() < deadline:
             tok, hub_port = "-", port
             if port is None:
@@ -146,12 +161,15 @@ class HostGroup:
             c = None
             try:
                 c = socket.create_connection((addr, hub_port), timeout=5.0)
-                _send_msg(c, f"{self.rank} {self.world} {my_port} {tok}".encode())
+                if lst is None:
+                    lst = socket.create_server((addr, 0))
+                    lst.settimeout(timeout)
+                _send_msg(c, f"{self.rank} {self.world} {lst.getsockname()[1]} {tok}".encode())
                 c.settimeout(max(1.0, deadline - time.monotonic()))
                 table = [int(x) for x in _recv_msg(c).decode().split()]
                 if len(table) != self.world:
                     raise ConnectionError(f"host group: a table of {len(table)} ranks")
-                return c, table
+                return c, table, lst
             except socket.timeout:
                 raise TimeoutError(f"host group: rank {self.rank} waited for the other ranks past the deadline")
             except (OSError, ConnectionError, ValueError) as e:
@@ -159,6 +177,8 @@ class HostGroup:
                 if c is not None:
                     c.close()
                 time.sleep(0.05)
+        if lst is not None:
+            lst.close()
         raise TimeoutError(f"host group: rank {self.rank} could not reach rank 0 ({last})")
 
     @classmethod
