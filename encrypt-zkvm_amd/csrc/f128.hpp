@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "addsub_asm.hpp"
+
 #define ZK_HD __host__ __device__ __forceinline__
 
 struct fe {
@@ -439,26 +441,45 @@ __device__ __forceinline__ fe fe_mul_w2(fe A, const fe_w2 &W) {
     return ws_fold(d0, e1, e2, e3, e4, 0u);
 }
 
-// ---- two butterflies' sums and differences at once: (a + b, a - b, c + d, c - d) mod p.  (A hand-interleaved
-// asm form with a separate SGPR carry pair per chain measured no faster inside the NTT: tools/ubench/fadd_lab.hip,
-// DESIGN.md "Measured dead ends".)
+// ---- two butterflies' sums and differences at once: (a + b, a - b, c + d, c - d) mod p.  ZK_ADDSUB_ASM (default):
+// the four carry chains as one list-scheduled asm block on their own SGPR pairs (addsub_asm.hpp, generated by
+// tools/gen_addsub_asm.py), so the wait states between a carry write and its read are filled by the other chains
+// instead of s_nop, and each difference takes one lane-mask select instead of two; otherwise the compiler's
+// chains through VCC, one after the other.  Same values either way.
+#ifndef ZK_ADDSUB_ASM
+#define ZK_ADDSUB_ASM 1
+#endif
+// V: 0 both sums canonical, 1 both lazy (fe_add_lazy's contract: a, c any value < 2^128; b, d canonical),
+// 2 the first lazy and the second canonical
+template <int V>
+__device__ __forceinline__ void addsub2_v(fe a, fe b, fe c, fe d, fe &apb, fe &amb, fe &cpd, fe &cmd) {
+    if constexpr (ZK_ADDSUB_ASM) {
+        uint32_t A[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+        uint32_t B[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+        uint32_t C[4] = {lo32(c.lo), hi32(c.lo), lo32(c.hi), hi32(c.hi)};
+        uint32_t D[4] = {lo32(d.lo), hi32(d.lo), lo32(d.hi), hi32(d.hi)};
+        uint32_t S[4], E[4];
+        if constexpr (V == 0) addsub2_asm_cc(A, B, C, D, S, E);
+        else if constexpr (V == 1) addsub2_asm_ll(A, B, C, D, S, E);
+        else addsub2_asm_lc(A, B, C, D, S, E);
+        apb = fe{join32(A[0], A[1]), join32(A[2], A[3])};
+        amb = fe{join32(S[0], S[1]), join32(S[2], S[3])};
+        cpd = fe{join32(C[0], C[1]), join32(C[2], C[3])};
+        cmd = fe{join32(E[0], E[1]), join32(E[2], E[3])};
+    } else {
+        apb = V != 0 ? fe_add_lazy(a, b) : fe_add(a, b);
+        amb = fe_sub(a, b);
+        cpd = V == 1 ? fe_add_lazy(c, d) : fe_add(c, d);
+        cmd = fe_sub(c, d);
+    }
+}
 __device__ __forceinline__ void fe_addsub2(fe a, fe b, fe c, fe d, fe &apb, fe &amb, fe &cpd, fe &cmd) {
-    apb = fe_add(a, b);
-    amb = fe_sub(a, b);
-    cpd = fe_add(c, d);
-    cmd = fe_sub(c, d);
+    addsub2_v<0>(a, b, c, d, apb, amb, cpd, cmd);
 }
 // the same with lazy sums (fe_add_lazy's contract: a, c any value < 2^128; b, d canonical)
 template <bool LZ>
 __device__ __forceinline__ void addsub2(fe a, fe b, fe c, fe d, fe &apb, fe &amb, fe &cpd, fe &cmd) {
-    if constexpr (LZ) {
-        apb = fe_add_lazy(a, b);
-        amb = fe_sub(a, b);
-        cpd = fe_add_lazy(c, d);
-        cmd = fe_sub(c, d);
-    } else {
-        fe_addsub2(a, b, c, d, apb, amb, cpd, cmd);
-    }
+    addsub2_v<LZ ? 1 : 0>(a, b, c, d, apb, amb, cpd, cmd);
 }
 
 // the W set tab[idx] for a wave-uniform idx, through scalar loads

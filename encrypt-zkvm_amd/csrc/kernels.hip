@@ -331,8 +331,7 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
     if constexpr (!CT) {
         const fe_ws W4 = load_fe_ws(ws, 1024);
         fe a0, a1, a2, d23;
-        fe_addsub2(x0, x1, x2, x3, a0, a1, a2, d23);  // a2 is a second operand below: keep it canonical
-        if constexpr (LZ) a0 = fe_add_lazy(x0, x1);
+        addsub2_v<LZ ? 2 : 0>(x0, x1, x2, x3, a0, a1, a2, d23);  // a2 is a second operand below: keep it canonical
         const fe a3 = fe_mul_uniform(d23, W4);
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, a2, a1, a3, o0, o2, o1, o3);
@@ -2989,6 +2988,19 @@ __global__ void k_field_op(int op, const fe *a, const fe *b, fe *out, size_t cou
     case 5: r = fe_add_lazy(x, y); break;  // the NTT's lazy forms: x any value < 2^128, y canonical
     case 6: r = fe_canon(x); break;
     case 7: r = fe_mul_w2(x, fe_w2{y, fe_mul(y, fe{0, 1})}); break;  // two-part constant (w, w 2^64)
+    case 8:
+    case 9:
+    case 10: {
+        // the NTT butterflies' addsub2 forms (V = op - 8: both sums canonical, both lazy, first lazy): inputs (x, y) and
+        // (a, b)[count - 1 - t]; lane t returns output t & 3 of (x + y, x - y, x2 + y2, x2 - y2)
+        const fe x2 = a[count - 1 - t], y2 = b[count - 1 - t];
+        fe o[4];
+        if (op == 8) addsub2_v<0>(x, y, x2, y2, o[0], o[1], o[2], o[3]);
+        else if (op == 9) addsub2_v<1>(x, y, x2, y2, o[0], o[1], o[2], o[3]);
+        else addsub2_v<2>(x, y, x2, y2, o[0], o[1], o[2], o[3]);
+        r = o[t & 3];
+        break;
+    }
     default: r = fe_exp(x, y.lo, y.hi); break;
     }
     out[t] = r;

@@ -535,6 +535,17 @@ int zk_prover_stage_times(zk_prover *p, const char **names, float *ms, int cap, 
     return ZK_OK;
 }
 
+int zk_prover_proof_info(const zk_prover *p, zk_proof_info *out) {
+    if (!p || !out) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    memset(out, 0, sizeof *out);
+    out->schedule = p->last_sched;
+    out->hint_redos = p->hint_redos;
+    for (const auto &h : p->hint_sets) out->hint_sets += h.n != 0 && h.have ? 1u : 0u;
+    out->hinted_sparse = p->sp_hinted;
+    out->derived = p->clk_used ? 1u : 0u;
+    return ZK_OK;
+}
+
 int zk_prover_upload_stats(zk_prover *p, uint64_t *bytes, uint32_t *sparse_cols, uint32_t *narrow8_cols,
                            uint32_t *narrow32_cols) {
     if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
@@ -1143,7 +1154,28 @@ struct TraceSrc {
     const FixedCols *fixed = nullptr;  // with dev: only the dynamic columns are in dev (zk_vm_prove)
     bool hint_ok = true;               // host columns: the sparse hint of the previous proof may be used
     bool no_virtual = false;           // every trace LDE column written (stage dumps read them)
+    const uint8_t *key = nullptr;      // host columns: the program hash the hints are keyed by (with n)
 };
+
+// The hint set of (n, program), or null (prover state: zk_prover::HintSet)
+static zk_prover::HintSet *hint_find(zk_prover *p, size_t n, const uint8_t *key) {
+    if (!key) return nullptr;
+    for (auto &h : p->hint_sets)
+        if (h.n == n && !memcmp(h.key, key, 32)) return &h;
+    return nullptr;
+}
+// ... found or made, evicting the least recently used set
+static zk_prover::HintSet *hint_slot(zk_prover *p, size_t n, const uint8_t *key) {
+    zk_prover::HintSet *h = hint_find(p, n, key);
+    if (h) return h;
+    h = &p->hint_sets[0];
+    for (auto &e : p->hint_sets)
+        if (e.used < h->used) h = &e;
+    *h = zk_prover::HintSet{};
+    h->n = n;
+    memcpy(h->key, key, 32);
+    return h;
+}
 
 // Virtual columns: the first trace column no transition constraint or assertion reads -- the evaluator reads columns
 // 0 .. 12 + 2 lwe_size - 1 <= 21 (enforce_add2 reads 2 lwe_size stack items, lwe_size <= 5; constrains.rs) -- so a
@@ -1207,17 +1239,6 @@ bool zk::narrow_on() {
         return !(e && !strcmp(e, "0"));
     }();
     return on;
-}
-
-// The process-wide default of ZK_SCHED_AUTO provers (zk_prover_set_upload_schedule): ZK_LATENCY_SCHED=0 the throughput
-// schedule always, 1 (unset) the latency schedule for a proof that starts with no other proof in flight on its device,
-// 2 the latency one always
-static int latency_sched() {
-    static const int v = [] {
-        const char *e = getenv("ZK_LATENCY_SCHED");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
 }
 
 // The AIR clock (ZK_CLOCK=0 turns its derivation off)
@@ -1378,16 +1399,17 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
     // last row: nothing goes up but that value), and its narrow ones (8- or 32-bit values before the last row), which
     // go up packed.  Host threads check every hinted value while the other columns go up: a narrow column that does
     // not fit goes up whole, a sparse one that is not sparse voids the proof (prove_impl redoes it without hints).
-    const bool fresh = sp && src.hint_ok && p->sp_hint_n == n;
-    const uint32_t hint = fresh ? p->sp_hint : 0u;
-    const uint32_t nw8 = fresh && narrow_on() ? p->nw8_hint & ~hint : 0u;
-    uint32_t nw32 = fresh && narrow_on() ? p->nw32_hint & ~hint & ~nw8 : 0u;
+    const zk_prover::HintSet *H = sp && src.hint_ok ? hint_find(p, n, src.key) : nullptr;
+    const bool fresh = H && H->have;
+    const uint32_t hint = fresh ? H->sparse : 0u;
+    const uint32_t nw8 = fresh && narrow_on() ? H->nw8 & ~hint : 0u;
+    uint32_t nw32 = fresh && narrow_on() ? H->nw32 & ~hint & ~nw8 : 0u;
     // The AIR clock: constraint 0 (clk' = clk + 1, air/src/constrains.rs) and the assertion clk[0] = 0 force rows
     // 0 .. n-2 of column 0 of any trace the AIR accepts to 0 .. n-2, so its interpolant and LDE are the identity
     // column's (per plan) plus (last - (n - 1)) times e_(n-1)'s: no upload, no transform.  Taken once the previous
     // proof found column 0 narrow (32-bit), checked by host threads while the other columns go up; a column that is
     // not 0 .. n-2 voids the proof, which is redone without hints (and this length is not speculated again).
-    const bool clk = fresh && clock_on() && (nw32 & 1u) && p->clk_off_n != n;
+    const bool clk = fresh && clock_on() && (nw32 & 1u) && !H->clk_off;
     if (clk) nw32 &= ~1u;
     p->clk_used = clk;
     p->clk_bad = false;
@@ -1506,7 +1528,7 @@ static int trace_lde_commit(zk_prover *p, Plan *pl, const TraceSrc &src, size_t 
             if (p->h_pack) (void)hipHostFree(p->h_pack);
             p->h_pack = nullptr;
             p->h_pack_cap = 0;
-            ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocDefault));
+            ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, pack_bytes, hipHostMallocMapped | hipHostMallocCoherent));
             p->h_pack_cap = pack_bytes;
         }
         for (int k = 0; k < np; k++) packed[k].reset((int)(perp * (pb[k + 1] - pb[k])));
@@ -1837,6 +1859,7 @@ static int prove_impl(zk_prover *p, const TraceSrc &src_in, size_t n, const zk_o
                       uint8_t *proof_out, size_t *proof_len, zk_record *rec, const zk_dump *dump) {
     TraceSrc src = src_in;
     if (dump) src.no_virtual = true;  // the stage dumps read every trace LDE column
+    if (src.cols && pub) src.key = &pub->program_hash[0][0];  // hints are per (n, program)
     p->sp_used = false;
     p->sp_hinted = 0;
     p->sp_bad = 0;
@@ -1845,10 +1868,16 @@ static int prove_impl(zk_prover *p, const TraceSrc &src_in, size_t n, const zk_o
     int rc = prove_once(p, src, n, opt, pub, proof_out, proof_len, rec, dump);
     if (!src.cols || !p->sp_used) return rc;
     if (p->sp_bad || p->clk_bad) {
-        if (p->clk_bad) p->clk_off_n = n;
+        // a hint of this (n, program) was refuted: forget its column classes (and stop speculating the clock for it if
+        // that was refuted), prove again from every column
+        zk_prover::HintSet *h = hint_find(p, n, src.key);
+        if (h) {
+            if (p->clk_bad) h->clk_off = true;
+            h->have = false;
+            h->sparse = h->nw8 = h->nw32 = 0;
+        }
+        p->hint_redos++;
         p->clk_used = p->clk_bad = false;
-        p->sp_hint = p->nw8_hint = p->nw32_hint = 0;
-        p->sp_hint_n = 0;
         TraceSrc s2 = src;
         s2.hint_ok = false;
         p->sp_used = false;
@@ -1870,10 +1899,14 @@ static int prove_impl(zk_prover *p, const TraceSrc &src_in, size_t n, const zk_o
             w8 &= ~1u;
             w32 |= 1u;
         }
-        p->sp_hint = found;
-        p->nw8_hint = w8;
-        p->nw32_hint = w32;
-        p->sp_hint_n = n;
+        if (src.key) {
+            zk_prover::HintSet *h = hint_slot(p, n, src.key);
+            h->have = true;
+            h->sparse = found;
+            h->nw8 = w8;
+            h->nw32 = w32;
+            h->used = ++p->hint_stamp;
+        }
     }
     return rc;
 }
@@ -1887,6 +1920,9 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
     // may free those columns as soon as this returns (a completed proof has long finished them).  Kernels of
     // a failed proof may also still be queued on st: the next proof's uploads into d_trace (on the upload stream,
     // ordered only by the previous proof having drained st) must not race them, so both drain here.
+    // proofs in flight on the device: alone, the trace goes up on the latency schedule (trace_lde_commit).  Declared
+    // before the copy guard, so this proof counts as in flight until its uploads and kernels have drained.
+    DeviceBusy busy{p->dev_busy};
     struct CopyGuard {
         zk_prover *p;
         ~CopyGuard() {
@@ -1894,18 +1930,10 @@ static int prove_once(zk_prover *p, const TraceSrc &src, size_t n, const zk_opti
             (void)hipStreamSynchronize(p->st);
         }
     } copy_guard{p};
-    // proofs in flight on the device: alone, the trace goes up on the latency schedule (trace_lde_commit)
-    struct Busy {
-        std::atomic<int> *b;
-        int others;
-        explicit Busy(std::atomic<int> *x) : b(x), others(x->fetch_add(1)) {}
-        ~Busy() { b->fetch_sub(1); }
-    } busy{p->dev_busy};
-    const int sched = p->upload_sched != ZK_SCHED_AUTO ? p->upload_sched
-                      : latency_sched() == 0                ? ZK_SCHED_THROUGHPUT
-                      : latency_sched() == 2                ? ZK_SCHED_LATENCY
-                                                            : ZK_SCHED_AUTO;
+    // the AUTO rule (include/zkvm_gpu.h, zk_proof_info): the latency schedule iff no other proof is in flight here
+    const int sched = p->upload_sched;
     p->lat_sched = sched == ZK_SCHED_LATENCY || (sched == ZK_SCHED_AUTO && busy.others == 0);
+    p->last_sched = src.cols ? (p->lat_sched ? ZK_SCHED_LATENCY : ZK_SCHED_THROUGHPUT) : 0;
     const uint32_t B = opt->blowup, fold = opt->fri_folding;
     const size_t N = n * B;
     ZK_CHECK_HIP(hipSetDevice(p->device));

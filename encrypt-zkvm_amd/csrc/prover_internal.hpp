@@ -126,10 +126,11 @@ struct zk_prover {
     hipStream_t up = nullptr;
     std::mutex *up_mu = nullptr;
     // proofs in flight on this device (process-wide, beside the upload stream), and whether this proof started alone:
-    // then trace_lde_commit takes the latency schedule (upload_sched: zk_prover_set_upload_schedule; AUTO follows
-    // ZK_LATENCY_SCHED: 0 never, 2 always, default when alone)
+    // then trace_lde_commit takes the latency schedule (upload_sched: zk_prover_set_upload_schedule; AUTO: the
+    // latency schedule iff no other proof is in flight on the device)
     std::atomic<int> *dev_busy = nullptr;
     bool lat_sched = false;
+    int last_sched = 0;  // the schedule the last host-column proof ran (zk_prover_proof_info), 0 otherwise
     int upload_sched = ZK_SCHED_AUTO;  // zk_prover_set_upload_schedule
     // ... each group's event gating its kernels on st.  Measured (tools/ubench/upload_probe.hip): an event recorded
     // between the 16 MiB column copies of one stream halves their rate (29.7 vs 55 GB/s), but not between 112 MiB
@@ -188,26 +189,38 @@ struct zk_prover {
     fe_ws *fix_ws = nullptr;      // zk_vm_prove: the W sets of the last-row values of the preprocessed columns
     unsigned *sp_nz = nullptr;    // sparse-column flags of the current trace (SparseCols), W entries + 2W width flags
     fe *sp_last = nullptr;        // ... and the trace's last row
-    // Hints (host-resident traces, prove_impl): the columns the previous proof of the same length found sparse are
-    // taken as sparse from their last row alone and never uploaded; host threads check them during the proof (sp_bad:
-    // the hinted columns that were not sparse; the proof is then redone without hints)
-    uint32_t sp_hint = 0, sp_hinted = 0, sp_bad = 0;
+    // Hints (host-resident traces, prove_impl): the columns the previous proof of the same trace length AND program
+    // (zk_pub_inputs::program_hash: column classes are a property of the program) found sparse are taken as sparse from
+    // their last row alone and never uploaded; host threads check them during the proof (sp_bad: the hinted columns
+    // that were not sparse; the proof is then redone without hints).  Narrow hint: the columns found to hold 8-bit
+    // (nw8) or 32-bit (nw32) values in rows 0 .. n-2 are packed by host threads (which check every value: a column that
+    // does not fit goes up whole instead) and go up as 1 or 4 bytes per element (h_pack, pinned), expanded on the
+    // device.  One HintSet per (n, program), ZK_HINT_SETS of them, least recently used evicted: a server alternating
+    // programs of one length keeps every program's hints instead of voiding each other's proofs (each refuted hint
+    // costs a redone proof: hint_redos).
+    struct HintSet {
+        size_t n = 0;          // 0: an empty slot
+        uint8_t key[32] = {};  // the program hash
+        bool have = false;     // sparse / nw8 / nw32 hold a completed proof's findings
+        uint32_t sparse = 0, nw8 = 0, nw32 = 0;
+        bool clk_off = false;  // this (n, program)'s traces refuted the clock derivation: not speculated again
+        uint64_t used = 0;     // LRU stamp
+    };
+    static constexpr int ZK_HINT_SETS = 8;
+    HintSet hint_sets[ZK_HINT_SETS];
+    uint64_t hint_stamp = 0;
+    uint32_t hint_redos = 0;  // proofs voided by a refuted hint and redone (zk_prover_proof_info)
+    uint32_t sp_hinted = 0, sp_bad = 0;
     bool sp_used = false;  // the last trace_lde_commit ran the detection (its flags are in sp_h)
-    size_t sp_hint_n = 0;
     unsigned *sp_h = nullptr;  // pinned: the detection's flags, [0, W) nonzero, [W, 2W) 8-bit, [2W, 3W) 32-bit
-    // Narrow hint (host-resident traces): columns the previous proof of the same length found to hold 8-bit (nw8) or
-    // 32-bit (nw32) values in rows 0 .. n-2 are packed by host threads (which check every value: a column that does
-    // not fit goes up whole instead) and go up as 1 or 4 bytes per element (h_pack, pinned), expanded on the device
-    uint32_t nw8_hint = 0, nw32_hint = 0;
     uint8_t *h_pack = nullptr;
     size_t h_pack_cap = 0;
     uint64_t up_bytes = 0;                        // zk_prover_upload_stats of the last host-column proof
     uint32_t up_sparse = 0, up_nw8 = 0, up_nw32 = 0;
     // Clock column (host-resident traces, trace_lde_commit): column 0 derived from the AIR's clock instead of
-    // uploaded and transformed (clk_used: the last proof did; clk_bad: the host check refuted it; clk_off_n: a length
-    // whose traces refuted it, not speculated again)
+    // uploaded and transformed (clk_used: the last proof did; clk_bad: the host check refuted it; HintSet::clk_off: a
+    // (length, program) whose traces refuted it, not speculated again)
     bool clk_used = false, clk_bad = false;
-    size_t clk_off_n = 0;
     // Virtual columns of the last host-trace commitment (trace_lde_commit): hinted sparse columns no constraint reads,
     // whose LDE is never written -- the row hashing and the openings form their values from the last row and e_(n-1)'s
     // LDE (virt_lagr) instead
@@ -220,6 +233,7 @@ struct zk_prover {
     bool sh_clock = false;
     size_t sh_hint_n = 0, sh_clock_off_n = 0;
     int sh_hint_g = 0;
+    uint8_t sh_hint_key[32] = {};  // ... for this program (zk_pub_inputs::program_hash)
     // coset-sharded proving (shard.hip), allocated on first use
     fe *sh_buf = nullptr;       // world x ZK_GATHER_CAP opened chunks (all-gathered)
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
@@ -260,6 +274,20 @@ struct zk_prover {
 };
 
 namespace zk {
+
+// One proof in flight on a device (zk_prover::dev_busy, process-wide per device) for the lifetime of the object;
+// `others` = the proofs already in flight when it started.  The single-GPU AUTO upload schedule reads it (prove_once);
+// sharded proofs count themselves on each local prover's device.
+struct DeviceBusy {
+    std::atomic<int> *b;
+    int others;
+    explicit DeviceBusy(std::atomic<int> *x) : b(x), others(x ? x->fetch_add(1) : 0) {}
+    ~DeviceBusy() {
+        if (b) b->fetch_sub(1);
+    }
+    DeviceBusy(const DeviceBusy &) = delete;
+    DeviceBusy &operator=(const DeviceBusy &) = delete;
+};
 
 // Upload gating (trace_lde_commit, shard.hip S2): the host thread waits for upload event ev before it enqueues the
 // kernels that read the group (the next group's copy is already queued).  The compute stream never parks on a

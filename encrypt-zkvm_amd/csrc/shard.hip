@@ -425,7 +425,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             const char *e = getenv("ZK_SHARD_HINTS");
             return !(e && !strcmp(e, "0"));
         }();
-        const bool fresh = hints_on && X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G;
+        // (keyed by length, world and program: column classes are a property of the program)
+        const bool fresh = hints_on && X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G &&
+                           !memcmp(H->sh_hint_key, pub->program_hash, 32);
         const uint32_t S = fresh ? H->sh_sparse : 0u;
         const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
         X.sh_clock = K;
@@ -691,6 +693,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 p->sh_clock = clk_next;
                 p->sh_hint_n = n;
                 p->sh_hint_g = G;
+                memcpy(p->sh_hint_key, pub->program_hash, 32);
             }
         }
     } else if (X.fixed) {
@@ -1362,6 +1365,9 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         return fixed ? prove_fixed(X.P[0], n, opt, pub, fixed, proof_out, proof_len)
                      : prove_single(X.P[0], trace, n, opt, pub, proof_out, proof_len, rec);
     X.fixed = fixed;
+    // every local rank's proof counts as in flight on its device (the single-GPU AUTO upload schedule reads it)
+    std::vector<std::unique_ptr<DeviceBusy>> busy;
+    for (auto *p : X.P) busy.push_back(std::make_unique<DeviceBusy>(p->dev_busy));
     // drop any staged reads an earlier failed proof left behind, and again on every way out of this one
     std::vector<std::unique_ptr<IoScope>> io_scopes;
     for (auto *p : X.P) {

@@ -515,12 +515,9 @@ int zk_vm_prove(zk_prover *p, zk_program *prog, const uint8_t *public_in, size_t
         fx.lagr_lde = f.lagr_lde;
         memcpy(fx.last, last, sizeof fx.last);
         // their share of the trace commitment needs only the last row: queued now, the GPU runs it while the host
-        // runs the stack pass below (one call alone: the pass and this work no longer add up)
-        static const bool prefix_on = [] {  // ZK_VM_PREFIX=0: all of it inside the proof, after the pass
-            const char *e = getenv("ZK_VM_PREFIX");
-            return !(e && !strcmp(e, "0"));
-        }();
-        if (prefix_on && prog->P.trace_len <= p->max_n) ZK_TRY(fixed_prefix(p, prog->P.trace_len, opt->blowup, fx));
+        // runs the stack pass below (one call alone: the pass and this work no longer add up; 11.54-11.61 vs
+        // 13.10-13.21 ms per call, profiles/r05k_vm_latency_ab_prefix.txt -- round 6 folded its switch into this default)
+        if (prog->P.trace_len <= p->max_n) ZK_TRY(fixed_prefix(p, prog->P.trace_len, opt->blowup, fx));
         ZK_TRY(vm_generate(p, prog, in, last, GenMode{false, f.md}, &n, outs, &md));
         if ((int)md != f.md) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the stack depth depends on the inputs");
     } else {

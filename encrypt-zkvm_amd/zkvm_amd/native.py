@@ -33,7 +33,7 @@ EXPORTED = (
     "zk_prover_acquire", "zk_prover_release", "zk_prover_pool_trim", "zk_prover_trace_buffer",
     "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
-    "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_prover_exchange_stats", "zk_prover_upload_stats", "zk_prover_upload_derived", "zk_prover_set_upload_schedule", "zk_vm_trace",
+    "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_prover_exchange_stats", "zk_prover_upload_stats", "zk_prover_upload_derived", "zk_prover_set_upload_schedule", "zk_prover_proof_info", "zk_vm_trace",
     "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_prove_sharded",
     "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error", "zk_vm_trace_device",
     "zk_vm_prove",
@@ -60,6 +60,12 @@ class Options(C.Structure):
 class PubInputs(C.Structure):
     _fields_ = [("program_hash", C.c_uint8 * 32), ("stack_outputs", C.c_uint8 * 256),
                 ("lwe_size", C.c_uint32), ("delta", C.c_uint32)]
+
+
+class ProofInfo(C.Structure):
+    """zk_proof_info (include/zkvm_gpu.h): what the last proof on a prover did."""
+    _fields_ = [("schedule", C.c_int32), ("hint_redos", C.c_uint32), ("hint_sets", C.c_uint32),
+                ("hinted_sparse", C.c_uint32), ("derived", C.c_uint32), ("_pad", C.c_uint32)]
 
 
 class Record(C.Structure):
@@ -182,6 +188,7 @@ def lib():
         L.zk_prover_stage_times.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32, C.POINTER(i32)]
         L.zk_prover_profile.argtypes = [vp, i32]
         L.zk_prover_set_upload_schedule.argtypes = [vp, i32]
+        L.zk_prover_proof_info.argtypes = [vp, C.POINTER(ProofInfo)]
         L.zk_prover_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(i32),
                                              C.POINTER(C.c_double), i32, C.POINTER(i32)]
         L.zk_prover_kernel_ops.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), i32, C.POINTER(i32)]

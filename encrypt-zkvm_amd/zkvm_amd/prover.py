@@ -180,6 +180,17 @@ class GpuProver:
 
     UPLOAD_SCHEDULES = {"auto": 0, "throughput": 1, "latency": 2}
 
+    def proof_info(self) -> dict:
+        """zk_prover_proof_info: the upload schedule the last host-column proof ran ("throughput" / "latency", None after
+        a device-trace proof), the proofs voided by a refuted column hint and redone (cumulative), the (n, program) hint
+        sets held, and the sparse / derived columns the last proof took from its hints."""
+        from .native import ProofInfo
+        info = ProofInfo()
+        check(lib().zk_prover_proof_info(self.handle, C.byref(info)))
+        cols = lambda m: [c for c in range(28) if (m >> c) & 1]  # noqa: E731
+        return {"schedule": {1: "throughput", 2: "latency"}.get(info.schedule), "hint_redos": info.hint_redos,
+                "hint_sets": info.hint_sets, "hinted_sparse": cols(info.hinted_sparse), "derived": cols(info.derived)}
+
     def set_upload_schedule(self, schedule: str):
         """zk_prover_set_upload_schedule: "auto" (latency when no other proof is in flight on the device), "throughput"
         or "latency" -- how a host-resident trace goes up; the proof bytes are the same."""

@@ -259,10 +259,25 @@ int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols);
  * ZK_SCHED_THROUGHPUT: the narrow (packed) columns in two parts through the copy engine between 64-MB column groups.
  * ZK_SCHED_LATENCY: the first two column groups start crossing at once and the packed narrow columns are expanded by a
  * kernel reading the pinned bytes, in small parts, so the first kernels start ~0.2 ms into the call.  Same proof bytes.
- * (No reference counterpart: winterfell's prover has no upload; a tuning knob for servers, ZK_LATENCY_SCHED=0 / 2 in
- * the environment sets the AUTO default process-wide.) */
+ * (No reference counterpart: winterfell's prover has no upload; a tuning knob for servers.) */
 enum { ZK_SCHED_AUTO = 0, ZK_SCHED_THROUGHPUT = 1, ZK_SCHED_LATENCY = 2 };
 int zk_prover_set_upload_schedule(zk_prover *p, int schedule);
+/* What the last proof on this prover did.  schedule: the upload schedule the last host-column proof ran
+ * (ZK_SCHED_THROUGHPUT or ZK_SCHED_LATENCY; 0 after a device-trace proof).  The AUTO rule, as a contract: a proof takes
+ * the latency schedule iff no other proof -- single-GPU or a rank of a sharded proof -- is in flight on its device
+ * when it starts (a proof counts as in flight from entry until its uploads and kernels have drained).
+ * hint_redos: proofs this prover voided and redid because a column hint was refuted (cumulative).  hint_sets: the
+ * (trace length, program hash) column-hint sets it holds (at most 8, least recently used evicted).  hinted_sparse /
+ * derived: the sparse columns (bit c) and derived columns (bit 0, the clock) the last proof took from its hints. */
+typedef struct {
+    int32_t schedule;
+    uint32_t hint_redos;
+    uint32_t hint_sets;
+    uint32_t hinted_sparse;
+    uint32_t derived;
+    uint32_t _pad;
+} zk_proof_info;
+int zk_prover_proof_info(const zk_prover *p, zk_proof_info *out);
 
 /* ---- verifier: winterfell::verify::<ProcessorAir, Blake3_256, DefaultRandomCoin> (vm/src/lib.rs:93-98)
  * for the proof layout above, on the host (no GPU needed).  min_security: conjectured bits required

@@ -77,6 +77,45 @@ def test_lazy_field_forms(gpu):
     assert run(6, a, b) == [x % P for x in a]
 
 
+def test_butterfly_addsub2_forms(gpu):
+    """The NTT butterflies' two sums and two differences in one interleaved asm block (f128.hpp addsub2_v,
+    addsub_asm.hpp from tools/gen_addsub_asm.py), all three forms, bit for bit against Python integers: a + b
+    canonical, or lazy (any first operand < 2^128: a + b, minus 2^128 - C on overflow), and a - b (+ p on a borrow).
+    Lane t returns output t % 4 of (x + y, x - y, x2 + y2, x2 - y2), x2 / y2 the inputs of the mirrored lane."""
+    rnd = random.Random(12)
+    C128 = 2**128 - P
+    canon = [0, 1, P - 1, P - 2, 2**64 - 1, 2**64, 2**127, P - 2**64, 45 * 2**40, 2**128 - 2**96 - 1]
+    anyv = canon + [2**128 - 1, 2**128 - 2, P, P + 1, 2**128 - 45 * 2**40]
+
+    def lazy(x, y):
+        s = x + y
+        return s if s < 2**128 else s - 2**128 + C128
+
+    def sub(x, y):
+        return x - y if x >= y else x - y + P
+
+    for op, lz1, lz2 in ((8, False, False), (9, True, True), (10, True, False)):
+        pool1, pool2 = (anyv if lz1 else canon), (anyv if lz2 else canon)
+        m = 4096
+        a = [pool1[i % len(pool1)] if i < 400 else rnd.choice([rnd.randrange(P), rnd.choice(pool1)]) for i in range(m)]
+        b = [canon[(i // len(pool1)) % len(canon)] if i < 400 else rnd.choice([rnd.randrange(P), P - 1]) for i in range(m)]
+        # the mirrored lanes feed the second pair: lanes whose mirror would hand a lazy value to a canonical-only slot
+        # take canonical first operands
+        if not lz2:
+            a[m // 2:] = [x % P for x in a[m // 2:]]
+            if not lz1:
+                a = [x % P for x in a]
+        out = C.create_string_buffer(16 * m)
+        native.check(native.lib().zk_diag_field_op(0, op, elems_bytes(a), elems_bytes(b), out, m))
+        got = bytes_elems(out.raw)
+        for t in range(m):
+            x, y, x2, y2 = a[t], b[t], a[m - 1 - t], b[m - 1 - t]
+            if (not lz1 and x >= P) or (not lz2 and x2 >= P):
+                continue  # outside that form's contract
+            want = [lazy(x, y) if lz1 else (x + y) % P, sub(x, y), lazy(x2, y2) if lz2 else (x2 + y2) % P, sub(x2, y2)]
+            assert got[t] == want[t & 3], (op, t, x, y, x2, y2, got[t], want[t & 3])
+
+
 @pytest.mark.parametrize("k", [1, 4, 7, 8, 28])
 def test_blake3_rows(gpu, oracle, k):
     rnd = random.Random(k)
