@@ -1,4 +1,6 @@
-// comm_rccl.cpp -- zk_comm over RCCL (xGMI within a node): one process per GPU.
+// comm_rccl.cpp -- zk_comm over RCCL (xGMI within a node): one process per GPU.  The collectives run on the stream
+// shard.hip hands in (the prover's exchange stream, ordered after its compute stream by an event), so they overlap
+// the compute that does not wait for them.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -17,16 +19,16 @@ struct RcclComm : zk_comm {
     }
     bool loopback() const override { return false; }
     int all_to_all(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
         if (P.size() != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "an RCCL communicator drives exactly one local rank");
-        ncclResult_t r = ncclAllToAll(send[0], recv[0], bytes, ncclUint8, comm, P[0]->st);
+        ncclResult_t r = ncclAllToAll(send[0], recv[0], bytes, ncclUint8, comm, is);
         if (r != ncclSuccess) ZK_FAIL(ZK_ERR_DEVICE, std::string("ncclAllToAll: ") + ncclGetErrorString(r));
         return ZK_OK;
     }
     int all_gather(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
         if (P.size() != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "an RCCL communicator drives exactly one local rank");
-        ncclResult_t r = ncclAllGather(send[0], recv[0], bytes, ncclUint8, comm, P[0]->st);
+        ncclResult_t r = ncclAllGather(send[0], recv[0], bytes, ncclUint8, comm, is);
         if (r != ncclSuccess) ZK_FAIL(ZK_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
         return ZK_OK;
     }

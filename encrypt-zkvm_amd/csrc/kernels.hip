@@ -1079,11 +1079,11 @@ void hash_rows_blocks(hipStream_t st, const fe *base, int ncols, int log_n, int 
 // last entry; with wstride > 0 also the width flags of SparseCols.  One pass over the columns (16 B per element read);
 // nz must be zeroed first.
 __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n, int c0, unsigned *nz, fe *last,
-                                                       int wstride, int idoff) {
+                                                       int wstride, int idoff, size_t blk0) {
     constexpr int PER = 16;  // independent loads per thread (unrolled: all in flight at once)
     const int c = blockIdx.y;
     const fe *col = trace + (size_t)(c0 + c) * n;
-    const size_t base = blockIdx.x * (size_t)(256 * PER) + threadIdx.x;
+    const size_t base = (blk0 + blockIdx.x) * (size_t)(256 * PER) + threadIdx.x;
     uint64_t any = 0, w8 = 0, w32 = 0, nid = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
@@ -1115,10 +1115,17 @@ __global__ void __launch_bounds__(256) k_sparse_detect(const fe *trace, size_t n
 }
 
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp) {
-    ZK_PROF(st, "sparse_detect", 16.0 * n * nc,
-            hipLaunchKernelGGL(k_sparse_detect, dim3(cdiv(n, 256 * 16), nc), dim3(256), 0, st, trace, n, c0,
+    sparse_detect_rows(st, trace, n, c0, nc, sp, 0, n);
+}
+// rows [r0, r1) only (r0 a multiple of 4096; the last row's values are read by every call): a sharded rank's share of
+// the detection, whose flags the ranks all-gather and OR (shard.hip)
+void sparse_detect_rows(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp, size_t r0,
+                        size_t r1) {
+    constexpr size_t BR = 256 * 16;
+    ZK_PROF(st, "sparse_detect", 16.0 * (double)(r1 - r0) * nc,
+            hipLaunchKernelGGL(k_sparse_detect, dim3(cdiv(r1 - r0, BR), nc), dim3(256), 0, st, trace, n, c0,
                                const_cast<unsigned *>(sp.nz), const_cast<fe *>(sp.last), sp.wstride,
-                               sp.id_poly ? sp.idoff : 0));
+                               sp.id_poly ? sp.idoff : 0, r0 / BR));
 }
 
 // Packed narrow columns -> field elements: grid (row blocks, column), 4 rows per thread

@@ -412,6 +412,11 @@ void zk_prover_destroy(zk_prover *p) {
     upload_drain(p);
     for (auto &e : p->stage_pool) (void)hipEventDestroy(e);
     for (auto &e : p->xchg_pool) (void)hipEventDestroy(e);
+    if (p->cst) {
+        (void)hipStreamSynchronize(p->cst);
+        (void)hipStreamDestroy(p->cst);
+    }
+    if (p->ev_ready) (void)hipEventDestroy(p->ev_ready);
     for (auto &e : p->ev_up)
         if (e) (void)hipEventDestroy(e);
     if (p->ev_vm) (void)hipEventDestroy(p->ev_vm);
@@ -503,6 +508,8 @@ void zk::stage_begin(zk_prover *p) {
     p->stage_names.clear();
     p->stage_done = false;
     p->xchg.clear();
+    p->xchg_next = 0;
+    p->sched.clear();
 }
 void zk::stage_mark(zk_prover *p, const char *name) {
     const size_t i = p->stage_names.size();
@@ -562,26 +569,29 @@ int zk_prover_upload_derived(zk_prover *p, uint32_t *derived_cols) {
     return ZK_OK;
 }
 
-int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
-                             int *count) {
+int zk_prover_exchange_stats_ex(zk_prover *p, const char **names, float *ms, float *exposed_ms, double *bytes,
+                                int *calls, int cap, int *count) {
     if (!p) ZK_FAIL(ZK_ERR_INVALID_ARG, "null prover");
     std::vector<const char *> nm;
-    std::vector<float> t;
+    std::vector<float> t, w;
     std::vector<double> b;
     std::vector<int> c;
     if (p->stage_done)
         for (const auto &r : p->xchg) {
-            float x = 0;
+            float x = 0, y = 0;
             (void)hipEventElapsedTime(&x, p->xchg_pool[r.ev], p->xchg_pool[r.ev + 1]);
+            if (r.waited) (void)hipEventElapsedTime(&y, p->xchg_pool[r.ev + 2], p->xchg_pool[r.ev + 3]);
             size_t i = 0;
             while (i < nm.size() && strcmp(nm[i], r.name)) i++;
             if (i == nm.size()) {
                 nm.push_back(r.name);
                 t.push_back(0);
+                w.push_back(0);
                 b.push_back(0);
                 c.push_back(0);
             }
             t[i] += x;
+            w[i] += y;
             b[i] += r.bytes;
             c[i] += 1;
         }
@@ -589,10 +599,51 @@ int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double
     for (int i = 0; i < k && i < cap; i++) {
         if (names) names[i] = nm[i];
         if (ms) ms[i] = t[i];
+        if (exposed_ms) exposed_ms[i] = w[i];
         if (bytes) bytes[i] = b[i];
         if (calls) calls[i] = c[i];
     }
     if (count) *count = k;
+    return ZK_OK;
+}
+
+int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
+                             int *count) {
+    return zk_prover_exchange_stats_ex(p, names, ms, nullptr, bytes, calls, cap, count);
+}
+
+int zk_prover_shard_schedule(zk_prover *p, char *buf, size_t cap, size_t *len) {
+    if (!p || !len) ZK_FAIL(ZK_ERR_INVALID_ARG, "null argument");
+    std::string js = "{\"world\": " + std::to_string(p->sched_world) +
+                     ", \"measure\": " + (p->sched_measure ? "true" : "false") + ", \"entries\": [";
+    char tmp[256];
+    auto el = [&](size_t a, size_t b) {
+        float x = 0;
+        (void)hipEventElapsedTime(&x, p->xchg_pool[a], p->xchg_pool[b]);
+        return x;
+    };
+    if (p->stage_done)
+        for (size_t i = 0; i < p->sched.size(); i++) {
+            const auto &e = p->sched[i];
+            // the compute segment before this entry
+            const float seg = i ? el(p->sched[i - 1].post, e.pre) : 0.f;
+            snprintf(tmp, sizeof tmp, "%s{\"seg_ms\": %.5f, \"lead\": %s}", i ? ", " : "", seg,
+                     e.lead ? "true" : "false");
+            js += tmp;
+            if (e.kind == 'S' || e.kind == 'W') {
+                const auto &r = p->xchg[e.x];
+                if (e.kind == 'S')
+                    snprintf(tmp, sizeof tmp, ", {\"start\": %d, \"name\": \"%s\", \"op\": \"%s\", \"bytes\": %.0f, "
+                             "\"ms\": %.5f}", e.x, r.name, r.op ? "ag" : "a2a", r.bytes, el(r.ev, r.ev + 1));
+                else
+                    snprintf(tmp, sizeof tmp, ", {\"wait\": %d, \"exposed_ms\": %.5f}", e.x, el(e.pre, e.post));
+                js += tmp;
+            }
+        }
+    js += "]}";
+    *len = js.size() + 1;
+    if (!buf || cap < js.size() + 1) ZK_FAIL(ZK_ERR_BUFFER_TOO_SMALL, "schedule buffer too small");
+    memcpy(buf, js.c_str(), js.size() + 1);
     return ZK_OK;
 }
 

@@ -254,15 +254,35 @@ struct zk_prover {
     std::vector<const char *> stage_names;  // stage_names[i] ends at event stage_pool[i]
     bool stage_done = false;                // the last proof completed: its events may be read
     std::vector<std::pair<const char *, float>> stage_ms;
-    // exchanges of the last sharded proof (shard.hip xchg): name, bytes this rank received from the other ranks,
-    // and the events bracketing the collective on the stream it ran on (pooled like the stage events)
+    // exchanges of the last sharded proof (shard.hip xchg_start / xchg_wait): name, collective, bytes this rank
+    // received from the other ranks, and the events bracketing the collective on the stream it ran on (ev, ev + 1)
+    // and the compute stream's wait for it (ev + 2, ev + 3: the exposed time), pooled like the stage events
     struct XchgRec {
         const char *name;
         double bytes;
-        size_t ev;  // xchg_pool[ev] before, xchg_pool[ev + 1] after
+        size_t ev;
+        int op;       // 0 all-to-all, 1 all-gather
+        bool waited;  // the compute streams have waited for it (xchg_wait)
     };
     std::vector<hipEvent_t> xchg_pool;
+    size_t xchg_next = 0;  // next free event of the pool (this proof)
     std::vector<XchgRec> xchg;
+    // the sharded proof's schedule on local rank 0 (zk_prover_shard_schedule: the dependency order the library issued,
+    // for tools/shard_model.py): entries in program order -- kind 'S' an exchange started, 'W' the compute stream
+    // waits for one, 'K' a segment boundary -- each with the events recorded on the compute stream just before (pre)
+    // and after (post) it; the compute segment before an entry spans [post of the previous entry, pre of this one],
+    // and `lead` marks segments only the lead rank (local rank 0 of each process) runs
+    struct SchedEnt {
+        char kind;
+        int x;  // exchange index (S, W)
+        size_t pre, post;
+        bool lead;  // the segment ENDING at this entry ran on the lead rank only
+    };
+    std::vector<SchedEnt> sched;
+    int sched_world = 0;
+    bool sched_measure = false;  // recorded in the serialised measurement mode (zk_comm_set_measure)
+    hipStream_t cst = nullptr;     // sharded proofs: the exchanges' stream (created on first use)
+    hipEvent_t ev_ready = nullptr;  // ... and the event that orders an exchange after this rank's compute stream
     // kernel stats (names / totals of the last profile)
     std::vector<std::string> kstat_names;
     std::vector<float> kstat_ms;

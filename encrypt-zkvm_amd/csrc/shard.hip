@@ -37,63 +37,59 @@ namespace {
 static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------- loopback communicator
+// Every rank in this process: the collective is device-to-device copies, all of them on the issue stream (ordered
+// after every rank's compute stream by xchg_start), so its completion covers every rank's reads and writes.
 struct LoopbackComm : zk_comm {
     bool loopback() const override { return true; }
-    static int sync(const std::vector<zk_prover *> &P) {
-        for (auto *p : P) ZK_CHECK_HIP(hipStreamSynchronize(p->st));
-        return ZK_OK;
-    }
     int all_to_all(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
         if ((int)P.size() != world) ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator drives every rank");
-        ZK_TRY(sync(P));
         for (int d = 0; d < world; d++)
             for (int s = 0; s < world; s++)
                 ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, (const uint8_t *)send[s] + d * bytes, bytes,
-                                            hipMemcpyDefault, P[d]->st));
-        return sync(P);
+                                            hipMemcpyDeviceToDevice, is));
+        return ZK_OK;
     }
     int all_gather(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
         if ((int)P.size() != world) ZK_FAIL(ZK_ERR_INVALID_ARG, "a loopback communicator drives every rank");
-        ZK_TRY(sync(P));
         for (int d = 0; d < world; d++)
             for (int s = 0; s < world; s++)
                 if ((uint8_t *)recv[d] + s * bytes != send[s])  // in place: a rank's own chunk is already there
-                    ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, send[s], bytes, hipMemcpyDefault, P[d]->st));
-        return sync(P);
+                    ZK_CHECK_HIP(hipMemcpyAsync((uint8_t *)recv[d] + s * bytes, send[s], bytes, hipMemcpyDeviceToDevice, is));
+        return ZK_OK;
     }
 };
 
 // ---------------------------------------------------------------- caller-transport communicator
 // One rank per process, exchanges through a caller callback over host memory (MPI, gloo, TCP across nodes).  The
-// staging is synchronous: device chunk -> host, callback, host -> device, in stream order of this rank's prover.
+// staging is synchronous on the host: device chunk -> host on the issue stream, callback, host -> device.
 struct HostComm : zk_comm {
     zk_exchange_fn fn = nullptr;
     void *ctx = nullptr;
     std::vector<uint8_t> sbuf, rbuf;
     bool loopback() const override { return false; }
-    int run(const std::vector<zk_prover *> &P, int op, const void *send, size_t sbytes, void *recv, size_t bytes) {
+    int run(const std::vector<zk_prover *> &P, int op, const void *send, size_t sbytes, void *recv, size_t bytes,
+            hipStream_t is) {
         if (P.size() != 1) ZK_FAIL(ZK_ERR_INVALID_ARG, "a host-exchange communicator drives exactly one local rank");
-        zk_prover *p = P[0];
         const size_t rbytes = bytes * (size_t)world;
         sbuf.resize(std::max<size_t>(sbytes, 1));
         rbuf.resize(std::max<size_t>(rbytes, 1));
-        if (sbytes) ZK_CHECK_HIP(hipMemcpyAsync(sbuf.data(), send, sbytes, hipMemcpyDeviceToHost, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));
+        if (sbytes) ZK_CHECK_HIP(hipMemcpyAsync(sbuf.data(), send, sbytes, hipMemcpyDeviceToHost, is));
+        ZK_CHECK_HIP(hipStreamSynchronize(is));
         const int rc = fn(ctx, op, sbuf.data(), rbuf.data(), bytes);
         if (rc != 0) ZK_FAIL(ZK_ERR_DEVICE, "exchange callback failed (" + std::to_string(rc) + ")");
-        if (rbytes) ZK_CHECK_HIP(hipMemcpyAsync(recv, rbuf.data(), rbytes, hipMemcpyHostToDevice, p->st));
-        ZK_CHECK_HIP(hipStreamSynchronize(p->st));  // rbuf is reused by the next exchange
+        if (rbytes) ZK_CHECK_HIP(hipMemcpyAsync(recv, rbuf.data(), rbytes, hipMemcpyHostToDevice, is));
+        ZK_CHECK_HIP(hipStreamSynchronize(is));  // rbuf is reused by the next exchange
         return ZK_OK;
     }
     int all_to_all(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
-        return run(P, ZK_XCHG_ALL_TO_ALL, send.at(0), bytes * (size_t)world, recv.at(0), bytes);
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
+        return run(P, ZK_XCHG_ALL_TO_ALL, send.at(0), bytes * (size_t)world, recv.at(0), bytes, is);
     }
     int all_gather(const std::vector<zk_prover *> &P, const std::vector<const void *> &send,
-                   const std::vector<void *> &recv, size_t bytes) override {
-        return run(P, ZK_XCHG_ALL_GATHER, send.at(0), bytes, recv.at(0), bytes);
+                   const std::vector<void *> &recv, size_t bytes, hipStream_t is) override {
+        return run(P, ZK_XCHG_ALL_GATHER, send.at(0), bytes, recv.at(0), bytes, is);
     }
 };
 
@@ -103,36 +99,45 @@ __device__ __forceinline__ void st_digest(uint8_t *dst, const uint32_t h[8]) {
     d[0] = make_uint4(h[0], h[1], h[2], h[3]);
     d[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
-// all-to-all slot of local coset j, position q when rank d receives positions [d*mg, (d+1)*mg)
-__device__ __forceinline__ size_t a2a_slot(size_t j, size_t q, int Bl, int log_mg) {
-    return ((((q >> log_mg) * Bl) + j) << log_mg) + (q & (((size_t)1 << log_mg) - 1));
+// The leaf digests of a distributed tree go out in K pieces (dist_commit), so piece k's all-to-all runs while piece
+// k + 1 is hashed.  Rank d receives positions [d mg, (d+1) mg) of every coset; piece k covers positions
+// d mg + k mgK + q'' (q'' < mgK = mg / K) for every d.  Thread t of a piece -> (local coset j, destination d, q''), q''
+// fastest (coalesced column reads); its digest goes to the piece's slot [d][j][q''] (Bl mgK digests per destination).
+struct Piece {
+    size_t j, d, q, slot;
+};
+__device__ __forceinline__ Piece piece_of(size_t t, int log_G, int log_mg, int log_K, int k, int Bl) {
+    const int log_mgK = log_mg - log_K;
+    const size_t qq = t & (((size_t)1 << log_mgK) - 1), rest = t >> log_mgK;
+    const size_t d = rest & (((size_t)1 << log_G) - 1), j = rest >> log_G;
+    return {j, d, (d << log_mg) + ((size_t)k << log_mgK) + qq, ((d * Bl + j) << log_mgK) + qq};
 }
 
-// leaf digests of the local LDE rows (column c, local coset j at base[(c*Bl + j)*n + q]), in all-to-all order
+// leaf digests of the local LDE rows (column c, local coset j at base[(c*Bl + j)*n + q]): piece k of K, all-to-all order
 __global__ void __launch_bounds__(256) k_sh_hash_rows(const fe *base, int ncols, int log_n, int Bl, int log_mg,
-                                                      uint8_t *send) {
+                                                      int log_K, int k, uint8_t *send) {
     const size_t n = (size_t)1 << log_n;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << log_n)) return;
-    const size_t j = t >> log_n, q = t & (n - 1);
-    const fe *p = base + j * n + q;
+    if (t >= ((size_t)Bl << (log_n - log_K))) return;
+    const Piece pc = piece_of(t, log_n - log_mg, log_mg, log_K, k, Bl);
+    const fe *p = base + pc.j * n + pc.q;
     const size_t cs = (size_t)Bl * n;
     uint32_t h[8];
     b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
-    st_digest(send + 32 * a2a_slot(j, q, Bl, log_mg), h);
+    st_digest(send + 32 * pc.slot, h);
 }
 
-// FRI layer-0 leaves of the local cosets: row r' = r + 8*q0 holds deep[j][q0 + k*m], m = n / fold
+// FRI layer-0 leaves of the local cosets: row r' = r + 8*q0 holds deep[j][q0 + k*m], m = n / fold (piece kp of K)
 __global__ void __launch_bounds__(256) k_sh_hash_fri0(const fe *deep, int log_n, int Bl, int fold, int log_m,
-                                                      int log_mg, uint8_t *send) {
+                                                      int log_mg, int log_K, int kp, uint8_t *send) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << log_m)) return;
-    const size_t j = t >> log_m, q0 = t & (m - 1);
-    const fe *p = deep + j * n + q0;
+    if (t >= ((size_t)Bl << (log_m - log_K))) return;
+    const Piece pc = piece_of(t, log_m - log_mg, log_mg, log_K, kp, Bl);
+    const fe *p = deep + pc.j * n + pc.q;
     uint32_t h[8];
     b3::hash_elements(fold, [&](int k) { return p[(size_t)k << log_m]; }, h);
-    st_digest(send + 32 * a2a_slot(j, q0, Bl, log_mg), h);
+    st_digest(send + 32 * pc.slot, h);
 }
 
 // received chunks [s][j][q'] (source chunk s at item s * src_stride) -> natural order of this rank's
@@ -181,15 +186,15 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
 
 // ---- FieldExtension::Quadratic versions: E buffers are planar with plane stride Bl*n (DEEP) / Bl*m (fold)
 __global__ void __launch_bounds__(256) k_sh_hash_fri0_ext(const fe *deep, int log_n, int Bl, int fold, int log_m,
-                                                          int log_mg, uint8_t *send) {
-    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n;
+                                                          int log_mg, int log_K, int kp, uint8_t *send) {
+    const size_t n = (size_t)1 << log_n, cs = (size_t)Bl * n;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << log_m)) return;
-    const size_t j = t >> log_m, q0 = t & (m - 1);
-    const fe *p = deep + j * n + q0;
+    if (t >= ((size_t)Bl << (log_m - log_K))) return;
+    const Piece pc = piece_of(t, log_m - log_mg, log_mg, log_K, kp, Bl);
+    const fe *p = deep + pc.j * n + pc.q;
     uint32_t h[8];
     b3::hash_elements(2 * fold, [&](int e) { return p[(size_t)(e & 1) * cs + ((size_t)(e >> 1) << log_m)]; }, h);
-    st_digest(send + 32 * a2a_slot(j, q0, Bl, log_mg), h);
+    st_digest(send + 32 * pc.slot, h);
 }
 
 __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int G, int fold,
@@ -273,33 +278,121 @@ struct Ctx {
     // ZK_SH_REDO, and prove_sharded_entry proves again without hints)
     bool hint_ok = true, sh_clock = false;
     uint32_t sh_refuted = 0;
+    bool lead_seg = false;  // the schedule segment being enqueued runs on the lead rank only (lead_segment)
 };
 constexpr int ZK_SH_REDO = 1000;  // (internal) a refuted column hint voided the proof on every rank
 
 
-// One collective of the proof, timed: events on local rank 0's stream before and after it (the time includes any
-// wait for slower ranks), and the bytes this rank receives from the others -- zk_prover_exchange_stats reports them
-// per name, so a multi-GPU run measures its own link rate.
+// ---------------------------------------------------------------- exchanges, overlapped with compute (round 6)
+// xchg_start issues a collective on the exchange stream of local rank 0 (its own stream per process: RCCL, host
+// transport; every rank's copies for the loopback), ordered after everything already enqueued on every local rank's
+// compute stream (an event per rank), and records its completion; xchg_wait makes every local compute stream wait
+// for that completion -- a device-side wait, enqueued after the completion was recorded, so it never parks a
+// queue on an event not yet recorded.  Between the two the compute streams run whatever does not read the received
+// data or write the sent data (the callers keep to that).  xchg = start + wait.  Timing: events around the collective
+// on its stream (total) and around the wait on rank 0's compute stream (exposed), and the schedule log
+// (zk_prover_shard_schedule) of every start, wait and segment boundary.
+// Measurement mode (zk_comm_set_measure, loopback): every rank's compute and the copies share rank 0's stream.
 enum XOp { A2A, AG };
-int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd, const std::vector<void *> &rcv,
-         size_t bytes) {
-    zk_prover *p = X.P[0];
-    const size_t e = p->xchg.size() * 2;
-    while (p->xchg_pool.size() < e + 2) {
+struct XH {
+    int idx = -1;
+};
+static int pool_events(zk_prover *p, size_t k, size_t *first) {
+    while (p->xchg_pool.size() < p->xchg_next + k) {
         hipEvent_t ev;
         ZK_CHECK_HIP(hipEventCreate(&ev));
         p->xchg_pool.push_back(ev);
     }
-    ZK_CHECK_HIP(hipSetDevice(p->device));
-    ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e], p->st));
-    ZK_TRY(op == A2A ? X.comm->all_to_all(X.P, snd, rcv, bytes) : X.comm->all_gather(X.P, snd, rcv, bytes));
-    ZK_CHECK_HIP(hipSetDevice(p->device));
-    ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e + 1], p->st));
-    p->xchg.push_back({name, (double)bytes * (X.G - 1), e});
+    *first = p->xchg_next;
+    p->xchg_next += k;
     return ZK_OK;
 }
+static int exchange_stream(zk_prover *p, hipStream_t *out) {
+    if (!p->cst) ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->cst, hipStreamNonBlocking));
+    if (!p->ev_ready) ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_ready, hipEventDisableTiming));
+    *out = p->cst;
+    return ZK_OK;
+}
+// a schedule entry on local rank 0's compute stream: kind 'S' / 'W' (exchange x) or 'K' (segment boundary);
+// `lead`: the segment ending here ran on the lead rank only
+static int sched_entry(Ctx &X, char kind, int x, bool post_now = true) {
+    zk_prover *p = X.P[0];
+    size_t e;
+    ZK_TRY(pool_events(p, 2, &e));
+    ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e], p->st));
+    if (post_now) ZK_CHECK_HIP(hipEventRecord(p->xchg_pool[e + 1], p->st));
+    p->sched.push_back({kind, x, e, e + 1, X.lead_seg});
+    X.lead_seg = false;
+    return ZK_OK;
+}
+// the segment starting here runs on the lead rank only (until the next entry)
+static int lead_segment(Ctx &X) {
+    ZK_TRY(sched_entry(X, 'K', -1));
+    X.lead_seg = true;
+    return ZK_OK;
+}
+int xchg_start(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd, const std::vector<void *> &rcv,
+               size_t bytes, XH *h) {
+    zk_prover *p0 = X.P[0];
+    ZK_CHECK_HIP(hipSetDevice(p0->device));
+    size_t e;
+    ZK_TRY(pool_events(p0, 4, &e));
+    const int x = (int)p0->xchg.size();
+    p0->xchg.push_back({name, (double)bytes * (X.G - 1), e, op == A2A ? 0 : 1, false});
+    hipStream_t is;
+    if (X.comm->measure) {
+        is = p0->st;  // every rank's stream is this one (prove_sharded_entry): program order, no overlap
+        ZK_TRY(sched_entry(X, 'S', x, false));
+    } else {
+        ZK_TRY(exchange_stream(p0, &is));
+        ZK_TRY(sched_entry(X, 'S', x));
+        for (zk_prover *p : X.P) {
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            if (!p->ev_ready) ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_ready, hipEventDisableTiming));
+            ZK_CHECK_HIP(hipEventRecord(p->ev_ready, p->st));
+            ZK_CHECK_HIP(hipStreamWaitEvent(is, p->ev_ready, 0));  // (captured now: the event may be recorded again)
+        }
+        ZK_CHECK_HIP(hipSetDevice(p0->device));
+    }
+    ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[e], is));
+    ZK_TRY(op == A2A ? X.comm->all_to_all(X.P, snd, rcv, bytes, is) : X.comm->all_gather(X.P, snd, rcv, bytes, is));
+    ZK_CHECK_HIP(hipSetDevice(p0->device));
+    ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[e + 1], is));
+    if (X.comm->measure) ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[p0->sched.back().post], p0->st));
+    h->idx = x;
+    return ZK_OK;
+}
+int xchg_wait(Ctx &X, XH &h) {
+    if (h.idx < 0) return ZK_OK;
+    zk_prover *p0 = X.P[0];
+    auto &r = p0->xchg[h.idx];
+    const int x = h.idx;
+    h.idx = -1;
+    if (r.waited) return ZK_OK;
+    r.waited = true;
+    ZK_CHECK_HIP(hipSetDevice(p0->device));
+    ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[r.ev + 2], p0->st));
+    ZK_TRY(sched_entry(X, 'W', x, false));
+    if (!X.comm->measure)
+        for (zk_prover *p : X.P) {
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p0->xchg_pool[r.ev + 1], 0));
+        }
+    ZK_CHECK_HIP(hipSetDevice(p0->device));
+    ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[r.ev + 3], p0->st));
+    ZK_CHECK_HIP(hipEventRecord(p0->xchg_pool[p0->sched.back().post], p0->st));
+    return ZK_OK;
+}
+int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd, const std::vector<void *> &rcv,
+         size_t bytes) {
+    XH h;
+    ZK_TRY(xchg_start(X, name, op, snd, rcv, bytes, &h));
+    return xchg_wait(X, h);
+}
 
-// leaves (hash kernel writes all-to-all order into a2a_send), all-to-all, permute, subtree, roots
+// leaves (the hash kernel writes all-to-all order into the scratch), all-to-all, permute, subtree, roots.  The leaves go
+// out in K pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed; the permutes follow
+// the pieces' arrival.  hash(l, send, log_mg, log_K, k) launches piece k of local rank l.
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
                 const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes, const char *digests_name,
@@ -312,22 +405,36 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     T.nodes = nodes;
     const size_t mg = T.Mr / 8;  // positions per destination rank per coset
     const int log_mg = ilog2(mg);
+    const int log_K = mg >= 4 * 256 ? 2 : 0, K = 1 << log_K;  // pieces of at least 256 positions per coset
+    const int log_mgK = log_mg - log_K;
+    const size_t piece = 32 * (size_t)X.G * X.Bl << log_mgK;  // bytes of one piece (all destinations)
+    std::vector<XH> h(K);
     std::vector<const void *> snd(nl);
     std::vector<void *> rcv(nl);
-    for (int l = 0; l < nl; l++) {
-        ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
-        hash(l, scratch[l], log_mg);
-        snd[l] = scratch[l];
-        rcv[l] = scratch[l] + 32 * T.Mr;
+    for (int k = 0; k < K; k++) {
+        for (int l = 0; l < nl; l++) {
+            ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
+            hash(l, scratch[l] + k * piece, log_mg, log_K, k);
+            snd[l] = scratch[l] + k * piece;
+            rcv[l] = scratch[l] + 32 * T.Mr + k * piece;
+        }
+        ZK_TRY(xchg_start(X, digests_name, A2A, snd, rcv, (32 * (size_t)X.Bl) << log_mgK, &h[k]));
     }
-    ZK_TRY(xchg(X, digests_name, A2A, snd, rcv, 32 * (size_t)X.Bl * mg));
+    for (int k = 0; k < K; k++) {
+        ZK_TRY(xchg_wait(X, h[k]));
+        for (int l = 0; l < nl; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr / K, 256)), dim3(256), 0, p->st,
+                               (const uint8_t *)scratch[l] + 32 * T.Mr + k * piece, X.G, X.Bl, log_mgK, 32,
+                               (size_t)X.Bl << log_mgK, leaves[l] + (32 * (size_t)8 << log_mgK) * k);
+        }
+    }
     std::vector<const void *> rs(nl);
     std::vector<void *> rr(nl);
     for (int l = 0; l < nl; l++) {
         zk_prover *p = X.P[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr, 256)), dim3(256), 0, p->st, (const uint8_t *)rcv[l], X.G, X.Bl,
-                           log_mg, 32, (size_t)X.Bl << log_mg, leaves[l]);
         merkle_tree(p->st, leaves[l], T.Mr, nodes[l]);
         rs[l] = T.Mr >= 2 ? nodes[l] + 32 : leaves[l];
         rr[l] = p->sh_roots;
@@ -375,15 +482,21 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     stage_mark(P0, "start");
     Coin coin = seed_coin(n, opt, pub);
 
-    // S2: the trace polynomials on every rank, then the local coset LDE and the distributed commitment.
-    //  * host trace: split by column, round robin -- in round k rank g uploads (copy stream) and interpolates column
-    //    c = g + G k, and an in-place all-gather fills columns [G k, G k + G) on every rank (p->polys holds
-    //    8 ceil(W / 8) columns; a column past W is padding), after which every rank extends those columns over its
-    //    cosets.  Each rank moves 1/G of the trace over its PCIe link instead of all of it, and round k + 1's upload
-    //    overlaps round k's interpolation, all-gather and coset LDE;
-    //  * trace already in every rank's HBM (trace = NULL): each rank interpolates all W columns itself, which costs
-    //    less than receiving (G-1)/G of the coefficients over xGMI.
+    // S2: the trace polynomials on every rank, then the local coset LDE and the distributed commitment.  Every trace
+    // source splits the interpolation by column, round robin: in round k rank g interpolates column U[g + G k] and an
+    // all-gather (in place when the round's columns are consecutive) fills the round's G columns on every rank, after
+    // which every rank extends them over its cosets.  Round k's all-gather runs on the exchange stream while the
+    // compute stream interpolates round k + 1 and extends round k - 1 (xchg_start / xchg_wait), so each rank computes
+    // 1/G of the coefficients and the exchange hides under the coset LDEs.  U (the columns transformed) leaves out
+    // what every rank forms from the last row alone (sparse columns, the AIR clock) or from per-program tables:
+    //  * host trace: rank g uploads (copy stream) only its own columns, so each rank moves 1/G of the trace over PCIe;
+    //    the previous sharded proof's column hints (sparse, clock, narrow) as the single-GPU host path (section 6c);
+    //  * trace already in every rank's HBM (trace = NULL): each rank detects the sparse columns and the clock over its
+    //    1/G of the rows, the flags are all-gathered (round 6: the interpolation was replicated before, 4.0 ms of
+    //    every rank's time at 2^22);
+    //  * zk_vm_prove_sharded: only the dynamic stack columns; the program-only columns from the preprocessed tables.
     const fe inv_n = h_inv(fe_make(n));
+    const size_t col = n * sizeof(fe);
     // on an early error return, copies from the caller's host trace may still be in flight: the caller may free it
     // as soon as this returns (the rounds of a completed S2 have waited for every copy)
     struct CopyGuard {
@@ -396,6 +509,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 upload_drain(p);
                 // (and the kernels of a failed proof: the next proof's uploads into d_trace must not overtake them)
                 (void)hipStreamSynchronize(p->st);
+                if (p->cst) (void)hipStreamSynchronize(p->cst);
             }
         }
     } copy_guard{X.P, trace != nullptr};
@@ -413,14 +527,23 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             b.wait();
         }
     } check_wait{checked, packed};
+    int U[W], nU = 0;     // the columns interpolated, ascending
+    uint32_t S = 0;       // sparse columns (zero but the last row): coefficients and LDE from the last row
+    bool clk = false;       // the AIR clock (column 0 = 0 .. n-2 but the last row): from the identity column's tables
+    fe lastv[W];          // the last row (host trace, device trace: read back with the flags)
+    std::vector<SparseCols> spc(nlp);
+    std::vector<const SparseCols *> spp(nlp, nullptr);
+    std::vector<NarrowCols> nar(nlp);
+    std::vector<uint32_t> went_packed(nlp, 0u);
+    uint32_t N8 = 0, N32 = 0;
+    zk_prover *H = X.P[0];
     if (trace) {
         // Column classes (round 4, as the single-GPU host path): the sparse columns (zero but the last row) and the AIR
-        // clock (rows 0 .. n-2 = 0 .. n-2) that the previous sharded proof of this length and world found -- the same
-        // hints on every rank, learned from all-gathered flags -- are neither uploaded, interpolated nor all-gathered:
-        // every rank forms their coefficients and local LDE from the last row (fills).  Each rank's host threads check
-        // its 1/G row range of them; the flags are all-gathered with the hints of the next proof, and a refuted hint
-        // voids the proof on every rank (prove_sharded_entry redoes it without hints).
-        zk_prover *H = X.P[0];
+        // clock (rows 0 .. n-2 = 0 .. n-2) that the previous sharded proof of this length, world and program found --
+        // the same hints on every rank, learned from all-gathered flags -- are neither uploaded, interpolated nor
+        // all-gathered: every rank forms their coefficients and local LDE from the last row (fills).  Each rank's host
+        // threads check its 1/G row range of them; the flags are all-gathered with the hints of the next proof, and a
+        // refuted hint voids the proof on every rank (prove_sharded_entry redoes it without hints).
         static const bool hints_on = [] {  // ZK_SHARD_HINTS=0: every column uploaded, interpolated and all-gathered
             const char *e = getenv("ZK_SHARD_HINTS");
             return !(e && !strcmp(e, "0"));
@@ -428,27 +551,23 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         // (keyed by length, world and program: column classes are a property of the program)
         const bool fresh = hints_on && X.hint_ok && sparse_on() && X.pl[0]->lagr && H->sh_hint_n == n && H->sh_hint_g == G &&
                            !memcmp(H->sh_hint_key, pub->program_hash, 32);
-        const uint32_t S = fresh ? H->sh_sparse : 0u;
-        const bool K = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
-        X.sh_clock = K;
-        const uint32_t derived = S | (K ? 1u : 0u);
-        const uint32_t N8 = fresh && narrow_on() ? H->sh_nw8 & ~derived : 0u;
-        const uint32_t N32 = fresh && narrow_on() ? H->sh_nw32 & ~derived & ~N8 : 0u;
-        int U[W], nu = 0;  // the uploaded columns, ascending
+        S = fresh ? H->sh_sparse : 0u;
+        clk = fresh && H->sh_clock && clock_on() && H->sh_clock_off_n != n && !(S & 1u);
+        X.sh_clock = clk;
+        const uint32_t derived = S | (clk ? 1u : 0u);
+        N8 = fresh && narrow_on() ? H->sh_nw8 & ~derived : 0u;
+        N32 = fresh && narrow_on() ? H->sh_nw32 & ~derived & ~N8 : 0u;
         for (int c = 0; c < W; c++)
-            if (!((S >> c) & 1u) && !(K && c == 0)) U[nu++] = c;
-        const int rounds = (nu + G - 1) / G;
+            if (!((S >> c) & 1u) && !(clk && c == 0)) U[nU++] = c;
         static_assert((W + 1) / 2 <= ZK_UPLOAD_GROUPS_MAX, "one upload event per round at G = 2");
-        const size_t col = n * sizeof(fe);
-        std::vector<SparseCols> spc(nlp);
-        std::vector<const SparseCols *> spp(nlp, nullptr);
+        for (int c = 0; c < W; c++) memcpy(&lastv[c], trace + (size_t)c * col + (n - 1) * sizeof(fe), sizeof(fe));
         for (int l = 0; l < nlp; l++) {
             ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
             ZK_TRY(sparse_begin(X.P[l], X.pl[l], &spc[l], &spp[l]));  // the flags the interpolation's pass 1 sets
             if (spp[l]) spc[l].wstride = W;
-            if (K) ZK_TRY(clock_tables(X.P[l], X.pl[l]));
+            if (clk) ZK_TRY(clock_tables(X.P[l], X.pl[l]));
         }
-        if (S | (K ? 1u : 0u)) {
+        if (S | (clk ? 1u : 0u)) {
             constexpr size_t R = (size_t)1 << 18;
             std::vector<std::pair<int, size_t>> tasks;  // (local rank, first row)
             for (int l = 0; l < nlp; l++) {
@@ -456,10 +575,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 for (size_t t = r0; t < r1; t += R) tasks.push_back({l, t});
             }
             int nt = 0;
-            for (int c = 0; c < W; c++) nt += ((S >> c) & 1u) || (K && c == 0) ? 1 : 0;
+            for (int c = 0; c < W; c++) nt += ((S >> c) & 1u) || (clk && c == 0) ? 1 : 0;
             checked.reset(nt * (int)tasks.size());
             for (int c = 0; c < W; c++) {
-                const bool sparse = (S >> c) & 1u, clock = K && c == 0;
+                const bool sparse = (S >> c) & 1u, clock = clk && c == 0;
                 if (!sparse && !clock) continue;
                 const uint8_t *cp = trace + (size_t)c * col;
                 for (const auto &tk : tasks) {
@@ -477,18 +596,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         // narrow columns (8- or 32-bit before the last row): their owner's host threads pack rows 0 .. n-2 into its
         // pinned staging while the other columns go up; a column goes up packed (expanded on the device), or whole if a
         // value does not fit
-        std::vector<NarrowCols> nar(nlp);
         for (int l = 0; l < nlp; l++) {
             NarrowCols &nc = nar[l];
             nc.count = 0;
             size_t bytes = 0;
-            for (int i = X.rank[l]; i < nu; i += G) {
+            for (int i = X.rank[l]; i < nU; i += G) {
                 const int c = U[i];
                 if (!(((N8 | N32) >> c) & 1u)) continue;
                 nc.col[nc.count] = c;
                 nc.width[nc.count] = ((N8 >> c) & 1u) ? 1 : 4;
                 nc.off[nc.count] = bytes;
-                memcpy(&nc.last[nc.count], trace + (size_t)c * col + (n - 1) * sizeof(fe), sizeof(fe));
+                nc.last[nc.count] = lastv[c];
                 bytes += ((size_t)nc.width[nc.count] * n + 15) & ~(size_t)15;
                 nc.count++;
             }
@@ -497,7 +615,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 if (p->h_pack) (void)hipHostFree(p->h_pack);
                 p->h_pack = nullptr;
                 p->h_pack_cap = 0;
-                ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, bytes, hipHostMallocDefault));
+                ZK_CHECK_HIP(hipHostMalloc((void **)&p->h_pack, bytes, hipHostMallocMapped | hipHostMallocCoherent));
                 p->h_pack_cap = bytes;
             }
         }
@@ -522,51 +640,105 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                         });
                     }
         }
-        // the narrow column k of local rank l, or -1
-        auto narrow_of = [&](int l, int c) {
-            for (int k = 0; k < nar[l].count; k++)
-                if (nar[l].col[k] == c) return k;
-            return -1;
-        };
-        std::vector<uint32_t> went_packed(nlp, 0u);
-        auto upload = [&](int k) -> int {
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                const int i = X.rank[l] + G * k;
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                const int q = i < nu ? narrow_of(l, U[i]) : -1;
-                if (q >= 0) packed.wait();  // (before the lock: the packing does not need it)
-                std::lock_guard<std::mutex> lk(*p->up_mu);
-                UploadEvent rec{p->ev_up[k], p->up};  // recorded on the error path too (CopyGuard drains it)
-                if (q >= 0 && !((pack_bad[l].load() >> U[i]) & 1u)) {
-                    const size_t w = (size_t)nar[l].width[q] * n;
-                    ZK_CHECK_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t *>(CLDE(p)) + nar[l].off[q],
-                                                p->h_pack + nar[l].off[q], w, hipMemcpyHostToDevice, p->up));
-                    went_packed[l] |= 1u << U[i];
-                } else if (i < nu) {
-                    ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)U[i] * n, trace + (size_t)U[i] * col, col,
-                                                hipMemcpyHostToDevice, p->up));
-                }
-                ZK_TRY(rec.record());
+    } else if (X.fixed) {
+        // vm::prove: the dynamic stack columns only (12 .. 12 + md - 1); the program-only columns and the zero registers
+        // from the per-program preprocessed columns of this rank's cosets (one streaming pass, after the rounds)
+        for (int c = 12; c < 12 + X.fixed[0].md; c++) U[nU++] = c;
+    } else {
+        // every rank holds the whole trace: each detects the sparse columns and the clock over its 1/G of the rows
+        // (whole 4096-row blocks; shorter traces: every row), the flags are all-gathered and OR-ed, and every rank reads
+        // them back with the last row (one host round trip) to plan the rounds
+        const size_t rr = n / (size_t)G;
+        const bool row_split = rr % 4096 == 0;
+        bool detect = true;
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_TRY(sparse_begin(p, X.pl[l], &spc[l], &spp[l]));
+            if (!spp[l]) {
+                detect = false;
+                continue;
             }
-            return ZK_OK;
-        };
-        if (rounds) ZK_TRY(upload(0));
+            const size_t r0 = row_split ? rr * (size_t)X.rank[l] : 0, r1 = row_split ? r0 + rr : n;
+            sparse_detect_rows(p->st, p->d_trace, n, 0, W, spc[l], r0, r1);
+        }
+        if (detect) {
+            std::vector<const void *> fs(nlp);
+            std::vector<void *> fr(nlp);
+            for (int l = 0; l < nlp; l++) {
+                fs[l] = X.P[l]->sp_nz;
+                fr[l] = X.P[l]->sh_buf;
+            }
+            ZK_TRY(xchg(X, "column_flags", AG, fs, fr, 4 * W * sizeof(unsigned)));
+            std::vector<unsigned> f((size_t)G * 4 * W);
+            ZK_CHECK_HIP(hipSetDevice(P0->device));
+            ZK_TRY(d2h_small(P0, f.data(), P0->sh_buf, f.size() * sizeof(unsigned)));
+            ZK_TRY(d2h_small(P0, lastv, P0->sp_last, sizeof lastv));
+            ZK_TRY(d2h_flush(P0));
+            unsigned nz[4 * W] = {};
+            for (int g = 0; g < G; g++)
+                for (int c = 0; c < 4 * W; c++) nz[c] |= f[(size_t)g * 4 * W + c];
+            for (int c = 0; c < W; c++)
+                if (nz[c] == 0) S |= 1u << c;
+            clk = clock_on() && !(S & 1u) && nz[3 * W] == 0 && spc[0].id_poly;
+        }
+        for (int c = 0; c < W; c++)
+            if (!((S >> c) & 1u) && !(clk && c == 0)) U[nU++] = c;
+        if (clk)
+            for (int l = 0; l < nlp; l++) ZK_TRY(clock_tables(X.P[l], X.pl[l]));
+    }
+    // the narrow column k of local rank l, or -1
+    auto narrow_of = [&](int l, int c) {
+        for (int k = 0; k < nar[l].count; k++)
+            if (nar[l].col[k] == c) return k;
+        return -1;
+    };
+    auto upload = [&](int k) -> int {  // host trace: round k's column of every local rank onto its copy stream
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            const int i = X.rank[l] + G * k;
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            const int q = i < nU ? narrow_of(l, U[i]) : -1;
+            if (q >= 0) packed.wait();  // (before the lock: the packing does not need it)
+            std::lock_guard<std::mutex> lk(*p->up_mu);
+            UploadEvent rec{p->ev_up[k], p->up};  // recorded on the error path too (CopyGuard drains it)
+            if (q >= 0 && !((pack_bad[l].load() >> U[i]) & 1u)) {
+                const size_t w = (size_t)nar[l].width[q] * n;
+                ZK_CHECK_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t *>(CLDE(p)) + nar[l].off[q],
+                                            p->h_pack + nar[l].off[q], w, hipMemcpyHostToDevice, p->up));
+                went_packed[l] |= 1u << U[i];
+            } else if (i < nU) {
+                ZK_CHECK_HIP(hipMemcpyAsync(p->d_trace + (size_t)U[i] * n, trace + (size_t)U[i] * col, col,
+                                            hipMemcpyHostToDevice, p->up));
+            }
+            ZK_TRY(rec.record());
+        }
+        return ZK_OK;
+    };
+    const int rounds = (nU + G - 1) / G;
+    std::vector<XH> hr(std::max(rounds, 1));
+    std::vector<char> inplace_r(std::max(rounds, 1));
+    // a round whose columns are not consecutive is gathered into a staging area, alternating between two buffers
+    // free until S3 / S4, so round k + 1's all-gather never overwrites what round k's copy-out still reads
+    auto stage_of = [&](zk_prover *p, int k) { return (k & 1) ? p->comp : p->ctmp; };
+    auto issue = [&](int k) -> int {  // interpolate this rank's column of round k, start the round's all-gather
+        if (trace && k + 1 < rounds) ZK_TRY(upload(k + 1));
+        const int i0 = G * k, real = std::min(G, nU - i0), first = U[i0];
+        // in place when the round's columns are consecutive (the padding slots of a short last round then land on
+        // columns nobody interpolates -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns)
+        const bool inplace = U[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
+        inplace_r[k] = inplace;
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
-        for (int k = 0; k < rounds; k++) {
-            if (k + 1 < rounds) ZK_TRY(upload(k + 1));
-            const int i0 = G * k, real = std::min(G, nu - i0), first = U[i0];
-            // in place when the round's columns are consecutive (the padding slots of a short last round then land on
-            // columns nobody uploads -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns); else
-            // through the composition scratch (free until S4) and copied out
-            const bool inplace = U[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                const int i = i0 + X.rank[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                ZK_TRY(upload_gate(p, p->ev_up[k]));
-                if (i < nu && ((went_packed[l] >> U[i]) & 1u)) {
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            const int i = i0 + X.rank[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            if (trace) {
+                // (a device-side wait: a sharded rank's process holds one prover, so its compute, exchange and upload
+                // streams have hardware queues of their own and the host never blocks on the link)
+                ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[k], 0));
+                if (i < nU && ((went_packed[l] >> U[i]) & 1u)) {
                     const int q = narrow_of(l, U[i]);
                     NarrowCols one{};
                     one.count = 1;
@@ -576,158 +748,143 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                     one.last[0] = nar[l].last[q];
                     expand_narrow(p->st, reinterpret_cast<const uint8_t *>(CLDE(p)), one, n, p->d_trace);
                 }
-                if (i < nu) {
-                    SparseCols g = spc[l];
-                    g.col0 = U[i];
-                    g.fused = true;
-                    ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)U[i] * n, n, p->polys + (size_t)U[i] * n, n, 1, true, nullptr,
-                        &inv_n, p->tmp, spp[l] ? &g : nullptr);
-                }
-                snd[l] = inplace ? p->polys + (size_t)(first + X.rank[l]) * n : p->polys + (size_t)(i < nu ? U[i] : 0) * n;
-                rcv[l] = inplace ? p->polys + (size_t)first * n : CTMP(p);
             }
-            ZK_TRY(xchg(X, "trace_coeffs", AG, snd, rcv, col));
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                if (!inplace)
-                    for (int g = 0; g < real; g++)
-                        if (g != X.rank[l])
-                            ZK_CHECK_HIP(hipMemcpyAsync(p->polys + (size_t)U[i0 + g] * n, CTMP(p) + (size_t)g * n, col,
-                                                        hipMemcpyDeviceToDevice, p->st));
-                // this round's columns are complete on every rank: extend them over the local cosets now, so the LDE
-                // runs under the next round's upload instead of after the last one
-                for (int a = 0; a < real;) {
-                    int b = a + 1;
-                    while (b < real && U[i0 + b] == U[i0 + b - 1] + 1) b++;
-                    const int c0 = U[i0 + a];
-                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
-                            p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
-                    a = b;
-                }
+            if (i < nU) {
+                SparseCols g = spc[l];
+                g.col0 = U[i];
+                g.fused = true;
+                ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)U[i] * n, n, p->polys + (size_t)U[i] * n, n, 1, true, nullptr,
+                    &inv_n, p->tmp, trace && spp[l] ? &g : nullptr);
+            }
+            snd[l] = inplace ? p->polys + (size_t)(first + X.rank[l]) * n : p->polys + (size_t)(i < nU ? U[i] : 0) * n;
+            rcv[l] = inplace ? p->polys + (size_t)first * n : stage_of(p, k);
+        }
+        return xchg_start(X, "trace_coeffs", AG, snd, rcv, col, &hr[k]);
+    };
+    auto finish = [&](int k) -> int {  // wait for round k's coefficients, extend them over the local cosets
+        ZK_TRY(xchg_wait(X, hr[k]));
+        const int i0 = G * k, real = std::min(G, nU - i0);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            if (!inplace_r[k])
+                for (int g = 0; g < real; g++)
+                    if (g != X.rank[l])
+                        ZK_CHECK_HIP(hipMemcpyAsync(p->polys + (size_t)U[i0 + g] * n, stage_of(p, k) + (size_t)g * n, col,
+                                                    hipMemcpyDeviceToDevice, p->st));
+            for (int a = 0; a < real;) {
+                int b = a + 1;
+                while (b < real && U[i0 + b] == U[i0 + b - 1] + 1) b++;
+                const int c0 = U[i0 + a];
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
+                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+                a = b;
             }
         }
-        // the hinted columns from the last row (after the last round: a short round's padding may have landed there)
-        if (S | (K ? 1u : 0u)) {
-            fe lastv[W];
-            for (int c = 0; c < W; c++) memcpy(&lastv[c], trace + (size_t)c * col + (n - 1) * sizeof(fe), sizeof(fe));
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                if (S) {
-                    ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));
-                    for (int c = 0; c < W;) {
-                        if (!((S >> c) & 1u)) {
-                            c++;
-                            continue;
-                        }
-                        int e = c + 1;
-                        while (e < W && ((S >> e) & 1u)) e++;
-                        SparseCols g = spc[l];
-                        g.col0 = c;
-                        g.fused = false;
-                        g.all = true;  // fills only
-                        ntt(p->st, X.pl[l]->Tn, p->polys + (size_t)c * n, n, p->polys + (size_t)c * n, n, e - c, true, nullptr,
-                            &inv_n, p->tmp, &g);
-                        ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c * n, n, e - c, X.rank[l], G, Bl,
-                                p->lde + (size_t)c * Bl * n, (size_t)Bl * n, n, p->tmp, &g);
-                        c = e;
-                    }
-                }
-                if (K) {
-                    const fe_ws d = make_fe_ws(fe_sub(lastv[0], fe_make(n - 1)));
-                    const Plan *pl = X.pl[l];
-                    axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
-                    for (int j = 0; j < Bl; j++) {
-                        const size_t r = (size_t)X.rank[l] + (size_t)G * j;
-                        axpy_fill(p->st, pl->id_lde + pl->lde_slot((int)r) * n, pl->lagr_lde + pl->lde_slot((int)r) * n, d,
-                                  n, p->lde + (size_t)j * n);
-                    }
-                }
-            }
-        }
-        // the flags of the columns each rank interpolated (for the next proof's hints) and each rank's check of the
-        // hinted ones, all-gathered: every rank then holds the same view
-        if (spp[0]) {
-            checked.wait();
-            std::vector<const void *> fs(nlp);
-            std::vector<void *> fr(nlp);
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                const uint32_t b = bad[l].load();
-                ZK_TRY(h2d_small(p, p->sp_nz + 3 * W + 1, &b, sizeof b));
-                fs[l] = p->sp_nz;
-                fr[l] = p->sh_buf;
-            }
-            ZK_TRY(xchg(X, "column_flags", AG, fs, fr, 4 * W * sizeof(unsigned)));
-            std::vector<unsigned> f((size_t)G * 4 * W);
-            ZK_TRY(d2h_small(P0, f.data(), P0->sh_buf, f.size() * sizeof(unsigned)));
-            ZK_TRY(d2h_flush(P0));
-            unsigned nz[3 * W] = {};
-            uint32_t refuted = 0;
-            for (int g = 0; g < G; g++) {
-                for (int c = 0; c < 3 * W; c++) nz[c] |= f[(size_t)g * 4 * W + c];
-                refuted |= f[(size_t)g * 4 * W + 3 * W + 1];
-            }
-            if (refuted) {
-                X.sh_refuted = refuted;
-                return ZK_SH_REDO;
-            }
-            // next proof: the columns found sparse (uploaded ones with no nonzero entry before the last row, and the
-            // hinted ones, which the checks confirmed), narrow (8- / 32-bit before the last row), and the clock when
-            // column 0 was found 32-bit (or was derived)
-            uint32_t sp_next = S, w8 = 0, w32 = 0;
-            for (int i = 0; i < nu; i++) {
-                const int c = U[i];
-                if (nz[c] == 0) sp_next |= 1u << c;
-                else if (nz[W + c] == 0) w8 |= 1u << c;
-                else if (nz[2 * W + c] == 0) w32 |= 1u << c;
-            }
-            const bool clk_next = K || (!(sp_next & 1u) && (w32 & 1u));
-            if (clk_next) w32 &= ~1u;
-            for (zk_prover *p : X.P) {
-                p->sh_sparse = sp_next;
-                p->sh_nw8 = w8;
-                p->sh_nw32 = w32;
-                p->sh_clock = clk_next;
-                p->sh_hint_n = n;
-                p->sh_hint_g = G;
-                memcpy(p->sh_hint_key, pub->program_hash, 32);
-            }
-        }
-    } else if (X.fixed) {
-        // vm::prove: interpolate and extend only the dynamic stack columns; the program-only columns and the zero
-        // registers from the per-program preprocessed columns of this rank's cosets (one streaming pass)
+        return ZK_OK;
+    };
+    if (trace && rounds) ZK_TRY(upload(0));
+    if (rounds) ZK_TRY(issue(0));
+    for (int k = 0; k < rounds; k++) {
+        if (k + 1 < rounds) ZK_TRY(issue(k + 1));
+        ZK_TRY(finish(k));
+    }
+    // the columns formed from the last row (after the last round: a short round's padding may have landed there)
+    if (X.fixed) {
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             const FixedCols &fx = X.fixed[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            constexpr size_t c0 = 12;
-            if (fx.md > 0) {
-                ntt(p->st, X.pl[l]->Tn, p->d_trace + c0 * n, n, p->polys + c0 * n, n, fx.md, true, nullptr, &inv_n, p->tmp);
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + c0 * n, n, fx.md, X.rank[l], G, Bl,
-                        p->lde + c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
-            }
             if (!p->fix_ws) ZK_CHECK_HIP(p->arena.alloc(&p->fix_ws, W));
             fe_ws ws[W];
             for (int c = 0; c < W; c++) ws[c] = make_fe_ws(fx.last[c]);
             ZK_TRY(h2d_small(p, p->fix_ws, ws, sizeof ws));
             fixed_axpy(p->st, fx, p->fix_ws, n, (size_t)Bl, p->polys, p->lde);
         }
-    } else {
+    } else if (S | (clk ? 1u : 0u)) {
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            // sparse columns (zero but the last row): no DFT, the LDE is last * the unit vector's (every rank
-            // detects them in its own copy of the trace)
-            SparseCols spc{};
-            const SparseCols *sp = nullptr;
-            ZK_TRY(sparse_begin(p, X.pl[l], &spc, &sp));
-            if (sp) sparse_detect(p->st, p->d_trace, n, 0, W, *sp);
-            ntt(p->st, X.pl[l]->Tn, p->d_trace, n, p->polys, n, W, true, nullptr, &inv_n, p->tmp, sp);
-            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys, n, W, X.rank[l], G, Bl, p->lde, (size_t)Bl * n, n, p->tmp,
-                    sp);
+            if (S) {
+                if (trace) ZK_TRY(h2d_small(p, p->sp_last, lastv, sizeof lastv));  // (device traces: the detection's)
+                for (int c = 0; c < W;) {
+                    if (!((S >> c) & 1u)) {
+                        c++;
+                        continue;
+                    }
+                    int e = c + 1;
+                    while (e < W && ((S >> e) & 1u)) e++;
+                    SparseCols g = spc[l];
+                    g.col0 = c;
+                    g.fused = false;
+                    g.all = true;  // fills only
+                    ntt(p->st, X.pl[l]->Tn, p->polys + (size_t)c * n, n, p->polys + (size_t)c * n, n, e - c, true, nullptr,
+                        &inv_n, p->tmp, &g);
+                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c * n, n, e - c, X.rank[l], G, Bl,
+                            p->lde + (size_t)c * Bl * n, (size_t)Bl * n, n, p->tmp, &g);
+                    c = e;
+                }
+            }
+            if (clk) {
+                const fe_ws d = make_fe_ws(fe_sub(lastv[0], fe_make(n - 1)));
+                const Plan *pl = X.pl[l];
+                axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
+                for (int j = 0; j < Bl; j++) {
+                    const size_t r = (size_t)X.rank[l] + (size_t)G * j;
+                    axpy_fill(p->st, pl->id_lde + pl->lde_slot((int)r) * n, pl->lagr_lde + pl->lde_slot((int)r) * n, d,
+                              n, p->lde + (size_t)j * n);
+                }
+            }
+        }
+    }
+    // host traces: the flags of the columns each rank interpolated (for the next proof's hints) and each rank's check
+    // of the hinted ones, all-gathered: every rank then holds the same view
+    if (trace && spp[0]) {
+        checked.wait();
+        std::vector<const void *> fs(nlp);
+        std::vector<void *> fr(nlp);
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            const uint32_t b = bad[l].load();
+            ZK_TRY(h2d_small(p, p->sp_nz + 3 * W + 1, &b, sizeof b));
+            fs[l] = p->sp_nz;
+            fr[l] = p->sh_buf;
+        }
+        ZK_TRY(xchg(X, "column_flags", AG, fs, fr, 4 * W * sizeof(unsigned)));
+        std::vector<unsigned> f((size_t)G * 4 * W);
+        ZK_TRY(d2h_small(P0, f.data(), P0->sh_buf, f.size() * sizeof(unsigned)));
+        ZK_TRY(d2h_flush(P0));
+        unsigned nz[3 * W] = {};
+        uint32_t refuted = 0;
+        for (int g = 0; g < G; g++) {
+            for (int c = 0; c < 3 * W; c++) nz[c] |= f[(size_t)g * 4 * W + c];
+            refuted |= f[(size_t)g * 4 * W + 3 * W + 1];
+        }
+        if (refuted) {
+            X.sh_refuted = refuted;
+            return ZK_SH_REDO;
+        }
+        // next proof: the columns found sparse (uploaded ones with no nonzero entry before the last row, and the
+        // hinted ones, which the checks confirmed), narrow (8- / 32-bit before the last row), and the clock when
+        // column 0 was found 32-bit (or was derived)
+        uint32_t sp_next = S, w8 = 0, w32 = 0;
+        for (int i = 0; i < nU; i++) {
+            const int c = U[i];
+            if (nz[c] == 0) sp_next |= 1u << c;
+            else if (nz[W + c] == 0) w8 |= 1u << c;
+            else if (nz[2 * W + c] == 0) w32 |= 1u << c;
+        }
+        const bool clk_next = clk || (!(sp_next & 1u) && (w32 & 1u));
+        if (clk_next) w32 &= ~1u;
+        for (zk_prover *p : X.P) {
+            p->sh_sparse = sp_next;
+            p->sh_nw8 = w8;
+            p->sh_nw32 = w32;
+            p->sh_clock = clk_next;
+            p->sh_hint_n = n;
+            p->sh_hint_g = G;
+            memcpy(p->sh_hint_key, pub->program_hash, 32);
         }
     }
     stage_mark(P0, "trace_lde");
@@ -738,10 +895,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         nd[l] = X.P[l]->nodes;
     }
     DistTree Ttrace;
-    ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_mg) {
+    ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
         zk_prover *p = X.P[l];
-        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, p->lde, W, log_n, Bl,
-                           log_mg, send);
+        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, p->lde, W,
+                           log_n, Bl, log_mg, log_K, k, send);
     }, scratch, lv, nd, "trace_digests", "trace_roots"));
     memcpy(R.trace_root, Ttrace.root, 32);
     stage_mark(P0, "trace_commit");
@@ -785,6 +942,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // S4: composition polynomial: per-coset inverse NTT, all-to-all of coefficient slices, cross-coset
     // step on this rank's slice, all-gather of the C columns; then local coset LDE + commitment
     const size_t kg = n / G;
+    XH hdeg;  // the degree flags' all-gather (read once the composition is committed)
     {
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
@@ -798,7 +956,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             snd[l] = p->tmp;
             rcv[l] = COMP(p);
         }
-        ZK_TRY(xchg(X, "comp_slices", A2A, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe)));
+        XH hs;
+        ZK_TRY(xchg_start(X, "comp_slices", A2A, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe), &hs));
+        // (the first plane's assertion quotient reads only the trace coefficients: it runs under the all-to-all)
+        std::vector<const void *> bnd0(nlp);
+        for (int l = 0; bnd_split && l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            bnd0[l] = boundary_range_begin(p->st, p->polys, log_n, KX == 1 ? K : Kp[0], K.g_last2, p->dscratch,
+                                           (size_t)X.rank[l] * kg, kg);
+        }
+        ZK_TRY(xchg_wait(X, hs));
         const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
         std::vector<const void *> fs(nlp);
         std::vector<void *> fr(nlp);
@@ -827,7 +995,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                s2[l] = boundary_range_begin(p->st, p->polys, log_n, Kb, K.g_last2, p->dscratch, (size_t)X.rank[l] * kg, kg);
+                s2[l] = pln == 0 ? bnd0[l]
+                                 : boundary_range_begin(p->st, p->polys, log_n, Kb, K.g_last2, p->dscratch,
+                                                        (size_t)X.rank[l] * kg, kg);
                 r2[l] = p->sh_buf;
             }
             ZK_TRY(xchg(X, "bnd_totals", AG, s2, r2, 2 * sizeof(fe)));
@@ -839,6 +1009,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 boundary_range_end(p->st, log_n, K.g_last2, p->dscratch, k0, kg, p->ood, CTMP(p) + pln * kg - k0, p->flag);
             }
         }
+        // the column polynomials: one all-gather per column, all started at once (they run back to back on the
+        // exchange stream); the coset LDE of a group of columns starts as soon as the group has arrived, so the later
+        // columns' all-gathers run under the earlier columns' LDEs.  Groups hold >= 2^22 LDE points per launch.
+        std::vector<XH> hc(CK);
         for (int c = 0; c < CK; c++) {
             std::vector<const void *> s2(nlp);
             std::vector<void *> r2(nlp);
@@ -846,13 +1020,19 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 s2[l] = CTMP(X.P[l]) + c * kg;
                 r2[l] = X.P[l]->cpolys + (size_t)c * n;
             }
-            ZK_TRY(xchg(X, "comp_columns", AG, s2, r2, kg * sizeof(fe)));
+            ZK_TRY(xchg_start(X, "comp_columns", AG, s2, r2, kg * sizeof(fe), &hc[c]));
         }
-        ZK_TRY(xchg(X, "degree_flags", AG, fs, fr, sizeof(unsigned)));
-        for (int l = 0; l < nlp; l++) {
-            zk_prover *p = X.P[l];
-            ZK_CHECK_HIP(hipSetDevice(p->device));
-            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys, n, CK, X.rank[l], G, Bl, CLDE(p), (size_t)Bl * n, n, p->tmp);
+        ZK_TRY(xchg_start(X, "degree_flags", AG, fs, fr, sizeof(unsigned), &hdeg));
+        const int grp = (int)std::max<size_t>(1, ((size_t)1 << 22) / ((size_t)Bl * n));
+        for (int c0 = 0; c0 < CK; c0 += grp) {
+            const int c1 = std::min(CK, c0 + grp);
+            for (int c = c0; c < c1; c++) ZK_TRY(xchg_wait(X, hc[c]));
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys + (size_t)c0 * n, n, c1 - c0, X.rank[l], G, Bl,
+                        CLDE(p) + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+            }
         }
     }
     for (int l = 0; l < nlp; l++) {
@@ -860,15 +1040,16 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         nd[l] = X.P[l]->cnodes;
     }
     DistTree Tcomp;
-    ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_mg) {
+    ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
         zk_prover *p = X.P[l];
-        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv((size_t)Bl * n, 256)), dim3(256), 0, p->st, CLDE(p), CK, log_n, Bl,
-                           log_mg, send);
+        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, CLDE(p), CK,
+                           log_n, Bl, log_mg, log_K, k, send);
     }, scratch, lv, nd, "comp_digests", "comp_roots"));
     memcpy(R.constraint_root, Tcomp.root, 32);
     stage_mark(P0, "composition");
     unsigned degree_flag = 0;
     {
+        ZK_TRY(xchg_wait(X, hdeg));
         std::vector<unsigned> f(G);
         ZK_TRY(d2h_small(P0, f.data(), P0->sh_flags, G * sizeof(unsigned)));
         ZK_TRY(d2h_flush(P0));
@@ -1030,6 +1211,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             rcv[l] = COMP(X.P[l]);
         }
         ZK_TRY(xchg(X, "remainder_layer", AG, snd, rcv, (size_t)KX * Bl * n * sizeof(fe)));
+        ZK_TRY(lead_segment(X));
         ZK_CHECK_HIP(hipSetDevice(P0->device));
         for (int pln = 0; pln < KX; pln++)
             hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(N, 256)), dim3(256), 0, P0->st,
@@ -1044,14 +1226,14 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             f0l[l] = (uint8_t *)X.P[l]->tmp;
             f0n[l] = f0l[l] + 32 * (rows0 / G);
         }
-        ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_mg) {
+        ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
             zk_prover *p = X.P[l];
             if (KX == 1)
-                hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n,
-                                   Bl, (int)fold, log_m, log_mg, send);
+                hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv(((size_t)Bl * m) >> log_K, 256)), dim3(256), 0, p->st,
+                                   p->deep, log_n, Bl, (int)fold, log_m, log_mg, log_K, k, send);
             else
-                hipLaunchKernelGGL(k_sh_hash_fri0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->x_deep,
-                                   log_n, Bl, (int)fold, log_m, log_mg, send);
+                hipLaunchKernelGGL(k_sh_hash_fri0_ext, dim3(cdiv(((size_t)Bl * m) >> log_K, 256)), dim3(256), 0, p->st,
+                                   p->x_deep, log_n, Bl, (int)fold, log_m, log_mg, log_K, k, send);
         }, scratch, f0l, f0n, "fri0_digests", "fri0_roots"));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
@@ -1088,6 +1270,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 rcv[l] = COMP(p);
             }
             ZK_TRY(xchg(X, "fri_layer1", AG, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
+            ZK_TRY(lead_segment(X));  // from here the FRI layers >= 1 and the queries run on the lead rank alone
             ZK_CHECK_HIP(hipSetDevice(P0->device));
             for (int pln = 0; pln < KX; pln++)
                 hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st,
@@ -1210,6 +1393,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             }
     const size_t NK = req.size();
     if (NK > ZK_GATHER_CAP) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many opened values for the gather buffer");
+    ZK_TRY(sched_entry(X, 'K', -1));  // (the lead-only segment ends: every rank gathers its openings)
     {
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
@@ -1307,6 +1491,13 @@ int zk_comm_create_host(int rank, int world, zk_exchange_fn fn, void *ctx, zk_co
 
 void zk_comm_destroy(zk_comm *c) { delete c; }
 
+int zk_comm_set_measure(zk_comm *c, int on) {
+    if (!c) ZK_FAIL(ZK_ERR_INVALID_ARG, "null communicator");
+    if (!c->loopback()) ZK_FAIL(ZK_ERR_INVALID_ARG, "the measurement mode needs a loopback communicator");
+    c->measure = on != 0;
+    return ZK_OK;
+}
+
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec) {
@@ -1365,6 +1556,26 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         return fixed ? prove_fixed(X.P[0], n, opt, pub, fixed, proof_out, proof_len)
                      : prove_single(X.P[0], trace, n, opt, pub, proof_out, proof_len, rec);
     X.fixed = fixed;
+    // measurement mode (loopback): every rank's kernels on rank 0's stream, in program order (restored on the way out)
+    struct SharedStream {
+        std::vector<zk_prover *> P;
+        std::vector<hipStream_t> own;
+        ~SharedStream() {
+            for (size_t l = 1; l < P.size(); l++) {
+                (void)hipStreamSynchronize(P[l]->st);
+                P[l]->st = own[l];
+            }
+        }
+    } shared;
+    if (comm->measure) {
+        for (auto *p : X.P) {
+            shared.P.push_back(p);
+            shared.own.push_back(p->st);
+        }
+        for (size_t l = 1; l < X.P.size(); l++) X.P[l]->st = X.P[0]->st;
+    }
+    X.P[0]->sched_world = X.G;
+    X.P[0]->sched_measure = comm->measure;
     // every local rank's proof counts as in flight on its device (the single-GPU AUTO upload schedule reads it)
     std::vector<std::unique_ptr<DeviceBusy>> busy;
     for (auto *p : X.P) busy.push_back(std::make_unique<DeviceBusy>(p->dev_busy));

@@ -131,6 +131,8 @@ struct SparseCols {
     int lde_r0 = 0, lde_shift = 0;
 };
 void sparse_detect(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp);
+void sparse_detect_rows(hipStream_t st, const fe *trace, size_t n, int c0, int nc, const SparseCols &sp, size_t r0,
+                        size_t r1);
 // Narrow trace columns uploaded packed (zk_prove from host columns): column col[k]'s rows 0 .. n-2 as width[k]-byte
 // integers (1 or 4) at src + off[k], its last row last[k]; written out as field elements into trace column col[k].
 struct NarrowCols {

@@ -121,16 +121,36 @@ class ShardedProver:
         lib().zk_prover_stage_times(self.provers[0], names, ms, 32, C.byref(cnt))
         return {names[i].decode(): ms[i] for i in range(cnt.value)}
 
-    def exchange_stats(self) -> dict:
-        """{collective: (ms, bytes received from the other ranks, calls)} of the last proof on local rank 0's
-        stream (zk_prover_exchange_stats): events around each collective, so the time includes waiting for peers."""
+    def exchange_stats(self, exposed: bool = False) -> dict:
+        """{collective: (ms, bytes received from the other ranks, calls)} of the last proof on local rank 0
+        (zk_prover_exchange_stats): events around each collective on the stream it ran on, so the time includes waiting
+        for peers.  exposed=True appends the exposed ms (how long the compute stream waited for it) to each tuple."""
         names = (C.c_char_p * 32)()
         ms = (C.c_float * 32)()
+        ex = (C.c_float * 32)()
         by = (C.c_double * 32)()
         calls = (C.c_int * 32)()
         cnt = C.c_int(0)
-        check(lib().zk_prover_exchange_stats(self.provers[0], names, ms, by, calls, 32, C.byref(cnt)))
-        return {names[i].decode(): (ms[i], by[i], calls[i]) for i in range(min(cnt.value, 32))}
+        check(lib().zk_prover_exchange_stats_ex(self.provers[0], names, ms, ex, by, calls, 32, C.byref(cnt)))
+        k = min(cnt.value, 32)
+        if exposed:
+            return {names[i].decode(): (ms[i], by[i], calls[i], ex[i]) for i in range(k)}
+        return {names[i].decode(): (ms[i], by[i], calls[i]) for i in range(k)}
+
+    def set_measure(self, on: bool):
+        """zk_comm_set_measure (loopback only): serialise every rank's compute and the exchange copies on one stream,
+        so the schedule's segments are the ranks' compute alone (tools/shard_model.py); the proof bytes are unchanged."""
+        check(lib().zk_comm_set_measure(self.comm, 1 if on else 0))
+
+    def schedule(self) -> dict:
+        """The last proof's schedule on local rank 0 (zk_prover_shard_schedule): exchange starts / waits in issue
+        order and the measured compute segments between them."""
+        import json
+        need = C.c_size_t(0)
+        lib().zk_prover_shard_schedule(self.provers[0], None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        check(lib().zk_prover_shard_schedule(self.provers[0], buf, need.value, C.byref(need)))
+        return json.loads(buf.value.decode())
 
     def close(self):
         for p in self.provers:

@@ -235,16 +235,32 @@ typedef int (*zk_exchange_fn)(void *ctx, int op, const void *send, void *recv, s
 enum { ZK_XCHG_ALL_TO_ALL = 0, ZK_XCHG_ALL_GATHER = 1 };
 int zk_comm_create_host(int rank, int world, zk_exchange_fn fn, void *ctx, zk_comm **out);
 void zk_comm_destroy(zk_comm *comm);
+/* Measurement mode of a loopback communicator (tools/shard_model.py): every rank's kernels and the exchange copies
+ * run on ONE stream in program order, so each compute segment of the schedule (zk_prover_shard_schedule) is the
+ * ranks' compute alone, serialised (no overlap, no exchange time inside); the proof bytes are unchanged.  on = 0
+ * returns to the normal mode (exchanges on their own stream, overlapped with compute).  Refused for RCCL and
+ * host-exchange communicators. */
+int zk_comm_set_measure(zk_comm *comm, int on);
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
                      zk_record *rec);
 /* The collectives of the last sharded proof on this (local rank 0) prover, aggregated by name (trace_coeffs,
  * trace_digests, trace_roots, comp_slices, comp_columns, degree_flags, comp_digests, comp_roots, ood_parts,
  * deep_totals, deep_slices, fri0_digests, fri0_roots, fri_layer1, openings): ms between HIP events recorded on the
- * prover's stream around each call (waiting for slower ranks included), bytes this rank received from the other
- * ranks, and the number of calls.  Valid once the proof has returned, until the next proof. */
+ * stream the collective runs on around each call (waiting for slower ranks included), bytes this rank received from
+ * the other ranks, and the number of calls.  Valid once the proof has returned, until the next proof. */
 int zk_prover_exchange_stats(zk_prover *p, const char **names, float *ms, double *bytes, int *calls, int cap,
                              int *count);
+/* The same with each collective's exposed time beside its total: exposed_ms is how long the compute stream waited
+ * for it (events around the stream wait; 0 when the collective finished under the compute issued meanwhile).  The
+ * collectives run on a stream of their own (round 6), so only what a stage waits for shows up as exposed. */
+int zk_prover_exchange_stats_ex(zk_prover *p, const char **names, float *ms, float *exposed_ms, double *bytes,
+                                int *calls, int cap, int *count);
+/* The last sharded proof's schedule on this (local rank 0) prover, as JSON: the order in which the library started
+ * exchanges, waited for them and ran the compute segments between (each segment's measured ms, and whether only the
+ * lead rank ran it), for tools/shard_model.py.  *len = bytes needed (with the NUL); ZK_ERR_BUFFER_TOO_SMALL when
+ * cap is short.  In the measurement mode (zk_comm_set_measure) the segments are the serialised ranks' compute. */
+int zk_prover_shard_schedule(zk_prover *p, char *buf, size_t cap, size_t *len);
 /* The host-to-device trace traffic of the last proof from host columns (zk_prove / zk_prove_columns): bytes copied,
  * the columns taken as sparse (zero but the last row: their last value only), and the columns uploaded packed as 8-
  * or 32-bit integers (narrow; each value checked on the host first).  Bit c = trace column c. */
