@@ -393,6 +393,91 @@ __device__ __forceinline__ fe fe_mul_wsv(fe A, const fe_ws &W) {
     return ws_fold(r0, r1, r2, r3, (uint32_t)a, (uint32_t)(a >> 32));
 }
 
+// ---- two independent W-set products at once (the NTT butterflies multiply in pairs: x1 and x3 by one twiddle, a2 and
+// a3 by two): the column products as above, then both final reductions in one list-scheduled asm block
+// (addsub_asm.hpp ws_fold2_asm), whose two carry chains fill each other's wait states instead of s_nop.  ZK_FOLD2=0:
+// two ws_folds, one after the other.  Same values.
+#ifndef ZK_FOLD2
+#define ZK_FOLD2 1
+#endif
+__device__ __forceinline__ void ws_fold2(uint32_t a[4], uint32_t as4, uint32_t as5, uint32_t b[4], uint32_t bs4,
+                                         uint32_t bs5, fe &ra, fe &rb) {
+    if constexpr (ZK_FOLD2) {
+        const uint32_t K = 0x2d00u;
+        const uint64_t ma = (uint64_t)as4 * K + K, mb = (uint64_t)bs4 * K + K;
+        ws_fold2_asm(a, as4, as5, lo32(ma), hi32(ma) + as5 * K, b, bs4, bs5, lo32(mb), hi32(mb) + bs5 * K);
+        ra = fe{join32(a[0], a[1]), join32(a[2], a[3])};
+        rb = fe{join32(b[0], b[1]), join32(b[2], b[3])};
+    } else {
+        ra = ws_fold(a[0], a[1], a[2], a[3], as4, as5);
+        rb = ws_fold(b[0], b[1], b[2], b[3], bs4, bs5);
+    }
+}
+// the 160-bit column sums of A x W (W words from SGPRs): r[0..4) and the top (s4, s5)
+__device__ __forceinline__ void ws_columns_s(fe A, const fe_ws &W, uint32_t r[4], uint32_t &s4, uint32_t &s5) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint32_t h = 0;
+    uint64_t a, kd;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a), "=s"(kd) : "v"(x0), "s"(W.w[0]));
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col3s(a, h, x1, W.w[1], x2, W.w[2], x3, W.w[3]);                 ZK_WSHIFT(r[0]);
+    col4s(a, h, x0, W.w[4], x1, W.w[5], x2, W.w[6], x3, W.w[7]);     ZK_WSHIFT(r[1]);
+    col4s(a, h, x0, W.w[8], x1, W.w[9], x2, W.w[10], x3, W.w[11]);   ZK_WSHIFT(r[2]);
+    col4s(a, h, x0, W.w[12], x1, W.w[13], x2, W.w[14], x3, W.w[15]); ZK_WSHIFT(r[3]);
+#undef ZK_WSHIFT
+    s4 = (uint32_t)a;
+    s5 = (uint32_t)(a >> 32);
+}
+// ... the W words in VGPRs (a W set shared by a group of lanes)
+__device__ __forceinline__ void ws_columns_v(fe A, const fe_ws &W, uint32_t r[4], uint32_t &s4, uint32_t &s5) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    uint32_t h = 0;
+    uint64_t a = (uint64_t)x0 * W.w[0];
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col3v(a, h, x1, W.w[1], x2, W.w[2], x3, W.w[3]);                 ZK_WSHIFT(r[0]);
+    col4v(a, h, x0, W.w[4], x1, W.w[5], x2, W.w[6], x3, W.w[7]);     ZK_WSHIFT(r[1]);
+    col4v(a, h, x0, W.w[8], x1, W.w[9], x2, W.w[10], x3, W.w[11]);   ZK_WSHIFT(r[2]);
+    col4v(a, h, x0, W.w[12], x1, W.w[13], x2, W.w[14], x3, W.w[15]); ZK_WSHIFT(r[3]);
+#undef ZK_WSHIFT
+    s4 = (uint32_t)a;
+    s5 = (uint32_t)(a >> 32);
+}
+// ra = A * WA, rb = B * WB (wave-uniform W sets, scalar loads)
+__device__ __forceinline__ void fe_mul_uniform2(fe A, const fe_ws &WA, fe B, const fe_ws &WB, fe &ra, fe &rb) {
+    uint32_t a[4], b[4], as4, as5, bs4, bs5;
+    ws_columns_s(A, WA, a, as4, as5);
+    ws_columns_s(B, WB, b, bs4, bs5);
+    ws_fold2(a, as4, as5, b, bs4, bs5, ra, rb);
+}
+// ... group-uniform W sets (vector loads)
+__device__ __forceinline__ void fe_mul_wsv2(fe A, const fe_ws &WA, fe B, const fe_ws &WB, fe &ra, fe &rb) {
+    uint32_t a[4], b[4], as4, as5, bs4, bs5;
+    ws_columns_v(A, WA, a, as4, as5);
+    ws_columns_v(B, WB, b, bs4, bs5);
+    ws_fold2(a, as4, as5, b, bs4, bs5, ra, rb);
+}
+
+// The pair forms where the kernel's register budget has room for them (F2: kernels.hip chooses per call site), else
+// the two products one after the other.  Same values.
+template <bool F2>
+__device__ __forceinline__ void mul_uniform_pair(fe A, const fe_ws &WA, fe B, const fe_ws &WB, fe &ra, fe &rb) {
+    if constexpr (F2) {
+        fe_mul_uniform2(A, WA, B, WB, ra, rb);
+    } else {
+        ra = fe_mul_uniform(A, WA);
+        rb = fe_mul_uniform(B, WB);
+    }
+}
+template <bool F2>
+__device__ __forceinline__ void mul_wsv_pair(fe A, const fe_ws &WA, fe B, const fe_ws &WB, fe &ra, fe &rb) {
+    if constexpr (F2) {
+        fe_mul_wsv2(A, WA, B, WB, ra, rb);
+    } else {
+        ra = fe_mul_wsv(A, WA);
+        rb = fe_mul_wsv(B, WB);
+    }
+}
+
 // ---- per-lane constant in two parts (32 B): a w = (a mod 2^64) w + (a >> 64) (w 2^64 mod p), a 193-bit sum
 // of two 64 x 128-bit products (five columns), one K-fold of its top 65 bits (H C = H K 2^32 - H), then
 // ws_fold's final step.  99 issue slots against fe_mul's 113 (tools/ubench/fmul_lab.hip v5): for per-lane
@@ -439,6 +524,60 @@ __device__ __forceinline__ fe fe_mul_w2(fe A, const fe_w2 &W) {
           "=&s"(sC)
         : "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(s5), "v"(s6), "v"(q0), "v"(q1), "v"(q2));
     return ws_fold(d0, e1, e2, e3, e4, 0u);
+}
+// two per-lane two-part products (fe_mul_w2) with their final reductions paired (ws_fold2)
+__device__ __forceinline__ void w2_head(fe A, const fe_w2 &W, uint32_t o[4], uint32_t &o4) {
+    const uint32_t x0 = lo32(A.lo), x1 = hi32(A.lo), x2 = lo32(A.hi), x3 = hi32(A.hi);
+    const uint32_t a0 = lo32(W.w.lo), a1 = hi32(W.w.lo), a2 = lo32(W.w.hi), a3 = hi32(W.w.hi);
+    const uint32_t b0 = lo32(W.w64.lo), b1 = hi32(W.w64.lo), b2 = lo32(W.w64.hi), b3 = hi32(W.w64.hi);
+    uint32_t r0, r1, r2, r3, r4, h = 0;
+    uint64_t a = (uint64_t)x0 * a0;
+#define ZK_WSHIFT(out) do { out = (uint32_t)a; a = (a >> 32) | ((uint64_t)h << 32); h = 0; } while (0)
+    col1(a, h, x2, b0);                          ZK_WSHIFT(r0);
+    col4(a, h, x0, a1, x1, a0, x2, b1, x3, b0);  ZK_WSHIFT(r1);
+    col4(a, h, x0, a2, x1, a1, x2, b2, x3, b1);  ZK_WSHIFT(r2);
+    col4(a, h, x0, a3, x1, a2, x2, b3, x3, b2);  ZK_WSHIFT(r3);
+    col2(a, h, x1, a3, x3, b3);                  ZK_WSHIFT(r4);
+#undef ZK_WSHIFT
+    const uint32_t s5 = (uint32_t)a, s6 = (uint32_t)(a >> 32);
+    const uint32_t K = 0x2d00u;
+    uint64_t q = (uint64_t)r4 * K;
+    const uint32_t q0 = lo32(q);
+    q = (uint64_t)s5 * K + (q >> 32);
+    const uint32_t q1 = lo32(q), q2 = hi32(q) + s6 * K;
+    uint32_t d1, d2, d3, dm;
+    uint64_t sB, sC;
+    asm("v_sub_co_u32 %0, %9, %11, %15\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32 %1, %9, %12, %16, %9\n\t"
+        "v_add_co_u32 %5, %10, %1, %18\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %2, %9, %13, %17, %9\n\t"
+        "v_addc_co_u32 %6, %10, %2, %19, %10\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %3, %9, %14, 0, %9\n\t"
+        "v_addc_co_u32 %7, %10, %3, %20, %10\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32 %4, %9, 0, 0, %9\n\t"
+        "v_addc_co_u32 %8, %10, %4, 0, %10"
+        : "=&v"(o[0]), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(dm), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o4),
+          "=&s"(sB), "=&s"(sC)
+        : "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(s5), "v"(s6), "v"(q0), "v"(q1), "v"(q2));
+}
+__device__ __forceinline__ void fe_mul_w2_2(fe A, const fe_w2 &WA, fe B, const fe_w2 &WB, fe &ra, fe &rb) {
+    uint32_t a[4], b[4], a4, b4;
+    w2_head(A, WA, a, a4);
+    w2_head(B, WB, b, b4);
+    ws_fold2(a, a4, 0u, b, b4, 0u, ra, rb);
+}
+template <bool F2>
+__device__ __forceinline__ void mul_w2_pair(fe A, const fe_w2 &WA, fe B, const fe_w2 &WB, fe &ra, fe &rb) {
+    if constexpr (F2) {
+        fe_mul_w2_2(A, WA, B, WB, ra, rb);
+    } else {
+        ra = fe_mul_w2(A, WA);
+        rb = fe_mul_w2(B, WB);
+    }
 }
 
 // ---- two butterflies' sums and differences at once: (a + b, a - b, c + d, c - d) mod p.  ZK_ADDSUB_ASM (default):

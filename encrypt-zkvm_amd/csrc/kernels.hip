@@ -116,6 +116,10 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
     constexpr int Q = TILE / 4;
     constexpr int h = 1 << (LG - 1);
     using L = Lds<LOGM, TILE>;
+    // paired final reductions (f128.hpp ws_fold2) only where the sums are plain and canonical (pass 2 and the odd
+    // splits): in the coset and lazy pass-1 rounds the pairs' extra live registers spill at the 64-VGPR budget
+    // (tools/isa_census.py), and the A/B of profiles/r06b_ab_fold2.txt found no gain to pay for that
+    constexpr bool F2 = !CT && !LZ;
     if constexpr (L::UNI && h <= 16) {
         constexpr int LH = LG - 1;
         const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), l = threadIdx.x & 63;
@@ -131,18 +135,26 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         fe t1 = x1, t3 = x3;
         if (!triv) {
             const fe_ws W1 = load_fe_ws(ws, CT ? h + j : j << (12 - LG));
-            t1 = fe_mul_uniform(x1, W1);
-            t3 = fe_mul_uniform(x3, W1);
+            mul_uniform_pair<F2>(x1, W1, x3, W1, t1, t3);
         } else if (LZ) {
             t1 = fe_canon(x1);
             t3 = fe_canon(x3);
         }
         fe a0, a1, a2, a3;
         addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        fe u2 = a2;
-        if (!triv) u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
-        else if (LZ) u2 = fe_canon(a2);
-        const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
+        fe u2 = a2, u3;
+        if constexpr (F2) {
+            const fe_ws W3 = load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG));
+            if (!triv) {
+                mul_uniform_pair<true>(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)), a3, W3, u2, u3);
+            } else {
+                u3 = fe_mul_uniform(a3, W3);
+            }
+        } else {
+            if (!triv) u2 = fe_mul_uniform(a2, load_fe_ws(ws, CT ? 2 * h + j : j << (11 - LG)));
+            else if (LZ) u2 = fe_canon(a2);
+            u3 = fe_mul_uniform(a3, load_fe_ws(ws, CT ? 3 * h + j : (j + h) << (11 - LG)));
+        }
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
@@ -168,11 +180,12 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
         const fe_ws W1 = ws[CT ? h + j : j << (12 - LG)];
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-        const fe t1 = fe_mul_wsv(x1, W1), t3 = fe_mul_wsv(x3, W1);
+        fe t1, t3;
+        mul_wsv_pair<F2>(x1, W1, x3, W1, t1, t3);
         fe a0, a1, a2, a3;
         addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        const fe u2 = fe_mul_wsv(a2, ws[CT ? 2 * h + j : j << (11 - LG)]);
-        const fe u3 = fe_mul_wsv(a3, ws[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+        fe u2, u3;
+        mul_wsv_pair<F2>(a2, ws[CT ? 2 * h + j : j << (11 - LG)], a3, ws[CT ? 3 * h + j : (j + h) << (11 - LG)], u2, u3);
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
@@ -190,11 +203,12 @@ __device__ __forceinline__ void r4_round(fe *s, const fe *tw4096, const fe_ws *w
         const int p = L::idx(line, grp * 4 * h + j), ph = L::at(p, h), p2h = L::at(p, 2 * h), p3h = L::at(p, 3 * h);
         const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
         const fe x0 = s[p], x1 = s[ph], x2 = s[p2h], x3 = s[p3h];
-        const fe t1 = fe_mul_w2(x1, w1), t3 = fe_mul_w2(x3, w1);
+        fe t1, t3;
+        mul_w2_pair<F2>(x1, w1, x3, w1, t1, t3);
         fe a0, a1, a2, a3;
         addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        const fe u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
-        const fe u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+        fe u2, u3;
+        mul_w2_pair<F2>(a2, w2t[CT ? 2 * h + j : j << (11 - LG)], a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)], u2, u3);
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
@@ -341,11 +355,12 @@ __device__ __forceinline__ void first_round_from(fe *s, Load load, const fe_ws *
         s[p3] = o3;
     } else {
         const fe_ws W1 = load_fe_ws(ws, 1);
-        const fe t1 = fe_mul_uniform(x1, W1), t3 = fe_mul_uniform(x3, W1);
+        fe t1, t3;
+        mul_uniform_pair<false>(x1, W1, x3, W1, t1, t3);
         fe a0, a1, a2, a3;
         addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-        const fe u2 = fe_mul_uniform(a2, load_fe_ws(ws, 2));
-        const fe u3 = fe_mul_uniform(a3, load_fe_ws(ws, 3));
+        fe u2, u3;
+        mul_uniform_pair<false>(a2, load_fe_ws(ws, 2), a3, load_fe_ws(ws, 3), u2, u3);
         fe o0, o1, o2, o3;
         addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);
         s[p] = o0;
@@ -367,11 +382,9 @@ __device__ __forceinline__ void last_round_to(const fe *s, const fe_ws *ws, cons
     fe t1, t3, u2, u3, a0, a1, a2, a3;
     // (W sets through vector loads for the 4 lanes of one j measured within noise: profiles/r04_ab_kernels_2p20.txt)
     const fe_w2 w1 = w2t[CT ? h + j : j << (12 - LG)];
-    t1 = fe_mul_w2(x1, w1);
-    t3 = fe_mul_w2(x3, w1);
+    mul_w2_pair<!CT && !LZ>(x1, w1, x3, w1, t1, t3);
     addsub2<LZ>(x0, t1, x2, t3, a0, a1, a2, a3);
-    u2 = fe_mul_w2(a2, w2t[CT ? 2 * h + j : j << (11 - LG)]);
-    u3 = fe_mul_w2(a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)]);
+    mul_w2_pair<!CT && !LZ>(a2, w2t[CT ? 2 * h + j : j << (11 - LG)], a3, w2t[CT ? 3 * h + j : (j + h) << (11 - LG)], u2, u3);
     fe o0, o1, o2, o3;
     addsub2<LZ>(a0, u2, a1, u3, o0, o2, o1, o3);  // LZ: the store canonicalises (a multiply or fe_canon)
     store(line, j, o0);

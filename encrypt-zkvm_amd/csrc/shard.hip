@@ -1569,6 +1569,9 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
     } shared;
     if (comm->measure) {
         for (auto *p : X.P) {
+            // (work the caller queued on a rank's own stream -- zk_vm_prove_sharded's trace rows -- completes first)
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            ZK_CHECK_HIP(hipStreamSynchronize(p->st));
             shared.P.push_back(p);
             shared.own.push_back(p->st);
         }

@@ -53,6 +53,17 @@ def _recv_msg(s: socket.socket) -> bytes:
     return bytes(_recv_exact(s, n)) if n else b""
 
 
+def _require_local(addr: str) -> None:
+    """Every rank runs on the MASTER_ADDR host (the rendezvous file lives in its temp directory and every listener
+    binds that address): fail at once, with the reason, instead of retrying to the deadline on another host."""
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as t:
+            t.bind((addr, 0))
+    except OSError as e:
+        raise RuntimeError(f"host group: MASTER_ADDR={addr} is not an address of this host ({e}); the torch-free host "
+                           f"group serves single-node runs only (one process per GPU of one node)") from None
+
+
 def _rdzv_file(addr: str, key: str) -> str:
     safe = "".join(ch if ch.isalnum() else "_" for ch in f"{addr}-{key}")
     return os.path.join(tempfile.gettempdir(), f"zkvm-hostgroup-{safe}")
@@ -70,6 +81,7 @@ class HostGroup:
         self._pool = ThreadPoolExecutor(max_workers=max(2, 2 * (world - 1))) if world > 1 else None
         if world == 1:
             return
+        _require_local(addr)
         deadline = time.monotonic() + timeout
         # every rank's own listener for the mesh connections of the ranks above it, on an ephemeral port -- created
         # only once rank 0's hub is bound (rank 0: after binding it; the others: after reaching it), so that no
@@ -94,6 +106,9 @@ class HostGroup:
                 c, _ = hub.accept()
                 c.settimeout(timeout)
                 try:
+                    # greet first: a rank that reached a stale port (a rendezvous file of an earlier run) learns at
+                    # once that no hub of this run answers there, and re-reads the file
+                    _send_msg(c, f"zkhub {nonce}".encode())
                     r, w, p, tok = _recv_msg(c).decode().split()
                 except Exception:
                     c.close()
@@ -158,20 +173,30 @@ class HostGroup:
                 except (OSError, ValueError):
                     time.sleep(0.05)
                     continue
-            c = None
+            c, greeted = None, False
             try:
                 c = socket.create_connection((addr, hub_port), timeout=5.0)
+                c.settimeout(5.0)  # the hub greets at once; a silent listener is not this run's hub
+                hello = _recv_msg(c).decode().split()
+                if len(hello) != 2 or hello[0] != "zkhub" or (port is None and hello[1] != tok):
+                    raise ConnectionError("host group: not this run's hub")
                 if lst is None:
                     lst = socket.create_server((addr, 0))
                     lst.settimeout(timeout)
                 _send_msg(c, f"{self.rank} {self.world} {lst.getsockname()[1]} {tok}".encode())
+                greeted = True  # (a timeout from here on is the other ranks', not a stale port)
                 c.settimeout(max(1.0, deadline - time.monotonic()))
                 table = [int(x) for x in _recv_msg(c).decode().split()]
                 if len(table) != self.world:
                     raise ConnectionError(f"host group: a table of {len(table)} ranks")
                 return c, table, lst
-            except socket.timeout:
-                raise TimeoutError(f"host group: rank {self.rank} waited for the other ranks past the deadline")
+            except socket.timeout as e:
+                if greeted:
+                    raise TimeoutError(f"host group: rank {self.rank} waited for the other ranks past the deadline")
+                last = e  # no greeting within 5 s: a stale rendezvous file's port; read the file again
+                if c is not None:
+                    c.close()
+                time.sleep(0.05)
             except (OSError, ConnectionError, ValueError) as e:
                 last = e
                 if c is not None:

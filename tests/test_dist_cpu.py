@@ -11,6 +11,7 @@ import json
 import os
 import socket
 import subprocess
+import time
 import sys
 from pathlib import Path
 
@@ -192,3 +193,46 @@ def test_numa_cpulist_parsing():
     before = os.sched_getaffinity(0)
     assert bench.bind_to_gpu_numa_node(0) is None
     assert os.sched_getaffinity(0) == before
+
+
+def test_host_group_refuses_an_address_of_another_host():
+    """every rank of the torch-free host group runs on the MASTER_ADDR host; another host's address fails
+    at once with the reason instead of retrying to the deadline."""
+    import time
+    from zkvm_amd.hostgroup import HostGroup
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="not an address of this host"):
+        HostGroup(1, 2, addr="192.0.2.1", rdzv_key="no-such-run", timeout=30)  # TEST-NET-1: never local
+    assert time.monotonic() - t0 < 5
+
+
+def test_host_group_skips_a_stale_rendezvous_port(tmp_path):
+    """A rendezvous file left by an earlier run can name a port that now belongs to a listener that accepts but never
+    answers: the connecting rank gives up on it within seconds (the hub greets first) and reads the file again."""
+    import threading
+    from zkvm_amd import hostgroup
+    from zkvm_amd.hostgroup import HostGroup
+    key = f"stale-{os.getpid()}"
+    silent = socket.create_server(("127.0.0.1", 0))  # accepts (backlog), never replies
+    path = hostgroup._rdzv_file("127.0.0.1", key)
+    with open(path, "w") as f:
+        f.write(f"{silent.getsockname()[1]} deadbeef00000000\n")
+    out = {}
+
+    def rank1():
+        try:
+            g = HostGroup(1, 2, addr="127.0.0.1", rdzv_key=key, timeout=60)
+            out[1] = g.all_gather(b"r1")
+            g.close()
+        except Exception as e:  # reported below
+            out[1] = e
+
+    t = threading.Thread(target=rank1)
+    t.start()
+    time.sleep(1.0)  # rank 1 has read the stale file and sits on the silent port
+    g0 = HostGroup(0, 2, addr="127.0.0.1", rdzv_key=key, timeout=60)
+    got0 = g0.all_gather(b"r0")
+    g0.close()
+    t.join(60)
+    silent.close()
+    assert got0 == [b"r0", b"r1"] and out[1] == [b"r0", b"r1"], out

@@ -213,8 +213,103 @@ __device__ __forceinline__ void {name}(uint32_t a[4], uint32_t b[4], uint32_t c[
     return fn, census
 
 
+def build_fold2():
+    """Two independent ws_fold reductions (f128.hpp): (r0..r3) + (s4 + s5 2^32) 2^128 mod p, in place in r."""
+    ins = []
+    for X in "AB":
+        R = lambda k: f"{X}{k}"  # noqa: E731
+        sB, sC, sD = f"{X}sB", f"{X}sC", f"{X}sD"
+        ins.append(Ins(f"v_subb_co_u32 {{{R(0)}}}, {{{sB}}}, {{{R(0)}}}, {{{X}s4}}, {{ones}}", vdst=(R(0),),
+                       vsrc=(R(0), f"{X}s4"), sdst=(sB,), ssrc=("ones",)))
+        ins.append(Ins(f"v_subb_co_u32 {{{R(1)}}}, {{{sB}}}, {{{R(1)}}}, {{{X}s5}}, {{{sB}}}", vdst=(R(1),),
+                       vsrc=(R(1), f"{X}s5"), sdst=(sB,), ssrc=(sB,)))
+        for k in (2, 3):
+            ins.append(Ins(f"v_subb_co_u32 {{{R(k)}}}, {{{sB}}}, {{{R(k)}}}, 0, {{{sB}}}", vdst=(R(k),), vsrc=(R(k),),
+                           sdst=(sB,), ssrc=(sB,)))
+        ins.append(Ins(f"v_subb_co_u32 {{{R(4)}}}, {{{sB}}}, 0, 0, {{{sB}}}", vdst=(R(4),), sdst=(sB,), ssrc=(sB,)))
+        ins.append(Ins(f"v_add_co_u32 {{{R(1)}}}, {{{sC}}}, {{{R(1)}}}, {{{X}m0}}", vdst=(R(1),), vsrc=(R(1), f"{X}m0"),
+                       sdst=(sC,)))
+        ins.append(Ins(f"v_addc_co_u32 {{{R(2)}}}, {{{sC}}}, {{{R(2)}}}, {{{X}m1}}, {{{sC}}}", vdst=(R(2),),
+                       vsrc=(R(2), f"{X}m1"), sdst=(sC,), ssrc=(sC,)))
+        for k in (3, 4):
+            ins.append(Ins(f"v_addc_co_u32 {{{R(k)}}}, {{{sC}}}, {{{R(k)}}}, 0, {{{sC}}}", vdst=(R(k),), vsrc=(R(k),),
+                           sdst=(sC,), ssrc=(sC,)))
+        ins.append(Ins(f"v_add_u32 {{{X}n}}, -1, {{{R(4)}}}", vdst=(f"{X}n",), vsrc=(R(4),)))
+        ins.append(Ins(f"v_and_b32 {{{X}c}}, 0x2cff, {{{X}n}}", vdst=(f"{X}c",), vsrc=(f"{X}n",)))
+        ins.append(Ins(f"v_sub_co_u32 {{{R(0)}}}, {{{sD}}}, {{{R(0)}}}, {{{X}n}}", vdst=(R(0),), vsrc=(R(0), f"{X}n"),
+                       sdst=(sD,)))
+        ins.append(Ins(f"v_subb_co_u32 {{{R(1)}}}, {{{sD}}}, {{{R(1)}}}, {{{X}c}}, {{{sD}}}", vdst=(R(1),),
+                       vsrc=(R(1), f"{X}c"), sdst=(sD,), ssrc=(sD,)))
+        for k in (2, 3):
+            ins.append(Ins(f"v_subb_co_u32 {{{R(k)}}}, {{{sD}}}, {{{R(k)}}}, 0, {{{sD}}}", vdst=(R(k),), vsrc=(R(k),),
+                           sdst=(sD,), ssrc=(sD,)))
+    return ins
+
+
+def lines_of(ins, seq):
+    lines, nop = [], 0
+    for i in seq + ["end"]:
+        if i is None:
+            nop += 1
+            continue
+        if nop:
+            lines.append(f"s_nop {nop - 1}")
+            nop = 0
+        if i != "end":
+            lines.append(ins[i].text)
+    return lines
+
+
+def emit_fold2():
+    ins = build_fold2()
+    seq = schedule(ins)
+    lines = lines_of(ins, seq)
+    ops = []  # (name, constraint, c expression)
+    for X, x in (("A", "a"), ("B", "b")):
+        ops += [(f"{X}{k}", "+v", f"{x}[{k}]") for k in range(4)]
+        ops += [(f"{X}4", "=&v", f"{x}4"), (f"{X}n", "=&v", f"{x}n"), (f"{X}c", "=&v", f"{x}c")]
+        ops += [(f"{X}s{t}", "=&s", f"{x}s{t}") for t in "BCD"]
+    ins_ops = []
+    for X, x in (("A", "a"), ("B", "b")):
+        ins_ops += [(f"{X}s4", "v", f"{x}s4"), (f"{X}s5", "v", f"{x}s5"), (f"{X}m0", "v", f"{x}m0"),
+                    (f"{X}m1", "v", f"{x}m1")]
+    ins_ops.append(("ones", "s", "ones"))
+    num = {o[0]: i for i, o in enumerate(ops + ins_ops)}
+    body = []
+    for ln in lines:
+        for o, i in sorted(num.items(), key=lambda kv: -len(kv[0])):
+            ln = ln.replace("{%s}" % o, f"%{i}")
+        body.append(ln)
+    census = {"instructions": sum(1 for x in seq if x is not None), "wait_states": sum(1 for x in seq if x is None),
+              "s_nop": sum(1 for ln in lines if ln.startswith("s_nop")),
+              "sgpr_touching": sum(1 for x in ins if (x.sdst or x.ssrc) and not x.salu)}
+    asm = "\n".join(f'        "{ln}\\n\\t"' for ln in body[:-1]) + f'\n        "{body[-1]}"'
+    outc = ", ".join(f'"{c}"({e})' for _, c, e in ops)
+    inc = ", ".join(f'"{c}"({e})' for _, c, e in ins_ops)
+    fn = f"""// ws_fold2_asm: two independent ws_fold reductions (f128.hpp) interleaved.  {census['instructions']} instructions,
+// {census['s_nop']} s_nop ({census['wait_states']} wait states), {census['sgpr_touching']} SGPR-touching VALU.  a, b: the low 128 bits
+// in, the reduced values out; (as4, as5), (bs4, bs5): the words above 2^128 (s5 < 2^3); am0 / am1, bm0 / bm1: the
+// low / high word of (s4 + 1) K + s5 K 2^32 (ws_fold's m0, m1).
+__device__ __forceinline__ void ws_fold2_asm(uint32_t a[4], uint32_t as4, uint32_t as5, uint32_t am0, uint32_t am1,
+                                             uint32_t b[4], uint32_t bs4, uint32_t bs5, uint32_t bm0, uint32_t bm1) {{
+    uint32_t a4, an, ac, b4, bn, bc;
+    uint64_t asB, asC, asD, bsB, bsC, bsD;
+    const uint64_t ones = ~0ull;
+#ifdef __HIP_DEVICE_COMPILE__  // (the host pass never emits this device function, but would parse "s"(ones) as x86's)
+    asm({asm}
+        : {outc}
+        : {inc});
+#endif
+}}
+"""
+    return fn, census
+
+
 def main():
     parts, cen = [], {}
+    fn, c = emit_fold2()
+    parts.append(fn)
+    cen["ws_fold2_asm"] = c
     for name, la, lc in (("addsub2_asm_cc", False, False), ("addsub2_asm_ll", True, True),
                          ("addsub2_asm_lc", True, False)):
         fn, c = emit(name, la, lc)
@@ -222,7 +317,8 @@ def main():
         cen[name] = c
     hdr = f"""// addsub_asm.hpp -- GENERATED by tools/gen_addsub_asm.py; do not edit.
 //
-// Two butterflies' sums and differences mod p in one asm block: on entry a, b, c, d (32-bit limbs, little
+// ws_fold2_asm: two multiplies' final reductions interleaved (their carry chains fill each other's wait states).
+// addsub2_asm_*: two butterflies' sums and differences mod p in one asm block: on entry a, b, c, d (32-bit limbs, little
 // endian); on exit a = a + b, S = a - b, c = c + d, D = c - d (b and d clobbered).  The four carry chains run
 // interleaved on their own SGPR pairs (list-scheduled; every gfx950 carry hazard checked by the generator), so
 // the wait states a carry hand-off needs are filled by the other chains instead of s_nop.  Sums are canonical
