@@ -17,6 +17,7 @@ struct zk_comm {
     int world = 1;
     int rank = 0;  // the rank this process drives (RCCL); loopback drives 0 .. world-1
     bool measure = false;  // loopback only: the serialised measurement mode (zk_comm_set_measure)
+    int split_rep = -1;    // zk_comm_set_trace_split: trace columns every rank interpolates itself (-1: by world)
     virtual ~zk_comm() {}
     virtual bool loopback() const = 0;
     // for every local rank l: send[l] holds `world` chunks of `bytes` (chunk d goes to rank d);

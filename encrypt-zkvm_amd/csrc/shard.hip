@@ -715,7 +715,20 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
         return ZK_OK;
     };
-    const int rounds = (nU + G - 1) / G;
+    // device-resident traces: the first `rep` columns of U are interpolated by every rank itself (no exchange), right
+    // after round 0's all-gather starts, so they fill the time it takes; the rest go round robin.  A host trace splits
+    // every column: replicating one would make every rank upload it.
+    int rep = 0;
+    if (!trace) {
+        // from the replayed schedules of 2^22 proofs (profiles/r06d_split_sweep_2p22.json): at
+        // G = 2 the link is the bound and replicating every column wins; from G = 4 on four columns hide round 0
+        const int dflt = G == 2 ? W : 4;
+        rep = std::min(nU, X.comm->split_rep >= 0 ? X.comm->split_rep : dflt);
+    }
+    const int nrep = rep;  // U[0 .. rep) replicated
+    int *US = U + rep;     // the split columns
+    const int nS = nU - rep;
+    const int rounds = (nS + G - 1) / G;
     std::vector<XH> hr(std::max(rounds, 1));
     std::vector<char> inplace_r(std::max(rounds, 1));
     // a round whose columns are not consecutive is gathered into a staging area, alternating between two buffers
@@ -723,10 +736,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     auto stage_of = [&](zk_prover *p, int k) { return (k & 1) ? p->comp : p->ctmp; };
     auto issue = [&](int k) -> int {  // interpolate this rank's column of round k, start the round's all-gather
         if (trace && k + 1 < rounds) ZK_TRY(upload(k + 1));
-        const int i0 = G * k, real = std::min(G, nU - i0), first = U[i0];
+        const int i0 = G * k, real = std::min(G, nS - i0), first = US[i0];
         // in place when the round's columns are consecutive (the padding slots of a short last round then land on
         // columns nobody interpolates -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns)
-        const bool inplace = U[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
+        const bool inplace = US[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
         inplace_r[k] = inplace;
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
@@ -738,44 +751,44 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 // (a device-side wait: a sharded rank's process holds one prover, so its compute, exchange and upload
                 // streams have hardware queues of their own and the host never blocks on the link)
                 ZK_CHECK_HIP(hipStreamWaitEvent(p->st, p->ev_up[k], 0));
-                if (i < nU && ((went_packed[l] >> U[i]) & 1u)) {
-                    const int q = narrow_of(l, U[i]);
+                if (i < nS && ((went_packed[l] >> US[i]) & 1u)) {
+                    const int q = narrow_of(l, US[i]);
                     NarrowCols one{};
                     one.count = 1;
-                    one.col[0] = U[i];
+                    one.col[0] = US[i];
                     one.width[0] = nar[l].width[q];
                     one.off[0] = nar[l].off[q];
                     one.last[0] = nar[l].last[q];
                     expand_narrow(p->st, reinterpret_cast<const uint8_t *>(CLDE(p)), one, n, p->d_trace);
                 }
             }
-            if (i < nU) {
+            if (i < nS) {
                 SparseCols g = spc[l];
-                g.col0 = U[i];
+                g.col0 = US[i];
                 g.fused = true;
-                ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)U[i] * n, n, p->polys + (size_t)U[i] * n, n, 1, true, nullptr,
+                ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)US[i] * n, n, p->polys + (size_t)US[i] * n, n, 1, true, nullptr,
                     &inv_n, p->tmp, trace && spp[l] ? &g : nullptr);
             }
-            snd[l] = inplace ? p->polys + (size_t)(first + X.rank[l]) * n : p->polys + (size_t)(i < nU ? U[i] : 0) * n;
+            snd[l] = inplace ? p->polys + (size_t)(first + X.rank[l]) * n : p->polys + (size_t)(i < nS ? US[i] : 0) * n;
             rcv[l] = inplace ? p->polys + (size_t)first * n : stage_of(p, k);
         }
         return xchg_start(X, "trace_coeffs", AG, snd, rcv, col, &hr[k]);
     };
     auto finish = [&](int k) -> int {  // wait for round k's coefficients, extend them over the local cosets
         ZK_TRY(xchg_wait(X, hr[k]));
-        const int i0 = G * k, real = std::min(G, nU - i0);
+        const int i0 = G * k, real = std::min(G, nS - i0);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             if (!inplace_r[k])
                 for (int g = 0; g < real; g++)
                     if (g != X.rank[l])
-                        ZK_CHECK_HIP(hipMemcpyAsync(p->polys + (size_t)U[i0 + g] * n, stage_of(p, k) + (size_t)g * n, col,
+                        ZK_CHECK_HIP(hipMemcpyAsync(p->polys + (size_t)US[i0 + g] * n, stage_of(p, k) + (size_t)g * n, col,
                                                     hipMemcpyDeviceToDevice, p->st));
             for (int a = 0; a < real;) {
                 int b = a + 1;
-                while (b < real && U[i0 + b] == U[i0 + b - 1] + 1) b++;
-                const int c0 = U[i0 + a];
+                while (b < real && US[i0 + b] == US[i0 + b - 1] + 1) b++;
+                const int c0 = US[i0 + a];
                 ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
                         p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
                 a = b;
@@ -785,6 +798,23 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     };
     if (trace && rounds) ZK_TRY(upload(0));
     if (rounds) ZK_TRY(issue(0));
+    if (nrep) {
+        ZK_TRY(sched_entry(X, 'K', -1));
+        for (int l = 0; l < nlp; l++) {
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            for (int a = 0; a < nrep;) {
+                int b = a + 1;
+                while (b < nrep && U[b] == U[b - 1] + 1) b++;
+                const int c0 = U[a];
+                ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, b - a, true, nullptr,
+                    &inv_n, p->tmp);
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
+                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+                a = b;
+            }
+        }
+    }
     for (int k = 0; k < rounds; k++) {
         if (k + 1 < rounds) ZK_TRY(issue(k + 1));
         ZK_TRY(finish(k));
@@ -1490,6 +1520,13 @@ int zk_comm_create_host(int rank, int world, zk_exchange_fn fn, void *ctx, zk_co
 }
 
 void zk_comm_destroy(zk_comm *c) { delete c; }
+
+int zk_comm_set_trace_split(zk_comm *c, int replicated) {
+    if (!c) ZK_FAIL(ZK_ERR_INVALID_ARG, "null communicator");
+    if (replicated < -1) ZK_FAIL(ZK_ERR_INVALID_ARG, "replicated columns: -1 (default) or a count");
+    c->split_rep = replicated;
+    return ZK_OK;
+}
 
 int zk_comm_set_measure(zk_comm *c, int on) {
     if (!c) ZK_FAIL(ZK_ERR_INVALID_ARG, "null communicator");

@@ -34,7 +34,7 @@ EXPORTED = (
     "zk_prove", "zk_prove_columns", "zk_prove_columns_ex", "zk_host_alloc", "zk_host_free", "zk_host_register",
     "zk_host_unregister", "zk_prove_device", "zk_lde_new", "zk_lde_read_frame", "zk_lde_query", "zk_lde_free",
     "zk_eval_constraints", "zk_commit_composition", "zk_comp_query", "zk_comp_free", "zk_prover_stage_times", "zk_prover_profile", "zk_prover_kernel_stats", "zk_prover_kernel_ops", "zk_prover_exchange_stats", "zk_prover_exchange_stats_ex", "zk_prover_shard_schedule", "zk_prover_upload_stats", "zk_prover_upload_derived", "zk_prover_set_upload_schedule", "zk_prover_proof_info", "zk_vm_trace",
-    "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_comm_set_measure", "zk_prove_sharded",
+    "zk_verify", "zk_comm_create_loopback", "zk_comm_unique_id", "zk_comm_create_rccl", "zk_comm_create_host", "zk_comm_destroy", "zk_comm_set_measure", "zk_comm_set_trace_split", "zk_prove_sharded",
     "zk_program_compile", "zk_program_trace", "zk_program_free", "zk_vm_last_error", "zk_vm_trace_device",
     "zk_vm_prove",
     "zk_vm_prove_sharded",
@@ -204,6 +204,7 @@ def lib():
         L.zk_comm_destroy.argtypes = [vp]
         L.zk_comm_destroy.restype = None
         L.zk_comm_set_measure.argtypes = [vp, i32]
+        L.zk_comm_set_trace_split.argtypes = [vp, i32]
         L.zk_prover_exchange_stats_ex.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                                   C.POINTER(C.c_double), C.POINTER(i32), i32, C.POINTER(i32)]
         L.zk_prover_shard_schedule.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]

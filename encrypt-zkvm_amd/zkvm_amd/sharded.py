@@ -142,6 +142,11 @@ class ShardedProver:
         so the schedule's segments are the ranks' compute alone (tools/shard_model.py); the proof bytes are unchanged."""
         check(lib().zk_comm_set_measure(self.comm, 1 if on else 0))
 
+    def set_trace_split(self, replicated: int = -1):
+        """zk_comm_set_trace_split: trace columns every rank interpolates itself when the trace is in every rank's HBM
+        (-1: the library's choice per world size); the proof bytes do not depend on it."""
+        check(lib().zk_comm_set_trace_split(self.comm, int(replicated)))
+
     def schedule(self) -> dict:
         """The last proof's schedule on local rank 0 (zk_prover_shard_schedule): exchange starts / waits in issue
         order and the measured compute segments between them."""

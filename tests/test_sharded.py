@@ -267,3 +267,47 @@ def test_sharded_host_column_hints(world, ext):
     finally:
         sp.close()
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_trace_split_and_measurement_mode_keep_the_bytes(world):
+    """Round 6: the trace interpolation of device-resident traces splits any number of columns round robin and
+    interpolates the rest on every rank (zk_comm_set_trace_split), and the exchanges overlap compute on a stream of
+    their own; the measurement mode serialises everything on one stream and logs the schedule.  Every split, both
+    modes and the vm::prove path give the single-GPU proof, and the schedule log accounts for every exchange."""
+    from zkvm_amd.prover import Program, vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(16, "cipher")
+    w = make_workload(src, seed=61)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    n = trace.shape[1]
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    g = GpuProver(0, max_trace_len=n)
+    try:
+        want = g.prove_host(trace, pub, ProofOptions())[0]
+    finally:
+        g.close()
+    prog = Program(src)
+    inp = Program.encode_inputs(w.public, w.secret, w.server_key)
+    sp = ShardedProver.loopback(world, max_trace_len=n)
+    try:
+        for measure in (False, True):
+            sp.set_measure(measure)
+            for rep in (-1, 0, 3, 28):
+                sp.set_trace_split(rep)
+                sp.upload_trace(trace)
+                assert sp.prove(None, pub, ProofOptions(), n=n)[0] == want, (measure, rep)
+                sc = sp.schedule()
+                starts = [e for e in sc["entries"] if "start" in e]
+                waits = {e["wait"] for e in sc["entries"] if "wait" in e}
+                assert sc["world"] == world and sc["measure"] == measure
+                assert {e["start"] for e in starts} == waits  # every exchange started is waited for
+                assert all(e["seg_ms"] >= 0 for e in sc["entries"] if "seg_ms" in e)
+                assert sp.prove_program(prog, inp, w.last_row)[2] == want, (measure, rep)
+            assert sp.prove(trace, pub, ProofOptions())[0] == want  # host trace: every column split
+        stats = sp.exchange_stats(exposed=True)
+        assert stats and all(len(v) == 4 and v[3] >= 0 for v in stats.values())
+    finally:
+        sp.close()
+        prog.close()

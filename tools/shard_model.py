@@ -135,6 +135,57 @@ def schedule_model(log_n, steps=3):
     return out
 
 
+def split_sweep(log_n, reps=(0, 2, 4, 6, 8, 12, 16, 28), steps=2):
+    """The replicated-column count of the trace interpolation (zk_comm_set_trace_split) swept per world size: the
+    device-trace and vm schedules in the measurement mode, replayed per rank (the library's default table comes from
+    this)."""
+    from zkvm_amd.prover import Program, ProofOptions, make_pub_inputs, vm_trace
+    from zkvm_amd.sharded import ShardedProver
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(log_n, "cipher")
+    w = make_workload(src, seed=1000)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    n = trace.shape[1]
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    prog = Program(src)
+    inp = Program.encode_inputs(w.public, w.secret, w.server_key)
+    out = {"log_n": log_n, "sweep": {}}
+    proofs = set()
+    for G in (2, 4, 8):
+        sp = ShardedProver.loopback(G, max_trace_len=n)
+        res = {}
+        try:
+            sp.set_measure(True)
+            for kind in ("device", "vm"):
+                for rep in reps:
+                    if kind == "vm" and rep > 12:
+                        continue
+                    sp.set_trace_split(rep)
+                    best = None
+                    for _ in range(steps + 1):
+                        if kind == "device":
+                            sp.upload_trace(trace)
+                            proofs.add(sp.prove(None, pub, ProofOptions(), n=n)[0])
+                        else:
+                            proofs.add(sp.prove_program(prog, inp, w.last_row)[2])
+                        sc = sp.schedule()
+                        tot = sum(e.get("seg_ms", 0.0) for e in sc["entries"])
+                        if best is None or tot < best[0]:
+                            best = (tot, sc)
+                    t, comp, x, exp_, lead = simulate(best[1], G)
+                    res.setdefault(kind, {})[rep] = {"per_rank_ms": round(t, 2), "compute_ms": round(comp, 2),
+                                                     "exchange_ms": round(x, 2), "exposed_ms": round(exp_, 2)}
+                    print(f"G={G} {kind} rep={rep}: {t:.2f} ms per rank (compute {comp:.2f}, exposed {exp_:.2f})",
+                          file=sys.stderr, flush=True)
+            sp.set_trace_split(-1)
+        finally:
+            sp.close()
+        out["sweep"][G] = res
+    prog.close()
+    assert len(proofs) == 1, "the split changed the proof bytes"
+    return out
+
+
 def project(schedules):
     """Per trace source and G: the replayed per-rank time with the code's overlap and with every exchange blocking, and
     the R / S fit of the serialised compute (sum of segments at G = G R + S)."""
@@ -173,6 +224,10 @@ def main():
         if any(k in res for k in ("stage_ms", "stage_ms_host", "stage_ms_vm")):
             out["stage_split"] = stage_split(res)
         print(json.dumps(out, indent=1))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "--sweep":
+        log_n = int(sys.argv[2]) if len(sys.argv) > 2 else 22
+        print(json.dumps(split_sweep(log_n)))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "--schedule":
         log_n = int(sys.argv[2]) if len(sys.argv) > 2 else 22
