@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(256, KE == 1 ? ZK_EVAL_WAVES : ZK_EVAL_WAVES_E
     ZK_SEQ(cb, t.lo);
     // divisors (per-row factors from divisor_tables): transition (x^n - 1)/((x - g^(n-2))(x - g^(n-1)));
     // boundary groups (x - 1) and (x - g^(n-2)).  res = t dT + bs0 d0 + bs1 d1 as one lazy sum.
-    const size_t P = CE;
+    const size_t P = map.dplane ? map.dplane : CE;
     const fe dT = divs[t_id];
     if constexpr (!BND) {
         comp[t_id] = fe_mul(t, dT);  // coset-major, like the divisor tables

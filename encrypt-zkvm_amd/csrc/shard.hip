@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -127,6 +128,16 @@ __global__ void __launch_bounds__(256) k_sh_hash_rows(const fe *base, int ncols,
     st_digest(send + 32 * pc.slot, h);
 }
 
+// leaf digests of one local coset's rows (coset pieces): row q of the coset at base[c * cs + q] -> send[q]
+__global__ void __launch_bounds__(256) k_sh_hash_coset(const fe *base, int ncols, int log_n, size_t cs, uint8_t *send) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= ((size_t)1 << log_n)) return;
+    const fe *p = base + t;
+    uint32_t h[8];
+    b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
+    st_digest(send + 32 * t, h);
+}
+
 // FRI layer-0 leaves of the local cosets: row r' = r + 8*q0 holds deep[j][q0 + k*m], m = n / fold (piece kp of K)
 __global__ void __launch_bounds__(256) k_sh_hash_fri0(const fe *deep, int log_n, int Bl, int fold, int log_m,
                                                       int log_mg, int log_K, int kp, uint8_t *send) {
@@ -161,6 +172,15 @@ __global__ void k_sh_pack(const fe *c, int log_n, int Bl, int log_kg, fe *send) 
     if (t >= ((size_t)Bl << log_n)) return;
     const size_t j = t >> log_n, k = t & (n - 1);
     send[((((k >> log_kg) * Bl) + j) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[t];
+}
+
+// one coset's coefficient slices (KX planes at plane_stride) for its all-to-all: send[d][plane][k'] = c[plane][d*kg + k']
+__global__ void k_sh_pack_coset(const fe *c, size_t plane_stride, int log_n, int KX, int log_kg, fe *send) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= (size_t)KX * n) return;
+    const size_t pln = t >> log_n, k = t & (n - 1);
+    send[((((k >> log_kg) * KX) + pln) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[pln * plane_stride + k];
 }
 
 // first FRI fold over the local cosets: row r' = r + 8*q0 (values deep[j][q0 + k*m]) -> out[j*m + q0]
@@ -392,11 +412,14 @@ int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd,
 
 // leaves (the hash kernel writes all-to-all order into the scratch), all-to-all, permute, subtree, roots.  The leaves go
 // out in K pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed; the permutes follow
-// the pieces' arrival.  hash(l, send, log_mg, log_K, k) launches piece k of local rank l.
+// the pieces' arrival.  hash(l, send, log_mg, log_K, k) launches piece k of local rank l.  Pieces are either position
+// ranges of every local coset (piece k: positions d mg + k mg / K + q''), or, with `prep` (coset pieces, round 6),
+// the local cosets themselves: prep(l, j) enqueues what coset j's rows need (its LDE) and hash(l, send, log_mg, -1, j)
+// hashes coset j's n rows into send[q] (row q goes to rank q / mg), so coset j's all-to-all runs under coset j + 1's LDE.
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
                 const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes, const char *digests_name,
-                const char *roots_name) {
+                const char *roots_name, const std::function<int(int, int)> &prep = nullptr) {
     const int nl = (int)X.P.size();
     T.M = M;
     T.G = X.G;
@@ -405,29 +428,35 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     T.nodes = nodes;
     const size_t mg = T.Mr / 8;  // positions per destination rank per coset
     const int log_mg = ilog2(mg);
-    const int log_K = mg >= 4 * 256 ? 2 : 0, K = 1 << log_K;  // pieces of at least 256 positions per coset
-    const int log_mgK = log_mg - log_K;
-    const size_t piece = 32 * (size_t)X.G * X.Bl << log_mgK;  // bytes of one piece (all destinations)
+    const bool by_coset = (bool)prep;
+    const int log_K = by_coset ? -1 : mg >= 4 * 256 ? 2 : 0;  // pieces of at least 256 positions per coset
+    const int K = by_coset ? X.Bl : 1 << log_K;
+    const int log_mgK = by_coset ? log_mg : log_mg - log_K;
+    const int Bp = by_coset ? 1 : X.Bl;                        // local cosets per piece
+    const size_t piece = 32 * (size_t)X.G * Bp << log_mgK;     // bytes of one piece (all destinations)
     std::vector<XH> h(K);
     std::vector<const void *> snd(nl);
     std::vector<void *> rcv(nl);
     for (int k = 0; k < K; k++) {
         for (int l = 0; l < nl; l++) {
             ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
+            if (by_coset) ZK_TRY(prep(l, k));
             hash(l, scratch[l] + k * piece, log_mg, log_K, k);
             snd[l] = scratch[l] + k * piece;
             rcv[l] = scratch[l] + 32 * T.Mr + k * piece;
         }
-        ZK_TRY(xchg_start(X, digests_name, A2A, snd, rcv, (32 * (size_t)X.Bl) << log_mgK, &h[k]));
+        ZK_TRY(xchg_start(X, digests_name, A2A, snd, rcv, (32 * (size_t)Bp) << log_mgK, &h[k]));
     }
     for (int k = 0; k < K; k++) {
         ZK_TRY(xchg_wait(X, h[k]));
         for (int l = 0; l < nl; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
+            // (coset piece k: local coset k of every source s is global coset s + G k, at leaf s + G k + 8 q')
+            uint8_t *dst = by_coset ? leaves[l] + 32 * (size_t)X.G * k : leaves[l] + (32 * (size_t)8 << log_mgK) * k;
             hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr / K, 256)), dim3(256), 0, p->st,
-                               (const uint8_t *)scratch[l] + 32 * T.Mr + k * piece, X.G, X.Bl, log_mgK, 32,
-                               (size_t)X.Bl << log_mgK, leaves[l] + (32 * (size_t)8 << log_mgK) * k);
+                               (const uint8_t *)scratch[l] + 32 * T.Mr + k * piece, X.G, Bp, log_mgK, 32,
+                               (size_t)Bp << log_mgK, dst);
         }
     }
     std::vector<const void *> rs(nl);
@@ -798,6 +827,21 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     };
     if (trace && rounds) ZK_TRY(upload(0));
     if (rounds) ZK_TRY(issue(0));
+    // every column replicated (no rounds) over several local cosets: the coset LDE runs coset by coset inside the
+    // commitment below (dist_commit's coset pieces), so each coset's digests travel under the next coset's LDE
+    const bool coset_major = rounds == 0 && nrep > 0 && Bl > 1;
+    // the LDE of the replicated columns U[0 .. nrep) over local coset slots [j0, j0 + nj)
+    auto lde_rep = [&](int l, int j0, int nj) {
+        zk_prover *p = X.P[l];
+        for (int a = 0; a < nrep;) {
+            int b = a + 1;
+            while (b < nrep && U[b] == U[b - 1] + 1) b++;
+            const int c0 = U[a];
+            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l] + G * j0, G, nj,
+                    p->lde + (size_t)c0 * Bl * n + (size_t)j0 * n, (size_t)Bl * n, n, p->tmp);
+            a = b;
+        }
+    };
     if (nrep) {
         ZK_TRY(sched_entry(X, 'K', -1));
         for (int l = 0; l < nlp; l++) {
@@ -809,10 +853,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 const int c0 = U[a];
                 ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, b - a, true, nullptr,
                     &inv_n, p->tmp);
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
-                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
                 a = b;
             }
+            if (!coset_major) lde_rep(l, 0, Bl);
         }
     }
     for (int k = 0; k < rounds; k++) {
@@ -925,11 +968,20 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         nd[l] = X.P[l]->nodes;
     }
     DistTree Ttrace;
+    std::function<int(int, int)> prep;
+    if (coset_major) prep = [&](int l, int j) {
+        lde_rep(l, j, 1);
+        return ZK_OK;
+    };
     ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
         zk_prover *p = X.P[l];
-        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, p->lde, W,
-                           log_n, Bl, log_mg, log_K, k, send);
-    }, scratch, lv, nd, "trace_digests", "trace_roots"));
+        if (log_K < 0)
+            hipLaunchKernelGGL(k_sh_hash_coset, dim3(cdiv(n, 256)), dim3(256), 0, p->st, p->lde + (size_t)k * n, W, log_n,
+                               (size_t)Bl * n, send);
+        else
+            hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, p->lde,
+                               W, log_n, Bl, log_mg, log_K, k, send);
+    }, scratch, lv, nd, "trace_digests", "trace_roots", prep));
     memcpy(R.trace_root, Ttrace.root, 32);
     stage_mark(P0, "trace_commit");
     coin.reseed(R.trace_root);
@@ -956,38 +1008,49 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         Fe8 zloc{};
         for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] + G * j];
         divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, p->tmp);
-        const EvalMap em{Bl, X.rank[l], G, 0, Bl};
-        if (KX == 1) {
-            ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
-            ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                                 (const AirConsts *)p->air_consts, p->comp, !bnd_split));
-        } else {
-            ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
-            ZK_CHECK_HIP(eval_constraints_ext_mapped(p->st, p->lde, log_n, em, pl->periodic, p->tmp,
-                                                     (const AirConsts *)p->x_air, (size_t)Bl * n, p->x_comp, !bnd_split));
-        }
+        if (KX == 1) ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
+        else ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
     }
-    stage_mark(P0, "constraints");
 
-    // S4: composition polynomial: per-coset inverse NTT, all-to-all of coefficient slices, cross-coset
-    // step on this rank's slice, all-gather of the C columns; then local coset LDE + commitment
+    // S3 + S4's first step, coset by coset (round 6): evaluate local coset j, inverse-transform it (KX planes), pack
+    // its coefficient slices [d][plane][k'] and start its all-to-all, which then runs under coset j + 1's evaluation
+    // instead of after the last one.  Piece j lands in the receive area [j][s][plane][k'] (after the KX*Bl*n
+    // evaluations in COMP); the NTT scratch and the send areas follow the divisor tables' 3 planes in p->tmp.
     const size_t kg = n / G;
-    XH hdeg;  // the degree flags' all-gather (read once the composition is committed)
-    {
+    const size_t recv0 = (size_t)KX * Bl * n;  // the receive area's offset in COMP
+    std::vector<XH> hs(Bl);
+    for (int j = 0; j < Bl; j++) {
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
+            Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            // planes are Bl columns each and contiguous: KX*Bl columns, sent as [d][plane*Bl + j][k']
-            ntt(p->st, X.pl[l]->Tn, COMP(p), n, CTMP(p), n, KX * Bl, true, nullptr, nullptr, p->tmp);
-            hipLaunchKernelGGL(k_sh_pack, dim3(cdiv((size_t)KX * Bl * n, 256)), dim3(256), 0, p->st, CTMP(p), log_n,
-                               KX * Bl, ilog2(kg), p->tmp);
-            snd[l] = p->tmp;
-            rcv[l] = COMP(p);
+            const EvalMap em{1, X.rank[l] + G * j, G, 0, Bl, (size_t)Bl * n};
+            if (KX == 1)
+                ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde + (size_t)j * n, log_n, em, pl->periodic,
+                                                     p->tmp + (size_t)j * n, (const AirConsts *)p->air_consts,
+                                                     p->comp + (size_t)j * n, !bnd_split));
+            else
+                ZK_CHECK_HIP(eval_constraints_ext_mapped(p->st, p->lde + (size_t)j * n, log_n, em, pl->periodic,
+                                                         p->tmp + (size_t)j * n, (const AirConsts *)p->x_air,
+                                                         (size_t)Bl * n, p->x_comp + (size_t)j * n, !bnd_split));
+            fe *scr = p->tmp + (size_t)3 * Bl * n, *send = scr + (size_t)KX * n * (1 + j);
+            ntt(p->st, pl->Tn, COMP(p) + (size_t)j * n, (size_t)Bl * n, CTMP(p) + (size_t)j * n, (size_t)Bl * n, KX, true,
+                nullptr, nullptr, scr);
+            hipLaunchKernelGGL(k_sh_pack_coset, dim3(cdiv((size_t)KX * n, 256)), dim3(256), 0, p->st,
+                               (const fe *)CTMP(p) + (size_t)j * n, (size_t)Bl * n, log_n, KX, ilog2(kg), send);
+            snd[l] = send;
+            rcv[l] = COMP(p) + recv0 + (size_t)j * KX * n;
         }
-        XH hs;
-        ZK_TRY(xchg_start(X, "comp_slices", A2A, snd, rcv, (size_t)KX * Bl * kg * sizeof(fe), &hs));
+        ZK_TRY(xchg_start(X, "comp_slices", A2A, snd, rcv, (size_t)KX * kg * sizeof(fe), &hs[j]));
+    }
+    stage_mark(P0, "constraints");
+
+    // S4: composition polynomial: the cross-coset step on this rank's slice, all-gather of the C columns; then local
+    // coset LDE + commitment
+    XH hdeg;  // the degree flags' all-gather (read once the composition is committed)
+    {
         // (the first plane's assertion quotient reads only the trace coefficients: it runs under the all-to-all)
         std::vector<const void *> bnd0(nlp);
         for (int l = 0; bnd_split && l < nlp; l++) {
@@ -996,7 +1059,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             bnd0[l] = boundary_range_begin(p->st, p->polys, log_n, KX == 1 ? K : Kp[0], K.g_last2, p->dscratch,
                                            (size_t)X.rank[l] * kg, kg);
         }
-        ZK_TRY(xchg_wait(X, hs));
+        for (XH &h : hs) ZK_TRY(xchg_wait(X, h));
         const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
         std::vector<const void *> fs(nlp);
         std::vector<void *> fr(nlp);
@@ -1006,7 +1069,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
             for (int pln = 0; pln < KX; pln++) {  // base column (c, pln) of E column c -> CTMP slice c*KX + pln
                 CrossMap cm;
-                for (int r = 0; r < 8; r++) cm.c[r] = COMP(p) + ((size_t)(r % G) * KX * Bl + pln * Bl + r / G) * kg;
+                for (int r = 0; r < 8; r++)  // global coset r = s + G j: piece j, source s
+                    cm.c[r] = COMP(p) + recv0 + ((size_t)(r / G) * G * KX + (size_t)(r % G) * KX + pln) * kg;
                 cm.k0 = (size_t)X.rank[l] * kg;
                 cm.kcount = kg;
                 cm.pstride = (size_t)KX * kg;

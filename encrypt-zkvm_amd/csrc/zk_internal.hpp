@@ -250,9 +250,11 @@ struct Fe8 {
 void divisor_tables(hipStream_t st, const NttTables &Tn, const fe *xr, int log_cos, int log_n, fe g1, fe g2,
                     const Fe8 &inv_zn, fe *out);
 // Which CE cosets one launch evaluates: local coset jl < nce is global CE coset ce0 + cestep*jl, and its
-// LDE rows are LDE coset slot jl << lshift of a buffer holding lde_cosets cosets per column.
+// LDE rows are LDE coset slot jl << lshift of a buffer holding lde_cosets cosets per column.  dplane: the stride of
+// the divisor tables' planes (0: nce * n, the launch's own cosets; a launch over one coset of several passes theirs).
 struct EvalMap {
     int nce, ce0, cestep, lshift, lde_cosets;
+    size_t dplane = 0;
 };
 // Rescue MDS / inverse-MDS __constant__ tables on the current device (once per device; thread-safe).
 // zk_prover_create calls it; the evaluator launches check it again (the plug point may run first).
