@@ -1303,14 +1303,14 @@ bool zk::clock_on() {
 
 int zk::plan_rank_tables(zk_prover *p, Plan *pl, int r0, int G) {
     if (p->shard_world <= 1 || !pl->lagr) return ZK_OK;  // a full prover's tables hold every coset
-    const int shift = ilog2((size_t)G);
-    if (pl->lagr_lde && pl->lde_r0 == r0 && pl->lde_shift == shift) return ZK_OK;
-    const size_t n = (size_t)1 << pl->log_n, Bl = ((size_t)1 << pl->log_b) >> shift;
+    const size_t n = (size_t)1 << pl->log_n, Bl = ((size_t)1 << pl->log_b) >> ilog2((size_t)G);
+    // the rank's block of cosets r0 .. r0 + Bl - 1 (shard.hip: rank g owns g Bl + j)
+    if (pl->lagr_lde && pl->lde_r0 == r0 && pl->lde_shift == 0 && pl->lde_cos == (int)Bl) return ZK_OK;
     if (!pl->lagr_lde) ZK_CHECK_HIP(p->arena.alloc(&pl->lagr_lde, Bl * n));
-    ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, r0, G, (int)Bl, pl->lagr_lde, Bl * n, n, p->tmp);
-    if (pl->id_lde) ntt_lde(p->st, pl->Tn, pl->ct, pl->id_poly, n, 1, r0, G, (int)Bl, pl->id_lde, Bl * n, n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, pl->lagr, n, 1, r0, 1, (int)Bl, pl->lagr_lde, Bl * n, n, p->tmp);
+    if (pl->id_lde) ntt_lde(p->st, pl->Tn, pl->ct, pl->id_poly, n, 1, r0, 1, (int)Bl, pl->id_lde, Bl * n, n, p->tmp);
     pl->lde_r0 = r0;
-    pl->lde_shift = shift;
+    pl->lde_shift = 0;
     pl->lde_cos = (int)Bl;
     ZK_CHECK_HIP(hipStreamSynchronize(p->st));
     return ZK_OK;

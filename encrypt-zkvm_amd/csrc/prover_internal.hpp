@@ -102,8 +102,8 @@ struct Plan {  // everything that depends only on (n, B)
     int lde_r0 = 0, lde_shift = 0, lde_cos = 0;
     size_t lde_slot(int r) const { return (size_t)((r - lde_r0) >> lde_shift); }
 };
-// A rank-sized prover's lagr_lde / id_lde over the cosets of rank r0 of G (r0 + G j): built on the first sharded proof
-// of the plan, rebuilt if the prover serves another rank
+// A rank-sized prover's lagr_lde / id_lde over its rank's block of B / G cosets r0 .. r0 + B / G - 1: built on the first
+// sharded proof of the plan, rebuilt if the prover serves another rank
 int plan_rank_tables(zk_prover *p, Plan *pl, int r0, int G);
 // the plan's cached boundary-divisor inverses, computed on first use (stream-ordered)
 // the evaluator's divisor tables for the 8 CE cosets (divisor_tables: 3 planes of 8n), built once per plan
@@ -239,6 +239,9 @@ struct zk_prover {
     fe *sh_xr = nullptr;        // 3 * w_N^r of the local cosets
     fe *sh_zero = nullptr;      // one zero chunk (stands in for openings another rank owns)
     uint8_t *sh_roots = nullptr;  // world subtree roots
+    // the block levels (0 .. log2 Bl) of the trace, composition and FRI layer-0 trees over this rank's cosets
+    // (shard.hip DistTree): (2 Bl - 1) x n digests for the row trees, (2 Bl - 1) x n / 2 for layer 0 (fold >= 2)
+    uint8_t *sh_blk = nullptr, *sh_cblk = nullptr, *sh_fblk = nullptr;
     unsigned *sh_flags = nullptr;  // world degree flags
     // FieldExtension::Quadratic working set (planar E buffers), allocated on first use
     fe *x_comp = nullptr, *x_ctmp = nullptr, *x_clde = nullptr, *x_deep = nullptr, *x_fri = nullptr,

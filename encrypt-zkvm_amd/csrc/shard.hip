@@ -1,14 +1,16 @@
 // shard.hip -- one proof with the LDE domain sharded by coset over `world` GPUs.
 //
-// Rank g of G owns the LDE cosets r = g + G*j, j < Bl = 8/G (blowup 8).  Per stage:
+// Rank g of G owns the LDE cosets r = g*Bl + j, j < Bl = 8/G (blowup 8; round 6: a block, so that the Merkle leaves
+// 8q + r of a group q that one rank holds are siblings).  Per stage:
 //   trace interpolation          host trace: split by column (a rank uploads and interpolates W/G columns,
 //                                round robin), in-place all-gathers of the coefficients; device trace: replicated
 //   trace LDE, constraint eval,  local: a coset's LDE is an independent size-n NTT, and constraint
 //   DEEP LDE, first FRI fold     row i+8 / a fold row {e[r' + k N/fold]} stay inside one coset
 //   OOD values, DEEP coefficients  split by coefficient range; all-gathers of partial sums / range totals and of
 //                                the quotient slices
-//   Merkle trees                 all-to-all of leaf digests into contiguous leaf ranges, a local
-//   (trace, composition, FRI 0)  subtree per rank, all-gather of the G subtree roots
+//   Merkle trees                 each rank hashes its leaves and their subtree up to its block of Bl siblings,
+//   (trace, composition, FRI 0)  all-to-all of the block nodes into contiguous ranges, a local subtree per rank,
+//                                all-gather of the G subtree roots
 //   composition interpolation    per-coset inverse NTT local; all-to-all of coefficient slices for the
 //                                cross-coset radix-8 step; all-gather of the 7 column polynomials
 //   FRI layers >= 1              all-gather of layer 1, then replicated (small)
@@ -21,7 +23,6 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
-#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -100,66 +101,109 @@ __device__ __forceinline__ void st_digest(uint8_t *dst, const uint32_t h[8]) {
     d[0] = make_uint4(h[0], h[1], h[2], h[3]);
     d[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
-// The leaf digests of a distributed tree go out in K pieces (dist_commit), so piece k's all-to-all runs while piece
-// k + 1 is hashed.  Rank d receives positions [d mg, (d+1) mg) of every coset; piece k covers positions
-// d mg + k mgK + q'' (q'' < mgK = mg / K) for every d.  Thread t of a piece -> (local coset j, destination d, q''), q''
-// fastest (coalesced column reads); its digest goes to the piece's slot [d][j][q''] (Bl mgK digests per destination).
-struct Piece {
-    size_t j, d, q, slot;
-};
-__device__ __forceinline__ Piece piece_of(size_t t, int log_G, int log_mg, int log_K, int k, int Bl) {
-    const int log_mgK = log_mg - log_K;
-    const size_t qq = t & (((size_t)1 << log_mgK) - 1), rest = t >> log_mgK;
-    const size_t d = rest & (((size_t)1 << log_G) - 1), j = rest >> log_G;
-    return {j, d, (d << log_mg) + ((size_t)k << log_mgK) + qq, ((d * Bl + j) << log_mgK) + qq};
+// Block ownership (round 6): rank g owns the cosets g Bl .. g Bl + Bl - 1, so in every group q of 8 consecutive leaves
+// 8q .. 8q + 7 (leaf 8q + r: row q of coset r) its Bl leaves are siblings: it hashes them and their subtree up to level
+// Lb = log2 Bl itself, and only that block node -- 1/Bl of the leaf digests -- crosses the link.  Each tree keeps the
+// levels 0 .. Lb of its own leaves in a block buffer (level l: node (q, i) at lvl_off(l) + q (Bl >> l) + i, for the
+// openings) and sends the block nodes out in K pieces: piece k holds, for every destination d, the groups
+// q = d QG + k QGK + q'' (QG = Q / G groups per destination, QGK = QG / K), in send order [d][q''].
+__device__ __forceinline__ size_t blk_group(size_t t, int log_QG, int log_K, int k) {
+    const int log_QGK = log_QG - log_K;
+    const size_t qq = t & (((size_t)1 << log_QGK) - 1), d = t >> log_QGK;
+    return (d << log_QG) + ((size_t)k << log_QGK) + qq;
+}
+// the Bl leaves of group q (leaf(j, h): local coset slot j), their subtree into blk, the block node into send_slot
+template <int BL, typename Leaf>
+__device__ __forceinline__ void blk_levels(size_t Q, size_t q, uint8_t *blk, uint8_t *send_slot, Leaf leaf) {
+    static_assert(BL == 1 || BL == 2 || BL == 4, "a sharded rank holds 1, 2 or 4 cosets");
+    uint32_t a[8];
+    leaf(0, a);
+    st_digest(blk + 32 * (q * BL), a);
+    if constexpr (BL >= 2) {
+        uint32_t b[8];
+        leaf(1, b);
+        st_digest(blk + 32 * (q * BL + 1), b);
+        b3::merge(a, b, a);
+        st_digest(blk + 32 * (Q * BL + q * (BL / 2)), a);
+        if constexpr (BL == 4) {
+            uint32_t c[8], d[8];
+            leaf(2, c);
+            st_digest(blk + 32 * (q * 4 + 2), c);
+            leaf(3, d);
+            st_digest(blk + 32 * (q * 4 + 3), d);
+            b3::merge(c, d, c);
+            st_digest(blk + 32 * (Q * 4 + q * 2 + 1), c);
+            b3::merge(a, c, a);
+            st_digest(blk + 32 * (Q * 6 + q), a);
+        }
+    }
+    st_digest(send_slot, a);
 }
 
-// leaf digests of the local LDE rows (column c, local coset j at base[(c*Bl + j)*n + q]): piece k of K, all-to-all order
-__global__ void __launch_bounds__(256) k_sh_hash_rows(const fe *base, int ncols, int log_n, int Bl, int log_mg,
-                                                      int log_K, int k, uint8_t *send) {
+// LDE rows (column c, local coset j at base[(c*Bl + j)*n + q]; Q = n groups): piece k of K
+template <int BL>
+__global__ void __launch_bounds__(256) k_sh_hash_rows_blk(const fe *base, int ncols, int log_n, int log_QG, int log_K,
+                                                          int k, uint8_t *blk, uint8_t *send) {
     const size_t n = (size_t)1 << log_n;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << (log_n - log_K))) return;
-    const Piece pc = piece_of(t, log_n - log_mg, log_mg, log_K, k, Bl);
-    const fe *p = base + pc.j * n + pc.q;
-    const size_t cs = (size_t)Bl * n;
-    uint32_t h[8];
-    b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
-    st_digest(send + 32 * pc.slot, h);
+    if (t >= (n >> log_K)) return;
+    const size_t q = blk_group(t, log_QG, log_K, k), cs = (size_t)BL * n;
+    blk_levels<BL>(n, q, blk, send + 32 * t, [&](int j, uint32_t h[8]) {
+        const fe *p = base + (size_t)j * n + q;
+        b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
+    });
 }
 
-// leaf digests of one local coset's rows (coset pieces): row q of the coset at base[c * cs + q] -> send[q]
-__global__ void __launch_bounds__(256) k_sh_hash_coset(const fe *base, int ncols, int log_n, size_t cs, uint8_t *send) {
+// FRI layer-0 leaves (Q = m groups): leaf (j, q0) holds deep[j][q0 + k m], k < fold (KX planes at stride Bl n)
+template <int BL, int KX>
+__global__ void __launch_bounds__(256) k_sh_hash_fri0_blk(const fe *deep, int log_n, int fold, int log_m, int log_QG,
+                                                          int log_K, int kp, uint8_t *blk, uint8_t *send) {
+    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)BL * n;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)1 << log_n)) return;
-    const fe *p = base + t;
-    uint32_t h[8];
-    b3::hash_elements(ncols, [&](int c) { return p[(size_t)c * cs]; }, h);
-    st_digest(send + 32 * t, h);
+    if (t >= (m >> log_K)) return;
+    const size_t q = blk_group(t, log_QG, log_K, kp);
+    blk_levels<BL>(m, q, blk, send + 32 * t, [&](int j, uint32_t h[8]) {
+        const fe *p = deep + (size_t)j * n + q;
+        if constexpr (KX == 1)
+            b3::hash_elements(fold, [&](int e) { return p[(size_t)e << log_m]; }, h);
+        else
+            b3::hash_elements(2 * fold, [&](int e) { return p[(size_t)(e & 1) * cs + ((size_t)(e >> 1) << log_m)]; }, h);
+    });
 }
 
-// FRI layer-0 leaves of the local cosets: row r' = r + 8*q0 holds deep[j][q0 + k*m], m = n / fold (piece kp of K)
-__global__ void __launch_bounds__(256) k_sh_hash_fri0(const fe *deep, int log_n, int Bl, int fold, int log_m,
-                                                      int log_mg, int log_K, int kp, uint8_t *send) {
-    const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
+template <int BL>
+static void launch_fri0_blk(hipStream_t st, int KX, const fe *deep, int log_n, int fold, int log_m, int log_QG,
+                            int log_K, int k, uint8_t *blk, uint8_t *send) {
+    const dim3 grid(cdiv(((size_t)1 << log_m) >> log_K, 256));
+    if (KX == 1)
+        hipLaunchKernelGGL((k_sh_hash_fri0_blk<BL, 1>), grid, dim3(256), 0, st, deep, log_n, fold, log_m, log_QG, log_K, k,
+                           blk, send);
+    else
+        hipLaunchKernelGGL((k_sh_hash_fri0_blk<BL, 2>), grid, dim3(256), 0, st, deep, log_n, fold, log_m, log_QG, log_K, k,
+                           blk, send);
+}
+
+// piece k's received block nodes [s][q''] -> the rank's level-Lb array in tree order: group q' = k QGK + q'' of source s
+// is node q' G + s (the block of coset owner s in group q')
+__global__ void k_sh_blk_place(const uint8_t *recv, int G, int log_QGK, int k, uint8_t *lv) {
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << (log_m - log_K))) return;
-    const Piece pc = piece_of(t, log_m - log_mg, log_mg, log_K, kp, Bl);
-    const fe *p = deep + pc.j * n + pc.q;
-    uint32_t h[8];
-    b3::hash_elements(fold, [&](int k) { return p[(size_t)k << log_m]; }, h);
-    st_digest(send + 32 * pc.slot, h);
+    if (t >= ((size_t)G << log_QGK)) return;
+    const size_t s = t >> log_QGK, qq = t & (((size_t)1 << log_QGK) - 1);
+    const uint4 *src = reinterpret_cast<const uint4 *>(recv + 32 * t);
+    uint4 *dst = reinterpret_cast<uint4 *>(lv + 32 * ((((size_t)k << log_QGK) + qq) * G + s));
+    dst[0] = src[0];
+    dst[1] = src[1];
 }
 
-// received chunks [s][j][q'] (source chunk s at item s * src_stride) -> natural order of this rank's
-// range: item (s + G*j) + 8*q'.  src_stride > Bl << log_mg when each source sent several planes.
+// all-gathered chunks [s][j][q'] (source chunk s at item s * src_stride) -> natural order: item (s Bl + j) + 8 q' (local
+// coset j of rank s is coset s Bl + j).  src_stride > Bl << log_mg when each source sent several planes.
 __global__ void k_sh_permute(const uint8_t *recv, int G, int Bl, int log_mg, int esize, size_t src_stride,
                              uint8_t *out) {
     const size_t per = (size_t)Bl << log_mg;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= per * G) return;
     const size_t s = t / per, rem = t % per, j = rem >> log_mg, qp = rem & (((size_t)1 << log_mg) - 1);
-    const size_t idx = (s + (size_t)G * j) + 8 * qp;
+    const size_t idx = (s * Bl + j) + 8 * qp;
     const uint4 *src = reinterpret_cast<const uint4 *>(recv + (s * src_stride + rem) * esize);
     uint4 *dst = reinterpret_cast<uint4 *>(out + idx * esize);
     for (int w = 0; w < esize / 16; w++) dst[w] = src[w];
@@ -191,7 +235,7 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= ((size_t)Bl << log_m)) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
-    const size_t rp = (size_t)(g + G * (int)j) + 8 * q0;  // row index in layer 0 (size N, wstride 1)
+    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;  // row index in layer 0 (size N, wstride 1)
     fe v[16];
     for (int k = 0; k < fold; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
     const fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
@@ -205,18 +249,6 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
 }
 
 // ---- FieldExtension::Quadratic versions: E buffers are planar with plane stride Bl*n (DEEP) / Bl*m (fold)
-__global__ void __launch_bounds__(256) k_sh_hash_fri0_ext(const fe *deep, int log_n, int Bl, int fold, int log_m,
-                                                          int log_mg, int log_K, int kp, uint8_t *send) {
-    const size_t n = (size_t)1 << log_n, cs = (size_t)Bl * n;
-    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << (log_m - log_K))) return;
-    const Piece pc = piece_of(t, log_m - log_mg, log_mg, log_K, kp, Bl);
-    const fe *p = deep + pc.j * n + pc.q;
-    uint32_t h[8];
-    b3::hash_elements(2 * fold, [&](int e) { return p[(size_t)(e & 1) * cs + ((size_t)(e >> 1) << log_m)]; }, h);
-    st_digest(send + 32 * pc.slot, h);
-}
-
 __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int G, int fold,
                                                           int log_m, const FoldConstsE *F, const fe *wi_lo,
                                                           const fe *wi_hi, fe *out) {
@@ -224,7 +256,7 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int lo
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= om) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
-    const size_t rp = (size_t)(g + G * (int)j) + 8 * q0;
+    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;
     fe va[16], vb[16];
     for (int k = 0; k < fold; k++) {
         va[k] = deep[j * n + q0 + ((size_t)k << log_m)];
@@ -256,30 +288,42 @@ __global__ void k_sh_suffix_carry(const fe *all, int G, int rank, int nc, fe *ou
 }
 
 // ---------------------------------------------------------------- a Merkle tree split over G ranks
-// M leaves in natural order; rank d holds leaves [d*M/G, (d+1)*M/G) and the subtree above them; the
-// top (G leaves = subtree roots) is kept on the host.
+// M leaves in natural order (leaf 8q + r: group q, coset r).  Levels 0 .. Lb (Lb = log2 Bl) live in each coset owner's
+// block buffer (blk_levels); above them rank d holds the subtree over level-Lb nodes [d Q, (d+1) Q) (Q = M / 8: its
+// level-Lb array `leaves` and the internal nodes `nodes`); the top (G subtree roots) is kept on the host.
 struct DistTree {
-    size_t M = 0, Mr = 0;
-    int G = 1;
-    std::vector<uint8_t *> leaves, nodes;            // per local rank
+    size_t M = 0, Mr = 0, Q = 0;
+    int G = 1, Bl = 1, Lb = 0;
+    std::vector<uint8_t *> blk, leaves, nodes;       // per local rank
     std::vector<std::array<uint8_t, 32>> top;        // heap nodes 1 .. 2G-1
     uint8_t root[32];
-    // chunk source of global heap node k (leaves are M + i): owner rank, buffer, byte offset; owner -1 =
-    // host top node (copied into `host`)
+    // chunk source of global leaf idx (is_node 0) or heap node idx (leaves are M + i): owner rank, buffer (0 the level-Lb
+    // array, 1 subtree nodes, 2 block buffer), byte offset; owner -1 = host top node (copied into `host`)
     struct Loc {
         int owner;
-        int which;  // 0 leaves, 1 nodes
+        int which;
         size_t off;
     };
+    size_t lvl_off(int l) const {  // level l's first node in a block buffer
+        size_t o = 0;
+        for (int t = 0; t < l; t++) o += Q * (size_t)(Bl >> t);
+        return o;
+    }
     Loc locate(int is_node, uint64_t idx) const {
-        if (!is_node) return {(int)(idx / Mr), 0, 32 * (idx % Mr)};
-        const uint64_t k = idx;
-        int L = 1;
-        while ((M >> L) > k) L++;
+        int L = 0;
+        uint64_t i = idx;
+        if (is_node) {
+            L = 1;
+            while ((M >> L) > idx) L++;
+            i = idx - (M >> L);
+        }
+        if (L <= Lb) {  // a block level: on the owner of the node's cosets
+            const uint64_t per = (uint64_t)8 >> L, bl = (uint64_t)Bl >> L, q = i / per, rr = i % per;
+            return {(int)(rr / bl), 2, 32 * (lvl_off(L) + q * bl + rr % bl)};
+        }
         const size_t c = Mr >> L;
-        if (c == 0) return {-1, 0, 32 * k};
-        const size_t mpos = k - (M >> L);
-        return {(int)(mpos / c), 1, 32 * (c + mpos % c)};
+        if (c == 0) return {-1, 0, 32 * idx};
+        return {(int)(i / c), 1, 32 * (c + i % c)};
     }
 };
 
@@ -410,53 +454,48 @@ int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd,
     return xchg_wait(X, h);
 }
 
-// leaves (the hash kernel writes all-to-all order into the scratch), all-to-all, permute, subtree, roots.  The leaves go
-// out in K pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed; the permutes follow
-// the pieces' arrival.  hash(l, send, log_mg, log_K, k) launches piece k of local rank l.  Pieces are either position
-// ranges of every local coset (piece k: positions d mg + k mg / K + q''), or, with `prep` (coset pieces, round 6),
-// the local cosets themselves: prep(l, j) enqueues what coset j's rows need (its LDE) and hash(l, send, log_mg, -1, j)
-// hashes coset j's n rows into send[q] (row q goes to rank q / mg), so coset j's all-to-all runs under coset j + 1's LDE.
+// the block levels (the hash kernel: leaves, their subtree up to Lb into blk, block nodes into the send scratch in piece
+// order), all-to-all of the block nodes, placed into the level-Lb array, subtree, roots.  The block nodes go out in K
+// pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed; the placements follow the
+// pieces' arrival.  hash(l, send, log_QG, log_K, k) launches piece k of local rank l.
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
-                const std::vector<uint8_t *> &leaves, const std::vector<uint8_t *> &nodes, const char *digests_name,
-                const char *roots_name, const std::function<int(int, int)> &prep = nullptr) {
+                const std::vector<uint8_t *> &blk, const std::vector<uint8_t *> &leaves,
+                const std::vector<uint8_t *> &nodes, const char *digests_name, const char *roots_name) {
     const int nl = (int)X.P.size();
     T.M = M;
     T.G = X.G;
     T.Mr = M / X.G;
+    T.Q = M / 8;
+    T.Bl = X.Bl;
+    T.Lb = ilog2((size_t)X.Bl);
+    T.blk = blk;
     T.leaves = leaves;
     T.nodes = nodes;
-    const size_t mg = T.Mr / 8;  // positions per destination rank per coset
-    const int log_mg = ilog2(mg);
-    const bool by_coset = (bool)prep;
-    const int log_K = by_coset ? -1 : mg >= 4 * 256 ? 2 : 0;  // pieces of at least 256 positions per coset
-    const int K = by_coset ? X.Bl : 1 << log_K;
-    const int log_mgK = by_coset ? log_mg : log_mg - log_K;
-    const int Bp = by_coset ? 1 : X.Bl;                        // local cosets per piece
-    const size_t piece = 32 * (size_t)X.G * Bp << log_mgK;     // bytes of one piece (all destinations)
+    const size_t Q = T.Q, QG = Q / X.G;  // groups per destination rank
+    const int log_QG = ilog2(QG);
+    const int log_K = QG >= 4 * 256 ? 2 : 0, K = 1 << log_K;  // pieces of at least 256 groups per destination
+    const int log_QGK = log_QG - log_K;
+    const size_t piece = 32 * (size_t)X.G << log_QGK;  // bytes of one piece (all destinations)
     std::vector<XH> h(K);
     std::vector<const void *> snd(nl);
     std::vector<void *> rcv(nl);
     for (int k = 0; k < K; k++) {
         for (int l = 0; l < nl; l++) {
             ZK_CHECK_HIP(hipSetDevice(X.P[l]->device));
-            if (by_coset) ZK_TRY(prep(l, k));
-            hash(l, scratch[l] + k * piece, log_mg, log_K, k);
+            hash(l, scratch[l] + k * piece, log_QG, log_K, k);
             snd[l] = scratch[l] + k * piece;
-            rcv[l] = scratch[l] + 32 * T.Mr + k * piece;
+            rcv[l] = scratch[l] + 32 * Q + k * piece;
         }
-        ZK_TRY(xchg_start(X, digests_name, A2A, snd, rcv, (32 * (size_t)Bp) << log_mgK, &h[k]));
+        ZK_TRY(xchg_start(X, digests_name, A2A, snd, rcv, (size_t)32 << log_QGK, &h[k]));
     }
     for (int k = 0; k < K; k++) {
         ZK_TRY(xchg_wait(X, h[k]));
         for (int l = 0; l < nl; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            // (coset piece k: local coset k of every source s is global coset s + G k, at leaf s + G k + 8 q')
-            uint8_t *dst = by_coset ? leaves[l] + 32 * (size_t)X.G * k : leaves[l] + (32 * (size_t)8 << log_mgK) * k;
-            hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(T.Mr / K, 256)), dim3(256), 0, p->st,
-                               (const uint8_t *)scratch[l] + 32 * T.Mr + k * piece, X.G, Bp, log_mgK, 32,
-                               (size_t)Bp << log_mgK, dst);
+            hipLaunchKernelGGL(k_sh_blk_place, dim3(cdiv(Q / K, 256)), dim3(256), 0, p->st,
+                               (const uint8_t *)scratch[l] + 32 * Q + k * piece, X.G, log_QGK, k, leaves[l]);
         }
     }
     std::vector<const void *> rs(nl);
@@ -464,8 +503,8 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     for (int l = 0; l < nl; l++) {
         zk_prover *p = X.P[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        merkle_tree(p->st, leaves[l], T.Mr, nodes[l]);
-        rs[l] = T.Mr >= 2 ? nodes[l] + 32 : leaves[l];
+        merkle_tree(p->st, leaves[l], Q, nodes[l]);
+        rs[l] = Q >= 2 ? nodes[l] + 32 : leaves[l];
         rr[l] = p->sh_roots;
     }
     ZK_TRY(xchg(X, roots_name, AG, rs, rr, 32));
@@ -818,7 +857,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 int b = a + 1;
                 while (b < real && US[i0 + b] == US[i0 + b - 1] + 1) b++;
                 const int c0 = US[i0 + a];
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l], G, Bl,
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l] * Bl, 1, Bl,
                         p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
                 a = b;
             }
@@ -827,21 +866,6 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     };
     if (trace && rounds) ZK_TRY(upload(0));
     if (rounds) ZK_TRY(issue(0));
-    // every column replicated (no rounds) over several local cosets: the coset LDE runs coset by coset inside the
-    // commitment below (dist_commit's coset pieces), so each coset's digests travel under the next coset's LDE
-    const bool coset_major = rounds == 0 && nrep > 0 && Bl > 1;
-    // the LDE of the replicated columns U[0 .. nrep) over local coset slots [j0, j0 + nj)
-    auto lde_rep = [&](int l, int j0, int nj) {
-        zk_prover *p = X.P[l];
-        for (int a = 0; a < nrep;) {
-            int b = a + 1;
-            while (b < nrep && U[b] == U[b - 1] + 1) b++;
-            const int c0 = U[a];
-            ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l] + G * j0, G, nj,
-                    p->lde + (size_t)c0 * Bl * n + (size_t)j0 * n, (size_t)Bl * n, n, p->tmp);
-            a = b;
-        }
-    };
     if (nrep) {
         ZK_TRY(sched_entry(X, 'K', -1));
         for (int l = 0; l < nlp; l++) {
@@ -853,9 +877,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 const int c0 = U[a];
                 ntt(p->st, X.pl[l]->Tn, p->d_trace + (size_t)c0 * n, n, p->polys + (size_t)c0 * n, n, b - a, true, nullptr,
                     &inv_n, p->tmp);
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c0 * n, n, b - a, X.rank[l] * Bl, 1, Bl,
+                        p->lde + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
                 a = b;
             }
-            if (!coset_major) lde_rep(l, 0, Bl);
         }
     }
     for (int k = 0; k < rounds; k++) {
@@ -893,7 +918,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                     g.all = true;  // fills only
                     ntt(p->st, X.pl[l]->Tn, p->polys + (size_t)c * n, n, p->polys + (size_t)c * n, n, e - c, true, nullptr,
                         &inv_n, p->tmp, &g);
-                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c * n, n, e - c, X.rank[l], G, Bl,
+                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->polys + (size_t)c * n, n, e - c, X.rank[l] * Bl, 1, Bl,
                             p->lde + (size_t)c * Bl * n, (size_t)Bl * n, n, p->tmp, &g);
                     c = e;
                 }
@@ -903,7 +928,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 const Plan *pl = X.pl[l];
                 axpy_fill(p->st, pl->id_poly, pl->lagr, d, n, p->polys);
                 for (int j = 0; j < Bl; j++) {
-                    const size_t r = (size_t)X.rank[l] + (size_t)G * j;
+                    const size_t r = (size_t)X.rank[l] * Bl + j;
                     axpy_fill(p->st, pl->id_lde + pl->lde_slot((int)r) * n, pl->lagr_lde + pl->lde_slot((int)r) * n, d,
                               n, p->lde + (size_t)j * n);
                 }
@@ -968,20 +993,19 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         nd[l] = X.P[l]->nodes;
     }
     DistTree Ttrace;
-    std::function<int(int, int)> prep;
-    if (coset_major) prep = [&](int l, int j) {
-        lde_rep(l, j, 1);
-        return ZK_OK;
+    // the row hashes of local rank l's cosets, piece k (Bl = 1, 2, 4 -> its template instance)
+    auto hash_rows = [&](int l, const fe *base, int ncols, uint8_t *blk, uint8_t *send, int log_QG, int log_K, int k) {
+        const dim3 grid(cdiv(n >> log_K, 256));
+        hipStream_t st = X.P[l]->st;
+        if (Bl == 4) hipLaunchKernelGGL(k_sh_hash_rows_blk<4>, grid, dim3(256), 0, st, base, ncols, log_n, log_QG, log_K, k, blk, send);
+        else if (Bl == 2) hipLaunchKernelGGL(k_sh_hash_rows_blk<2>, grid, dim3(256), 0, st, base, ncols, log_n, log_QG, log_K, k, blk, send);
+        else hipLaunchKernelGGL(k_sh_hash_rows_blk<1>, grid, dim3(256), 0, st, base, ncols, log_n, log_QG, log_K, k, blk, send);
     };
-    ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
-        zk_prover *p = X.P[l];
-        if (log_K < 0)
-            hipLaunchKernelGGL(k_sh_hash_coset, dim3(cdiv(n, 256)), dim3(256), 0, p->st, p->lde + (size_t)k * n, W, log_n,
-                               (size_t)Bl * n, send);
-        else
-            hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, p->lde,
-                               W, log_n, Bl, log_mg, log_K, k, send);
-    }, scratch, lv, nd, "trace_digests", "trace_roots", prep));
+    std::vector<uint8_t *> bk(nlp);
+    for (int l = 0; l < nlp; l++) bk[l] = X.P[l]->sh_blk;
+    ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
+        hash_rows(l, X.P[l]->lde, W, X.P[l]->sh_blk, send, log_QG, log_K, k);
+    }, scratch, bk, lv, nd, "trace_digests", "trace_roots"));
     memcpy(R.trace_root, Ttrace.root, 32);
     stage_mark(P0, "trace_commit");
     coin.reseed(R.trace_root);
@@ -1002,11 +1026,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         Plan *pl = X.pl[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
         fe xr[8];
-        for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] + G * j];
+        for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] * Bl + j];
         ZK_TRY(h2d_small(p, p->sh_xr, xr, Bl * sizeof(fe)));
         // divisor tables of the local CE cosets (3 planes of Bl*n) in the NTT scratch, free until S4
         Fe8 zloc{};
-        for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] + G * j];
+        for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] * Bl + j];
         divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, p->tmp);
         if (KX == 1) ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
         else ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
@@ -1026,7 +1050,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            const EvalMap em{1, X.rank[l] + G * j, G, 0, Bl, (size_t)Bl * n};
+            const EvalMap em{1, X.rank[l] * Bl + j, 1, 0, Bl, (size_t)Bl * n};
             if (KX == 1)
                 ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde + (size_t)j * n, log_n, em, pl->periodic,
                                                      p->tmp + (size_t)j * n, (const AirConsts *)p->air_consts,
@@ -1069,8 +1093,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             ZK_CHECK_HIP(hipMemsetAsync(p->flag, 0, 4, p->st));
             for (int pln = 0; pln < KX; pln++) {  // base column (c, pln) of E column c -> CTMP slice c*KX + pln
                 CrossMap cm;
-                for (int r = 0; r < 8; r++)  // global coset r = s + G j: piece j, source s
-                    cm.c[r] = COMP(p) + recv0 + ((size_t)(r / G) * G * KX + (size_t)(r % G) * KX + pln) * kg;
+                for (int r = 0; r < 8; r++)  // global coset r = s Bl + j: piece j, source s
+                    cm.c[r] = COMP(p) + recv0 + ((size_t)(r % Bl) * G * KX + (size_t)(r / Bl) * KX + pln) * kg;
                 cm.k0 = (size_t)X.rank[l] * kg;
                 cm.kcount = kg;
                 cm.pstride = (size_t)KX * kg;
@@ -1124,7 +1148,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys + (size_t)c0 * n, n, c1 - c0, X.rank[l], G, Bl,
+                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys + (size_t)c0 * n, n, c1 - c0, X.rank[l] * Bl, 1, Bl,
                         CLDE(p) + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
             }
         }
@@ -1134,11 +1158,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         nd[l] = X.P[l]->cnodes;
     }
     DistTree Tcomp;
-    ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
-        zk_prover *p = X.P[l];
-        hipLaunchKernelGGL(k_sh_hash_rows, dim3(cdiv(((size_t)Bl * n) >> log_K, 256)), dim3(256), 0, p->st, CLDE(p), CK,
-                           log_n, Bl, log_mg, log_K, k, send);
-    }, scratch, lv, nd, "comp_digests", "comp_roots"));
+    for (int l = 0; l < nlp; l++) bk[l] = X.P[l]->sh_cblk;
+    ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
+        hash_rows(l, CLDE(X.P[l]), CK, X.P[l]->sh_cblk, send, log_QG, log_K, k);
+    }, scratch, bk, lv, nd, "comp_digests", "comp_roots"));
     memcpy(R.constraint_root, Tcomp.root, 32);
     stage_mark(P0, "composition");
     unsigned degree_flag = 0;
@@ -1238,7 +1261,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             zk_prover *p = X.P[l];
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            lde_cosets(p->st, pl->Tn, pl->ct, Dk[l], n, X.rank[l], G, Bl, p->deep, p->tmp);  // local cosets g + G j
+            lde_cosets(p->st, pl->Tn, pl->ct, Dk[l], n, X.rank[l] * Bl, 1, Bl, p->deep, p->tmp);  // local cosets g Bl + j
         }
     } else {
         const fe2 z = coin.draw_ext(2), zg = fe2_mulb(z, g);
@@ -1273,7 +1296,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             Plan *pl = X.pl[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             for (int plane = 0; plane < 2; plane++)  // planar per rank: plane stride Bl * n
-                lde_cosets(p->st, pl->Tn, pl->ct, Dk[l] + plane * n, n, X.rank[l], G, Bl,
+                lde_cosets(p->st, pl->Tn, pl->ct, Dk[l] + plane * n, n, X.rank[l] * Bl, 1, Bl,
                            p->x_deep + (size_t)plane * Bl * n, p->tmp);
         }
     }
@@ -1318,17 +1341,18 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     } else {
         for (int l = 0; l < nlp; l++) {
             f0l[l] = (uint8_t *)X.P[l]->tmp;
-            f0n[l] = f0l[l] + 32 * (rows0 / G);
+            f0n[l] = f0l[l] + 32 * m;  // (the level-Lb array holds m = rows0 / 8 nodes)
+            bk[l] = X.P[l]->sh_fblk;
         }
-        ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_mg, int log_K, int k) {
+        ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
             zk_prover *p = X.P[l];
-            if (KX == 1)
-                hipLaunchKernelGGL(k_sh_hash_fri0, dim3(cdiv(((size_t)Bl * m) >> log_K, 256)), dim3(256), 0, p->st,
-                                   p->deep, log_n, Bl, (int)fold, log_m, log_mg, log_K, k, send);
-            else
-                hipLaunchKernelGGL(k_sh_hash_fri0_ext, dim3(cdiv(((size_t)Bl * m) >> log_K, 256)), dim3(256), 0, p->st,
-                                   p->x_deep, log_n, Bl, (int)fold, log_m, log_mg, log_K, k, send);
-        }, scratch, f0l, f0n, "fri0_digests", "fri0_roots"));
+            uint8_t *b = p->sh_fblk;
+            const int f = (int)fold;
+            const fe *d = KX == 1 ? p->deep : p->x_deep;
+            if (Bl == 4) launch_fri0_blk<4>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
+            else if (Bl == 2) launch_fri0_blk<2>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
+            else launch_fri0_blk<1>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
+        }, scratch, bk, f0l, f0n, "fri0_digests", "fri0_roots"));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
         {
@@ -1431,7 +1455,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     O.plans.push_back(plan_batch(N, pos));
     for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l]));
     // chunk requests: owner rank (-1: host top node), local buffer id, byte offset
-    enum { B_LDE, B_CLDE, B_DEEP, B_TL, B_TN, B_CL, B_CN, B_F0L, B_F0N, B_FRI };
+    enum { B_LDE, B_CLDE, B_DEEP, B_TL, B_TN, B_CL, B_CN, B_F0L, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B };
     struct Req {
         int owner, buf;
         size_t off;
@@ -1439,14 +1463,14 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     };
     std::vector<Req> req;
     auto lde_row = [&](int buf, int ncols, uint64_t i) {
-        const int r = (int)(i & 7), own = r % G, j = r / G;
+        const int r = (int)(i & 7), own = r / Bl, j = r % Bl;
         const size_t q = i >> 3;
         for (int c = 0; c < ncols; c++) req.push_back({own, buf, 16 * (((size_t)c * Bl + j) * n + q), nullptr});
     };
     for (size_t q = 0; q < nu; q++) lde_row(B_LDE, W, pos[q]);
     for (size_t q = 0; q < nu; q++) lde_row(B_CLDE, CK, pos[q]);
     for (uint64_t rp : (nl > 0 ? fri_pos[0] : std::vector<uint64_t>())) {
-        const int r = (int)(rp & 7), own = r % G, j = r / G;
+        const int r = (int)(rp & 7), own = r / Bl, j = r % Bl;
         const size_t q0 = rp >> 3;
         for (uint32_t k = 0; k < fold; k++)
             for (int pln = 0; pln < KX; pln++)
@@ -1464,7 +1488,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     const size_t off_dig = req.size();
     const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
-    const int tbuf[3][2] = {{B_TL, B_TN}, {B_CL, B_CN}, {B_F0L, B_F0N}};
+    const int tbuf[3][3] = {{B_TL, B_TN, B_TB}, {B_CL, B_CN, B_CB}, {B_F0L, B_F0N, B_F0B}};
     for (int b = 0; b < 2 + nl; b++)
         for (auto &path : O.plans[b].paths)
             for (auto &e : path) {
@@ -1481,8 +1505,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 } else {  // replicated FRI layers >= 1 (local rank 0 of every process, i.e. rank 0 serves)
                     const uint8_t *base = e.first ? layer_nodes[b - 2] : layer_leaves[b - 2];
                     const size_t off = (size_t)(base + 32 * e.second - P0->fri_dig);
-                    req.push_back({0, B_FRI + 1, off, nullptr});
-                    req.push_back({0, B_FRI + 1, off + 16, nullptr});
+                    req.push_back({0, B_FRI_DIG, off, nullptr});
+                    req.push_back({0, B_FRI_DIG, off + 16, nullptr});
                 }
             }
     const size_t NK = req.size();
@@ -1493,9 +1517,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
-            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
+            const uint8_t *bases[14] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
                                         p->leaves, p->nodes, p->cleaves, p->cnodes, f0l[l], f0n[l],
-                                        (const uint8_t *)FRI(p), p->fri_dig};
+                                        (const uint8_t *)FRI(p), p->fri_dig, p->sh_blk, p->sh_cblk, p->sh_fblk};
             std::vector<uint64_t> addr(NK);
             for (size_t t = 0; t < NK; t++) {
                 const Req &q = req[t];
@@ -1639,7 +1663,7 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
         ZK_CHECK_HIP(hipSetDevice(p->device));
         Plan *pl = nullptr;
         ZK_TRY(get_plan(p, n, 8, &pl));
-        ZK_TRY(plan_rank_tables(p, pl, X.rank[X.pl.size()], X.G));  // its fill tables over this rank's cosets
+        ZK_TRY(plan_rank_tables(p, pl, X.rank[X.pl.size()] * X.Bl, X.G));  // its fill tables over this rank's cosets
         X.pl.push_back(pl);
         if (opt->field_extension == 2) ZK_TRY(ensure_ext(p));
         if (!p->sh_buf) {
@@ -1649,6 +1673,11 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_roots, 32 * 8));
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_flags, 8));
             ZK_CHECK_HIP(hipMemset(p->sh_zero, 0, sizeof(fe)));
+            // a rank-sized prover's Bl cosets; a full prover may serve any G >= 2 (Bl <= 4)
+            const size_t bl = p->shard_world ? (size_t)8 / p->shard_world : 4, mn = p->max_n;
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_blk, 32 * (2 * bl - 1) * mn));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_cblk, 32 * (2 * bl - 1) * mn));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_fblk, 32 * (2 * bl - 1) * (mn / 2)));
         }
     }
     // one rank: nothing to shard or exchange, so the single-GPU path proves it (the same proof bytes; its

@@ -372,24 +372,25 @@ int vm_generate(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, const 
 // The preprocessed columns of (prog, lwe_size, blowup) on p's device (zk_program::Fixed), built on first use with
 // this call's inputs: the full trace with a zero last row, its columns 0..11 interpolated and extended, and the
 // Lagrange polynomial of the last row.  Returned by value (the cache may grow while the caller proves).
-// r0, rstride: the LDE cosets to hold (a sharded rank's r0 + rstride j, j < B / rstride; 0, 1 for all of them).
+// r0, ncos: the LDE cosets to hold (a sharded rank's block r0 .. r0 + ncos - 1; 0, 0 for all B of them).
 int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint32_t B, zk_program::Fixed *out,
-                  int r0 = 0, int rstride = 1) {
+                  int r0 = 0, int ncos = 0) {
+    if (!ncos) ncos = (int)B;
     std::lock_guard<std::mutex> lk(prog->mu);
     zk_program::Device *d = nullptr;
     ZK_TRY(device_program_locked(prog, p->device, &d));
     for (const auto &f : d->fixed)
-        if (f.L == in.L && f.B == B && f.r0 == r0 && f.rstride == rstride) {
+        if (f.L == in.L && f.B == B && f.r0 == r0 && f.ncos == ncos) {
             *out = f;
             return ZK_OK;
         }
     const size_t n = prog->P.trace_len;
-    const uint32_t nb = B / (uint32_t)rstride;  // cosets held
+    const uint32_t nb = (uint32_t)ncos;  // cosets held
     Plan *pl = nullptr;
     ZK_TRY(get_plan(p, n, B, &pl));
     // built in a local entry and cached only once complete: a call whose inputs the VM refuses (too few inputs, ...)
     // leaves no half-built entry behind for the program's later calls
-    zk_program::Fixed g{in.L, B, 0, nullptr, nullptr, nullptr, nullptr, r0, rstride};
+    zk_program::Fixed g{in.L, B, 0, nullptr, nullptr, nullptr, nullptr, r0, ncos};
     struct Unwind {
         zk_program::Fixed *g;
         ~Unwind() {
@@ -413,13 +414,13 @@ int fixed_columns(zk_prover *p, zk_program *prog, const zk::vm::Inputs &in, uint
     ZK_TRY(vm_generate(p, prog, in, zero, GenMode{true, NREG}, &nn, outs, &md, &dp));
     const fe inv_n = h_inv(fe_make(n));
     ntt(p->st, pl->Tn, p->d_trace, n, g.fpolys, n, 12, true, nullptr, &inv_n, p->tmp);
-    ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, r0, rstride, (int)nb, g.flde, nb * n, n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.fpolys, n, 12, r0, 1, (int)nb, g.flde, nb * n, n, p->tmp);
     // e_(n-1): zeros but a one in the last row
     ZK_CHECK_HIP(hipMemsetAsync(p->polys, 0, n * sizeof(fe), p->st));
     const fe one = fe_one();
     ZK_TRY(h2d_small(p, p->polys + (n - 1), &one, sizeof one));
     ntt(p->st, pl->Tn, p->polys, n, g.lagr, n, 1, true, nullptr, &inv_n, p->tmp);
-    ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, r0, rstride, (int)nb, g.lagr_lde, nb * n, n, p->tmp);
+    ntt_lde(p->st, pl->Tn, pl->ct, g.lagr, n, 1, r0, 1, (int)nb, g.lagr_lde, nb * n, n, p->tmp);
     ZK_TRY(io_rewind(p));  // sync: the cache is complete, the staging area starts over
     g.md = (int)md;
     d->fixed.push_back(g);  // freed by ~zk_program from here on
@@ -563,7 +564,8 @@ int zk_vm_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, zk_progr
         size_t nl = 0;
         if (pre) {
             zk_program::Fixed f{};
-            ZK_TRY(fixed_columns(provers[l], prog, in, opt->blowup, &f, shard_rank_of(comm, l), G));
+            const int bl = (int)opt->blowup / G;  // the rank's block of cosets
+            ZK_TRY(fixed_columns(provers[l], prog, in, opt->blowup, &f, shard_rank_of(comm, l) * bl, bl));
             uint32_t md = 0;
             ZK_TRY(vm_generate(provers[l], prog, in, last, GenMode{false, f.md}, &nl, outs, &md));
             if ((int)md != f.md) ZK_FAIL(ZK_ERR_INVALID_ARG, "internal error: the stack depth depends on the inputs");

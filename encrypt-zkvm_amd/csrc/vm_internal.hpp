@@ -73,8 +73,8 @@ struct zk_program {
         uint32_t L, B;
         int md;  // maximum stack depth
         fe *fpolys, *flde, *lagr, *lagr_lde;
-        // the LDE cosets held: r0 + rstride * j, j < B / rstride (a sharded rank's own cosets; 0, 1: all B)
-        int r0 = 0, rstride = 1;
+        // the LDE cosets held: r0 + j, j < ncos (a sharded rank's own block of B / G cosets; 0, B: all of them)
+        int r0 = 0, ncos = 0;
     };
     struct Device {
         int device;
