@@ -212,8 +212,9 @@ int zk_comp_query(zk_comp_commit *comp, const uint64_t *positions, size_t k, uin
 void zk_comp_free(zk_comp_commit *comp);
 
 /* ---- one proof sharded over several GPUs ----
- * The LDE domain is split by coset: rank g of `world` (1, 2, 4 or 8; blowup 8) owns cosets
- * r = g (mod world).  Exchanges (leaf digests, composition coefficient slices, FRI layer 1, openings)
+ * The LDE domain is split by coset: rank g of `world` (1, 2, 4 or 8; blowup 8) owns the block of cosets
+ * g * 8/world .. (g + 1) * 8/world - 1.  Exchanges (Merkle block nodes, composition coefficient slices, FRI layer 1,
+ * openings)
  * go through a zk_comm: RCCL over xGMI with one process per GPU (zk_comm_unique_id on rank 0,
  * shared out of band, then zk_comm_create_rccl on every rank), or an in-process loopback that drives
  * every rank from one process (tests; one prover per rank), or a caller transport (zk_comm_create_host).
