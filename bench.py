@@ -626,6 +626,7 @@ def main():
         out["runtime"] = native.runtime_info()
         if mixed is not None:
             mixed["vs_single_program"] = round(mixed["ms_per_proof"] / out["ms_per_step"], 4)
+            mixed["vs_programs_alone"] = round(mixed["ms_per_proof"] / ((out["ms_per_step"] + mixed["pushadd_alone_ms"]) / 2), 4)
         out["mixed_programs"] = mixed
     if out is not None and world == 1 and not args.no_compare and not args.ab:
         q = queues_leg(args, P)
@@ -760,9 +761,18 @@ def mixed_programs_leg(args, n, sets, provers, opts, pg, local):
     ms = 1e3 * run_proofs_timed(mfns, count, pg, local) / count
     redos = sum(g.proof_info()["hint_redos"] for g in provers) - redos0
     info = provers[0].proof_info()
+
+    # the push/add program alone, the same window: the mixed stream's cost against its two programs' own
+    # (vs_programs_alone = mixed / mean(headline, push/add alone); 1.0 = alternating costs nothing)
+    def bstep(k):
+        return lambda: provers[k].prove_host(tb, pb, opts)
+
+    bfns = [bstep(k) for k in range(P)]
+    run_proofs(bfns, P)
+    ms_b = 1e3 * run_proofs_timed(bfns, count, pg, local) / count
     hb.close()
     return {"ms_per_proof": round(ms, 3), "proofs": count, "hint_redos": redos,
-            "hint_sets_per_prover": info["hint_sets"],
+            "hint_sets_per_prover": info["hint_sets"], "pushadd_alone_ms": round(ms_b, 3),
             "programs": f"cipher mix (configs[2], {len(sets)} input sets) alternating with a 2^{args.log_n}-step "
                         f"push/add program, P = {P} in flight"}
 
