@@ -183,16 +183,22 @@ static void launch_fri0_blk(hipStream_t st, int KX, const fe *deep, int log_n, i
                            blk, send);
 }
 
-// piece k's received block nodes [s][q''] -> the rank's level-Lb array in tree order: group q' = k QGK + q'' of source s
-// is node q' G + s (the block of coset owner s in group q')
-__global__ void k_sh_blk_place(const uint8_t *recv, int G, int log_QGK, int k, uint8_t *lv) {
+// piece k's received block nodes [s][q''] (group q' = k QGK + q'' of source s is level-Lb node q' G + s of this rank's
+// subtree) merged straight into their parents: level Lb + 1 node q' G/2 + j = merge(node q' G + 2j, node q' G + 2j + 1),
+// into lvl1 (j fastest: the stores are contiguous, the loads 32-B runs of G/2 chunks)
+__global__ void k_sh_blk_merge(const uint8_t *recv, int G, int log_QGK, int k, uint8_t *lvl1) {
+    const int hg = G / 2, log_hg = G >= 4 ? (G >= 8 ? 2 : 1) : 0;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)G << log_QGK)) return;
-    const size_t s = t >> log_QGK, qq = t & (((size_t)1 << log_QGK) - 1);
-    const uint4 *src = reinterpret_cast<const uint4 *>(recv + 32 * t);
-    uint4 *dst = reinterpret_cast<uint4 *>(lv + 32 * ((((size_t)k << log_QGK) + qq) * G + s));
-    dst[0] = src[0];
-    dst[1] = src[1];
+    if (t >= ((size_t)hg << log_QGK)) return;
+    const size_t j = t & (size_t)(hg - 1), qq = t >> log_hg;
+    uint32_t l[8], r[8], h[8];
+    const uint4 *a = reinterpret_cast<const uint4 *>(recv + 32 * (((2 * j) << log_QGK) + qq));
+    const uint4 *c = reinterpret_cast<const uint4 *>(recv + 32 * (((2 * j + 1) << log_QGK) + qq));
+    const uint4 a0 = a[0], a1 = a[1], c0 = c[0], c1 = c[1];
+    l[0] = a0.x; l[1] = a0.y; l[2] = a0.z; l[3] = a0.w; l[4] = a1.x; l[5] = a1.y; l[6] = a1.z; l[7] = a1.w;
+    r[0] = c0.x; r[1] = c0.y; r[2] = c0.z; r[3] = c0.w; r[4] = c1.x; r[5] = c1.y; r[6] = c1.z; r[7] = c1.w;
+    b3::merge(l, r, h);
+    st_digest(lvl1 + 32 * ((((size_t)k << log_QGK) + qq) * hg + j), h);
 }
 
 // all-gathered chunks [s][j][q'] (source chunk s at item s * src_stride) -> natural order: item (s Bl + j) + 8 q' (local
@@ -289,16 +295,16 @@ __global__ void k_sh_suffix_carry(const fe *all, int G, int rank, int nc, fe *ou
 
 // ---------------------------------------------------------------- a Merkle tree split over G ranks
 // M leaves in natural order (leaf 8q + r: group q, coset r).  Levels 0 .. Lb (Lb = log2 Bl) live in each coset owner's
-// block buffer (blk_levels); above them rank d holds the subtree over level-Lb nodes [d Q, (d+1) Q) (Q = M / 8: its
-// level-Lb array `leaves` and the internal nodes `nodes`); the top (G subtree roots) is kept on the host.
+// block buffer (blk_levels); above them rank d holds the subtree over level-Lb nodes [d Q, (d+1) Q) (Q = M / 8), as a
+// heap `nodes` (level Lb + 1 at [Q/2, Q), ..., its root at 1); the top (G subtree roots) is kept on the host.
 struct DistTree {
     size_t M = 0, Mr = 0, Q = 0;
     int G = 1, Bl = 1, Lb = 0;
-    std::vector<uint8_t *> blk, leaves, nodes;       // per local rank
+    std::vector<uint8_t *> blk, nodes;               // per local rank
     std::vector<std::array<uint8_t, 32>> top;        // heap nodes 1 .. 2G-1
     uint8_t root[32];
-    // chunk source of global leaf idx (is_node 0) or heap node idx (leaves are M + i): owner rank, buffer (0 the level-Lb
-    // array, 1 subtree nodes, 2 block buffer), byte offset; owner -1 = host top node (copied into `host`)
+    // chunk source of global leaf idx (is_node 0) or heap node idx (leaves are M + i): owner rank, buffer (1 subtree
+    // nodes, 2 block buffer), byte offset; owner -1 = host top node (copied into `host`)
     struct Loc {
         int owner;
         int which;
@@ -372,7 +378,13 @@ static int pool_events(zk_prover *p, size_t k, size_t *first) {
     return ZK_OK;
 }
 static int exchange_stream(zk_prover *p, hipStream_t *out) {
-    if (!p->cst) ZK_CHECK_HIP(hipStreamCreateWithFlags(&p->cst, hipStreamNonBlocking));
+    if (!p->cst) {
+        // the highest priority the device offers: an RCCL collective's workgroups are dispatched ahead of the queued
+        // workgroups of the compute stream's long launches instead of behind them
+        int least = 0, greatest = 0;
+        ZK_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        ZK_CHECK_HIP(hipStreamCreateWithPriority(&p->cst, hipStreamNonBlocking, greatest));
+    }
     if (!p->ev_ready) ZK_CHECK_HIP(hipEventCreateWithFlags(&p->ev_ready, hipEventDisableTiming));
     *out = p->cst;
     return ZK_OK;
@@ -455,13 +467,13 @@ int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd,
 }
 
 // the block levels (the hash kernel: leaves, their subtree up to Lb into blk, block nodes into the send scratch in piece
-// order), all-to-all of the block nodes, placed into the level-Lb array, subtree, roots.  The block nodes go out in K
-// pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed; the placements follow the
-// pieces' arrival.  hash(l, send, log_QG, log_K, k) launches piece k of local rank l.
+// order), all-to-all of the block nodes, merged on arrival into level Lb + 1 of the subtree, the subtree, roots.  The
+// block nodes go out in K pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed.
+// hash(l, send, log_QG, log_K, k) launches piece k of local rank l.
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
-                const std::vector<uint8_t *> &blk, const std::vector<uint8_t *> &leaves,
-                const std::vector<uint8_t *> &nodes, const char *digests_name, const char *roots_name) {
+                const std::vector<uint8_t *> &blk, const std::vector<uint8_t *> &nodes, const char *digests_name,
+                const char *roots_name) {
     const int nl = (int)X.P.size();
     T.M = M;
     T.G = X.G;
@@ -470,7 +482,6 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     T.Bl = X.Bl;
     T.Lb = ilog2((size_t)X.Bl);
     T.blk = blk;
-    T.leaves = leaves;
     T.nodes = nodes;
     const size_t Q = T.Q, QG = Q / X.G;  // groups per destination rank
     const int log_QG = ilog2(QG);
@@ -494,8 +505,8 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
         for (int l = 0; l < nl; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            hipLaunchKernelGGL(k_sh_blk_place, dim3(cdiv(Q / K, 256)), dim3(256), 0, p->st,
-                               (const uint8_t *)scratch[l] + 32 * Q + k * piece, X.G, log_QGK, k, leaves[l]);
+            hipLaunchKernelGGL(k_sh_blk_merge, dim3(cdiv(Q / K / 2, 256)), dim3(256), 0, p->st,
+                               (const uint8_t *)scratch[l] + 32 * Q + k * piece, X.G, log_QGK, k, nodes[l] + 32 * (Q / 2));
         }
     }
     std::vector<const void *> rs(nl);
@@ -503,8 +514,8 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     for (int l = 0; l < nl; l++) {
         zk_prover *p = X.P[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        merkle_tree(p->st, leaves[l], Q, nodes[l]);
-        rs[l] = Q >= 2 ? nodes[l] + 32 : leaves[l];
+        merkle_tree(p->st, nodes[l] + 32 * (Q / 2), Q / 2, nodes[l]);  // (Q >= G >= 2)
+        rs[l] = nodes[l] + 32;
         rr[l] = p->sh_roots;
     }
     ZK_TRY(xchg(X, roots_name, AG, rs, rr, 32));
@@ -986,10 +997,9 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
     }
     stage_mark(P0, "trace_lde");
-    std::vector<uint8_t *> scratch(nlp), lv(nlp), nd(nlp);
+    std::vector<uint8_t *> scratch(nlp), nd(nlp);
     for (int l = 0; l < nlp; l++) {
         scratch[l] = X.P[l]->fri_dig;
-        lv[l] = X.P[l]->leaves;
         nd[l] = X.P[l]->nodes;
     }
     DistTree Ttrace;
@@ -1005,7 +1015,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     for (int l = 0; l < nlp; l++) bk[l] = X.P[l]->sh_blk;
     ZK_TRY(dist_commit(X, Ttrace, N, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
         hash_rows(l, X.P[l]->lde, W, X.P[l]->sh_blk, send, log_QG, log_K, k);
-    }, scratch, bk, lv, nd, "trace_digests", "trace_roots"));
+    }, scratch, bk, nd, "trace_digests", "trace_roots"));
     memcpy(R.trace_root, Ttrace.root, 32);
     stage_mark(P0, "trace_commit");
     coin.reseed(R.trace_root);
@@ -1025,13 +1035,21 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         zk_prover *p = X.P[l];
         Plan *pl = X.pl[l];
         ZK_CHECK_HIP(hipSetDevice(p->device));
-        fe xr[8];
-        for (int j = 0; j < Bl; j++) xr[j] = K.xr[X.rank[l] * Bl + j];
-        ZK_TRY(h2d_small(p, p->sh_xr, xr, Bl * sizeof(fe)));
-        // divisor tables of the local CE cosets (3 planes of Bl*n) in the NTT scratch, free until S4
-        Fe8 zloc{};
-        for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[X.rank[l] * Bl + j];
-        divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, p->tmp);
+        // divisor tables of the local CE cosets (3 planes of Bl*n): they depend on n and the cosets only, so the plan
+        // keeps them for the rank's next proofs (round 6: 0.26 ms per rank and proof at G = 8, 2^22)
+        const int r0 = X.rank[l] * Bl;
+        if (!pl->sh_divs || pl->sh_divs_r0 != r0 || pl->sh_divs_cos != Bl) {
+            if (pl->sh_divs && pl->sh_divs_cos < Bl) pl->sh_divs = nullptr;  // (a full prover serving a smaller world)
+            if (!pl->sh_divs) ZK_CHECK_HIP(p->arena.alloc(&pl->sh_divs, (size_t)3 * Bl * n));
+            fe xr[8];
+            for (int j = 0; j < Bl; j++) xr[j] = K.xr[r0 + j];
+            ZK_TRY(h2d_small(p, p->sh_xr, xr, Bl * sizeof(fe)));
+            Fe8 zloc{};
+            for (int j = 0; j < Bl; j++) zloc.v[j] = K.inv_zn[r0 + j];
+            divisor_tables(p->st, pl->Tn, p->sh_xr, ilog2(Bl), log_n, K.g_last1, K.g_last2, zloc, pl->sh_divs);
+            pl->sh_divs_r0 = r0;
+            pl->sh_divs_cos = Bl;
+        }
         if (KX == 1) ZK_TRY(h2d_small(p, p->air_consts, &K, sizeof K));
         else ZK_TRY(h2d_small(p, p->x_air, Kp, sizeof Kp));
     }
@@ -1039,7 +1057,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // S3 + S4's first step, coset by coset (round 6): evaluate local coset j, inverse-transform it (KX planes), pack
     // its coefficient slices [d][plane][k'] and start its all-to-all, which then runs under coset j + 1's evaluation
     // instead of after the last one.  Piece j lands in the receive area [j][s][plane][k'] (after the KX*Bl*n
-    // evaluations in COMP); the NTT scratch and the send areas follow the divisor tables' 3 planes in p->tmp.
+    // evaluations in COMP); the NTT scratch and the send areas are in p->tmp.
     const size_t kg = n / G;
     const size_t recv0 = (size_t)KX * Bl * n;  // the receive area's offset in COMP
     std::vector<XH> hs(Bl);
@@ -1053,13 +1071,13 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             const EvalMap em{1, X.rank[l] * Bl + j, 1, 0, Bl, (size_t)Bl * n};
             if (KX == 1)
                 ZK_CHECK_HIP(eval_constraints_mapped(p->st, p->lde + (size_t)j * n, log_n, em, pl->periodic,
-                                                     p->tmp + (size_t)j * n, (const AirConsts *)p->air_consts,
+                                                     pl->sh_divs + (size_t)j * n, (const AirConsts *)p->air_consts,
                                                      p->comp + (size_t)j * n, !bnd_split));
             else
                 ZK_CHECK_HIP(eval_constraints_ext_mapped(p->st, p->lde + (size_t)j * n, log_n, em, pl->periodic,
-                                                         p->tmp + (size_t)j * n, (const AirConsts *)p->x_air,
+                                                         pl->sh_divs + (size_t)j * n, (const AirConsts *)p->x_air,
                                                          (size_t)Bl * n, p->x_comp + (size_t)j * n, !bnd_split));
-            fe *scr = p->tmp + (size_t)3 * Bl * n, *send = scr + (size_t)KX * n * (1 + j);
+            fe *scr = p->tmp, *send = scr + (size_t)KX * n * (1 + j);
             ntt(p->st, pl->Tn, COMP(p) + (size_t)j * n, (size_t)Bl * n, CTMP(p) + (size_t)j * n, (size_t)Bl * n, KX, true,
                 nullptr, nullptr, scr);
             hipLaunchKernelGGL(k_sh_pack_coset, dim3(cdiv((size_t)KX * n, 256)), dim3(256), 0, p->st,
@@ -1153,15 +1171,12 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             }
         }
     }
-    for (int l = 0; l < nlp; l++) {
-        lv[l] = X.P[l]->cleaves;
-        nd[l] = X.P[l]->cnodes;
-    }
+    for (int l = 0; l < nlp; l++) nd[l] = X.P[l]->cnodes;
     DistTree Tcomp;
     for (int l = 0; l < nlp; l++) bk[l] = X.P[l]->sh_cblk;
     ZK_TRY(dist_commit(X, Tcomp, N, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
         hash_rows(l, CLDE(X.P[l]), CK, X.P[l]->sh_cblk, send, log_QG, log_K, k);
-    }, scratch, bk, lv, nd, "comp_digests", "comp_roots"));
+    }, scratch, bk, nd, "comp_digests", "comp_roots"));
     memcpy(R.constraint_root, Tcomp.root, 32);
     stage_mark(P0, "composition");
     unsigned degree_flag = 0;
@@ -1307,7 +1322,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     const int nl = fri_num_layers(N, opt);
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
-    std::vector<uint8_t *> f0l(nlp), f0n(nlp);
+    std::vector<uint8_t *> f0n(nlp);  // the layer-0 tree's subtree heap (m nodes) in the NTT scratch
     const size_t rows0 = N / fold;  // layer-0 Merkle leaves
     std::vector<const fe *> layer_vals(nl + 1);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
@@ -1340,8 +1355,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         ZK_TRY(remainder(rv));
     } else {
         for (int l = 0; l < nlp; l++) {
-            f0l[l] = (uint8_t *)X.P[l]->tmp;
-            f0n[l] = f0l[l] + 32 * m;  // (the level-Lb array holds m = rows0 / 8 nodes)
+            f0n[l] = (uint8_t *)X.P[l]->tmp;
             bk[l] = X.P[l]->sh_fblk;
         }
         ZK_TRY(dist_commit(X, Tfri0, rows0, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
@@ -1352,7 +1366,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             if (Bl == 4) launch_fri0_blk<4>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
             else if (Bl == 2) launch_fri0_blk<2>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
             else launch_fri0_blk<1>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
-        }, scratch, bk, f0l, f0n, "fri0_digests", "fri0_roots"));
+        }, scratch, bk, f0n, "fri0_digests", "fri0_roots"));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
         {
@@ -1455,7 +1469,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     O.plans.push_back(plan_batch(N, pos));
     for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l]));
     // chunk requests: owner rank (-1: host top node), local buffer id, byte offset
-    enum { B_LDE, B_CLDE, B_DEEP, B_TL, B_TN, B_CL, B_CN, B_F0L, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B };
+    enum { B_LDE, B_CLDE, B_DEEP, B_TN, B_CN, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B };
     struct Req {
         int owner, buf;
         size_t off;
@@ -1488,7 +1502,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     const size_t off_dig = req.size();
     const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
-    const int tbuf[3][3] = {{B_TL, B_TN, B_TB}, {B_CL, B_CN, B_CB}, {B_F0L, B_F0N, B_F0B}};
+    const int tbuf[3][3] = {{-1, B_TN, B_TB}, {-1, B_CN, B_CB}, {-1, B_F0N, B_F0B}};  // (DistTree::Loc::which)
     for (int b = 0; b < 2 + nl; b++)
         for (auto &path : O.plans[b].paths)
             for (auto &e : path) {
@@ -1517,8 +1531,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
-            const uint8_t *bases[14] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
-                                        p->leaves, p->nodes, p->cleaves, p->cnodes, f0l[l], f0n[l],
+            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
+                                        p->nodes, p->cnodes, f0n[l],
                                         (const uint8_t *)FRI(p), p->fri_dig, p->sh_blk, p->sh_cblk, p->sh_fblk};
             std::vector<uint64_t> addr(NK);
             for (size_t t = 0; t < NK; t++) {
