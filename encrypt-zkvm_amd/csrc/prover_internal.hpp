@@ -91,6 +91,10 @@ struct Plan {  // everything that depends only on (n, B)
     // 1 / ((x - 1)(x - g^(n-2))) over the CE domain (coset-major): the two boundary divisors
     // depend only on n, so they are inverted once per plan (first proof) and reused
     fe *bnd_inv = nullptr;
+    // ... and the same three planes over a sharded rank's block of cosets sh_divs_r0 .. + sh_divs_cos - 1 (shard.hip S3:
+    // built on the rank's first proof of this length, reused by the next)
+    fe *sh_divs = nullptr;
+    int sh_divs_r0 = -1, sh_divs_cos = 0;
     // four-step plans: the interpolant of e_(n-1) (n coefficients) and its coset LDE (B n, coset-major) -- what a
     // trace column that is zero but in its random last row interpolates and extends to, times that row (SparseCols)
     fe *lagr = nullptr, *lagr_lde = nullptr;
