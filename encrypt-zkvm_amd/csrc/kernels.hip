@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "blake3.hpp"
+#include "fri_small.hpp"
 #include "rescue_consts.hpp"
 #include "zk_internal.hpp"
 
@@ -2664,35 +2665,7 @@ void fri_coin_launch(hipStream_t st, uint32_t *seed_dev, const uint8_t *root_dev
 // ================================================================ FRI fold (K7)
 // next[r] = p_r(alpha), p_r of degree < fold interpolating the layer values at x_r * zeta^k:
 //   p_r(alpha) = (1/fold) * sum_m V_m (alpha / x_r)^m,  V_m = sum_k v_k zeta^(-k m)
-// V_m = sum_k v_k * zeta^(-k m), m < F: in-register radix-2 DIT on bit-reversed input (zinv[t] = zeta^-t);
-// the j = 0 twiddles are compile-time 1, so F = 8 costs 5 multiplies instead of 64.
-template <int F>
-__device__ __forceinline__ void idft_small(fe v[F], const fe *zinv) {
-    constexpr int LOGF = F == 2 ? 1 : F == 4 ? 2 : F == 8 ? 3 : 4;
-    fe w[F];
-#pragma unroll
-    for (int k = 0; k < F; k++) {
-        int r = 0;
-#pragma unroll
-        for (int b = 0; b < LOGF; b++) r |= ((k >> b) & 1) << (LOGF - 1 - b);
-        w[r] = v[k];
-    }
-#pragma unroll
-    for (int len = 2; len <= F; len <<= 1) {
-#pragma unroll
-        for (int start = 0; start < F; start += len) {
-#pragma unroll
-            for (int j = 0; j < len / 2; j++) {
-                const fe u = w[start + j];
-                const fe t = j == 0 ? w[start + j + len / 2] : fe_mul(w[start + j + len / 2], zinv[j * (F / len)]);
-                w[start + j] = fe_add(u, t);
-                w[start + j + len / 2] = fe_sub(u, t);
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < F; k++) v[k] = w[k];
-}
+// V_m = sum_k v_k * zeta^(-k m), m < F: idft_small (fri_small.hpp)
 
 // One FRI fold: row r = [e(r + k*rows)] at x_r * zeta^k -> the degree-respecting projection at alpha:
 // sum_m V_m (alpha / x_r)^m / F, with x_r = offset * w_L^r.

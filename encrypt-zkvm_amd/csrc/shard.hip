@@ -29,6 +29,7 @@
 
 #include "blake3.hpp"
 #include "comm.hpp"
+#include "fri_small.hpp"
 #include "host_pool.hpp"
 #include "prover_internal.hpp"
 
@@ -215,15 +216,6 @@ __global__ void k_sh_permute(const uint8_t *recv, int G, int Bl, int log_mg, int
     for (int w = 0; w < esize / 16; w++) dst[w] = src[w];
 }
 
-// coefficient slices for the cross-coset all-to-all: send[d][j][k'] = c[j][d*kg + k']
-__global__ void k_sh_pack(const fe *c, int log_n, int Bl, int log_kg, fe *send) {
-    const size_t n = (size_t)1 << log_n;
-    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= ((size_t)Bl << log_n)) return;
-    const size_t j = t >> log_n, k = t & (n - 1);
-    send[((((k >> log_kg) * Bl) + j) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[t];
-}
-
 // one coset's coefficient slices (KX planes at plane_stride) for its all-to-all: send[d][plane][k'] = c[plane][d*kg + k']
 __global__ void k_sh_pack_coset(const fe *c, size_t plane_stride, int log_n, int KX, int log_kg, fe *send) {
     const size_t n = (size_t)1 << log_n;
@@ -233,55 +225,74 @@ __global__ void k_sh_pack_coset(const fe *c, size_t plane_stride, int log_n, int
     send[((((k >> log_kg) * KX) + pln) << log_kg) + (k & (((size_t)1 << log_kg) - 1))] = c[pln * plane_stride + k];
 }
 
-// first FRI fold over the local cosets: row r' = r + 8*q0 (values deep[j][q0 + k*m]) -> out[j*m + q0]
-__global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n, int Bl, int g, int G, int fold,
-                                                      int log_m, const FoldConsts *F, const fe *wi_lo,
-                                                      const fe *wi_hi, fe *out) {
+// first FRI fold over the local cosets: row r' = r + 8*q0 (values deep[j][q0 + k*m]) -> out[j*m + q0], as the
+// single-GPU fold (kernels.hip k_fri_fold: idft_small, then Horner at beta = alpha / x_r')
+template <int F>
+__global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n, int Bl, int g, int log_m,
+                                                      const FoldConsts *Fc, const fe *wi_lo, const fe *wi_hi, fe *out) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= ((size_t)Bl << log_m)) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
     const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;  // row index in layer 0 (size N, wstride 1)
-    fe v[16];
-    for (int k = 0; k < fold; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
-    const fe beta = fe_mul(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
-    fe acc = fe_zero();
-    for (int mm = fold - 1; mm >= 0; mm--) {  // direct form: this fold runs once per proof on 1/G of layer 0
-        fe Vm = fe_zero();
-        for (int k = 0; k < fold; k++) Vm = fe_add(Vm, fe_mul(v[k], F->zinv[(k * mm) & (fold - 1)]));
-        acc = fe_add(fe_mul(acc, beta), Vm);
-    }
-    out[t] = fe_mul(acc, F->inv_fold);
+    fe v[F];
+#pragma unroll
+    for (int k = 0; k < F; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
+    const fe beta = fe_mul(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    idft_small<F>(v, Fc->zinv);
+    fe acc = v[F - 1];
+#pragma unroll
+    for (int mm = F - 2; mm >= 0; mm--) acc = fe_add(fe_mul(acc, beta), v[mm]);
+    out[t] = fe_mul(acc, Fc->inv_fold);
 }
 
 // ---- FieldExtension::Quadratic versions: E buffers are planar with plane stride Bl*n (DEEP) / Bl*m (fold)
-__global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int G, int fold,
-                                                          int log_m, const FoldConstsE *F, const fe *wi_lo,
-                                                          const fe *wi_hi, fe *out) {
+template <int F>
+__global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int log_m,
+                                                          const FoldConstsE *Fc, const fe *wi_lo, const fe *wi_hi,
+                                                          fe *out) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n, om = (size_t)Bl * m;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= om) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
     const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;
-    fe va[16], vb[16];
-    for (int k = 0; k < fold; k++) {
+    fe va[F], vb[F];
+#pragma unroll
+    for (int k = 0; k < F; k++) {
         va[k] = deep[j * n + q0 + ((size_t)k << log_m)];
         vb[k] = deep[cs + j * n + q0 + ((size_t)k << log_m)];
     }
-    const fe2 beta = fe2_mulb(F->alpha, fe_mul(F->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
-    fe2 acc = fe2_zero();
-    for (int mm = fold - 1; mm >= 0; mm--) {  // direct form per component, Horner in E
-        fe Va = fe_zero(), Vb = fe_zero();
-        for (int k = 0; k < fold; k++) {
-            const fe z = F->zinv[(k * mm) & (fold - 1)];
-            Va = fe_add(Va, fe_mul(va[k], z));
-            Vb = fe_add(Vb, fe_mul(vb[k], z));
-        }
-        acc = fe2_add(fe2_mul(acc, beta), fe2{Va, Vb});
-    }
-    acc = fe2_mulb(acc, F->inv_fold);
+    const fe2 beta = fe2_mulb(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    idft_small<F>(va, Fc->zinv);
+    idft_small<F>(vb, Fc->zinv);
+    fe2 acc = fe2{va[F - 1], vb[F - 1]};
+#pragma unroll
+    for (int mm = F - 2; mm >= 0; mm--) acc = fe2_add(fe2_mul(acc, beta), fe2{va[mm], vb[mm]});
+    acc = fe2_mulb(acc, Fc->inv_fold);
     out[t] = acc.a;
     out[om + t] = acc.b;
+}
+
+// the first fold's launch for fold 2 / 4 / 8 / 16 (KX planes)
+static void sh_fri_fold0(hipStream_t st, int KX, int fold, const fe *deep, int log_n, int Bl, int g, int log_m,
+                         const void *consts, const fe *wi_lo, const fe *wi_hi, fe *out) {
+    const dim3 grid(cdiv((size_t)Bl << log_m, 256));
+#define ZK_SH_FOLD(FF)                                                                                              \
+    do {                                                                                                            \
+        if (KX == 1)                                                                                                \
+            hipLaunchKernelGGL(k_sh_fri_fold0<FF>, grid, dim3(256), 0, st, deep, log_n, Bl, g, log_m,               \
+                               (const FoldConsts *)consts, wi_lo, wi_hi, out);                                      \
+        else                                                                                                        \
+            hipLaunchKernelGGL(k_sh_fri_fold0_ext<FF>, grid, dim3(256), 0, st, deep, log_n, Bl, g, log_m,           \
+                               (const FoldConstsE *)consts, wi_lo, wi_hi, out);                                     \
+    } while (0)
+    switch (fold) {
+        case 2: ZK_SH_FOLD(2); break;
+        case 4: ZK_SH_FOLD(4); break;
+        case 8: ZK_SH_FOLD(8); break;
+        default: ZK_SH_FOLD(16); break;
+    }
+#undef ZK_SH_FOLD
 }
 
 // the suffix carried into rank `rank`'s DEEP range: out[c] = sum over later ranks h of all[h * nc + c]
@@ -1386,18 +1397,11 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
-                if (KX == 1) {
-                    ZK_TRY(h2d_small(p, p->fold_consts, &F, sizeof F));
-                    hipLaunchKernelGGL(k_sh_fri_fold0, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st, p->deep, log_n,
-                                       Bl, X.rank[l], G, (int)fold, log_m, (const FoldConsts *)p->fold_consts,
-                                       X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, p->ctmp);
-                } else {
-                    ZK_TRY(h2d_small(p, p->x_fold_consts, &FE, sizeof FE));
-                    hipLaunchKernelGGL(k_sh_fri_fold0_ext, dim3(cdiv((size_t)Bl * m, 256)), dim3(256), 0, p->st,
-                                       p->x_deep, log_n, Bl, X.rank[l], G, (int)fold, log_m,
-                                       (const FoldConstsE *)p->x_fold_consts, X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi,
-                                       p->x_ctmp);
-                }
+                if (KX == 1) ZK_TRY(h2d_small(p, p->fold_consts, &F, sizeof F));
+                else ZK_TRY(h2d_small(p, p->x_fold_consts, &FE, sizeof FE));
+                sh_fri_fold0(p->st, KX, (int)fold, DEEP(p), log_n, Bl, X.rank[l], log_m,
+                             KX == 1 ? (const void *)p->fold_consts : (const void *)p->x_fold_consts,
+                             X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, CTMP(p));
                 snd[l] = CTMP(p);
                 rcv[l] = COMP(p);
             }
