@@ -931,14 +931,14 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
 
     elapsed = timed_loop(step_host, steps, warmup, pg, local)
     stages = sp.stage_times()
-    xchg_host = sp.exchange_stats()
+    xchg_host = sp.exchange_stats(exposed=True)
     sp.upload_trace(trace)
 
     def step_dev():
         last["proof_dev"] = sp.prove(None, pub, opts, n=n)[0]
 
     elapsed_dev = timed_loop(step_dev, steps, 1, pg, local)
-    xchg_dev = sp.exchange_stats()
+    xchg_dev = sp.exchange_stats(exposed=True)
     # vm::prove sharded (zk_vm_prove_sharded): every rank writes the trace into its own HBM from the program and the
     # inputs (its host runs the stack pass), then the same sharded proof -- no trace over PCIe or xGMI
     inp = Program.encode_inputs(w.public, w.secret, w.server_key)
@@ -974,20 +974,50 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
             "pin": pin["pin"] if pin else None, "proof_matches_pin": all_pin,
             "all_ranks_verified_by_zk_verify": all_verify,
             "exchange": exchange_record(xchg_host), "exchange_device_resident": exchange_record(xchg_dev),
+            "model": model_record(log_n, world, config5, {"host": 1e3 * elapsed / steps,
+                                                          "device": 1e3 * elapsed_dev / steps,
+                                                          "vm": 1e3 * elapsed_vm / steps}),
             "pub": pub, "proof": proof, "n": n, "min_sec": 128 if config5 else 95}
 
 
+SHARD_MODEL = "profiles/r06n_shard_schedule_2p22.json"
+
+
+def model_record(log_n, world, config5, measured):
+    """The one-GPU replay model's per-rank projection for this world size (tools/shard_model.py --schedule, committed
+    under profiles/) beside the measured ms per proof of each trace source, so a multi-GPU run checks the model."""
+    path = Path(__file__).resolve().parent / SHARD_MODEL
+    if config5 or not path.exists():
+        return None
+    d = json.loads(path.read_text())
+    if d.get("log_n") != log_n:
+        return None
+    out = {"source": SHARD_MODEL}
+    for kind, ms in measured.items():
+        pr = d.get("projection", {}).get(kind, {}).get(str(world))
+        if pr:
+            out[kind] = {"measured_ms": round(ms, 3), "modelled_per_rank_ms": pr["per_rank_ms"],
+                         "measured_over_modelled": round(ms / pr["per_rank_ms"], 3)}
+    return out
+
+
 def exchange_record(stats):
-    """Per collective of the last sharded proof on rank 0: ms (HIP events around it on the prover's stream, waiting
-    for peers included), MB received from the other ranks, calls, and the effective receive rate."""
+    """Per collective of the last sharded proof on rank 0: ms (HIP events around it on the exchange stream, waiting
+    for peers included), exposed ms (how long the compute stream waited for it, when the stats carry it), MB received
+    from the other ranks, calls, and the effective receive rate."""
     out = {}
-    for name, (ms, by, calls) in stats.items():
+    for name, v in stats.items():
+        ms, by, calls = v[0], v[1], v[2]
         out[name] = {"ms": round(ms, 3), "mb_received": round(by / 1e6, 3), "calls": calls,
                      "gb_per_s": round(by / 1e6 / ms, 2) if ms > 0 else None}
+        if len(v) > 3:
+            out[name]["exposed_ms"] = round(v[3], 3)
     tot_ms = sum(v[0] for v in stats.values())
     tot_b = sum(v[1] for v in stats.values())
     out["total"] = {"ms": round(tot_ms, 3), "mb_received": round(tot_b / 1e6, 3),
                     "gb_per_s": round(tot_b / 1e6 / tot_ms, 2) if tot_ms > 0 else None}
+    if any(len(v) > 3 for v in stats.values()):
+        out["total"]["exposed_ms"] = round(sum(v[3] for v in stats.values() if len(v) > 3), 3)
     return out
 
 

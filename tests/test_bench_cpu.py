@@ -42,6 +42,18 @@ def test_exchange_record():
     assert rec["trace_digests"] == {"ms": 2.0, "mb_received": 400.0, "calls": 1, "gb_per_s": 200.0}
     assert rec["total"]["mb_received"] == round((4e8 + 224) / 1e6, 3)
     assert bench.exchange_record({})["total"]["gb_per_s"] is None
+    # with the exposed time (zk_prover_exchange_stats_ex): per collective and summed
+    rec = bench.exchange_record({"a": (2.0, 4e8, 4, 0.5), "b": (1.0, 1e8, 1, 0.25)})
+    assert rec["a"]["exposed_ms"] == 0.5 and rec["total"]["exposed_ms"] == 0.75
+
+
+def test_model_record_reads_the_committed_projection():
+    rec = bench.model_record(22, 8, False, {"device": 22.0, "host": 11.0})
+    assert rec["source"] == bench.SHARD_MODEL
+    assert 5.0 < rec["device"]["modelled_per_rank_ms"] < 20.0
+    assert rec["device"]["measured_over_modelled"] == round(22.0 / rec["device"]["modelled_per_rank_ms"], 3)
+    assert bench.model_record(20, 8, False, {"device": 1.0}) is None  # other trace length: no projection
+    assert bench.model_record(22, 8, True, {"device": 1.0}) is None   # configs[4]: not modelled
 
 
 def test_all_ranks_true_single_process():
