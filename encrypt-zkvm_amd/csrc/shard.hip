@@ -1468,10 +1468,14 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     ZK_TRY(grind_and_positions(P0, coin, opt, N, R, pos));
     const size_t nu = pos.size();
     const auto fri_pos = fri_fold_positions(pos, N, fold, nl);
-    Openings O;
-    O.plans.push_back(plan_batch(N, pos));
-    O.plans.push_back(plan_batch(N, pos));
-    for (int l = 0; l < nl; l++) O.plans.push_back(plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l]));
+    // (the openings, their plans and the request list keep their storage across proofs: this host work sits on every
+    // rank's critical path, in the lead rank's segment, where fresh allocations cost page faults)
+    if (!P0->open) P0->open = new Openings();
+    Openings &O = *P0->open;
+    O.reset(2 + nl);
+    plan_batch(N, pos, O.plans[0]);
+    O.plans[1] = O.plans[0];  // the composition tree opens the same positions
+    for (int l = 0; l < nl; l++) plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l], O.plans[2 + l]);
     // chunk requests: owner rank (-1: host top node), local buffer id, byte offset
     enum { B_LDE, B_CLDE, B_DEEP, B_TN, B_CN, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B };
     struct Req {
@@ -1479,7 +1483,8 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         size_t off;
         const uint8_t *host;
     };
-    std::vector<Req> req;
+    static thread_local std::vector<Req> req;
+    req.clear();
     auto lde_row = [&](int buf, int ncols, uint64_t i) {
         const int r = (int)(i & 7), own = r / Bl, j = r % Bl;
         const size_t q = i >> 3;
@@ -1538,16 +1543,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
                                         p->nodes, p->cnodes, f0n[l],
                                         (const uint8_t *)FRI(p), p->fri_dig, p->sh_blk, p->sh_cblk, p->sh_fblk};
-            std::vector<uint64_t> addr(NK);
+            // (the prover's pinned staging: an asynchronous copy, no wait -- the next proof on this prover writes it again
+            // only after this one has drained)
+            uint64_t *addr = p->h_gather_idx;
             for (size_t t = 0; t < NK; t++) {
                 const Req &q = req[t];
                 addr[t] = (q.owner == X.rank[l]) ? (uint64_t)(uintptr_t)(bases[q.buf] + q.off)
                                                  : (uint64_t)(uintptr_t)p->sh_zero;
             }
             ZK_CHECK_HIP(hipSetDevice(p->device));
-            ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, addr.data(), NK * 8, hipMemcpyHostToDevice, p->st));
+            ZK_CHECK_HIP(hipMemcpyAsync(p->gather_idx, addr, NK * 8, hipMemcpyHostToDevice, p->st));
             gather_chunks(p->st, p->gather_idx, NK, p->gather_out);
-            ZK_CHECK_HIP(hipStreamSynchronize(p->st));  // addr is a host temporary
             snd[l] = p->gather_out;
             rcv[l] = p->sh_buf;
         }
@@ -1569,13 +1575,13 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         O.comp_rows.assign(got.begin() + off, got.begin() + off + nu * CK);
         off += nu * CK;
         for (int l = 0; l < nl; l++) {
-            O.fri_rows.emplace_back(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold * KX);
+            O.fri_rows[l].assign(got.begin() + off, got.begin() + off + fri_pos[l].size() * fold * KX);
             off += fri_pos[l].size() * fold * KX;
         }
         const uint8_t *dg = (const uint8_t *)(got.data() + off_dig);
         for (int b = 0; b < 2 + nl; b++) {
             const size_t bytes = 32 * O.plans[b].count();
-            O.digests.emplace_back(dg, dg + bytes);
+            O.digests[b].assign(dg, dg + bytes);
             dg += bytes;
         }
     }
