@@ -1336,6 +1336,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     std::vector<uint8_t *> f0n(nlp);  // the layer-0 tree's subtree heap (m nodes) in the NTT scratch
     const size_t rows0 = N / fold;  // layer-0 Merkle leaves
     std::vector<const fe *> layer_vals(nl + 1);
+    int lb1 = 0;  // layer 1's storage: natural (0) or coset-major over 8 cosets (3; FriLayout)
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
     std::vector<fe> rem_flat;
@@ -1403,16 +1404,20 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                              KX == 1 ? (const void *)p->fold_consts : (const void *)p->x_fold_consts,
                              X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, CTMP(p));
                 snd[l] = CTMP(p);
-                rcv[l] = COMP(p);
+                // (base field with layers after it: the gathered chunks [s][j][q0] are layer 1 coset-major -- coset
+                // s Bl + j, position q0 -- which the layer kernels read in place; over E each source's chunk holds both
+                // planes, and a last layer goes to the host in natural order)
+                rcv[l] = KX == 1 && nl > 1 ? FRI(p) : COMP(p);
             }
             ZK_TRY(xchg(X, "fri_layer1", AG, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
             ZK_TRY(lead_segment(X));  // from here the FRI layers >= 1 and the queries run on the lead rank alone
             ZK_CHECK_HIP(hipSetDevice(P0->device));
-            for (int pln = 0; pln < KX; pln++)
+            for (int pln = 0; !(KX == 1 && nl > 1) && pln < KX; pln++)
                 hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st,
                                    (const uint8_t *)(COMP(P0) + (size_t)pln * Bl * m), G, Bl, log_m, 16,
                                    (size_t)KX * Bl * m, (uint8_t *)(FRI(P0) + pln * rows0));
         }
+        lb1 = KX == 1 && nl > 1 ? 3 : 0;
         layer_vals[1] = FRI(P0);
         layer_len[1] = rows0;
         {
@@ -1436,11 +1441,12 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 layer_leaves[l] = dig;
                 layer_nodes[l] = dig + 32 * rows;
                 dig += 64 * rows;
-                if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
-                else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l]);
+                const int lb = l == 1 ? lb1 : 0;  // layer 1 as gathered (coset-major over 8 cosets, base field)
+                if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
+                else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
                 fri_coin_launch(P0->st, (uint32_t *)P0->fri_seed, layer_nodes[l] + 32, KX, alpha_dev, P0->fri_alphas + 2 * l);
-                if (KX == 1) fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next);
-                else fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L, next);
+                if (KX == 1) fri_fold_launch(P0->st, layer_vals[l], L, (int)fold, P0->fold_consts, X.pl[0]->TN, N / L, next, lb);
+                else fri_fold_ext_launch(P0->st, layer_vals[l], L, (int)fold, P0->x_fold_consts, X.pl[0]->TN, N / L, next, lb);
                 layer_vals[l + 1] = next;
                 layer_len[l + 1] = rows;
                 next += KX * rows;
@@ -1501,13 +1507,15 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     for (int l = 1; l < nl; l++) {
         const size_t L = layer_len[l], rows = L / fold;
+        const int lb = l == 1 ? lb1 : 0, lcn = ilog2(L) - lb;
         for (uint64_t r : fri_pos[l])
             for (uint32_t k = 0; k < fold; k++)
-                for (int pln = 0; pln < KX; pln++)
+                for (int pln = 0; pln < KX; pln++) {
+                    const size_t i = r + k * rows, at = ((i & (((size_t)1 << lb) - 1)) << lcn) + (i >> lb);
                     req.push_back({0, B_FRI,
-                                   (size_t)((const uint8_t *)(layer_vals[l] + pln * L + r + k * rows) -
-                                            (const uint8_t *)FRI(P0)),
+                                   (size_t)((const uint8_t *)(layer_vals[l] + pln * L + at) - (const uint8_t *)FRI(P0)),
                                    nullptr});
+                }
     }
     const size_t off_dig = req.size();
     const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
