@@ -980,7 +980,7 @@ def sharded_leg(args, log_n, world, rank, local, pg, steps, warmup, config5=Fals
             "pub": pub, "proof": proof, "n": n, "min_sec": 128 if config5 else 95}
 
 
-SHARD_MODEL = "profiles/r06n_shard_schedule_2p22.json"
+SHARD_MODEL = "profiles/r06fin_shard_schedule_2p22.json"
 
 
 def model_record(log_n, world, config5, measured):
