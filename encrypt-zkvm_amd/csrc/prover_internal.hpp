@@ -246,6 +246,7 @@ struct zk_prover {
     // the block levels (0 .. log2 Bl) of the trace, composition and FRI layer-0 trees over this rank's cosets
     // (shard.hip DistTree): (2 Bl - 1) x n digests for the row trees, (2 Bl - 1) x n / 2 for layer 0 (fold >= 2)
     uint8_t *sh_blk = nullptr, *sh_cblk = nullptr, *sh_fblk = nullptr;
+    uint8_t *sh_f1blk = nullptr;  // ... and FRI layer 1's, (2 Bl - 1) x n / 4 (committed on every rank, shard.hip S6)
     unsigned *sh_flags = nullptr;  // world degree flags
     // FieldExtension::Quadratic working set (planar E buffers), allocated on first use
     fe *x_comp = nullptr, *x_ctmp = nullptr, *x_clde = nullptr, *x_deep = nullptr, *x_fri = nullptr,

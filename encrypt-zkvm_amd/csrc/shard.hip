@@ -13,7 +13,8 @@
 //                                all-gather of the G subtree roots
 //   composition interpolation    per-coset inverse NTT local; all-to-all of coefficient slices for the
 //                                cross-coset radix-8 step; all-gather of the 7 column polynomials
-//   FRI layers >= 1              all-gather of layer 1, then replicated (small)
+//   FRI layers 1, >= 2           layer 1 as layer 0 (block trees, local fold), all-gather of layer 2, then the
+//                                rest on the lead rank (small)
 //   openings                     every rank gathers what it owns, all-gather, the host combines
 // The Fiat-Shamir transcript runs on every process's host over identical (all-gathered) roots, so no
 // challenge is ever broadcast.  The proof bytes equal the single-GPU prover's (tests/test_sharded.py).
@@ -229,16 +230,18 @@ __global__ void k_sh_pack_coset(const fe *c, size_t plane_stride, int log_n, int
 // single-GPU fold (kernels.hip k_fri_fold: idft_small, then Horner at beta = alpha / x_r')
 template <int F>
 __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n, int Bl, int g, int log_m,
-                                                      const FoldConsts *Fc, const fe *wi_lo, const fe *wi_hi, fe *out) {
+                                                      const FoldConsts *Fc, const fe *wi_lo, const fe *wi_hi,
+                                                      size_t wstride, fe *out) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= ((size_t)Bl << log_m)) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
-    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;  // row index in layer 0 (size N, wstride 1)
+    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;  // row index in the layer (1/x_r: w_N^-(rp wstride))
+    const size_t wi = rp * wstride;
     fe v[F];
 #pragma unroll
     for (int k = 0; k < F; k++) v[k] = deep[j * n + q0 + ((size_t)k << log_m)];
-    const fe beta = fe_mul(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    const fe beta = fe_mul(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[wi & 2047], wi_hi[wi >> 11])));
     idft_small<F>(v, Fc->zinv);
     fe acc = v[F - 1];
 #pragma unroll
@@ -250,19 +253,19 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0(const fe *deep, int log_n,
 template <int F>
 __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int log_n, int Bl, int g, int log_m,
                                                           const FoldConstsE *Fc, const fe *wi_lo, const fe *wi_hi,
-                                                          fe *out) {
+                                                          size_t wstride, fe *out) {
     const size_t n = (size_t)1 << log_n, m = (size_t)1 << log_m, cs = (size_t)Bl * n, om = (size_t)Bl * m;
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= om) return;
     const size_t j = t >> log_m, q0 = t & (m - 1);
-    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0;
+    const size_t rp = (size_t)(g * Bl + (int)j) + 8 * q0, wi = rp * wstride;
     fe va[F], vb[F];
 #pragma unroll
     for (int k = 0; k < F; k++) {
         va[k] = deep[j * n + q0 + ((size_t)k << log_m)];
         vb[k] = deep[cs + j * n + q0 + ((size_t)k << log_m)];
     }
-    const fe2 beta = fe2_mulb(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[rp & 2047], wi_hi[rp >> 11])));
+    const fe2 beta = fe2_mulb(Fc->alpha, fe_mul(Fc->inv_offset, fe_mul(wi_lo[wi & 2047], wi_hi[wi >> 11])));
     idft_small<F>(va, Fc->zinv);
     idft_small<F>(vb, Fc->zinv);
     fe2 acc = fe2{va[F - 1], vb[F - 1]};
@@ -273,18 +276,18 @@ __global__ void __launch_bounds__(256) k_sh_fri_fold0_ext(const fe *deep, int lo
     out[om + t] = acc.b;
 }
 
-// the first fold's launch for fold 2 / 4 / 8 / 16 (KX planes)
+// a fold over the local cosets (layer 0, or layer 1 with wstride = fold) for fold 2 / 4 / 8 / 16 (KX planes)
 static void sh_fri_fold0(hipStream_t st, int KX, int fold, const fe *deep, int log_n, int Bl, int g, int log_m,
-                         const void *consts, const fe *wi_lo, const fe *wi_hi, fe *out) {
+                         const void *consts, const fe *wi_lo, const fe *wi_hi, size_t wstride, fe *out) {
     const dim3 grid(cdiv((size_t)Bl << log_m, 256));
 #define ZK_SH_FOLD(FF)                                                                                              \
     do {                                                                                                            \
         if (KX == 1)                                                                                                \
             hipLaunchKernelGGL(k_sh_fri_fold0<FF>, grid, dim3(256), 0, st, deep, log_n, Bl, g, log_m,               \
-                               (const FoldConsts *)consts, wi_lo, wi_hi, out);                                      \
+                               (const FoldConsts *)consts, wi_lo, wi_hi, wstride, out);                             \
         else                                                                                                        \
             hipLaunchKernelGGL(k_sh_fri_fold0_ext<FF>, grid, dim3(256), 0, st, deep, log_n, Bl, g, log_m,           \
-                               (const FoldConstsE *)consts, wi_lo, wi_hi, out);                                     \
+                               (const FoldConstsE *)consts, wi_lo, wi_hi, wstride, out);                            \
     } while (0)
     switch (fold) {
         case 2: ZK_SH_FOLD(2); break;
@@ -496,7 +499,9 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     T.nodes = nodes;
     const size_t Q = T.Q, QG = Q / X.G;  // groups per destination rank
     const int log_QG = ilog2(QG);
-    const int log_K = QG >= 4 * 256 ? 2 : 0, K = 1 << log_K;  // pieces of at least 256 groups per destination
+    // pieces only where the transfer outweighs the latency of three more collectives: >= 1 MiB per destination and
+    // piece (the trace and composition trees at 2^20 and up; small FRI trees go in one piece)
+    const int log_K = QG >= ((size_t)1 << 17) ? 2 : 0, K = 1 << log_K;
     const int log_QGK = log_QG - log_K;
     const size_t piece = 32 * (size_t)X.G << log_QGK;  // bytes of one piece (all destinations)
     std::vector<XH> h(K);
@@ -1328,15 +1333,22 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     stage_mark(P0, "deep");
 
-    // S6: FRI.  Layer 0 is sharded (its fold rows stay in one coset); layer 1 is all-gathered and the
-    // remaining layers run on local rank 0 of every process.
+    // S6: FRI.  Layer 0 is sharded (its fold rows stay in one coset), and so is layer 1 when a layer follows it and
+    // every rank holds enough of its rows; the next layer is all-gathered and the remaining layers run on local rank 0
+    // of every process.
     const int nl = fri_num_layers(N, opt);
     if (nl > ZK_MAX_FRI_LAYERS) ZK_FAIL(ZK_ERR_INVALID_ARG, "too many FRI layers");
     R.num_fri_layers = (uint32_t)nl;
     std::vector<uint8_t *> f0n(nlp);  // the layer-0 tree's subtree heap (m nodes) in the NTT scratch
     const size_t rows0 = N / fold;  // layer-0 Merkle leaves
     std::vector<const fe *> layer_vals(nl + 1);
-    int lb1 = 0;  // layer 1's storage: natural (0) or coset-major over 8 cosets (3; FriLayout)
+    // layer 1 committed and folded on every rank (sh1) and then layer lg = 2 all-gathered, else layer lg = 1; the
+    // gathered layer's storage: natural (lbg 0) or coset-major over 8 cosets (3; FriLayout)
+    const size_t m1 = m / fold;
+    bool sh1 = false;
+    int lg = 1, lbg = 0;
+    DistTree Tfri1;
+    std::vector<uint8_t *> f1n(nlp);
     std::vector<uint8_t *> layer_leaves(nl), layer_nodes(nl);
     std::vector<size_t> layer_len(nl + 1);
     std::vector<fe> rem_flat;
@@ -1381,18 +1393,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }, scratch, bk, f0n, "fri0_digests", "fri0_roots"));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
-        {
-            std::vector<const void *> snd(nlp);
-            std::vector<void *> rcv(nlp);
+        // alpha of `layer` from the host coin, into every local rank's fold constants
+        auto draw_fold = [&](int layer) -> int {
             FoldConsts F;
             FoldConstsE FE;
             if (KX == 1) {
                 const fe alpha = coin.draw();
-                fe_to_bytes(alpha, R.fri_alphas[0]);
+                fe_to_bytes(alpha, R.fri_alphas[layer]);
                 F = fold_consts(alpha, fold);
             } else {
                 const fe2 alpha = coin.draw_ext(2);
-                fe_to_bytes(alpha.a, R.fri_alphas[0]);
+                fe_to_bytes(alpha.a, R.fri_alphas[layer]);
                 FE = fold_consts_ext(alpha, fold);
             }
             for (int l = 0; l < nlp; l++) {
@@ -1400,31 +1411,79 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 ZK_CHECK_HIP(hipSetDevice(p->device));
                 if (KX == 1) ZK_TRY(h2d_small(p, p->fold_consts, &F, sizeof F));
                 else ZK_TRY(h2d_small(p, p->x_fold_consts, &FE, sizeof FE));
-                sh_fri_fold0(p->st, KX, (int)fold, DEEP(p), log_n, Bl, X.rank[l], log_m,
-                             KX == 1 ? (const void *)p->fold_consts : (const void *)p->x_fold_consts,
-                             X.pl[l]->TN.inv_lo, X.pl[l]->TN.inv_hi, CTMP(p));
-                snd[l] = CTMP(p);
-                // (base field with layers after it: the gathered chunks [s][j][q0] are layer 1 coset-major -- coset
-                // s Bl + j, position q0 -- which the layer kernels read in place; over E each source's chunk holds both
-                // planes, and a last layer goes to the host in natural order)
-                rcv[l] = KX == 1 && nl > 1 ? FRI(p) : COMP(p);
             }
-            ZK_TRY(xchg(X, "fri_layer1", AG, snd, rcv, (size_t)KX * Bl * m * sizeof(fe)));
-            ZK_TRY(lead_segment(X));  // from here the FRI layers >= 1 and the queries run on the lead rank alone
-            ZK_CHECK_HIP(hipSetDevice(P0->device));
-            for (int pln = 0; !(KX == 1 && nl > 1) && pln < KX; pln++)
-                hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(rows0, 256)), dim3(256), 0, P0->st,
-                                   (const uint8_t *)(COMP(P0) + (size_t)pln * Bl * m), G, Bl, log_m, 16,
-                                   (size_t)KX * Bl * m, (uint8_t *)(FRI(P0) + pln * rows0));
+            return ZK_OK;
+        };
+        ZK_TRY(draw_fold(0));
+        for (int l = 0; l < nlp; l++) {  // layer 0 -> this rank's layer-1 values [plane][j][q0] in CTMP
+            zk_prover *p = X.P[l];
+            ZK_CHECK_HIP(hipSetDevice(p->device));
+            sh_fri_fold0(p->st, KX, (int)fold, DEEP(p), log_n, Bl, X.rank[l], log_m,
+                         KX == 1 ? (const void *)p->fold_consts : (const void *)p->x_fold_consts, X.pl[l]->TN.inv_lo,
+                         X.pl[l]->TN.inv_hi, 1, CTMP(p));
         }
-        lb1 = KX == 1 && nl > 1 ? 3 : 0;
-        layer_vals[1] = FRI(P0);
-        layer_len[1] = rows0;
+        // Layer 1 (round 6): with a layer after it and enough rows per rank it is committed and folded on every rank over
+        // its own cosets, as layer 0 (block ownership keeps its leaves and fold rows local), and layer 2 is all-gathered
+        // instead of layer 1; the lead rank runs the layers after the gathered one.
+        sh1 = nl >= 2 && m1 >= 8 * (size_t)G;
+        lg = sh1 ? 2 : 1;
+        const size_t mg = sh1 ? m1 : m, Lg = 8 * mg;  // the gathered layer: positions per coset, length
+        if (sh1) {
+            for (int l = 0; l < nlp; l++) {
+                f1n[l] = f0n[l] + 32 * m;  // (after the layer-0 subtree's m nodes)
+                bk[l] = X.P[l]->sh_f1blk;
+            }
+            const int log_m1 = ilog2(m1);
+            ZK_TRY(dist_commit(X, Tfri1, rows0 / fold, [&](int l, uint8_t *send, int log_QG, int log_K, int k) {
+                zk_prover *p = X.P[l];
+                uint8_t *b = p->sh_f1blk;
+                const int f = (int)fold;
+                if (Bl == 4) launch_fri0_blk<4>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
+                else if (Bl == 2) launch_fri0_blk<2>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
+                else launch_fri0_blk<1>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
+            }, scratch, bk, f1n, "fri1_digests", "fri1_roots"));
+            memcpy(R.fri_roots[1], Tfri1.root, 32);
+            coin.reseed(R.fri_roots[1]);
+            ZK_TRY(draw_fold(1));
+            for (int l = 0; l < nlp; l++) {  // layer 1 -> this rank's layer-2 values in COMP (N / fold: wstride fold)
+                zk_prover *p = X.P[l];
+                ZK_CHECK_HIP(hipSetDevice(p->device));
+                sh_fri_fold0(p->st, KX, (int)fold, CTMP(p), log_m, Bl, X.rank[l], log_m1,
+                             KX == 1 ? (const void *)p->fold_consts : (const void *)p->x_fold_consts, X.pl[l]->TN.inv_lo,
+                             X.pl[l]->TN.inv_hi, fold, COMP(p));
+            }
+        }
         {
-            // layers >= 1 are replicated on local rank 0: their coins run on the device as in the single-GPU path
-            // (fri_coin_launch: no host round trip per layer), the host replays the transcript after one flush
-            fe *next = FRI(P0) + KX * rows0;
-            uint8_t *dig = P0->fri_dig;  // the all-to-all scratch is free once layer 0 is committed
+            // the gathered layer into the lead's FRI buffer: base field with layers after it, in place (chunk [s][j] is
+            // coset s Bl + j: the layer arrives coset-major, which the layer kernels read through FriLayout); else through
+            // a staging area, permuted into natural order per plane (over E each source's chunk holds both planes, and a
+            // last layer goes to the host in natural order)
+            const bool inplace = KX == 1 && nl > lg;
+            std::vector<const void *> snd(nlp);
+            std::vector<void *> rcv(nlp);
+            for (int l = 0; l < nlp; l++) {
+                zk_prover *p = X.P[l];
+                snd[l] = sh1 ? COMP(p) : CTMP(p);
+                rcv[l] = inplace ? FRI(p) : sh1 ? FRI(p) + KX * Lg : COMP(p);
+            }
+            ZK_TRY(xchg(X, sh1 ? "fri_layer2" : "fri_layer1", AG, snd, rcv, (size_t)KX * Bl * mg * sizeof(fe)));
+            ZK_TRY(lead_segment(X));  // from here the FRI layers after it and the queries run on the lead rank alone
+            ZK_CHECK_HIP(hipSetDevice(P0->device));
+            const fe *stage = sh1 ? FRI(P0) + KX * Lg : COMP(P0);
+            for (int pln = 0; !inplace && pln < KX; pln++)
+                hipLaunchKernelGGL(k_sh_permute, dim3(cdiv(Lg, 256)), dim3(256), 0, P0->st,
+                                   (const uint8_t *)(stage + (size_t)pln * Bl * mg), G, Bl, ilog2(mg), 16,
+                                   (size_t)KX * Bl * mg, (uint8_t *)(FRI(P0) + pln * Lg));
+            lbg = inplace ? 3 : 0;
+        }
+        layer_len[1] = rows0;
+        layer_vals[lg] = FRI(P0);
+        layer_len[lg] = Lg;
+        {
+            // the lead's layers: their coins run on the device as in the single-GPU path (fri_coin_launch: no host round
+            // trip per layer), the host replays the transcript after one flush
+            fe *next = FRI(P0) + KX * Lg;
+            uint8_t *dig = P0->fri_dig;  // the all-to-all scratch is free once layers 0 (and 1) are committed
             fe *alpha_dev = nullptr;
             if (KX == 1) {
                 const FoldConsts F = fold_consts(fe_zero(), fold);
@@ -1435,13 +1494,13 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 ZK_TRY(h2d_small(P0, P0->x_fold_consts, &F, sizeof F));
                 alpha_dev = &((FoldConstsE *)P0->x_fold_consts)->alpha.a;
             }
-            ZK_TRY(h2d_small(P0, P0->fri_seed, coin.seed, 32));  // reseeded with layer 0's root: the counter restarts
-            for (int l = 1; l < nl; l++) {
+            ZK_TRY(h2d_small(P0, P0->fri_seed, coin.seed, 32));  // (the next reseed restarts the counter)
+            for (int l = lg; l < nl; l++) {
                 const size_t L = layer_len[l], rows = L / fold;
                 layer_leaves[l] = dig;
                 layer_nodes[l] = dig + 32 * rows;
                 dig += 64 * rows;
-                const int lb = l == 1 ? lb1 : 0;  // layer 1 as gathered (coset-major over 8 cosets, base field)
+                const int lb = l == lg ? lbg : 0;  // the gathered layer as it arrived
                 if (KX == 1) commit_fri_layer(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
                 else commit_fri_layer_ext(P0->st, layer_vals[l], L, (int)fold, layer_leaves[l], layer_nodes[l], lb);
                 fri_coin_launch(P0->st, (uint32_t *)P0->fri_seed, layer_nodes[l] + 32, KX, alpha_dev, P0->fri_alphas + 2 * l);
@@ -1451,13 +1510,14 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 layer_len[l + 1] = rows;
                 next += KX * rows;
             }
-            // one round trip: roots and device alphas of layers >= 1, the last layer
+            // one round trip: roots and device alphas of the lead's layers, the last layer
             std::vector<fe> rv(KX * layer_len[nl]), dalpha(2 * nl);
-            for (int l = 1; l < nl; l++) ZK_TRY(d2h_small(P0, R.fri_roots[l], layer_nodes[l] + 32, 32));
-            if (nl > 1) ZK_TRY(d2h_small(P0, dalpha.data() + 2, P0->fri_alphas + 2, 2 * (nl - 1) * sizeof(fe)));
+            for (int l = lg; l < nl; l++) ZK_TRY(d2h_small(P0, R.fri_roots[l], layer_nodes[l] + 32, 32));
+            if (nl > lg)
+                ZK_TRY(d2h_small(P0, dalpha.data() + 2 * lg, P0->fri_alphas + 2 * lg, 2 * (nl - lg) * sizeof(fe)));
             ZK_TRY(d2h_small(P0, rv.data(), layer_vals[nl], rv.size() * sizeof(fe)));
             ZK_TRY(d2h_flush(P0));
-            for (int l = 1; l < nl; l++) {  // host replay of the same transcript
+            for (int l = lg; l < nl; l++) {  // host replay of the same transcript
                 coin.reseed(R.fri_roots[l]);
                 const fe2 alpha = KX == 1 ? fe2{coin.draw(), fe_zero()} : coin.draw_ext(2);
                 fe_to_bytes(alpha.a, R.fri_alphas[l]);
@@ -1483,7 +1543,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     O.plans[1] = O.plans[0];  // the composition tree opens the same positions
     for (int l = 0; l < nl; l++) plan_batch(l == 0 ? rows0 : layer_len[l] / fold, fri_pos[l], O.plans[2 + l]);
     // chunk requests: owner rank (-1: host top node), local buffer id, byte offset
-    enum { B_LDE, B_CLDE, B_DEEP, B_TN, B_CN, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B };
+    enum { B_LDE, B_CLDE, B_DEEP, B_TN, B_CN, B_F0N, B_FRI, B_FRI_DIG, B_TB, B_CB, B_F0B, B_CT, B_F1N, B_F1B };
     struct Req {
         int owner, buf;
         size_t off;
@@ -1507,7 +1567,17 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     }
     for (int l = 1; l < nl; l++) {
         const size_t L = layer_len[l], rows = L / fold;
-        const int lb = l == 1 ? lb1 : 0, lcn = ilog2(L) - lb;
+        if (l == 1 && sh1) {  // layer 1 on the owners of its cosets: value i at CTMP [plane][j][i >> 3], coset i & 7
+            for (uint64_t r : fri_pos[1])
+                for (uint32_t k = 0; k < fold; k++)
+                    for (int pln = 0; pln < KX; pln++) {
+                        const size_t i = r + k * rows;
+                        const int c = (int)(i & 7), own = c / Bl, j = c % Bl;
+                        req.push_back({own, B_CT, 16 * ((size_t)pln * Bl * m + (size_t)j * m + (i >> 3)), nullptr});
+                    }
+            continue;
+        }
+        const int lb = l == lg ? lbg : 0, lcn = ilog2(L) - lb;
         for (uint64_t r : fri_pos[l])
             for (uint32_t k = 0; k < fold; k++)
                 for (int pln = 0; pln < KX; pln++) {
@@ -1518,12 +1588,13 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 }
     }
     const size_t off_dig = req.size();
-    const DistTree *trees[3] = {&Ttrace, &Tcomp, &Tfri0};
-    const int tbuf[3][3] = {{-1, B_TN, B_TB}, {-1, B_CN, B_CB}, {-1, B_F0N, B_F0B}};  // (DistTree::Loc::which)
+    const DistTree *trees[4] = {&Ttrace, &Tcomp, &Tfri0, &Tfri1};
+    const int tbuf[4][3] = {{-1, B_TN, B_TB}, {-1, B_CN, B_CB}, {-1, B_F0N, B_F0B}, {-1, B_F1N, B_F1B}};  // (Loc::which)
+    const int ndist = sh1 ? 4 : 3;  // distributed trees: trace, composition, FRI layer 0 (and 1)
     for (int b = 0; b < 2 + nl; b++)
         for (auto &path : O.plans[b].paths)
             for (auto &e : path) {
-                if (b < 3) {
+                if (b < ndist) {
                     const DistTree::Loc L = trees[b]->locate(e.first, e.second);
                     if (L.owner < 0) {
                         const uint8_t *hp = trees[b]->top[e.second].data();
@@ -1533,7 +1604,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                         req.push_back({L.owner, tbuf[b][L.which], L.off, nullptr});
                         req.push_back({L.owner, tbuf[b][L.which], L.off + 16, nullptr});
                     }
-                } else {  // replicated FRI layers >= 1 (local rank 0 of every process, i.e. rank 0 serves)
+                } else {  // the lead's FRI layers (local rank 0 of every process, i.e. rank 0 serves)
                     const uint8_t *base = e.first ? layer_nodes[b - 2] : layer_leaves[b - 2];
                     const size_t off = (size_t)(base + 32 * e.second - P0->fri_dig);
                     req.push_back({0, B_FRI_DIG, off, nullptr});
@@ -1548,9 +1619,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         std::vector<void *> rcv(nlp);
         for (int l = 0; l < nlp; l++) {
             zk_prover *p = X.P[l];
-            const uint8_t *bases[11] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
+            const uint8_t *bases[14] = {(const uint8_t *)p->lde, (const uint8_t *)CLDE(p), (const uint8_t *)DEEP(p),
                                         p->nodes, p->cnodes, f0n[l],
-                                        (const uint8_t *)FRI(p), p->fri_dig, p->sh_blk, p->sh_cblk, p->sh_fblk};
+                                        (const uint8_t *)FRI(p), p->fri_dig, p->sh_blk, p->sh_cblk, p->sh_fblk,
+                                        (const uint8_t *)CTMP(p), f1n[l], p->sh_f1blk};
             // (the prover's pinned staging: an asynchronous copy, no wait -- the next proof on this prover writes it again
             // only after this one has drained)
             uint64_t *addr = p->h_gather_idx;
@@ -1710,6 +1782,7 @@ int zk::prove_sharded_entry(zk_comm *comm, zk_prover **provers, int nlocal, cons
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_blk, 32 * (2 * bl - 1) * mn));
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_cblk, 32 * (2 * bl - 1) * mn));
             ZK_CHECK_HIP(p->arena.alloc(&p->sh_fblk, 32 * (2 * bl - 1) * (mn / 2)));
+            ZK_CHECK_HIP(p->arena.alloc(&p->sh_f1blk, 32 * (2 * bl - 1) * (mn / 4)));
         }
     }
     // one rank: nothing to shard or exchange, so the single-GPU path proves it (the same proof bytes; its
