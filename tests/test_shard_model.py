@@ -63,3 +63,16 @@ def test_project_fits_replicated_and_divided_work():
     assert pr["fit_all_rank_segments"]["replicated_ms_R"] == pytest.approx(1.0, abs=1e-3)
     assert pr["fit_all_rank_segments"]["divided_ms_S"] == pytest.approx(16.0, abs=1e-3)
     assert pr[8]["per_rank_ms"] == pytest.approx(1.0 + 2.0, abs=0.01)
+
+
+def test_committed_projection_replays_from_its_schedules():
+    """The projection committed with the round's final sharded schedules (bench.py's `model`) is
+    what tools/shard_model.py computes from those schedules: the per-rank figures are reproducible from the file."""
+    import json
+    path = Path(__file__).resolve().parent.parent / "profiles" / "r06fin_shard_schedule_2p22.json"
+    d = json.loads(path.read_text())
+    pr = sm.project(d["schedules"])
+    for kind, rec in d["projection"].items():
+        for G in ("2", "4", "8"):
+            assert pr[kind][int(G)]["per_rank_ms"] == pytest.approx(rec[G]["per_rank_ms"], abs=0.011), (kind, G)
+            assert pr[kind][int(G)]["exposed_exchange_ms"] == pytest.approx(rec[G]["exposed_exchange_ms"], abs=0.011)
