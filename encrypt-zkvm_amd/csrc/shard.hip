@@ -483,11 +483,12 @@ int xchg(Ctx &X, const char *name, XOp op, const std::vector<const void *> &snd,
 // the block levels (the hash kernel: leaves, their subtree up to Lb into blk, block nodes into the send scratch in piece
 // order), all-to-all of the block nodes, merged on arrival into level Lb + 1 of the subtree, the subtree, roots.  The
 // block nodes go out in K pieces: piece k's all-to-all runs on the exchange stream while piece k + 1 is hashed.
-// hash(l, send, log_QG, log_K, k) launches piece k of local rank l.
+// hash(l, send, log_QG, log_K, k) launches piece k of local rank l.  `rows`: the leaves are LDE rows (7 or 2 BLAKE3
+// blocks each), whose hashing the pieces hide; the FRI trees' leaves hash in a fraction of that and go in one piece.
 template <typename HashFn>
 int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<uint8_t *> &scratch,
                 const std::vector<uint8_t *> &blk, const std::vector<uint8_t *> &nodes, const char *digests_name,
-                const char *roots_name) {
+                const char *roots_name, bool rows = true) {
     const int nl = (int)X.P.size();
     T.M = M;
     T.G = X.G;
@@ -501,7 +502,7 @@ int dist_commit(Ctx &X, DistTree &T, size_t M, HashFn hash, const std::vector<ui
     const int log_QG = ilog2(QG);
     // pieces only where the transfer outweighs the latency of three more collectives: >= 1 MiB per destination and
     // piece (the trace and composition trees at 2^20 and up; small FRI trees go in one piece)
-    const int log_K = QG >= ((size_t)1 << 17) ? 2 : 0, K = 1 << log_K;
+    const int log_K = rows && QG >= ((size_t)1 << 17) ? 2 : 0, K = 1 << log_K;
     const int log_QGK = log_QG - log_K;
     const size_t piece = 32 * (size_t)X.G << log_QGK;  // bytes of one piece (all destinations)
     std::vector<XH> h(K);
@@ -1390,7 +1391,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             if (Bl == 4) launch_fri0_blk<4>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
             else if (Bl == 2) launch_fri0_blk<2>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
             else launch_fri0_blk<1>(p->st, KX, d, log_n, f, log_m, log_QG, log_K, k, b, send);
-        }, scratch, bk, f0n, "fri0_digests", "fri0_roots"));
+        }, scratch, bk, f0n, "fri0_digests", "fri0_roots", false));
         memcpy(R.fri_roots[0], Tfri0.root, 32);
         coin.reseed(R.fri_roots[0]);
         // alpha of `layer` from the host coin, into every local rank's fold constants
@@ -1441,7 +1442,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 if (Bl == 4) launch_fri0_blk<4>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
                 else if (Bl == 2) launch_fri0_blk<2>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
                 else launch_fri0_blk<1>(p->st, KX, CTMP(p), log_m, f, log_m1, log_QG, log_K, k, b, send);
-            }, scratch, bk, f1n, "fri1_digests", "fri1_roots"));
+            }, scratch, bk, f1n, "fri1_digests", "fri1_roots", false));
             memcpy(R.fri_roots[1], Tfri1.root, 32);
             coin.reseed(R.fri_roots[1]);
             ZK_TRY(draw_fold(1));
