@@ -993,6 +993,8 @@ def model_record(log_n, world, config5, measured):
     if d.get("log_n") != log_n:
         return None
     out = {"source": SHARD_MODEL}
+    if REHEARSE:  # ranks sharing one GPU over TCP: the comparison is not a measurement of the model
+        out["rehearsal"] = True
     for kind, ms in measured.items():
         pr = d.get("projection", {}).get(kind, {}).get(str(world))
         if pr:
