@@ -1,7 +1,7 @@
 """One proof with the LDE domain sharded by coset over several GPUs (zk_prove_sharded).
 
-Rank g of `world` owns LDE cosets r = g (mod world); leaf digests, composition coefficient slices,
-FRI layer 1 and the openings are exchanged through a communicator:
+Rank g of `world` owns the block of LDE cosets g*Bl .. g*Bl+Bl-1 (Bl = blowup / world); block Merkle nodes,
+composition coefficient slices, FRI layers 0-1 and the openings are exchanged through a communicator:
 
   * ShardedProver.loopback(world)       -- every rank driven from this process (one prover per rank,
                                            in-process copies); used by the tests on one GPU;

@@ -96,6 +96,33 @@ def test_sharded_matches_single_gpu_2_14(world, ext):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fold,rem,ext", [(2, 127, 1), (4, 127, 2), (16, 127, 1), (16, 63, 2), (8, 31, 2)])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_fri_layer1_folds_2_14(world, fold, rem, ext):
+    """Sharded FRI layer 1 (taken when the prover has two or more layers and layer 1 holds >= 8 points per rank) at
+    every folding factor, both extensions and the in-place / staged gathered layer: byte-identical to one GPU."""
+    from zkvm_amd.prover import vm_trace
+    from zkvm_amd.workloads import make_workload, ops_for_trace_len
+    src = ops_for_trace_len(14, "pushadd")
+    w = make_workload(src, seed=5 + fold)
+    trace, outputs, h = vm_trace(src, w.public, w.secret, w.server_key, w.last_row)
+    pub = make_pub_inputs(h, outputs, w.server_key.lwe_size(), w.server_key.parameters.delta)
+    opts = ProofOptions(field_extension=ext, fri_folding_factor=fold, fri_remainder_max_degree=rem)
+    g = GpuProver(0, max_trace_len=trace.shape[1])
+    try:
+        single, _, _, rc = g.prove(trace, pub, opts)
+    finally:
+        g.close()
+    assert rc == 0
+    sp = ShardedProver.loopback(world, max_trace_len=trace.shape[1])
+    try:
+        got, _ = sp.prove(trace, pub, opts)
+    finally:
+        sp.close()
+    assert got == single
+
+
+@pytest.mark.gpu
 def test_sharded_rccl_world1_and_device_trace():
     """The RCCL communicator (one rank on this GPU) and the device-resident trace path."""
     c = next(c for c in CASES if c["name"] == "cipher20")
