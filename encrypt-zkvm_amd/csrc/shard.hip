@@ -812,7 +812,7 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         return ZK_OK;
     };
     // device-resident traces: the first `rep` columns of U are interpolated by every rank itself (no exchange), right
-    // after round 0's all-gather starts, so they fill the time it takes; the rest go round robin.  A host trace splits
+    // after rounds 0 and 1's all-gathers start, so they fill the time those take; the rest go round robin.  A host trace splits
     // every column: replicating one would make every rank upload it.
     int rep = 0;
     if (!trace) {
@@ -830,12 +830,16 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // a round whose columns are not consecutive is gathered into a staging area, alternating between two buffers
     // free until S3 / S4, so round k + 1's all-gather never overwrites what round k's copy-out still reads
     auto stage_of = [&](zk_prover *p, int k) { return (k & 1) ? p->comp : p->ctmp; };
+    // in place when the round's columns are consecutive (the padding slots of a short last round then land on columns
+    // nobody interpolates -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns)
+    auto inplace_of = [&](int k) {
+        const int i0 = G * k, real = std::min(G, nS - i0), first = US[i0];
+        return US[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
+    };
     auto issue = [&](int k) -> int {  // interpolate this rank's column of round k, start the round's all-gather
         if (trace && k + 1 < rounds) ZK_TRY(upload(k + 1));
         const int i0 = G * k, real = std::min(G, nS - i0), first = US[i0];
-        // in place when the round's columns are consecutive (the padding slots of a short last round then land on
-        // columns nobody interpolates -- filled below -- or past W: p->polys holds 8 ceil(W / 8) columns)
-        const bool inplace = US[i0 + real - 1] - first == real - 1 && first + G <= 8 * ((W + 7) / 8);
+        const bool inplace = inplace_of(k);
         inplace_r[k] = inplace;
         std::vector<const void *> snd(nlp);
         std::vector<void *> rcv(nlp);
@@ -893,7 +897,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         return ZK_OK;
     };
     if (trace && rounds) ZK_TRY(upload(0));
-    if (rounds) ZK_TRY(issue(0));
+    // two rounds in flight: rounds 0 and 1 go out before the replicated columns, and round k + 2 before round k's
+    // extension when it is gathered in place (after it when staged: it reuses round k's staging buffer), so the link
+    // always has the next round queued
+    for (int k = 0; k < std::min(rounds, 2); k++) ZK_TRY(issue(k));
     if (nrep) {
         ZK_TRY(sched_entry(X, 'K', -1));
         for (int l = 0; l < nlp; l++) {
@@ -912,8 +919,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
         }
     }
     for (int k = 0; k < rounds; k++) {
-        if (k + 1 < rounds) ZK_TRY(issue(k + 1));
+        const bool next = k + 2 < rounds, ahead = next && inplace_of(k + 2);
+        if (ahead) ZK_TRY(issue(k + 2));
         ZK_TRY(finish(k));
+        if (next && !ahead) ZK_TRY(issue(k + 2));
     }
     // the columns formed from the last row (after the last round: a short round's padding may have landed there)
     if (X.fixed) {
@@ -1110,14 +1119,19 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // coset LDE + commitment
     XH hdeg;  // the degree flags' all-gather (read once the composition is committed)
     {
-        // (the first plane's assertion quotient reads only the trace coefficients: it runs under the all-to-all)
+        // (the first plane's assertion quotient reads only the trace coefficients: it runs under the all-to-all, and
+        // its range sums' all-gather follows the all-to-all's pieces on the exchange stream)
         std::vector<const void *> bnd0(nlp);
+        std::vector<void *> bsum(nlp);
+        XH hb0;
         for (int l = 0; bnd_split && l < nlp; l++) {
             zk_prover *p = X.P[l];
             ZK_CHECK_HIP(hipSetDevice(p->device));
             bnd0[l] = boundary_range_begin(p->st, p->polys, log_n, KX == 1 ? K : Kp[0], K.g_last2, p->dscratch,
                                            (size_t)X.rank[l] * kg, kg);
+            bsum[l] = p->sh_buf;
         }
+        if (bnd_split) ZK_TRY(xchg_start(X, "bnd_totals", AG, bnd0, bsum, 2 * sizeof(fe), &hb0));
         for (XH &h : hs) ZK_TRY(xchg_wait(X, h));
         const fe scale = h_inv(fe_make(CE)), w8inv = h_inv(h_root_of_unity(3)), inv3n = h_inv(h_pow(three, n));
         std::vector<const void *> fs(nlp);
@@ -1139,21 +1153,41 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             fs[l] = p->flag;
             fr[l] = p->sh_flags;
         }
+        // the column polynomials: one all-gather per column, started in order on the exchange stream (they run back to
+        // back); the coset LDE of a group of columns starts as soon as the group has arrived, so the later columns'
+        // all-gathers run under the earlier columns' LDEs.  Over F the columns after column 0 go out before its
+        // assertion quotient is added (over E the second plane's range sums would queue behind them).
+        std::vector<XH> hc(CK);
+        auto start_columns = [&](int c0, int c1) -> int {
+            for (int c = c0; c < c1; c++) {
+                std::vector<const void *> s2(nlp);
+                std::vector<void *> r2(nlp);
+                for (int l = 0; l < nlp; l++) {
+                    s2[l] = CTMP(X.P[l]) + c * kg;
+                    r2[l] = X.P[l]->cpolys + (size_t)c * n;
+                }
+                ZK_TRY(xchg_start(X, "comp_columns", AG, s2, r2, kg * sizeof(fe), &hc[c]));
+            }
+            return ZK_OK;
+        };
+        const int early = KX == 1 ? 1 : CK;  // columns [early, CK) start before the quotient
+        if (early < CK) ZK_TRY(start_columns(early, CK));
         // assertion quotient over this rank's slice of composition column 0 (plane by plane: the division scratch is
         // shared); the range sums are all-gathered and each rank adds the later ranks' as its carry
         for (int pln = 0; bnd_split && pln < KX; pln++) {
             const AirConsts &Kb = KX == 1 ? K : Kp[pln];
-            std::vector<const void *> s2(nlp);
-            std::vector<void *> r2(nlp);
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                s2[l] = pln == 0 ? bnd0[l]
-                                 : boundary_range_begin(p->st, p->polys, log_n, Kb, K.g_last2, p->dscratch,
-                                                        (size_t)X.rank[l] * kg, kg);
-                r2[l] = p->sh_buf;
+            if (pln == 0) {
+                ZK_TRY(xchg_wait(X, hb0));
+            } else {
+                std::vector<const void *> s2(nlp);
+                for (int l = 0; l < nlp; l++) {
+                    zk_prover *p = X.P[l];
+                    ZK_CHECK_HIP(hipSetDevice(p->device));
+                    s2[l] = boundary_range_begin(p->st, p->polys, log_n, Kb, K.g_last2, p->dscratch,
+                                                 (size_t)X.rank[l] * kg, kg);
+                }
+                ZK_TRY(xchg(X, "bnd_totals", AG, s2, bsum, 2 * sizeof(fe)));
             }
-            ZK_TRY(xchg(X, "bnd_totals", AG, s2, r2, 2 * sizeof(fe)));
             for (int l = 0; l < nlp; l++) {
                 zk_prover *p = X.P[l];
                 ZK_CHECK_HIP(hipSetDevice(p->device));
@@ -1162,31 +1196,25 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
                 boundary_range_end(p->st, log_n, K.g_last2, p->dscratch, k0, kg, p->ood, CTMP(p) + pln * kg - k0, p->flag);
             }
         }
-        // the column polynomials: one all-gather per column, all started at once (they run back to back on the
-        // exchange stream); the coset LDE of a group of columns starts as soon as the group has arrived, so the later
-        // columns' all-gathers run under the earlier columns' LDEs.  Groups hold >= 2^22 LDE points per launch.
-        std::vector<XH> hc(CK);
-        for (int c = 0; c < CK; c++) {
-            std::vector<const void *> s2(nlp);
-            std::vector<void *> r2(nlp);
-            for (int l = 0; l < nlp; l++) {
-                s2[l] = CTMP(X.P[l]) + c * kg;
-                r2[l] = X.P[l]->cpolys + (size_t)c * n;
-            }
-            ZK_TRY(xchg_start(X, "comp_columns", AG, s2, r2, kg * sizeof(fe), &hc[c]));
-        }
+        ZK_TRY(start_columns(0, early));
         ZK_TRY(xchg_start(X, "degree_flags", AG, fs, fr, sizeof(unsigned), &hdeg));
+        // groups hold >= 2^22 LDE points per launch, in the order the columns went out
         const int grp = (int)std::max<size_t>(1, ((size_t)1 << 22) / ((size_t)Bl * n));
-        for (int c0 = 0; c0 < CK; c0 += grp) {
-            const int c1 = std::min(CK, c0 + grp);
-            for (int c = c0; c < c1; c++) ZK_TRY(xchg_wait(X, hc[c]));
-            for (int l = 0; l < nlp; l++) {
-                zk_prover *p = X.P[l];
-                ZK_CHECK_HIP(hipSetDevice(p->device));
-                ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys + (size_t)c0 * n, n, c1 - c0, X.rank[l] * Bl, 1, Bl,
-                        CLDE(p) + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+        auto extend = [&](int a, int b) -> int {
+            for (int c0 = a; c0 < b; c0 += grp) {
+                const int c1 = std::min(b, c0 + grp);
+                for (int c = c0; c < c1; c++) ZK_TRY(xchg_wait(X, hc[c]));
+                for (int l = 0; l < nlp; l++) {
+                    zk_prover *p = X.P[l];
+                    ZK_CHECK_HIP(hipSetDevice(p->device));
+                    ntt_lde(p->st, X.pl[l]->Tn, X.pl[l]->ct, p->cpolys + (size_t)c0 * n, n, c1 - c0, X.rank[l] * Bl, 1,
+                            Bl, CLDE(p) + (size_t)c0 * Bl * n, (size_t)Bl * n, n, p->tmp);
+                }
             }
-        }
+            return ZK_OK;
+        };
+        ZK_TRY(extend(early, CK));
+        ZK_TRY(extend(0, early));
     }
     for (int l = 0; l < nlp; l++) nd[l] = X.P[l]->cnodes;
     DistTree Tcomp;
@@ -1228,13 +1256,15 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
             hipLaunchKernelGGL(k_sh_suffix_carry, dim3(1), dim3(64), 0, p->st, p->sh_buf, G, X.rank[l], nc, p->ood);
             Dk[l] = end(p, (size_t)X.rank[l] * nr, p->ood);
         }
+        XH hp[2];  // (both planes' all-gathers go out before either is waited for)
         for (int plane = 0; plane < kx; plane++) {
             for (int l = 0; l < nlp; l++) {
                 snd[l] = Dk[l] + (size_t)plane * n + (size_t)X.rank[l] * nr;
                 rcv[l] = (void *)(Dk[l] + (size_t)plane * n);
             }
-            ZK_TRY(xchg(X, "deep_slices", AG, snd, rcv, nr * sizeof(fe)));
+            ZK_TRY(xchg_start(X, "deep_slices", AG, snd, rcv, nr * sizeof(fe), &hp[plane]));
         }
+        for (int plane = 0; plane < kx; plane++) ZK_TRY(xchg_wait(X, hp[plane]));
         return ZK_OK;
     };
 
