@@ -816,9 +816,10 @@ int prove_sharded(Ctx &X, const uint8_t *trace, const zk_options *opt, const zk_
     // every column: replicating one would make every rank upload it.
     int rep = 0;
     if (!trace) {
-        // from the replayed schedules of 2^22 proofs (profiles/r06d_split_sweep_2p22.json): at
-        // G = 2 the link is the bound and replicating every column wins; from G = 4 on four columns hide round 0
-        const int dflt = G == 2 ? W : 4;
+        // from the replayed schedules of 2^22 proofs (profiles/r06zc_split_sweep_2p22.json):
+        // with two rounds in flight four columns hide rounds 0 and 1 at every world size (at G = 2 replicating every
+        // column, the one-round-in-flight optimum, is 1.1 ms slower)
+        const int dflt = 4;
         rep = std::min(nU, X.comm->split_rep >= 0 ? X.comm->split_rep : dflt);
     }
     const int nrep = rep;  // U[0 .. rep) replicated

@@ -244,9 +244,9 @@ void zk_comm_destroy(zk_comm *comm);
 int zk_comm_set_measure(zk_comm *comm, int on);
 /* The trace interpolation's split when the trace is already in every rank's HBM (trace = NULL, zk_vm_prove_sharded):
  * `replicated` of the columns to interpolate are interpolated and extended by every rank itself, at the start, under
- * the first coefficient all-gather; the others are split round robin and all-gathered.  -1 (the default): the
- * library's choice per world size, from tools/shard_model.py's replay of measured schedules --
- * few links make an all-gathered column cost more than interpolating it.  Same proof bytes for every value. */
+ * the first two coefficient all-gathers; the others are split round robin and all-gathered.  -1 (the default): the
+ * library's choice (four columns), from tools/shard_model.py's replay of measured schedules.
+ * Same proof bytes for every value. */
 int zk_comm_set_trace_split(zk_comm *comm, int replicated);
 int zk_prove_sharded(zk_comm *comm, zk_prover **provers, int nlocal, const uint8_t *trace, size_t n,
                      const zk_options *opt, const zk_pub_inputs *pub, uint8_t *proof_out, size_t *proof_len,
